@@ -1,0 +1,184 @@
+/*
+ * srtp_mi355x.h -- C ABI of the MI355X SRTP/SRTCP packet-crypto engine.
+ *
+ * Drop-in boundary for libjitsi's SRTP hot path.  Each entry point replaces a
+ * reference Java API (paths relative to src/org/jitsi/impl/neomedia/):
+ *
+ *   srtp_factory_create        <- new SRTPContextFactory(sender, masterKey,
+ *                                 masterSalt, srtpPolicy, srtcpPolicy)
+ *                                 transform/srtp/SRTPContextFactory.java:50-68
+ *   srtp_factory_close         <- SRTPContextFactory.close()          :74-86
+ *   srtp_transformer_create    <- new SRTPTransformer(fwd, rev)
+ *                                 transform/srtp/SRTPTransformer.java:82-90,
+ *                                 new SRTCPTransformer(fwd, rev)
+ *                                 transform/srtp/SRTCPTransformer.java:73-80
+ *   srtp_transformer_set_factory <- SRTPTransformer.setContextFactory :100-125,
+ *                                 SRTCPTransformer.updateFactory      :92-117
+ *   srtp_transformer_close     <- SRTPTransformer.close() :132-150,
+ *                                 SRTCPTransformer.close() :124-142
+ *   srtp_transform_device /    <- PacketTransformer.transform(RawPacket[]) and
+ *   srtp_transform_host           .reverseTransform(RawPacket[])
+ *                                 transform/PacketTransformer.java:28-53 as
+ *                                 implemented by SinglePacketTransformer
+ *                                 transform/SinglePacketTransformer.java:121-216
+ *                                 over SRTPTransformer.transform/reverseTransform
+ *                                 transform/srtp/SRTPTransformer.java:185-219
+ *                                 (per packet: SRTPCryptoContext.transformPacket
+ *                                 :658-705 / reverseTransformPacket :572-642,
+ *                                 SRTCPCryptoContext.transformPacket :391-427 /
+ *                                 reverseTransformPacket :315-374)
+ *   srtp_engine_opts.check_replay <- ConfigurationService property
+ *                                 ...srtp.SRTPCryptoContext.checkReplay
+ *                                 (SRTPCryptoContext.java:80-121)
+ *
+ * Packet bundle model (RawPacket[] -> packed segment).  Packet i occupies
+ * seg[off[i] .. off[i] + cap[i]) and its current RTP/RTCP length is len[i]
+ * (RawPacket.length).  The engine works in place: protect appends the tag (and
+ * for SRTCP the E|index word) inside cap[i]; unprotect shrinks len[i].
+ * Requirements: off[i] % 16 == 0, cap[i] <= 65535, and the segment must be
+ * readable and writable up to off[i] + roundup16(cap[i]) for every packet.
+ * status[i] receives one SRTP_STATUS_* value; "drop" statuses correspond to
+ * the reference returning null for that element.
+ *
+ * Ownership: the caller owns every buffer; the engine owns contexts, session
+ * keys and device scratch, and zeroes keys when factories are closed.
+ * Threading: calls on one engine are serialised internally; work is enqueued
+ * on the given HIP stream (NULL = the engine's own stream), so bundles that
+ * touch the same transformer must be submitted on one stream (submission order
+ * == processing order, as the reference's `synchronized` contexts give).
+ */
+#ifndef SRTP_MI355X_H
+#define SRTP_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRTP_MI355X_ABI_VERSION 1
+
+/* SRTPPolicy constants (transform/srtp/SRTPPolicy.java:29-63) */
+#define SRTP_NULL_ENCRYPTION 0
+#define SRTP_AESCM_ENCRYPTION 1
+#define SRTP_NULL_AUTHENTICATION 0
+#define SRTP_HMACSHA1_AUTHENTICATION 1
+
+/* transformer kinds */
+#define SRTP_KIND_RTP 0  /* SRTPTransformer */
+#define SRTP_KIND_RTCP 1 /* SRTCPTransformer */
+
+/* per-packet status */
+#define SRTP_STATUS_OK 0
+#define SRTP_STATUS_DROP_REPLAY 1     /* checkReplay() false */
+#define SRTP_STATUS_DROP_AUTH 2       /* authenticatePacket() false */
+#define SRTP_STATUS_DROP_VERSION 3    /* (byte0 & 0xC0) != 0x80 (SRTPTransformer.java:189) */
+#define SRTP_STATUS_DROP_NO_CONTEXT 4 /* factory closed, no context for the SSRC */
+#define SRTP_STATUS_ERR_CAPACITY 5    /* cap[i] too small for the appended trailer */
+#define SRTP_STATUS_ERR_MALFORMED 6   /* the reference throws on this packet */
+#define SRTP_STATUS_DROP_INVALID 7    /* len < 12 or len > cap (RawPacket.isInvalid) */
+#define SRTP_STATUS_NOT_PROCESSED 8   /* after an ERR_MALFORMED with abort_on_error */
+#define SRTP_STATUS_SKIPPED 9         /* SRTP_PKT_FLAG_SKIP (null element / predicate) */
+
+/* per-packet flags (javax.media.Buffer values read at SRTPCryptoContext.java:609) */
+#define SRTP_PKT_FLAG_DISCARD 0x2u
+#define SRTP_PKT_FLAG_SILENCE 0x4u
+#define SRTP_PKT_FLAG_SKIP 0x80000000u
+
+/* return codes */
+#define SRTP_OK 0
+#define SRTP_EINVAL -1
+#define SRTP_ENOMEM -2
+#define SRTP_EFULL -3   /* context / factory / transformer table full */
+#define SRTP_EDEVICE -4 /* HIP runtime error */
+#define SRTP_EPOLICY -5 /* policy outside AES_CM_128 / NULL x HMAC_SHA1 / NULL */
+
+typedef struct srtp_engine srtp_engine;
+
+/* SRTPPolicy(encType, encKeyLength, authType, authKeyLength, authTagLength,
+ * saltKeyLength) -- SRTPPolicy.java:107-120 */
+typedef struct {
+    int32_t enc_type, enc_key_len, auth_type, auth_key_len, auth_tag_len, salt_key_len;
+} srtp_policy;
+
+typedef struct {
+    int32_t device;            /* HIP device ordinal */
+    int32_t check_replay;      /* SRTPCryptoContext.checkReplay, default 1 */
+    int32_t abort_on_error;    /* SinglePacketTransformer rethrow semantics, default 1 */
+    uint32_t max_contexts;     /* (transformer, SSRC) contexts, default 1<<21 */
+    uint32_t max_factories;    /* default 1<<16 */
+    uint32_t max_transformers; /* default 1<<16 */
+    uint32_t max_batch;        /* initial scratch size in packets (grows), default 1<<16 */
+} srtp_engine_opts;
+
+typedef struct {
+    int32_t roc, s_l, seq_num_set, guessed_roc; /* SRTP context */
+    int32_t sent_index, received_index;         /* SRTCP context */
+    uint64_t replay_window;
+    uint32_t key_set;                           /* internal session-key slot */
+} srtp_ctx_state;
+
+int srtp_engine_opts_default(srtp_engine_opts *opts);
+int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out);
+void srtp_engine_destroy(srtp_engine *e);
+const char *srtp_engine_last_error(srtp_engine *e);
+
+int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *master_key,
+                        int32_t key_len, const uint8_t *master_salt, int32_t salt_len,
+                        const srtp_policy *srtp, const srtp_policy *srtcp, int32_t *out_factory);
+int srtp_factory_close(srtp_engine *e, int32_t factory);
+
+int srtp_transformer_create(srtp_engine *e, int32_t kind, int32_t fwd_factory,
+                            int32_t rev_factory, int32_t *out_transformer);
+int srtp_transformer_set_factory(srtp_engine *e, int32_t transformer, int32_t factory,
+                                 int32_t forward);
+int srtp_transformer_close(srtp_engine *e, int32_t transformer);
+
+/* Process one bundle whose buffers are device (HBM) pointers; asynchronous on
+ * `stream` (a hipStream_t, NULL = engine stream).  tids == NULL means every
+ * packet belongs to `tid`; otherwise tids[i] (device array) names packet i's
+ * transformer.  flags may be NULL.  reverse = 0: transform (protect),
+ * reverse = 1: reverseTransform (unprotect). */
+int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
+                          uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
+                          const uint32_t *flags, int32_t *status, uint32_t n, void *stream);
+
+/* Same with host buffers: copies to HBM, runs, copies back, synchronises.
+ * seg_bytes is the size of the host segment. */
+int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
+                        uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                        const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n);
+
+int srtp_engine_sync(srtp_engine *e, void *stream);
+/* returns 1 and fills *out if the transformer has a context for ssrc, else 0 */
+int srtp_get_context_state(srtp_engine *e, int32_t transformer, uint32_t ssrc,
+                           srtp_ctx_state *out);
+/* number of live contexts in the engine's table */
+int64_t srtp_engine_num_contexts(srtp_engine *e);
+
+/* Per-stage kernel timing with HIP events recorded on the bundle's stream
+ * (measurement hook for bench.py; off by default). */
+#define SRTP_STAGE_PARSE 0
+#define SRTP_STAGE_SORT 1
+#define SRTP_STAGE_VERIFY 2
+#define SRTP_STAGE_WALK 3
+#define SRTP_STAGE_PROTECT 4
+#define SRTP_STAGE_DECRYPT 5
+#define SRTP_NUM_STAGES 6
+int srtp_engine_set_timing(srtp_engine *e, int32_t enable);
+/* Waits for the recorded events, adds each stage's total milliseconds and
+ * bundle count since the last read into ms[] / count[], and resets. */
+int srtp_engine_read_timing(srtp_engine *e, double *ms, uint64_t *count);
+
+/* Control-plane crypto without a GPU (used by CPU-side tests): RFC 3711 4.3
+ * session keys exactly as SRTPCryptoContext.deriveSrtpKeys (rtcp = 0) /
+ * SRTCPCryptoContext.deriveSrtcpKeys (rtcp = 1). */
+int srtp_derive_session_keys(const uint8_t master_key[16], const uint8_t master_salt[14],
+                             int32_t rtcp, uint8_t enc_key[16], uint8_t auth_key[20],
+                             uint8_t salt_key[14]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,110 @@
+"""ctypes binding of the C ABI in include/srtp_mi355x.h (libsrtp_mi355x.so).
+
+The shared library is built in-tree (``libjitsi_amd/csrc/Makefile``, driven by
+``__graft_entry__.build()``).  There is no CPU fallback: if the library is
+missing or no GPU is visible, engine creation raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsrtp_mi355x.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "srtp_mi355x.h")
+
+# include/srtp_mi355x.h
+NULL_ENCRYPTION, AESCM_ENCRYPTION = 0, 1
+NULL_AUTHENTICATION, HMACSHA1_AUTHENTICATION = 0, 1
+KIND_RTP, KIND_RTCP = 0, 1
+(STATUS_OK, STATUS_DROP_REPLAY, STATUS_DROP_AUTH, STATUS_DROP_VERSION, STATUS_DROP_NO_CONTEXT,
+ STATUS_ERR_CAPACITY, STATUS_ERR_MALFORMED, STATUS_DROP_INVALID, STATUS_NOT_PROCESSED,
+ STATUS_SKIPPED) = range(10)
+STATUS_NAMES = ["OK", "DROP_REPLAY", "DROP_AUTH", "DROP_VERSION", "DROP_NO_CONTEXT",
+                "ERR_CAPACITY", "ERR_MALFORMED", "DROP_INVALID", "NOT_PROCESSED", "SKIPPED"]
+PKT_FLAG_DISCARD, PKT_FLAG_SILENCE, PKT_FLAG_SKIP = 0x2, 0x4, 0x80000000
+RC = {0: "SRTP_OK", -1: "SRTP_EINVAL", -2: "SRTP_ENOMEM", -3: "SRTP_EFULL", -4: "SRTP_EDEVICE",
+      -5: "SRTP_EPOLICY"}
+
+EXPORTED = [
+    "srtp_engine_opts_default", "srtp_engine_create", "srtp_engine_destroy",
+    "srtp_engine_last_error", "srtp_factory_create", "srtp_factory_close",
+    "srtp_transformer_create", "srtp_transformer_set_factory", "srtp_transformer_close",
+    "srtp_transform_device", "srtp_transform_host", "srtp_engine_sync",
+    "srtp_get_context_state", "srtp_engine_num_contexts", "srtp_engine_set_timing",
+    "srtp_engine_read_timing", "srtp_derive_session_keys",
+]
+STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
+
+
+class SrtpError(RuntimeError):
+    pass
+
+
+class Policy(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "enc_type", "enc_key_len", "auth_type", "auth_key_len", "auth_tag_len", "salt_key_len")]
+
+
+class EngineOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("check_replay", C.c_int32),
+                ("abort_on_error", C.c_int32), ("max_contexts", C.c_uint32),
+                ("max_factories", C.c_uint32), ("max_transformers", C.c_uint32),
+                ("max_batch", C.c_uint32)]
+
+
+class CtxState(C.Structure):
+    _fields_ = [("roc", C.c_int32), ("s_l", C.c_int32), ("seq_num_set", C.c_int32),
+                ("guessed_roc", C.c_int32), ("sent_index", C.c_int32),
+                ("received_index", C.c_int32), ("replay_window", C.c_uint64),
+                ("key_set", C.c_uint32)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libsrtp_mi355x.so, failing loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SrtpError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; "
+                        f"g.build()'` (make -C libjitsi_amd/csrc)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, u32 = C.c_void_p, C.c_int32, C.c_uint32
+    pi32, pu32, pu8 = C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)
+    L.srtp_engine_opts_default.argtypes = [C.POINTER(EngineOpts)]
+    L.srtp_engine_create.argtypes = [C.POINTER(EngineOpts), C.POINTER(vp)]
+    L.srtp_engine_destroy.argtypes = [vp]
+    L.srtp_engine_destroy.restype = None
+    L.srtp_engine_last_error.argtypes = [vp]
+    L.srtp_engine_last_error.restype = C.c_char_p
+    L.srtp_factory_create.argtypes = [vp, i32, pu8, i32, pu8, i32, C.POINTER(Policy),
+                                      C.POINTER(Policy), pi32]
+    L.srtp_factory_close.argtypes = [vp, i32]
+    L.srtp_transformer_create.argtypes = [vp, i32, i32, i32, pi32]
+    L.srtp_transformer_set_factory.argtypes = [vp, i32, i32, i32]
+    L.srtp_transformer_close.argtypes = [vp, i32]
+    L.srtp_transform_device.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, u32, vp]
+    L.srtp_transform_host.argtypes = [vp, i32, vp, i32, vp, C.c_size_t, vp, vp, vp, vp, vp, u32]
+    L.srtp_engine_sync.argtypes = [vp, vp]
+    L.srtp_get_context_state.argtypes = [vp, i32, u32, C.POINTER(CtxState)]
+    L.srtp_engine_num_contexts.argtypes = [vp]
+    L.srtp_engine_num_contexts.restype = C.c_int64
+    L.srtp_engine_set_timing.argtypes = [vp, i32]
+    L.srtp_engine_read_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+    L.srtp_derive_session_keys.argtypes = [pu8, pu8, i32, pu8, pu8, pu8]
+    _lib = L
+    return L
+
+
+def check(rc: int, engine=None, what: str = "") -> int:
+    if rc < 0:
+        msg = RC.get(rc, str(rc))
+        if engine:
+            detail = lib().srtp_engine_last_error(engine)
+            if detail:
+                msg += ": " + detail.decode(errors="replace")
+        raise SrtpError(f"{what}: {msg}")
+    return rc

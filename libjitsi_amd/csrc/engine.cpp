@@ -1,0 +1,586 @@
+// engine.cpp -- host side of the MI355X SRTP engine: the C ABI of
+// include/srtp_mi355x.h.  Owns the HBM-resident tables (session keys,
+// factories, transformers, the (transformer, SSRC) context hash table) and
+// enqueues the bundle pipeline of srtp_kernels.hip on a HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include <string.h>
+
+#include "../../include/srtp_mi355x.h"
+#include "host_crypto.h"
+#include "srtp_kernels.h"
+
+using namespace srtp;
+
+struct srtp_engine {
+    srtp_engine_opts opts{};
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string last_error;
+
+    KeySet *d_keysets = nullptr;
+    uint32_t n_keysets = 0, max_keysets = 0;
+    FactoryRec *d_factories = nullptr;
+    std::vector<FactoryRec> factories;
+    TransformerRec *d_transformers = nullptr;
+    std::vector<TransformerRec> transformers;
+    uint64_t *d_ctx_keys = nullptr;
+    CtxState *d_ctx = nullptr;
+    uint32_t ctx_cap = 0;
+    int ctx_bits = 0;
+
+    // per-bundle scratch, sized for scratch_n packets
+    uint32_t scratch_n = 0;
+    uint32_t *p_slot = nullptr, *sk_in = nullptr, *sk_out = nullptr;
+    WalkRec *sv_in = nullptr, *sv_out = nullptr;
+    int32_t *w_status = nullptr;
+    uint32_t *w_cw = nullptr, *w_len = nullptr, *g0 = nullptr, *auth_ok = nullptr, *mid = nullptr;
+    void *sort_temp = nullptr;
+    size_t sort_temp_bytes = 0;
+    int32_t *e_min = nullptr;
+    BundleCtl *ctl = nullptr;
+    unsigned long long *d_count = nullptr;
+    uint32_t serial = 1;
+
+    // staging for srtp_transform_host
+    uint8_t *h_seg = nullptr;
+    size_t h_seg_bytes = 0;
+    uint32_t h_n = 0;
+    uint32_t *h_off = nullptr, *h_len = nullptr, *h_cap = nullptr, *h_flags = nullptr;
+    int32_t *h_status = nullptr, *h_tids = nullptr;
+
+    // optional per-stage timing (HIP events on the bundle stream)
+    bool timing = false;
+    struct Mark { int stage; hipEvent_t a, b; };
+    std::vector<Mark> marks;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+int fail(srtp_engine *e, int code, const std::string &msg) {
+    if (e) e->last_error = msg;
+    return code;
+}
+
+#define HIPCHK(e, x)                                                                     \
+    do {                                                                                 \
+        hipError_t _err = (x);                                                           \
+        if (_err != hipSuccess)                                                          \
+            return fail((e), SRTP_EDEVICE, std::string(#x ": ") + hipGetErrorString(_err)); \
+    } while (0)
+
+template <class T> hipError_t dalloc(T **p, size_t count) {
+    return hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+void dfree(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+// Profiles the engine implements: AES_CM_128 or NULL cipher x HMAC_SHA1 or NULL
+// auth (SRTPPolicy.java; profile tables DtlsPacketTransformer.java:574-612,
+// SDesTransformEngine.java:129-147).  Tag length <= 12 keeps the reference's
+// readRegionToBuff in range for every packet of >= 12 bytes.
+bool policy_ok(const srtp_policy *p) {
+    if (!p) return false;
+    if (p->enc_type != SRTP_NULL_ENCRYPTION && p->enc_type != SRTP_AESCM_ENCRYPTION) return false;
+    if (p->enc_type == SRTP_AESCM_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+        return false;
+    if (p->auth_type != SRTP_NULL_AUTHENTICATION && p->auth_type != SRTP_HMACSHA1_AUTHENTICATION)
+        return false;
+    if (p->auth_type == SRTP_HMACSHA1_AUTHENTICATION && p->auth_key_len != 20) return false;
+    if (p->auth_tag_len < 0 || p->auth_tag_len > 12) return false;
+    return true;
+}
+
+void build_keyset(const uint8_t mk[16], const uint8_t ms[14], bool rtcp, const srtp_policy *pol,
+                  KeySet *ks) {
+    memset(ks, 0, sizeof *ks);
+    uint8_t enc[16], auth[20], salt[16] = {0};
+    derive_session_keys(mk, ms, rtcp, enc, auth, salt);
+    aes128_expand_le(enc, ks->rk);
+    hmac_sha1_midstates(auth, ks->ipad, ks->opad);
+    for (int i = 0; i < 4; i++)
+        ks->salt[i] = (uint32_t)salt[4 * i] | ((uint32_t)salt[4 * i + 1] << 8) |
+                      ((uint32_t)salt[4 * i + 2] << 16) | ((uint32_t)salt[4 * i + 3] << 24);
+    ks->enc_type = pol->enc_type;
+    ks->auth_type = pol->auth_type;
+    ks->tag_len = pol->auth_tag_len;
+    ks->kind = rtcp ? SRTP_KIND_RTCP : SRTP_KIND_RTP;
+    memset(enc, 0, sizeof enc);
+    memset(auth, 0, sizeof auth);
+    memset(salt, 0, sizeof salt);
+}
+
+uint32_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return (uint32_t)std::min<uint64_t>(p, 1ull << 31);
+}
+
+void free_scratch(srtp_engine *e) {
+    void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
+                    e->w_len, e->g0, e->auth_ok, e->mid, e->sort_temp};
+    for (void *p : ptrs) dfree(p);
+    e->p_slot = e->sk_in = e->sk_out = nullptr;
+    e->sv_in = e->sv_out = nullptr;
+    e->w_status = nullptr;
+    e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = nullptr;
+    e->sort_temp = nullptr;
+    e->scratch_n = 0;
+}
+
+int ensure_scratch(srtp_engine *e, uint32_t n) {
+    if (n <= e->scratch_n) return SRTP_OK;
+    free_scratch(e);
+    uint32_t m = std::max<uint32_t>(n, 1024);
+    HIPCHK(e, dalloc(&e->p_slot, m));
+    HIPCHK(e, dalloc(&e->sk_in, m));
+    HIPCHK(e, dalloc(&e->sk_out, m));
+    HIPCHK(e, dalloc(&e->sv_in, m));
+    HIPCHK(e, dalloc(&e->sv_out, m));
+    HIPCHK(e, dalloc(&e->w_status, m));
+    HIPCHK(e, dalloc(&e->w_cw, m));
+    HIPCHK(e, dalloc(&e->w_len, m));
+    HIPCHK(e, dalloc(&e->g0, m));
+    HIPCHK(e, dalloc(&e->auth_ok, m));
+    HIPCHK(e, dalloc(&e->mid, (size_t)5 * m));
+    e->sort_temp_bytes = sort_temp_bytes(m);
+    HIPCHK(e, hipMalloc(&e->sort_temp, std::max<size_t>(e->sort_temp_bytes, 16)));
+    e->scratch_n = m;
+    return SRTP_OK;
+}
+
+int sync_factory(srtp_engine *e, int32_t id) {
+    HIPCHK(e, hipMemcpy(e->d_factories + id, &e->factories[id], sizeof(FactoryRec),
+                        hipMemcpyHostToDevice));
+    return SRTP_OK;
+}
+
+int sync_transformer(srtp_engine *e, int32_t id) {
+    HIPCHK(e, hipMemcpy(e->d_transformers + id, &e->transformers[id], sizeof(TransformerRec),
+                        hipMemcpyHostToDevice));
+    return SRTP_OK;
+}
+
+int close_factory_locked(srtp_engine *e, int32_t id) {
+    if (id < 0 || (size_t)id >= e->factories.size()) return SRTP_EINVAL;
+    if (!e->factories[id].open) return SRTP_OK;
+    e->factories[id].open = 0;
+    return sync_factory(e, id);
+}
+
+hipEvent_t take_event(srtp_engine *e) {
+    if (!e->event_pool.empty()) {
+        hipEvent_t ev = e->event_pool.back();
+        e->event_pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev = nullptr;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    return ev;
+}
+
+// Records an event before a stage; end_stage records the matching one after.
+struct StageTimer {
+    srtp_engine *e;
+    hipStream_t s;
+    int stage;
+    hipEvent_t a = nullptr;
+    StageTimer(srtp_engine *e_, hipStream_t s_, int stage_) : e(e_), s(s_), stage(stage_) {
+        if (!e->timing) return;
+        a = take_event(e);
+        if (a) (void)hipEventRecord(a, s);
+    }
+    ~StageTimer() {
+        if (!a) return;
+        hipEvent_t b = take_event(e);
+        if (!b) return;
+        (void)hipEventRecord(b, s);
+        e->marks.push_back({stage, a, b});
+    }
+};
+
+uint64_t mix64_host(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+} // namespace
+
+extern "C" {
+
+int srtp_engine_opts_default(srtp_engine_opts *o) {
+    if (!o) return SRTP_EINVAL;
+    o->device = 0;
+    o->check_replay = 1;
+    o->abort_on_error = 1;
+    o->max_contexts = 1u << 20;
+    o->max_factories = 1u << 16;
+    o->max_transformers = 1u << 16;
+    o->max_batch = 1u << 16;
+    return SRTP_OK;
+}
+
+int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
+    if (!out) return SRTP_EINVAL;
+    *out = nullptr;
+    srtp_engine_opts o;
+    if (opts) o = *opts;
+    else srtp_engine_opts_default(&o);
+    if (o.max_contexts == 0 || o.max_factories == 0 || o.max_transformers == 0) return SRTP_EINVAL;
+    srtp_engine *e = new (std::nothrow) srtp_engine();
+    if (!e) return SRTP_ENOMEM;
+    e->opts = o;
+    int rc = SRTP_OK;
+    do {
+        if (hipSetDevice(o.device) != hipSuccess) { rc = SRTP_EDEVICE; break; }
+        if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { rc = SRTP_EDEVICE; break; }
+        uint32_t te0[256];
+        aes_te0_le(te0);
+        if (upload_tables(te0) != hipSuccess) { rc = SRTP_EDEVICE; break; }
+        e->max_keysets = 2 * o.max_factories;
+        e->ctx_cap = next_pow2(2ull * o.max_contexts);
+        e->ctx_bits = 0;
+        while ((1u << e->ctx_bits) < e->ctx_cap) e->ctx_bits++;
+        if (dalloc(&e->d_keysets, e->max_keysets) != hipSuccess ||
+            dalloc(&e->d_factories, o.max_factories) != hipSuccess ||
+            dalloc(&e->d_transformers, o.max_transformers) != hipSuccess ||
+            dalloc(&e->d_ctx_keys, e->ctx_cap) != hipSuccess ||
+            dalloc(&e->d_ctx, e->ctx_cap) != hipSuccess ||
+            dalloc(&e->e_min, o.max_transformers) != hipSuccess ||
+            dalloc(&e->ctl, 1) != hipSuccess || dalloc(&e->d_count, 1) != hipSuccess) {
+            rc = SRTP_ENOMEM;
+            break;
+        }
+        if (hipMemset(e->d_ctx_keys, 0xff, (size_t)e->ctx_cap * sizeof(uint64_t)) != hipSuccess ||
+            hipMemset(e->d_ctx, 0, (size_t)e->ctx_cap * sizeof(CtxState)) != hipSuccess) {
+            rc = SRTP_EDEVICE;
+            break;
+        }
+        rc = ensure_scratch(e, o.max_batch);
+    } while (0);
+    if (rc != SRTP_OK) {
+        srtp_engine_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return SRTP_OK;
+}
+
+void srtp_engine_destroy(srtp_engine *e) {
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->d_keysets) // zero session keys before release
+        (void)hipMemset(e->d_keysets, 0, (size_t)e->max_keysets * sizeof(KeySet));
+    free_scratch(e);
+    for (auto &m : e->marks) {
+        (void)hipEventDestroy(m.a);
+        (void)hipEventDestroy(m.b);
+    }
+    for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
+    void *ptrs[] = {e->d_keysets, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
+                    e->e_min, e->ctl, e->d_count, e->h_seg, e->h_off, e->h_len, e->h_cap,
+                    e->h_flags, e->h_status, e->h_tids};
+    for (void *p : ptrs) dfree(p);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char *srtp_engine_last_error(srtp_engine *e) { return e ? e->last_error.c_str() : ""; }
+
+int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32_t key_len,
+                        const uint8_t *ms, int32_t salt_len, const srtp_policy *srtp_pol,
+                        const srtp_policy *srtcp_pol, int32_t *out) {
+    if (!e || !out || !mk || !ms) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    // NULL-cipher profiles keep a 16-B master key + 14-B salt for the RFC 3711
+    // 4.3 PRF (the reference throws there: SURVEY Q15) -- parity unpinned.
+    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp_pol) || !policy_ok(srtcp_pol))
+        return fail(e, SRTP_EPOLICY, "unsupported SRTP policy");
+    if (e->factories.size() >= e->opts.max_factories || e->n_keysets + 2 > e->max_keysets)
+        return fail(e, SRTP_EFULL, "factory table full");
+    KeySet ks[2];
+    build_keyset(mk, ms, false, srtp_pol, &ks[0]);
+    build_keyset(mk, ms, true, srtcp_pol, &ks[1]);
+    HIPCHK(e, hipMemcpy(e->d_keysets + e->n_keysets, ks, sizeof ks, hipMemcpyHostToDevice));
+    memset(ks, 0, sizeof ks);
+    FactoryRec f;
+    f.open = 1;
+    f.ks_rtp = (int32_t)e->n_keysets;
+    f.ks_rtcp = (int32_t)e->n_keysets + 1;
+    f.sender = sender;
+    e->n_keysets += 2;
+    e->factories.push_back(f);
+    int32_t id = (int32_t)e->factories.size() - 1;
+    int rc = sync_factory(e, id);
+    if (rc != SRTP_OK) return rc;
+    *out = id;
+    return SRTP_OK;
+}
+
+int srtp_factory_close(srtp_engine *e, int32_t factory) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return close_factory_locked(e, factory);
+}
+
+int srtp_transformer_create(srtp_engine *e, int32_t kind, int32_t fwd, int32_t rev, int32_t *out) {
+    if (!e || !out) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (kind != SRTP_KIND_RTP && kind != SRTP_KIND_RTCP) return fail(e, SRTP_EINVAL, "bad kind");
+    if (fwd < 0 || (size_t)fwd >= e->factories.size() || rev < 0 ||
+        (size_t)rev >= e->factories.size())
+        return fail(e, SRTP_EINVAL, "bad factory id");
+    if (e->transformers.size() >= e->opts.max_transformers)
+        return fail(e, SRTP_EFULL, "transformer table full");
+    TransformerRec t;
+    t.kind = kind; t.fwd = fwd; t.rev = rev; t.alive = 1;
+    e->transformers.push_back(t);
+    int32_t id = (int32_t)e->transformers.size() - 1;
+    int rc = sync_transformer(e, id);
+    if (rc != SRTP_OK) return rc;
+    *out = id;
+    return SRTP_OK;
+}
+
+int srtp_transformer_set_factory(srtp_engine *e, int32_t t, int32_t f, int32_t forward) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (t < 0 || (size_t)t >= e->transformers.size() || f < 0 || (size_t)f >= e->factories.size())
+        return fail(e, SRTP_EINVAL, "bad id");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    int32_t &slot = forward ? e->transformers[t].fwd : e->transformers[t].rev;
+    if (slot >= 0 && slot != f) {
+        int rc = close_factory_locked(e, slot);
+        if (rc != SRTP_OK) return rc;
+    }
+    slot = f;
+    return sync_transformer(e, t);
+}
+
+int srtp_transformer_close(srtp_engine *e, int32_t t) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (t < 0 || (size_t)t >= e->transformers.size()) return fail(e, SRTP_EINVAL, "bad id");
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    TransformerRec &tr = e->transformers[t];
+    int rc = close_factory_locked(e, tr.fwd);
+    if (rc != SRTP_OK) return rc;
+    if (tr.rev != tr.fwd) {
+        rc = close_factory_locked(e, tr.rev);
+        if (rc != SRTP_OK) return rc;
+    }
+    HIPCHK(e, launch_remove_transformer(e->d_ctx_keys, e->d_ctx, e->ctx_cap, (uint32_t)t, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return SRTP_OK;
+}
+
+static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
+                            uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
+                            const uint32_t *flags, int32_t *status, uint32_t n, hipStream_t s) {
+    if (n == 0) return SRTP_OK;
+    if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
+    if (n > kRecIdxMask) return fail(e, SRTP_EINVAL, "bundle too large");
+    if (!tids && (tid < 0 || (size_t)tid >= e->transformers.size()))
+        return fail(e, SRTP_EINVAL, "bad transformer id");
+    int rc = ensure_scratch(e, n);
+    if (rc != SRTP_OK) return rc;
+    BundleArgs a{};
+    a.keysets = e->d_keysets;
+    a.factories = e->d_factories;
+    a.transformers = e->d_transformers;
+    a.ctx_keys = e->d_ctx_keys;
+    a.ctx = e->d_ctx;
+    a.ctx_mask = e->ctx_cap - 1;
+    a.n_transformers = (uint32_t)e->transformers.size();
+    a.seg = seg; a.off = off; a.len = len; a.cap = cap; a.flags = flags; a.status = status;
+    a.tids = tids; a.tid = tid; a.n = n;
+    a.reverse = reverse ? 1 : 0;
+    a.check_replay = e->opts.check_replay;
+    a.abort_on_error = e->opts.abort_on_error;
+    a.serial = e->serial++;
+    a.p_slot = e->p_slot; a.sk_in = e->sk_in; a.sk_out = e->sk_out;
+    a.sv_in = e->sv_in; a.sv_out = e->sv_out;
+    a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
+    a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
+    a.e_min = e->e_min; a.ctl = e->ctl;
+    HIPCHK(e, hipMemsetAsync(e->ctl, 0, sizeof(BundleCtl), s));
+    if (a.abort_on_error)
+        HIPCHK(e, hipMemsetAsync(e->e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
+    {
+        StageTimer t(e, s, SRTP_STAGE_PARSE);
+        HIPCHK(e, launch_parse(a, s));
+    }
+    {
+        StageTimer t(e, s, SRTP_STAGE_SORT);
+        HIPCHK(e, launch_sort(a, e->sort_temp, e->sort_temp_bytes, e->ctx_bits + 1, s));
+    }
+    if (a.reverse) {
+        StageTimer t(e, s, SRTP_STAGE_VERIFY);
+        HIPCHK(e, launch_verify(a, s));
+    }
+    {
+        StageTimer t(e, s, SRTP_STAGE_WALK);
+        HIPCHK(e, launch_walk(a, 0, s));
+        HIPCHK(e, launch_walk(a, 1, s));
+    }
+    if (a.reverse) {
+        StageTimer t(e, s, SRTP_STAGE_DECRYPT);
+        HIPCHK(e, launch_decrypt(a, s));
+    } else {
+        StageTimer t(e, s, SRTP_STAGE_PROTECT);
+        HIPCHK(e, launch_protect(a, s));
+    }
+    return SRTP_OK;
+}
+
+int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
+                          uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
+                          const uint32_t *flags, int32_t *status, uint32_t n, void *stream) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s);
+}
+
+int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
+                        uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                        const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (n == 0) return SRTP_OK;
+    if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
+    for (uint32_t i = 0; i < n; i++) {
+        if (off[i] % 16 != 0) return fail(e, SRTP_EINVAL, "off[i] must be 16-byte aligned");
+        uint64_t end = (uint64_t)off[i] + ((cap[i] + 15u) & ~15u);
+        if (cap[i] > 65535u || end > seg_bytes)
+            return fail(e, SRTP_EINVAL, "packet region outside the segment");
+    }
+    hipStream_t s = e->stream;
+    size_t need = (seg_bytes + 15) & ~(size_t)15;
+    if (need > e->h_seg_bytes) {
+        dfree(e->h_seg);
+        e->h_seg = nullptr;
+        HIPCHK(e, hipMalloc(&e->h_seg, need));
+        e->h_seg_bytes = need;
+    }
+    if (n > e->h_n) {
+        void *ptrs[] = {e->h_off, e->h_len, e->h_cap, e->h_flags, e->h_status, e->h_tids};
+        for (void *p : ptrs) dfree(p);
+        HIPCHK(e, dalloc(&e->h_off, n));
+        HIPCHK(e, dalloc(&e->h_len, n));
+        HIPCHK(e, dalloc(&e->h_cap, n));
+        HIPCHK(e, dalloc(&e->h_flags, n));
+        HIPCHK(e, dalloc(&e->h_status, n));
+        HIPCHK(e, dalloc(&e->h_tids, n));
+        e->h_n = n;
+    }
+    HIPCHK(e, hipMemcpyAsync(e->h_seg, seg, seg_bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->h_off, off, n * 4ull, hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->h_len, len, n * 4ull, hipMemcpyHostToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->h_cap, cap, n * 4ull, hipMemcpyHostToDevice, s));
+    if (flags) HIPCHK(e, hipMemcpyAsync(e->h_flags, flags, n * 4ull, hipMemcpyHostToDevice, s));
+    if (tids) HIPCHK(e, hipMemcpyAsync(e->h_tids, tids, n * 4ull, hipMemcpyHostToDevice, s));
+    int rc = transform_locked(e, reverse, tids ? e->h_tids : nullptr, tid, e->h_seg, e->h_off,
+                              e->h_len, e->h_cap, flags ? e->h_flags : nullptr, e->h_status, n, s);
+    if (rc != SRTP_OK) return rc;
+    HIPCHK(e, hipMemcpyAsync(seg, e->h_seg, seg_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipMemcpyAsync(len, e->h_len, n * 4ull, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipMemcpyAsync(status, e->h_status, n * 4ull, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipStreamSynchronize(s));
+    return SRTP_OK;
+}
+
+int srtp_engine_sync(srtp_engine *e, void *stream) {
+    if (!e) return SRTP_EINVAL;
+    HIPCHK(e, hipStreamSynchronize(stream ? (hipStream_t)stream : e->stream));
+    return SRTP_OK;
+}
+
+int srtp_get_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, srtp_ctx_state *out) {
+    if (!e || !out) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    HIPCHK(e, hipDeviceSynchronize());
+    uint64_t key = ((uint64_t)(uint32_t)t << 32) | ssrc;
+    uint32_t mask = e->ctx_cap - 1;
+    uint32_t h = (uint32_t)mix64_host(key) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        uint64_t k;
+        HIPCHK(e, hipMemcpy(&k, e->d_ctx_keys + h, 8, hipMemcpyDeviceToHost));
+        if (k == kEmptyKey) return 0;
+        if (k != key) continue;
+        CtxState s;
+        HIPCHK(e, hipMemcpy(&s, e->d_ctx + h, sizeof s, hipMemcpyDeviceToHost));
+        KeySet ks;
+        HIPCHK(e, hipMemcpy(&ks, e->d_keysets + s.ks, sizeof ks, hipMemcpyDeviceToHost));
+        memset(out, 0, sizeof *out);
+        out->key_set = s.ks;
+        out->replay_window = s.window;
+        if (ks.kind == SRTP_KIND_RTP) {
+            out->roc = s.a; out->s_l = s.b; out->seq_num_set = (int32_t)(s.flags & 1u);
+            out->guessed_roc = s.g;
+        } else {
+            out->sent_index = s.a; out->received_index = s.b;
+        }
+        memset(&ks, 0, sizeof ks);
+        return 1;
+    }
+    return 0;
+}
+
+int64_t srtp_engine_num_contexts(srtp_engine *e) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    unsigned long long c = 0;
+    if (hipMemsetAsync(e->d_count, 0, 8, e->stream) != hipSuccess) return SRTP_EDEVICE;
+    if (launch_count_contexts(e->d_ctx_keys, e->ctx_cap, e->d_count, e->stream) != hipSuccess)
+        return SRTP_EDEVICE;
+    if (hipMemcpyAsync(&c, e->d_count, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+        return SRTP_EDEVICE;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return SRTP_EDEVICE;
+    return (int64_t)c;
+}
+
+int srtp_engine_set_timing(srtp_engine *e, int32_t enable) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    e->timing = enable != 0;
+    return SRTP_OK;
+}
+
+int srtp_engine_read_timing(srtp_engine *e, double *ms, uint64_t *count) {
+    if (!e || !ms || !count) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    for (int i = 0; i < SRTP_NUM_STAGES; i++) { ms[i] = 0.0; count[i] = 0; }
+    for (auto &m : e->marks) {
+        HIPCHK(e, hipEventSynchronize(m.b));
+        float t = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&t, m.a, m.b));
+        ms[m.stage] += t;
+        count[m.stage] += 1;
+        e->event_pool.push_back(m.a);
+        e->event_pool.push_back(m.b);
+    }
+    e->marks.clear();
+    return SRTP_OK;
+}
+
+int srtp_derive_session_keys(const uint8_t mk[16], const uint8_t ms[14], int32_t rtcp,
+                             uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]) {
+    if (!mk || !ms || !enc || !auth || !salt) return SRTP_EINVAL;
+    derive_session_keys(mk, ms, rtcp != 0, enc, auth, salt);
+    return SRTP_OK;
+}
+
+} // extern "C"

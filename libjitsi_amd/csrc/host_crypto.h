@@ -1,0 +1,29 @@
+// host_crypto.h -- control-plane crypto on the host: AES-128 key schedule and
+// single-block encrypt (for the RFC 3711 4.3 key derivation PRF) and the SHA-1
+// compression function (for the HMAC ipad/opad midstates).  Runs once per
+// factory; the per-packet path is on the GPU.
+#pragma once
+#include <stdint.h>
+
+namespace srtp {
+
+// Expanded AES-128 encryption key, 44 words.  Word i holds round-key bytes
+// 4i..4i+3 in little-endian order (byte 4i in bits 0..7), the layout the
+// gfx950 T-table rounds use.
+void aes128_expand_le(const uint8_t key[16], uint32_t rk_le[44]);
+void aes128_encrypt_block(const uint32_t rk_le[44], const uint8_t in[16], uint8_t out[16]);
+// SHA-1 compression of one 64-byte block into state[5].
+void sha1_compress(uint32_t state[5], const uint8_t block[64]);
+extern const uint32_t kSha1Init[5];
+// The AES forward T-table used by the device (LE layout: 2s | s<<8 | s<<16 | 3s<<24).
+void aes_te0_le(uint32_t te0[256]);
+
+// RFC 3711 4.3 key derivation exactly as SRTPCryptoContext.deriveSrtpKeys
+// (labels 0,1,2; :393-447) or SRTCPCryptoContext.deriveSrtcpKeys (3,4,5;
+// :158-211) with kdr == 0.
+void derive_session_keys(const uint8_t master_key[16], const uint8_t master_salt[14], bool rtcp,
+                         uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]);
+// HMAC-SHA1 ipad/opad midstates for a 20-byte key.
+void hmac_sha1_midstates(const uint8_t key[20], uint32_t ipad[5], uint32_t opad[5]);
+
+} // namespace srtp

@@ -1,0 +1,64 @@
+// srtp_kernels.h -- launch interface of the gfx950 SRTP kernels (srtp_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "srtp_types.h"
+
+namespace srtp {
+
+// Everything one bundle needs; passed by value to every kernel.
+struct BundleArgs {
+    // engine tables (HBM resident)
+    const KeySet *keysets;
+    const FactoryRec *factories;
+    const TransformerRec *transformers;
+    uint64_t *ctx_keys;
+    CtxState *ctx;
+    uint32_t ctx_mask;     // table capacity - 1 (power of two)
+    uint32_t n_transformers;
+    // caller's bundle
+    uint8_t *seg;
+    const uint32_t *off;
+    uint32_t *len;
+    const uint32_t *cap;
+    const uint32_t *flags; // may be null
+    int32_t *status;
+    const int32_t *tids;   // may be null -> tid
+    int32_t tid;
+    uint32_t n;
+    int32_t reverse;
+    int32_t check_replay;
+    int32_t abort_on_error;
+    uint32_t serial;       // bundle serial (context birth stamp)
+    // per-bundle scratch
+    uint32_t *p_slot;      // [n] context slot of packet p
+    uint32_t *sk_in, *sk_out; // [n] sort keys (slot)
+    WalkRec *sv_in, *sv_out;  // [n] sort values
+    int32_t *w_status;     // [n]
+    uint32_t *w_cw;        // [n] guessed ROC / SRTCP index word
+    uint32_t *w_len;       // [n] length after processing
+    uint32_t *g0;          // [n] unprotect: ROC the verify pass assumed
+    uint32_t *auth_ok;     // [n] unprotect: tag matched under g0
+    uint32_t *mid;         // [5n] unprotect: inner SHA-1 state before the ROC block
+    int32_t *e_min;        // [n_transformers] first throwing packet per transformer
+    BundleCtl *ctl;
+};
+
+hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
+size_t sort_temp_bytes(uint32_t n_max);
+hipError_t launch_sort(const BundleArgs &a, void *temp, size_t temp_bytes, int end_bit,
+                       hipStream_t s);
+hipError_t launch_verify(const BundleArgs &a, hipStream_t s);
+hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s);
+hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
+hipError_t launch_decrypt(const BundleArgs &a, hipStream_t s);
+hipError_t launch_remove_transformer(uint64_t *ctx_keys, CtxState *ctx, uint32_t cap,
+                                     uint32_t tid, hipStream_t s);
+hipError_t launch_count_contexts(const uint64_t *ctx_keys, uint32_t cap, unsigned long long *out,
+                                 hipStream_t s);
+// Upload the LE T-table used by the AES rounds (once per device).
+hipError_t upload_tables(const uint32_t te0[256]);
+
+} // namespace srtp

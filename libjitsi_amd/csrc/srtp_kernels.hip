@@ -1,0 +1,901 @@
+// srtp_kernels.hip -- gfx950 kernels of the SRTP/SRTCP engine.
+//
+// Bundle pipeline (one HIP stream, see engine.cpp):
+//   k_parse    one lane per packet: RawPacket accessors, version check,
+//              (transformer, SSRC) -> context slot in an HBM hash table
+//              (SRTPTransformer.getContext :152-175, lazily derived contexts),
+//              emits a 16-B walk record keyed by slot.
+//   radix sort (hipcub) by slot, stable -> each context's packets in array order.
+//   k_verify   [unprotect] one lane per packet: HMAC-SHA1 tag check under the ROC
+//              guessed from the context state at bundle start; keeps the inner
+//              SHA-1 midstate before the ROC-carrying block.
+//   k_walk     one lane per context segment: the serial integer state machine of
+//              SRTPCryptoContext (guessIndex :457-475, checkReplay :279-323,
+//              update :719-744) / SRTCPCryptoContext (:106-120, :435-451), in
+//              array order, committing the context state in HBM.  A second
+//              "limit" pass reproduces SinglePacketTransformer's abort-on-throw.
+//   k_protect  [protect] one lane per packet: fused AES-CM keystream + XOR +
+//              HMAC-SHA1 (one read and one write of the packet bytes).
+//   k_decrypt  [unprotect] one lane per packet: AES-CM over accepted packets.
+//
+// AES uses one little-endian T-table, replicated 32x in LDS so that lane l
+// only ever touches LDS bank (l & 31): 32 KB, conflict-free ds_read_b32.
+// Round keys live in VGPRs, SHA-1 runs per lane with v_alignbit rotates.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "../../include/srtp_mi355x.h"
+#include "srtp_kernels.h"
+
+namespace srtp {
+
+__device__ uint32_t d_te0[256];
+
+constexpr int kBlock = 256;
+
+// ----------------------------------------------------------------- helpers
+__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) {
+    return __builtin_amdgcn_alignbit(x, x, 32u - n);
+}
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
+__device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
+    return (ld_u8(p) << 24) | (ld_u8(p + 1) << 16) | (ld_u8(p + 2) << 8) | ld_u8(p + 3);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+__device__ __forceinline__ int32_t java_ishl1(int32_t n) { return (int32_t)(1u << (n & 31)); }
+__device__ __forceinline__ int64_t java_lshl(int64_t v, int64_t n) {
+    return (int64_t)((uint64_t)v << (n & 63));
+}
+
+// ----------------------------------------------------------------- AES-128
+// T-table lookup for byte value x: lane l reads copy (l & 31), i.e. LDS
+// byte address x*128 + 4*(l & 31) -> bank (l & 31).
+#define TE(x) te[(x) << 5]
+
+__device__ __forceinline__ void fill_te(uint32_t *s_te) {
+    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) s_te[i] = d_te0[i >> 5];
+    __syncthreads();
+}
+
+struct RoundKeys {
+    uint32_t k[44];
+};
+
+// FIPS-197 AES-128 encryption of one block held as four little-endian column
+// words (byte r of word j = state row r, column j).  Row r of output column j
+// comes from input column j+r (ShiftRows); T_r = rotl(T_0, 8r).
+__device__ __forceinline__ void aes_encrypt(const uint32_t *__restrict__ te, const RoundKeys &rk,
+                                            uint32_t &s0, uint32_t &s1, uint32_t &s2,
+                                            uint32_t &s3) {
+    s0 ^= rk.k[0]; s1 ^= rk.k[1]; s2 ^= rk.k[2]; s3 ^= rk.k[3];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t t0 = TE(s0 & 0xff) ^ rotl(TE((s1 >> 8) & 0xff), 8) ^
+                      rotl(TE((s2 >> 16) & 0xff), 16) ^ rotl(TE(s3 >> 24), 24) ^ rk.k[4 * r];
+        uint32_t t1 = TE(s1 & 0xff) ^ rotl(TE((s2 >> 8) & 0xff), 8) ^
+                      rotl(TE((s3 >> 16) & 0xff), 16) ^ rotl(TE(s0 >> 24), 24) ^ rk.k[4 * r + 1];
+        uint32_t t2 = TE(s2 & 0xff) ^ rotl(TE((s3 >> 8) & 0xff), 8) ^
+                      rotl(TE((s0 >> 16) & 0xff), 16) ^ rotl(TE(s1 >> 24), 24) ^ rk.k[4 * r + 2];
+        uint32_t t3 = TE(s3 & 0xff) ^ rotl(TE((s0 >> 8) & 0xff), 8) ^
+                      rotl(TE((s1 >> 16) & 0xff), 16) ^ rotl(TE(s2 >> 24), 24) ^ rk.k[4 * r + 3];
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    // last round: S(x) is byte 1 of T0[x] (T0 = 2s | s<<8 | s<<16 | 3s<<24)
+    uint32_t t0 = ((TE(s0 & 0xff) >> 8) & 0xffu) | (TE((s1 >> 8) & 0xff) & 0xff00u) |
+                  (TE((s2 >> 16) & 0xff) & 0xff0000u) | ((TE(s3 >> 24) << 8) & 0xff000000u);
+    uint32_t t1 = ((TE(s1 & 0xff) >> 8) & 0xffu) | (TE((s2 >> 8) & 0xff) & 0xff00u) |
+                  (TE((s3 >> 16) & 0xff) & 0xff0000u) | ((TE(s0 >> 24) << 8) & 0xff000000u);
+    uint32_t t2 = ((TE(s2 & 0xff) >> 8) & 0xffu) | (TE((s3 >> 8) & 0xff) & 0xff00u) |
+                  (TE((s0 >> 16) & 0xff) & 0xff0000u) | ((TE(s1 >> 24) << 8) & 0xff000000u);
+    uint32_t t3 = ((TE(s3 & 0xff) >> 8) & 0xffu) | (TE((s0 >> 8) & 0xff) & 0xff00u) |
+                  (TE((s1 >> 16) & 0xff) & 0xff0000u) | ((TE(s2 >> 24) << 8) & 0xff000000u);
+    s0 = t0 ^ rk.k[40]; s1 = t1 ^ rk.k[41]; s2 = t2 ^ rk.k[42]; s3 = t3 ^ rk.k[43];
+}
+
+// SRTPCipherCTR keystream block j: AES(iv[0..13] || u16_be(j))  (:77-84)
+__device__ __forceinline__ void ctr_block(const uint32_t *__restrict__ te, const RoundKeys &rk,
+                                          const uint32_t iv[4], uint32_t j, uint32_t out[4]) {
+    out[0] = iv[0]; out[1] = iv[1]; out[2] = iv[2];
+    out[3] = iv[3] | (((j >> 8) & 0xffu) << 16) | ((j & 0xffu) << 24);
+    aes_encrypt(te, rk, out[0], out[1], out[2], out[3]);
+}
+
+// ----------------------------------------------------------------- SHA-1
+__device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; t++) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        uint32_t f, k;
+        if (t < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
+        else if (t < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
+        else if (t < 60) { f = (b & c) | (d & (b | c)); k = 0x8F1BBCDCu; }
+        else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+        uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+        e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// Message word (big-endian) at byte position pos of the HMAC inner stream
+// pkt[0..mac_len) || u32_be(suffix) || 0x80 || 0...  where d is the LE packet
+// word at pos (ignored where pos >= mac_len).
+__device__ __forceinline__ uint32_t tail_word(uint32_t d, int pos, int mac_len, uint32_t suffix) {
+    int x = pos - mac_len;
+    if (x <= -4) return bswap(d);
+    if (x >= 5) return 0u;
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int y = x + i;
+        uint32_t byte;
+        if (y < 0) byte = (d >> (8 * i)) & 0xffu;
+        else if (y < 4) byte = (suffix >> (24 - 8 * y)) & 0xffu;
+        else if (y == 4) byte = 0x80u;
+        else byte = 0u;
+        w |= byte << (24 - 8 * i);
+    }
+    return w;
+}
+
+// HMAC inner block b as SHA-1 message words.  d[16] holds the LE packet words
+// at bytes 64b.. (only bytes below mac_len are used); blocks past the data see
+// the ROC/index suffix, the 0x80 pad and the 64-bit length.
+__device__ __forceinline__ void inner_words(uint32_t w[16], int b, int mac_len, uint32_t suffix) {
+    const int nb_full = mac_len >> 6;
+    const int nb_inner = ((mac_len + 12) >> 6) + 1;
+    if (b < nb_full) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = bswap(w[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = tail_word(w[k], 64 * b + 4 * k, mac_len, suffix);
+        if (b == nb_inner - 1) {
+            w[14] = 0u;
+            w[15] = (uint32_t)(64 + mac_len + 4) * 8u;
+        }
+    }
+}
+
+// HMAC outer block: opad midstate || inner digest.
+__device__ __forceinline__ void outer_words(uint32_t w[16], const uint32_t inner[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) w[k] = inner[k];
+    w[5] = 0x80000000u;
+#pragma unroll
+    for (int k = 6; k < 15; k++) w[k] = 0u;
+    w[15] = (64 + 20) * 8;
+}
+
+__device__ __forceinline__ uint32_t tag_byte(const uint32_t h[5], int i) {
+    uint32_t wv = h[0];
+#pragma unroll
+    for (int k = 1; k < 5; k++) if ((i >> 2) == k) wv = h[k];
+    return (wv >> (24 - 8 * (i & 3))) & 0xffu;
+}
+
+// ------------------------------------------------------- RawPacket helpers
+// getHeaderLength (RawPacket.java:602-614) with the signed extension length
+// (:544-556); kHdrThrow when reading the extension length leaves the buffer.
+__device__ __forceinline__ int32_t rtp_header_len(const uint8_t *pkt, uint32_t b0, int cap) {
+    int cc = (int)(b0 & 0x0fu);
+    int h = 12 + 4 * cc;
+    if (b0 & 0x10u) {
+        int idx = 12 + cc * 4 + 2;
+        if (idx + 1 >= cap) return kHdrThrow;
+        int ext = ((int)(int8_t)ld_u8(pkt + idx) * 256) | (int)ld_u8(pkt + idx + 1);
+        h += 4 + ext * 4;
+    }
+    return h;
+}
+
+// SRTPCipherCTR.process would throw on region [h, h+plen) (SRTPCipherCTR.java:99-120)
+__device__ __forceinline__ bool ctr_would_throw(int32_t h, int plen) {
+    if (h == kHdrThrow) return true;
+    if (plen < 0) return (plen % 16) != 0;
+    return plen > 0 && h < 0;
+}
+
+__device__ __forceinline__ int32_t packet_tid(const BundleArgs &a, uint32_t p) {
+    return a.tids ? a.tids[p] : a.tid;
+}
+
+// ------------------------------------------------------- context hash table
+__device__ uint32_t ctx_lookup_insert(const BundleArgs &a, uint64_t key, bool may_create,
+                                      uint32_t ks_new, bool *created) {
+    *created = false;
+    uint32_t mask = a.ctx_mask;
+    uint32_t h = (uint32_t)mix64(key) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        uint64_t cur = __hip_atomic_load(&a.ctx_keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == key) return h;
+        if (cur == kEmptyKey) {
+            if (!may_create) return kNoSlot;
+            unsigned long long prev =
+                atomicCAS((unsigned long long *)&a.ctx_keys[h], (unsigned long long)kEmptyKey,
+                          (unsigned long long)key);
+            if (prev == kEmptyKey) {
+                CtxState s;
+                s.ks = ks_new; s.a = 0; s.b = 0; s.g = 0; s.window = 0; s.flags = 0;
+                s.birth = a.serial;
+                a.ctx[h] = s;
+                *created = true;
+                return h;
+            }
+            if (prev == key) return h;
+        }
+    }
+    return kNoSlot;
+}
+
+// ============================================================== k_parse
+__global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    uint32_t invalid_key = a.ctx_mask + 1u;
+    a.sk_in[p] = invalid_key;
+    a.p_slot[p] = kNoSlot;
+    uint32_t L = a.len[p];
+    a.w_len[p] = L;
+    uint32_t fl = a.flags ? a.flags[p] : 0u;
+    int32_t tid = packet_tid(a, p);
+    if ((fl & SRTP_PKT_FLAG_SKIP) || tid < 0 || (uint32_t)tid >= a.n_transformers ||
+        !a.transformers[tid].alive) {
+        a.w_status[p] = SRTP_STATUS_SKIPPED;
+        return;
+    }
+    uint32_t C = a.cap[p];
+    if (L < 12 || L > C || C > 65535u) { // RawPacket.isInvalid :903-909
+        a.w_status[p] = SRTP_STATUS_DROP_INVALID;
+        return;
+    }
+    const uint8_t *pkt = a.seg + a.off[p];
+    uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const TransformerRec tr = a.transformers[tid];
+    uint32_t b0 = hdr.x & 0xffu;
+    uint32_t ssrc;
+    if (tr.kind == SRTP_KIND_RTP) {
+        // SRTPTransformer.reverseTransform: RTP version 2 only (:189-190)
+        if (a.reverse && (b0 & 0xC0u) != 0x80u) {
+            a.w_status[p] = SRTP_STATUS_DROP_VERSION;
+            return;
+        }
+        ssrc = bswap(hdr.z);  // RawPacket.getSSRC :839
+    } else {
+        ssrc = bswap(hdr.y);  // RawPacket.getRTCPSSRC :770
+    }
+    int32_t f = a.reverse ? tr.rev : tr.fwd;
+    bool may_create = f >= 0 && a.factories[f].open;
+    uint32_t ks_new = 0;
+    if (may_create) ks_new = (uint32_t)(tr.kind == SRTP_KIND_RTP ? a.factories[f].ks_rtp
+                                                                 : a.factories[f].ks_rtcp);
+    uint64_t key = ((uint64_t)(uint32_t)tid << 32) | ssrc;
+    bool created;
+    uint32_t slot = ctx_lookup_insert(a, key, may_create, ks_new, &created);
+    if (slot == kNoSlot) {
+        if (may_create) atomicOr(&a.ctl->overflow, 1u);
+        a.w_status[p] = SRTP_STATUS_DROP_NO_CONTEXT;
+        return;
+    }
+    a.p_slot[p] = slot;
+    WalkRec rec;
+    rec.p = p;
+    rec.lc = L | (C << 16);
+    bool maybe_throw = false;
+    if (tr.kind == SRTP_KIND_RTP) {
+        rec.word = bswap(hdr.x) & 0xffffu; // RawPacket.getSequenceNumber :804
+        rec.h = rtp_header_len(pkt, b0, (int)C);
+        if (a.reverse && (fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE))) rec.p |= kRecSkipDec;
+        // conservative: a throw is possible for some tag length 0..20
+        maybe_throw = rec.h == kHdrThrow || rec.h < 0 || (int)L - 20 - rec.h < 0;
+    } else if (a.reverse) {
+        // E|index word at length - (4 + tag) (RawPacket.getSRTCPIndex :815-819)
+        int T;
+        if (may_create) T = a.keysets[ks_new].tag_len;
+        else T = a.keysets[a.ctx[slot].ks].tag_len; // existing context (no insert possible)
+        int io = (int)L - 4 - T;
+        rec.word = io >= 0 ? ld_be32(pkt + io) : 0u;
+        rec.h = T;
+        maybe_throw = (int)L - 4 - 20 - 8 < 0;
+    } else {
+        rec.word = 0u;
+        rec.h = 0;
+    }
+    if (maybe_throw) atomicOr(&a.ctl->any_throw, 1u);
+    a.sk_in[p] = slot;
+    a.sv_in[p] = rec;
+    a.w_status[p] = kStPending;
+}
+
+// ============================================================== sort
+size_t sort_temp_bytes(uint32_t n_max) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                       (WalkRec *)nullptr, (WalkRec *)nullptr, (int)n_max, 0, 32);
+    return bytes;
+}
+
+hipError_t launch_sort(const BundleArgs &a, void *temp, size_t temp_bytes, int end_bit,
+                       hipStream_t s) {
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, a.sk_in, a.sk_out, a.sv_in,
+                                              a.sv_out, (int)a.n, 0, end_bit, s);
+}
+
+// Runs body(ks) once per distinct session-key set among this wave's lanes with
+// `todo` set; ks is wave-uniform, so round keys, salt and HMAC midstates are
+// scalar loads held in SGPRs (one iteration when the wave shares one key set,
+// the common case: every context of a factory shares its session keys, Q2).
+template <class F>
+__device__ __forceinline__ void for_each_keyset(bool todo, uint32_t ks_id, F &&body) {
+    while (true) {
+        const unsigned long long m = __ballot(todo);
+        if (m == 0ull) break;
+        const int lane = __ffsll((long long)m) - 1;
+        const uint32_t ks_u = (uint32_t)__builtin_amdgcn_readlane((int)ks_id, lane);
+        if (todo && ks_id == ks_u) {
+            body(ks_u);
+            todo = false;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t sgpr(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+
+// Round keys of a wave-uniform key set into SGPRs (a vector load of one line,
+// then v_readfirstlane: the kernel also stores to global memory, so the
+// compiler would not use the scalar cache for them).
+__device__ __forceinline__ void load_round_keys_uniform(const KeySet *__restrict__ ks,
+                                                        RoundKeys &rk) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(ks->rk);
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        const uint4 v = p[i];
+        rk.k[4 * i] = sgpr(v.x); rk.k[4 * i + 1] = sgpr(v.y);
+        rk.k[4 * i + 2] = sgpr(v.z); rk.k[4 * i + 3] = sgpr(v.w);
+    }
+}
+
+// ============================================================== k_verify
+// Unprotect, one lane per packet: tag check of SRTPCryptoContext.authenticatePacket
+// (:237-266) / SRTCPCryptoContext (:333-353) under the ROC guessed from the
+// context state at bundle start (exact unless the bundle itself moves s_l by
+// more than 2^15 or forged packets change the guess; k_walk re-checks those).
+__device__ __forceinline__ void verify_one(const BundleArgs &a, const KeySet *__restrict__ ks,
+                                           uint32_t p, const CtxState &st) {
+    const int L = (int)a.len[p];
+    const int T = ks->tag_len;
+    const uint8_t *pkt = a.seg + a.off[p];
+    int mac_len;
+    uint32_t suffix;
+    const bool rtp = ks->kind == SRTP_KIND_RTP;
+    if (rtp) {
+        const int32_t seq = (int32_t)((pkt[2] << 8) | pkt[3]);
+        int32_t g = st.a;
+        if (st.flags & 1u) { // guessIndex :457-475
+            const int32_t s_l = st.b;
+            if (s_l < 32768) g = (seq - s_l > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
+            else g = (s_l - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
+        }
+        a.g0[p] = (uint32_t)g;
+        mac_len = L - T;
+        suffix = (uint32_t)g;
+    } else {
+        const int io = L - 4 - T;
+        if (io < 0) return; // the reference throws here (k_walk)
+        suffix = ld_be32(pkt + io);
+        mac_len = io;
+    }
+    if (mac_len < 0) mac_len = 0;
+    uint32_t h[5], inner[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
+    const int nb_full = mac_len >> 6;
+    const int nb_data = (mac_len + 63) >> 6;
+    const int nb_inner = ((mac_len + 12) >> 6) + 1;
+    for (int b = 0; b <= nb_inner; b++) {
+        uint32_t w[16];
+        if (b < nb_data) {
+            const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (64 * b + 16 * m < mac_len) v = qp[m];
+                w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = 0u;
+        }
+        if (b == nb_full && rtp) { // midstate before the ROC-carrying block
+            uint32_t *mp = a.mid + 5 * (size_t)p;
+#pragma unroll
+            for (int k = 0; k < 5; k++) mp[k] = h[k];
+        }
+        if (b < nb_inner) {
+            inner_words(w, b, mac_len, suffix);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++) { inner[k] = h[k]; h[k] = sgpr(ks->opad[k]); }
+            outer_words(w, inner);
+        }
+        sha1_compress(h, w);
+    }
+    const uint8_t *tp = pkt + (L - T);
+    bool ok = true;
+    for (int i = 0; i < T; i++) ok &= (ld_u8(tp + i) == tag_byte(h, i));
+    a.auth_ok[p] = ok ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock, 4) void k_verify(BundleArgs a) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const uint32_t slot = a.p_slot[p];
+    if (slot == kNoSlot) return;
+    const CtxState st = a.ctx[slot];
+    const bool todo = a.keysets[st.ks].auth_type != SRTP_NULL_AUTHENTICATION;
+    for_each_keyset(todo, st.ks, [&](uint32_t ks_u) { verify_one(a, a.keysets + ks_u, p, st); });
+}
+
+// Re-check one SRTP tag under another ROC from the verify pass's midstate
+// (only the block(s) carrying the ROC are re-hashed).
+__device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks, uint32_t p, int L,
+                                          int32_t g) {
+    const int T = ks->tag_len;
+    int mac_len = L - T;
+    if (mac_len < 0) mac_len = 0;
+    const uint8_t *pkt = a.seg + a.off[p];
+    uint32_t h[5], inner[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = a.mid[5 * (size_t)p + k];
+    const int nb_full = mac_len >> 6;
+    const int nb_inner = ((mac_len + 12) >> 6) + 1;
+    for (int b = nb_full; b <= nb_inner; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (64 * b + 16 * m < mac_len) v = reinterpret_cast<const uint4 *>(pkt + 64 * b)[m];
+            w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+        }
+        if (b < nb_inner) {
+            inner_words(w, b, mac_len, (uint32_t)g);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++) { inner[k] = h[k]; h[k] = ks->opad[k]; }
+            outer_words(w, inner);
+        }
+        sha1_compress(h, w);
+    }
+    bool ok = true;
+    for (int i = 0; i < T; i++) ok &= (ld_u8(pkt + mac_len + i) == tag_byte(h, i));
+    return ok;
+}
+
+// ============================================================== k_walk
+// One lane per context: the packets of the context in array order.
+__global__ __launch_bounds__(kBlock) void k_walk(BundleArgs a, int limit_pass) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const BundleCtl ctl = *a.ctl;
+    const bool two_pass = a.abort_on_error && ctl.any_throw;
+    if (limit_pass && !two_pass) return;
+    if (i >= a.n) return;
+    const uint32_t key = a.sk_out[i];
+    if (key > a.ctx_mask) return;
+    if (i > 0 && a.sk_out[i - 1] == key) return;
+    const uint32_t slot = key;
+    CtxState st = a.ctx[slot];
+    const KeySet *ks = a.keysets + st.ks;
+    const int enc = ks->enc_type, auth = ks->auth_type, T = ks->tag_len, kind = ks->kind;
+    const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
+    const bool dry = two_pass && !limit_pass;
+    const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
+    const bool check_replay = a.check_replay != 0;
+    const uint32_t first_p = a.sv_out[i].p & kRecIdxMask;
+
+    for (uint32_t j = i; j < a.n && a.sk_out[j] == key; j++) {
+        const WalkRec rec = a.sv_out[j];
+        const uint32_t p = rec.p & kRecIdxMask;
+        if (limit_pass && (int32_t)p > E) break; // aborted (k_protect/k_decrypt label them)
+        const int L = (int)(rec.lc & 0xffffu), C = (int)(rec.lc >> 16);
+        bool threw = false;
+        if (kind == SRTP_KIND_RTP) {
+            const int seq = (int)rec.word;
+            if (!a.reverse) {
+                const int Tt = (auth != SRTP_NULL_AUTHENTICATION) ? T : 0;
+                if (L + Tt > C) { a.w_status[p] = SRTP_STATUS_ERR_CAPACITY; continue; }
+            }
+            if (!(st.flags & 1u)) { st.flags |= 1u; st.b = seq; } // seqNumSet (:587-591, :662-666)
+            // guessIndex :457-475
+            int32_t g;
+            if (st.b < 32768) g = (seq - st.b > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
+            else g = (st.b - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
+            st.g = g;
+            const int64_t gi = java_lshl((int64_t)g, 16) | seq;
+            const int64_t local = java_lshl((int64_t)st.a, 16) | st.b;
+            const int64_t delta = gi - local;
+            // checkReplay :279-323
+            bool replay_ok = true;
+            if (check_replay && delta <= 0) {
+                if (-delta > 64) replay_ok = false;
+                else if (((uint64_t)st.window >> ((-delta) & 63)) & 1u) replay_ok = false;
+            }
+            if (!replay_ok) { a.w_status[p] = SRTP_STATUS_DROP_REPLAY; continue; }
+            int newL = L;
+            if (a.reverse) {
+                if (auth != SRTP_NULL_AUTHENTICATION) {
+                    newL = L - T > 0 ? L - T : 0;
+                    a.w_len[p] = (uint32_t)newL;
+                    bool ok;
+                    if ((uint32_t)g == a.g0[p]) {
+                        ok = a.auth_ok[p] != 0;
+                    } else {
+                        ok = reverify_rtp(a, ks, p, L, g);
+                        atomicAdd(&a.ctl->n_mismatch, 1u);
+                    }
+                    if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; continue; }
+                }
+                if (enc == SRTP_AESCM_ENCRYPTION && !(rec.p & kRecSkipDec))
+                    threw = ctr_would_throw(rec.h, newL - rec.h);
+            } else {
+                if (enc == SRTP_AESCM_ENCRYPTION) threw = ctr_would_throw(rec.h, L - rec.h);
+                if (!threw && auth != SRTP_NULL_AUTHENTICATION) newL = L + T;
+            }
+            if (!threw) {
+                a.w_cw[p] = (uint32_t)g;
+                a.w_len[p] = (uint32_t)newL;
+                // update :719-744
+                if (delta > 0) {
+                    st.window = (uint64_t)java_lshl((int64_t)st.window, delta) | 1ull;
+                } else {
+                    st.window |= (uint64_t)(int64_t)java_ishl1((int32_t)(-delta));
+                }
+                if (g == st.a) {
+                    if (seq > st.b) st.b = seq & 0xffff;
+                } else if (g == (int32_t)((uint32_t)st.a + 1u)) {
+                    st.b = seq & 0xffff;
+                    st.a = g;
+                }
+            }
+        } else if (!a.reverse) {
+            // SRTCPCryptoContext.transformPacket :391-427
+            const int trailer = (auth != SRTP_NULL_AUTHENTICATION) ? 4 + T : 0;
+            if (L + trailer > C) { a.w_status[p] = SRTP_STATUS_ERR_CAPACITY; continue; }
+            a.w_cw[p] = (uint32_t)st.a;
+            a.w_len[p] = (uint32_t)(L + trailer);
+            st.a = (int32_t)(((uint32_t)st.a + 1u) & 0x7FFFFFFFu);
+        } else {
+            // SRTCPCryptoContext.reverseTransformPacket :315-374
+            const int io = L - 4 - T;
+            if (io < 0) {
+                threw = true;
+            } else {
+                uint32_t word = rec.word;
+                if (rec.h != T) word = ld_be32(a.seg + a.off[p] + io);
+                const int32_t index = (int32_t)(word & 0x7FFFFFFFu);
+                const bool decrypt = (word & 0x80000000u) != 0;
+                const int64_t delta = (int64_t)(int32_t)((uint32_t)index - (uint32_t)st.b);
+                bool replay_ok = true; // SRTCP checkReplay (:106-120) is not config-gated
+                if (delta <= 0) {
+                    if (-delta > 64) replay_ok = false;
+                    else if (((uint64_t)st.window >> ((-delta) & 63)) & 1u) replay_ok = false;
+                }
+                if (!replay_ok) { a.w_status[p] = SRTP_STATUS_DROP_REPLAY; continue; }
+                int newL = L;
+                if (auth != SRTP_NULL_AUTHENTICATION) {
+                    newL = L - T - 4 > 0 ? L - T - 4 : 0;
+                    a.w_len[p] = (uint32_t)newL;
+                    if (!a.auth_ok[p]) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; continue; }
+                }
+                if (decrypt && enc == SRTP_AESCM_ENCRYPTION && newL - 8 < 0) threw = true;
+                if (!threw) {
+                    a.w_cw[p] = word;
+                    // update :435-451 (reversed delta)
+                    const int32_t d2 = (int32_t)((uint32_t)st.b - (uint32_t)index);
+                    if (d2 > 0) st.window = (uint64_t)java_lshl((int64_t)st.window, d2) | 1ull;
+                    else st.window |= (uint64_t)(int64_t)java_ishl1(d2);
+                    st.b = index;
+                }
+            }
+        }
+        if (threw) {
+            a.w_status[p] = SRTP_STATUS_ERR_MALFORMED;
+            if (a.abort_on_error) {
+                if (dry) atomicMin(&a.e_min[tid], (int32_t)p);
+                break; // the rest of this transformer's array is aborted
+            }
+            continue;
+        }
+        a.w_status[p] = SRTP_STATUS_OK;
+    }
+    if (dry) return; // first of two passes: state is committed by the limit pass
+    if (limit_pass && st.birth == a.serial && (int32_t)first_p > E) {
+        // derived for a packet the reference never reached: forget it again
+        __hip_atomic_store(&a.ctx_keys[slot], kTombKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    a.ctx[slot] = st;
+}
+
+// ====================================================== final status helper
+// Final status of packet p (abort-aware); writes the caller's status/len.
+__device__ __forceinline__ int32_t finish_status(const BundleArgs &a, uint32_t p) {
+    int32_t st = a.w_status[p];
+    if (st != SRTP_STATUS_SKIPPED && a.abort_on_error && a.ctl->any_throw) {
+        const int32_t tid = packet_tid(a, p);
+        if ((int32_t)p > a.e_min[tid]) st = SRTP_STATUS_NOT_PROCESSED;
+    }
+    a.status[p] = st;
+    if (st != SRTP_STATUS_NOT_PROCESSED && st != SRTP_STATUS_SKIPPED) a.len[p] = a.w_len[p];
+    return st;
+}
+
+// Keystream word k of a data quad when payload words are shifted by s words
+// against the 16-B quad grid: concat(prev, cur)[4 - s + k].
+__device__ __forceinline__ uint32_t ks_word(int s, const uint32_t prev[4], const uint32_t cur[4],
+                                            int k) {
+    const uint32_t a0 = cur[k];
+    const uint32_t a1 = k >= 1 ? cur[k - 1] : prev[3 + k];
+    const uint32_t a2 = k >= 2 ? cur[k - 2] : prev[2 + k];
+    const uint32_t a3 = k >= 3 ? cur[k - 3] : prev[1 + k];
+    return (s & 2) ? ((s & 1) ? a3 : a2) : ((s & 1) ? a1 : a0);
+}
+
+// XOR the AES-CM keystream into data quad q (bytes 16q..16q+15) over
+// [enc_off, enc_end); keystream block j covers bytes enc_off + 16j ...
+__device__ __forceinline__ void ctr_quad(const uint32_t *__restrict__ te, const RoundKeys &rk,
+                                         const uint32_t iv[4], int q, int enc_off, int enc_end,
+                                         uint32_t prev[4], uint32_t cur[4], uint4 &v) {
+    const int hq = enc_off >> 4, s = (enc_off >> 2) & 3;
+#pragma unroll
+    for (int k = 0; k < 4; k++) prev[k] = cur[k];
+    ctr_block(te, rk, iv, (uint32_t)(q - hq), cur);
+    uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pos = 16 * q + 4 * k;
+        const uint32_t ksw = ks_word(s, prev, cur, k);
+        uint32_t m = 0u;
+        if (pos >= enc_off && pos < enc_end) {
+            const int rem = enc_end - pos;
+            m = rem >= 4 ? 0xffffffffu : ((1u << (8 * rem)) - 1u);
+        }
+        d[k] ^= ksw & m;
+    }
+    v = make_uint4(d[0], d[1], d[2], d[3]);
+}
+
+__device__ __forceinline__ void make_iv_rtp(const KeySet *ks, const uint4 &hdr, uint32_t roc,
+                                            uint32_t iv[4]) {
+    // processPacketAESCM :482-525: salt ^ (0, SSRC, ROC, SEQ, 0)
+    iv[0] = sgpr(ks->salt[0]);
+    iv[1] = sgpr(ks->salt[1]) ^ hdr.z;        // bytes 8..11 = SSRC (BE in memory)
+    iv[2] = sgpr(ks->salt[2]) ^ bswap(roc);
+    iv[3] = sgpr(ks->salt[3]) ^ (hdr.x >> 16); // bytes 2..3 = SEQ
+}
+
+__device__ __forceinline__ void make_iv_rtcp(const KeySet *ks, const uint4 &hdr, uint32_t index,
+                                             uint32_t iv[4]) {
+    // SRTCPCryptoContext.processPacketAESCM :218-260: salt ^ (0, SSRC, 0, index, 0)
+    iv[0] = sgpr(ks->salt[0]);
+    iv[1] = sgpr(ks->salt[1]) ^ hdr.y;        // bytes 4..7 = RTCP SSRC
+    iv[2] = sgpr(ks->salt[2]) ^ ((((index >> 24) & 0xffu) << 16) | (((index >> 16) & 0xffu) << 24));
+    iv[3] = sgpr(ks->salt[3]) ^ (((index >> 8) & 0xffu) | ((index & 0xffu) << 8));
+}
+
+// ============================================================== k_protect
+// Fused protect, one lane per packet: AES-CM in place (SRTPCipherCTR.process
+// :94-121) + HMAC-SHA1 over the ciphertext (authenticatePacketHMAC :269-278)
+// + trailer (RawPacket.append :203-220).  Packet bytes: one read, one write.
+__device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
+                                            const uint32_t *__restrict__ te, uint32_t p) {
+    uint8_t *pkt = a.seg + a.off[p];
+    const bool do_enc = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
+    const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    const bool rtcp = sgpr(ks->kind) == SRTP_KIND_RTCP;
+    const int T = (int)sgpr(ks->tag_len);
+    const int L = (int)a.w_len[p] - (do_mac ? (T + (rtcp ? 4 : 0)) : 0);
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const uint32_t cw = a.w_cw[p];
+    uint32_t iv[4];
+    int enc_off;
+    uint32_t suffix;
+    if (!rtcp) {
+        enc_off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        make_iv_rtp(ks, hdr, cw, iv);
+        suffix = cw;
+    } else {
+        enc_off = 8;
+        make_iv_rtcp(ks, hdr, cw, iv);
+        suffix = do_enc ? (cw | 0x80000000u) : 0u;
+    }
+    RoundKeys rk;
+    load_round_keys_uniform(ks, rk);
+    uint32_t prev[4] = {0, 0, 0, 0}, cur[4] = {0, 0, 0, 0};
+    uint32_t h[5], inner[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
+    const int nb_data = (L + 63) >> 6;
+    const int nb_inner = do_mac ? ((L + 12) >> 6) + 1 : 0;
+    const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
+    // One AES site and one SHA-1 site: block b gathers its four 16-B quads
+    // (encrypting them in place), then runs one compression (inner blocks,
+    // then the outer block).
+    for (int b = 0; b < n_blocks; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = 0u;
+        if (b < nb_data) {
+#pragma unroll 1
+            for (int m = 0; m < 4; m++) {
+                const int q = 4 * b + m;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (16 * q < L) {
+                    uint4 *qp = reinterpret_cast<uint4 *>(pkt + 16 * q);
+                    v = *qp;
+                    if (do_enc && 16 * q + 16 > enc_off) {
+                        ctr_quad(te, rk, iv, q, enc_off, L, prev, cur, v);
+                        *qp = v;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 12; k++) w[k] = w[k + 4];
+                w[12] = v.x; w[13] = v.y; w[14] = v.z; w[15] = v.w;
+            }
+        }
+        if (!do_mac) continue;
+        if (b < nb_inner) {
+            inner_words(w, b, L, suffix);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++) { inner[k] = h[k]; h[k] = sgpr(ks->opad[k]); }
+            outer_words(w, inner);
+        }
+        sha1_compress(h, w);
+    }
+    if (!do_mac) return;
+    int o = L;
+    if (rtcp) { // append E|index (rbStore) then the tag, SRTCPCryptoContext :419-424
+        pkt[o] = (uint8_t)(suffix >> 24); pkt[o + 1] = (uint8_t)(suffix >> 16);
+        pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
+        o += 4;
+    }
+    for (int i = 0; i < T; i++) pkt[o + i] = (uint8_t)tag_byte(h, i);
+}
+
+__global__ __launch_bounds__(kBlock, 4) void k_protect(BundleArgs a) {
+    __shared__ uint32_t s_te[256 * 32];
+    fill_te(s_te);
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const bool todo = finish_status(a, p) == SRTP_STATUS_OK;
+    const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
+    const uint32_t *te = s_te + (threadIdx.x & 31);
+    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { protect_one(a, a.keysets + ks_u, te, p); });
+}
+
+// ============================================================== k_decrypt
+// AES-CM decryption of accepted packets (SRTPCryptoContext :609-627,
+// SRTCPCryptoContext :355-370).
+__device__ __forceinline__ void decrypt_one(const BundleArgs &a, const KeySet *__restrict__ ks,
+                                            const uint32_t *__restrict__ te, uint32_t p) {
+    uint8_t *pkt = a.seg + a.off[p];
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const uint32_t cw = a.w_cw[p];
+    const int L = (int)a.w_len[p];
+    uint32_t iv[4];
+    int enc_off;
+    if (sgpr(ks->kind) == SRTP_KIND_RTP) {
+        enc_off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        make_iv_rtp(ks, hdr, cw, iv);
+    } else {
+        enc_off = 8;
+        make_iv_rtcp(ks, hdr, cw & 0x7FFFFFFFu, iv);
+    }
+    if (L - enc_off <= 0) return;
+    RoundKeys rk;
+    load_round_keys_uniform(ks, rk);
+    uint32_t prev[4] = {0, 0, 0, 0}, cur[4] = {0, 0, 0, 0};
+    for (int q = enc_off >> 4; 16 * q < L; q++) {
+        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 16 * q);
+        uint4 v = *qp;
+        ctr_quad(te, rk, iv, q, enc_off, L, prev, cur, v);
+        *qp = v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock, 4) void k_decrypt(BundleArgs a) {
+    __shared__ uint32_t s_te[256 * 32];
+    fill_te(s_te);
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    bool todo = finish_status(a, p) == SRTP_STATUS_OK;
+    uint32_t ks_id = 0;
+    if (todo) {
+        ks_id = a.ctx[a.p_slot[p]].ks;
+        const KeySet *ks = a.keysets + ks_id;
+        if (ks->enc_type != SRTP_AESCM_ENCRYPTION) todo = false;
+        else if (ks->kind == SRTP_KIND_RTP) {
+            const uint32_t fl = a.flags ? a.flags[p] : 0u;
+            if (fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) todo = false; // :609-611
+        } else if (!(a.w_cw[p] & 0x80000000u)) {
+            todo = false; // E flag clear: sent unencrypted
+        }
+    }
+    const uint32_t *te = s_te + (threadIdx.x & 31);
+    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { decrypt_one(a, a.keysets + ks_u, te, p); });
+}
+
+// ============================================================== maintenance
+__global__ void k_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    uint64_t k = keys[i];
+    if (k != kEmptyKey && k != kTombKey && (uint32_t)(k >> 32) == tid) {
+        keys[i] = kTombKey;
+        CtxState z = {};
+        ctx[i] = z;
+    }
+}
+
+__global__ void k_count_contexts(const uint64_t *keys, uint32_t cap, unsigned long long *out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool live = i < cap && keys[i] != kEmptyKey && keys[i] != kTombKey;
+    unsigned long long m = __ballot(live);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(out, (unsigned long long)__popcll(m));
+}
+
+// ============================================================== launchers
+static inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
+
+hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_parse, grid_for(a.n), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_verify(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_verify, grid_for(a.n), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
+    hipLaunchKernelGGL(k_walk, grid_for(a.n), dim3(kBlock), 0, s, a, limit_pass);
+    return hipGetLastError();
+}
+hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_protect, grid_for(a.n), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_decrypt(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_decrypt, grid_for(a.n), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,
+                                     hipStream_t s) {
+    hipLaunchKernelGGL(k_remove_transformer, grid_for(cap), dim3(kBlock), 0, s, keys, ctx, cap, tid);
+    return hipGetLastError();
+}
+hipError_t launch_count_contexts(const uint64_t *keys, uint32_t cap, unsigned long long *out,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_count_contexts, grid_for(cap), dim3(kBlock), 0, s, keys, cap, out);
+    return hipGetLastError();
+}
+hipError_t upload_tables(const uint32_t te0[256]) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(d_te0), te0, 256 * sizeof(uint32_t));
+}
+
+} // namespace srtp

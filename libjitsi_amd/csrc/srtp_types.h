@@ -1,0 +1,81 @@
+// srtp_types.h -- device-resident tables shared by the host engine and the
+// gfx950 kernels.  Layouts are sized for HBM: one 256-B session-key record per
+// (factory, RTP|RTCP), one 32-B state record per (transformer, SSRC) context.
+#pragma once
+#include <stdint.h>
+
+namespace srtp {
+
+constexpr int kAesRounds = 10;
+constexpr uint64_t kEmptyKey = ~0ull;       // hash slot never used
+constexpr uint64_t kTombKey = ~0ull - 1ull; // context removed (transformer close / abort)
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+// Session keys of one SRTPCryptoContext / SRTCPCryptoContext family.  Every
+// context derived from one factory shares them (kdr == 0):
+// SRTPCryptoContext.deriveSrtpKeys :393-447, SRTCPCryptoContext.deriveSrtcpKeys
+// :158-211.  The HMAC key is stored as its two SHA-1 midstates (ipad/opad),
+// so the per-packet MAC costs no key blocks.
+struct alignas(256) KeySet {
+    uint32_t rk[4 * (kAesRounds + 1)]; // AES-128 round keys, little-endian column words
+    uint32_t ipad[5];                  // SHA-1 state after (authKey ^ 0x36..) block
+    uint32_t opad[5];                  // SHA-1 state after (authKey ^ 0x5c..) block
+    uint32_t salt[4];                  // session salt bytes 0..13 as LE words (14,15 = 0)
+    int32_t enc_type;                  // SRTP_NULL_ENCRYPTION / SRTP_AESCM_ENCRYPTION
+    int32_t auth_type;                 // SRTP_NULL_AUTHENTICATION / SRTP_HMACSHA1_AUTHENTICATION
+    int32_t tag_len;                   // policy.getAuthTagLength()
+    int32_t kind;                      // SRTP_KIND_RTP / SRTP_KIND_RTCP
+    uint32_t pad[2];
+};
+static_assert(sizeof(KeySet) == 256, "KeySet is one 256-B record");
+
+struct FactoryRec {      // SRTPContextFactory
+    int32_t open;        // 0 after close(): getDefaultContext() == null
+    int32_t ks_rtp;      // key set of its default SRTPCryptoContext
+    int32_t ks_rtcp;     // key set of its default SRTCPCryptoContext
+    int32_t sender;
+};
+
+struct TransformerRec {  // SRTPTransformer / SRTCPTransformer
+    int32_t kind;
+    int32_t fwd;         // forwardFactory id (-1 none)
+    int32_t rev;         // reverseFactory id
+    int32_t alive;
+};
+
+// Per-(transformer, SSRC) context state, the mutable part of
+// SRTPCryptoContext (:130-164) / SRTCPCryptoContext (:54-59).
+struct alignas(32) CtxState {
+    uint32_t ks;     // key set (fixed at derivation; survives factory swaps, Q16)
+    int32_t a;       // SRTP roc            | SRTCP sentIndex
+    int32_t b;       // SRTP s_l            | SRTCP receivedIndex
+    int32_t g;       // SRTP guessedROC (last value, kept for state parity)
+    uint64_t window; // replayWindow (Java long)
+    uint32_t flags;  // bit0: seqNumSet
+    uint32_t birth;  // bundle serial in which the context was derived
+};
+static_assert(sizeof(CtxState) == 32, "CtxState is 32 B");
+
+// One packet as seen by the per-context walk (sorted by context slot).
+struct alignas(16) WalkRec {
+    uint32_t p;      // packet index | kRecSkipDec
+    uint32_t word;   // RTP: sequence number; RTCP unprotect: E|index word
+    uint32_t lc;     // len (low 16) | min(cap, 65535) (high 16)
+    int32_t h;       // RTP: header length or kHdrThrow; RTCP unprotect: tag length used for `word`
+};
+constexpr uint32_t kRecSkipDec = 0x80000000u; // FLAG_DISCARD|FLAG_SILENCE: no decrypt
+constexpr uint32_t kRecIdxMask = 0x0FFFFFFFu;
+constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
+
+// bundle control block (zeroed per bundle)
+struct BundleCtl {
+    uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk
+    uint32_t n_walk;
+    uint32_t n_mismatch;  // unprotect: guessed ROC differed from the verify pass
+    uint32_t overflow;    // context table full
+};
+
+// internal walk statuses (beyond SRTP_STATUS_*)
+constexpr int32_t kStPending = 100;
+
+} // namespace srtp

@@ -1,0 +1,414 @@
+"""Host-side mirror of libjitsi's SRTP transformer API over the MI355X engine.
+
+Same class and method names, argument meaning and error behaviour as the
+reference (paths relative to src/org/jitsi/impl/neomedia/):
+
+* ``SRTPPolicy``            transform/srtp/SRTPPolicy.java:24-120
+* ``SRTPContextFactory``    transform/srtp/SRTPContextFactory.java:24-108
+* ``RawPacket``             RawPacket.java (buffer/offset/length/flags + accessors)
+* ``PacketTransformer``     transform/PacketTransformer.java:28-53
+* ``SRTPTransformer``       transform/srtp/SRTPTransformer.java:53-219
+* ``SRTCPTransformer``      transform/srtp/SRTCPTransformer.java:30-207
+
+``transform(pkts)`` / ``reverseTransform(pkts)`` follow
+SinglePacketTransformer.java:121-216: packets are processed in array order,
+``None`` elements are skipped, each element is replaced by the transformed
+packet or ``None`` (drop), and a packet on which the reference would throw
+raises ``SRTPTransformException`` after the earlier packets were transformed
+(the remaining elements of the array are left untouched).
+
+All per-packet work runs on the GPU (libsrtp_mi355x.so); this module only
+packs RawPackets into one bundle and unpacks the results.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+class SRTPTransformException(RuntimeError):
+    """What SinglePacketTransformer rethrows (RuntimeException)."""
+
+
+class SRTPPolicy:
+    NULL_ENCRYPTION = 0
+    AESCM_ENCRYPTION = 1
+    AESF8_ENCRYPTION = 2
+    TWOFISH_ENCRYPTION = 3
+    TWOFISHF8_ENCRYPTION = 4
+    NULL_AUTHENTICATION = 0
+    HMACSHA1_AUTHENTICATION = 1
+    SKEIN_AUTHENTICATION = 2
+
+    def __init__(self, encType: int, encKeyLength: int, authType: int, authKeyLength: int,
+                 authTagLength: int, saltKeyLength: int):
+        self.encType = encType
+        self.encKeyLength = encKeyLength
+        self.authType = authType
+        self.authKeyLength = authKeyLength
+        self.authTagLength = authTagLength
+        self.saltKeyLength = saltKeyLength
+
+    def getEncType(self): return self.encType
+    def getEncKeyLength(self): return self.encKeyLength
+    def getAuthType(self): return self.authType
+    def getAuthKeyLength(self): return self.authKeyLength
+    def getAuthTagLength(self): return self.authTagLength
+    def getSaltKeyLength(self): return self.saltKeyLength
+
+    def _c(self) -> N.Policy:
+        return N.Policy(self.encType, self.encKeyLength, self.authType, self.authKeyLength,
+                        self.authTagLength, self.saltKeyLength)
+
+    def __repr__(self):
+        return (f"SRTPPolicy(enc={self.encType}/{self.encKeyLength}, auth={self.authType}/"
+                f"{self.authKeyLength}, tag={self.authTagLength}, salt={self.saltKeyLength})")
+
+
+def profile_policies(profile: str):
+    """(srtpPolicy, srtcpPolicy) of a DTLS-SRTP protection profile, as the table
+    in transform/dtls/DtlsPacketTransformer.java:574-612 builds them (note the
+    10-byte SRTCP tag of the _32 profiles)."""
+    P = SRTPPolicy
+    table = {
+        "AES_CM_128_HMAC_SHA1_80": (P.AESCM_ENCRYPTION, 16, 14, 10, 10),
+        "AES_CM_128_HMAC_SHA1_32": (P.AESCM_ENCRYPTION, 16, 14, 4, 10),
+        "NULL_HMAC_SHA1_80": (P.NULL_ENCRYPTION, 0, 0, 10, 10),
+        "NULL_HMAC_SHA1_32": (P.NULL_ENCRYPTION, 0, 0, 4, 10),
+    }
+    enc, klen, slen, rtp_tag, rtcp_tag = table[profile]
+    return (P(enc, klen, P.HMACSHA1_AUTHENTICATION, 20, rtp_tag, slen),
+            P(enc, klen, P.HMACSHA1_AUTHENTICATION, 20, rtcp_tag, slen))
+
+
+class SRTPEngine:
+    """One MI355X device's engine: HBM tables of session keys and contexts."""
+
+    _default = {}
+    _lock = threading.Lock()
+
+    def __init__(self, device: int = 0, check_replay: bool = True, abort_on_error: bool = True,
+                 max_contexts: int = 1 << 20, max_factories: int = 1 << 14,
+                 max_transformers: int = 1 << 16, max_batch: int = 1 << 16):
+        L = N.lib()
+        o = N.EngineOpts()
+        L.srtp_engine_opts_default(C.byref(o))
+        o.device, o.check_replay, o.abort_on_error = device, int(check_replay), int(abort_on_error)
+        o.max_contexts, o.max_factories = max_contexts, max_factories
+        o.max_transformers, o.max_batch = max_transformers, max_batch
+        h = C.c_void_p()
+        N.check(L.srtp_engine_create(C.byref(o), C.byref(h)), None, "srtp_engine_create")
+        self.h = h
+        self.device = device
+
+    @classmethod
+    def default(cls, device: int = 0) -> "SRTPEngine":
+        with cls._lock:
+            if device not in cls._default:
+                cls._default[device] = SRTPEngine(device)
+            return cls._default[device]
+
+    def close(self):
+        if self.h:
+            N.lib().srtp_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self, stream=None):
+        N.check(N.lib().srtp_engine_sync(self.h, stream), self.h, "srtp_engine_sync")
+
+    def set_timing(self, enable: bool) -> None:
+        N.check(N.lib().srtp_engine_set_timing(self.h, int(enable)), self.h, "set_timing")
+
+    def read_timing(self) -> dict:
+        """{stage: (total ms, bundles)} since the last read (HIP events)."""
+        ms = (C.c_double * len(N.STAGES))()
+        cnt = (C.c_uint64 * len(N.STAGES))()
+        N.check(N.lib().srtp_engine_read_timing(self.h, ms, cnt), self.h, "read_timing")
+        return {name: (ms[i], cnt[i]) for i, name in enumerate(N.STAGES)}
+
+    def num_contexts(self) -> int:
+        return N.check(N.lib().srtp_engine_num_contexts(self.h), self.h, "num_contexts")
+
+    def context_state(self, transformer: "_SRTPBase", ssrc: int) -> Optional[dict]:
+        st = N.CtxState()
+        rc = N.check(N.lib().srtp_get_context_state(self.h, transformer.tid, ssrc & 0xFFFFFFFF,
+                                                    C.byref(st)), self.h, "get_context_state")
+        if rc == 0:
+            return None
+        return {k: getattr(st, k) for k, _ in N.CtxState._fields_}
+
+    # -- bundle entry points -------------------------------------------------
+    def transform_host(self, reverse: bool, tid, seg: np.ndarray, off: np.ndarray,
+                       length: np.ndarray, cap: np.ndarray, flags=None) -> np.ndarray:
+        """Process a packed bundle held in host memory (copied to HBM and back).
+        ``tid`` is one transformer id or an int32 array with one id per packet."""
+        n = len(off)
+        assert seg.dtype == np.uint8 and seg.flags.c_contiguous
+        off = np.ascontiguousarray(off, np.uint32)
+        cap = np.ascontiguousarray(cap, np.uint32)
+        assert length.dtype == np.uint32 and length.flags.c_contiguous and len(length) == n
+        status = np.zeros(n, np.int32)
+        fl = None if flags is None else np.ascontiguousarray(flags, np.uint32)
+        if np.isscalar(tid):
+            tids_p, tid0 = None, int(tid)
+        else:
+            tids = np.ascontiguousarray(tid, np.int32)
+            tids_p, tid0 = tids.ctypes.data, -1
+        rc = N.lib().srtp_transform_host(
+            self.h, int(reverse), tids_p, tid0, seg.ctypes.data, seg.nbytes, off.ctypes.data,
+            length.ctypes.data, cap.ctypes.data, None if fl is None else fl.ctypes.data,
+            status.ctypes.data, n)
+        N.check(rc, self.h, "srtp_transform_host")
+        return status
+
+    def transform_device(self, reverse: bool, tid, seg, off, length, cap, status, flags=None,
+                         n: Optional[int] = None, stream=None) -> None:
+        """Enqueue a bundle whose buffers are device tensors (torch, on this
+        engine's GPU).  ``tid`` is an int or an int32 device tensor.  Async on
+        ``stream`` (a torch.cuda.Stream or raw hipStream_t pointer)."""
+        if n is None:
+            n = off.numel()
+        if np.isscalar(tid):
+            tids_p, tid0 = None, int(tid)
+        else:
+            tids_p, tid0 = tid.data_ptr(), -1
+        sp = getattr(stream, "cuda_stream", stream)
+        rc = N.lib().srtp_transform_device(
+            self.h, int(reverse), tids_p, tid0, seg.data_ptr(), off.data_ptr(), length.data_ptr(),
+            cap.data_ptr(), None if flags is None else flags.data_ptr(), status.data_ptr(), n, sp)
+        N.check(rc, self.h, "srtp_transform_device")
+
+
+class SRTPContextFactory:
+    """SRTPContextFactory(sender, masterKey, masterSalt, srtpPolicy, srtcpPolicy)."""
+
+    def __init__(self, sender: bool, masterKey: bytes, masterSalt: bytes, srtpPolicy: SRTPPolicy,
+                 srtcpPolicy: SRTPPolicy, engine: Optional[SRTPEngine] = None):
+        self.engine = engine or SRTPEngine.default()
+        key = (C.c_uint8 * len(masterKey)).from_buffer_copy(bytes(masterKey))
+        salt = (C.c_uint8 * len(masterSalt)).from_buffer_copy(bytes(masterSalt))
+        fid = C.c_int32()
+        rc = N.lib().srtp_factory_create(self.engine.h, int(sender), key, len(masterKey), salt,
+                                         len(masterSalt), C.byref(srtpPolicy._c()),
+                                         C.byref(srtcpPolicy._c()), C.byref(fid))
+        C.memset(key, 0, len(masterKey))
+        C.memset(salt, 0, len(masterSalt))
+        N.check(rc, self.engine.h, "SRTPContextFactory")
+        self.fid = fid.value
+        self.sender = sender
+
+    def close(self):
+        N.check(N.lib().srtp_factory_close(self.engine.h, self.fid), self.engine.h, "close")
+
+
+class RawPacket:
+    """Packet view (nm/RawPacket.java): buffer, offset, length, flags."""
+
+    FIXED_HEADER_SIZE = 12
+    EXT_HEADER_SIZE = 4
+
+    def __init__(self, buffer, offset: int = 0, length: Optional[int] = None, flags: int = 0):
+        self.buffer = bytearray(buffer)
+        self.offset = offset
+        self.length = len(self.buffer) - offset if length is None else length
+        self.flags = flags
+
+    def getBuffer(self): return self.buffer
+    def getOffset(self): return self.offset
+    def getLength(self): return self.length
+    def getFlags(self): return self.flags
+    def setFlags(self, f): self.flags = f
+
+    def data(self) -> bytes:
+        return bytes(self.buffer[self.offset:self.offset + self.length])
+
+    def readByte(self, off): return self.buffer[self.offset + off]
+
+    def readInt(self, off):
+        return int.from_bytes(self.buffer[self.offset + off:self.offset + off + 4], "big")
+
+    def getSequenceNumber(self):
+        return int.from_bytes(self.buffer[self.offset + 2:self.offset + 4], "big")
+
+    def getSSRC(self): return self.readInt(8)
+    def getRTCPSSRC(self): return self.readInt(4)
+
+    def getHeaderLength(self):
+        b0 = self.buffer[self.offset]
+        h = 12 + 4 * (b0 & 0x0F)
+        if b0 & 0x10:
+            i = self.offset + 12 + 4 * (b0 & 0x0F) + 2
+            hi = self.buffer[i] - 256 if self.buffer[i] >= 128 else self.buffer[i]
+            h += 4 + ((hi << 8) | self.buffer[i + 1]) * 4
+        return h
+
+    def getPayloadLength(self): return self.length - self.getHeaderLength()
+
+    def isInvalid(self):
+        return len(self.buffer) < self.offset + self.length or self.length < 12
+
+
+TRAILER_ROOM = 16  # largest trailer: SRTCP E|index (4) + 12-byte tag
+
+
+def derive_session_keys(masterKey: bytes, masterSalt: bytes, rtcp: bool = False):
+    """The engine's host-side RFC 3711 4.3 key derivation (no GPU needed)."""
+    mk = (C.c_uint8 * 16).from_buffer_copy(bytes(masterKey)[:16])
+    ms = (C.c_uint8 * 14).from_buffer_copy(bytes(masterSalt)[:14])
+    enc, auth, salt = (C.c_uint8 * 16)(), (C.c_uint8 * 20)(), (C.c_uint8 * 14)()
+    N.check(N.lib().srtp_derive_session_keys(mk, ms, int(rtcp), enc, auth, salt), None, "kdf")
+    return bytes(enc), bytes(auth), bytes(salt)
+
+
+def pack(pkts: Sequence[Optional[RawPacket]]):
+    """RawPacket[] -> (seg, off, len, cap, flags).  Each packet region is
+    16-byte aligned, holds the packet's buffer bytes from its offset, and has
+    room for the protect trailer (the in-place form of RawPacket.append/grow)."""
+    n = len(pkts)
+    off = np.zeros(n, np.uint32)
+    length = np.zeros(n, np.uint32)
+    cap = np.zeros(n, np.uint32)
+    flags = np.zeros(n, np.uint32)
+    pos = 0
+    for i, p in enumerate(pkts):
+        if p is None:
+            flags[i] = N.PKT_FLAG_SKIP
+            cap[i] = 16
+        else:
+            avail = len(p.buffer) - p.offset
+            cap[i] = max(avail, p.length + TRAILER_ROOM)
+            length[i] = p.length
+            flags[i] = p.flags & (N.PKT_FLAG_DISCARD | N.PKT_FLAG_SILENCE)
+        off[i] = pos
+        pos += (int(cap[i]) + 15) & ~15
+    seg = np.zeros(max(pos, 16), np.uint8)
+    for i, p in enumerate(pkts):
+        if p is not None:
+            src = np.frombuffer(bytes(p.buffer[p.offset:]), np.uint8)
+            seg[off[i]:off[i] + len(src)] = src
+    return seg, off, length, cap, flags
+
+
+class PacketTransformer:
+    """transform/PacketTransformer.java:28-53"""
+
+    def close(self):
+        raise NotImplementedError
+
+    def transform(self, pkts):
+        raise NotImplementedError
+
+    def reverseTransform(self, pkts):
+        raise NotImplementedError
+
+
+def _apply(pkts, seg, off, length, status) -> List[Optional[RawPacket]]:
+    """Write a processed bundle back into the RawPacket[] (in place)."""
+    err = None
+    for i, p in enumerate(pkts):
+        if p is None:
+            continue
+        st = int(status[i])
+        if st in (N.STATUS_SKIPPED, N.STATUS_NOT_PROCESSED):
+            continue
+        nl = int(length[i])
+        if st == N.STATUS_ERR_MALFORMED:
+            err = err if err is not None else i
+            continue
+        # RawPacket.append may reallocate: the packet gets a fresh buffer
+        p.buffer = bytearray(seg[off[i]:off[i] + nl].tobytes())
+        p.offset = 0
+        p.length = nl
+        if st != N.STATUS_OK:
+            pkts[i] = None
+    if err is not None:
+        raise SRTPTransformException(
+            f"Failed to transform RawPacket(s)! (packet {err}: malformed for SRTP)")
+    return pkts
+
+
+class _SRTPBase(PacketTransformer):
+    KIND = N.KIND_RTP
+
+    def __init__(self, forwardFactory: SRTPContextFactory,
+                 reverseFactory: Optional[SRTPContextFactory] = None):
+        reverseFactory = reverseFactory or forwardFactory
+        self.engine = forwardFactory.engine
+        self.forwardFactory, self.reverseFactory = forwardFactory, reverseFactory
+        tid = C.c_int32()
+        N.check(N.lib().srtp_transformer_create(self.engine.h, self.KIND, forwardFactory.fid,
+                                                reverseFactory.fid, C.byref(tid)),
+                self.engine.h, type(self).__name__)
+        self.tid = tid.value
+
+    def _set_factory(self, factory: SRTPContextFactory, forward: bool):
+        N.check(N.lib().srtp_transformer_set_factory(self.engine.h, self.tid, factory.fid,
+                                                     int(forward)), self.engine.h, "setFactory")
+        if forward:
+            self.forwardFactory = factory
+        else:
+            self.reverseFactory = factory
+
+    def close(self):
+        N.check(N.lib().srtp_transformer_close(self.engine.h, self.tid), self.engine.h, "close")
+
+    def _run(self, pkts, reverse):
+        if pkts is None:
+            return None
+        if len(pkts) == 0:
+            return pkts
+        seg, off, length, cap, flags = pack(pkts)
+        status = self.engine.transform_host(reverse, self.tid, seg, off, length, cap, flags)
+        return _apply(pkts, seg, off, length, status)
+
+    def transform(self, pkts):
+        return self._run(pkts, False)
+
+    def reverseTransform(self, pkts):
+        return self._run(pkts, True)
+
+
+class SRTPTransformer(_SRTPBase):
+    """SRTPTransformer(forwardFactory, reverseFactory)"""
+
+    KIND = N.KIND_RTP
+
+    def setContextFactory(self, factory: SRTPContextFactory, forward: bool):
+        self._set_factory(factory, forward)
+
+
+class SRTCPTransformer(_SRTPBase):
+    """SRTCPTransformer(forwardFactory, reverseFactory) or SRTCPTransformer(srtpTransformer)"""
+
+    KIND = N.KIND_RTCP
+
+    def __init__(self, forwardFactory, reverseFactory=None):
+        if isinstance(forwardFactory, SRTPTransformer):
+            t = forwardFactory
+            forwardFactory, reverseFactory = t.forwardFactory, t.reverseFactory
+        super().__init__(forwardFactory, reverseFactory)
+
+    def updateFactory(self, factory: SRTPContextFactory, forward: bool):
+        self._set_factory(factory, forward)
+
+
+def transform_bundle(transformers: Sequence[Optional[_SRTPBase]], pkts, reverse: bool):
+    """Process packets of many transformers in one GPU bundle (the batching the
+    reference's 1-element arrays cannot express).  Equivalent to calling each
+    transformer's transform()/reverseTransform() on its packets in order."""
+    eng = next(t for t in transformers if t is not None).engine
+    seg, off, length, cap, flags = pack(pkts)
+    tids = np.array([t.tid if t is not None else -1 for t in transformers], np.int32)
+    status = eng.transform_host(reverse, tids, seg, off, length, cap, flags)
+    return _apply(list(pkts), seg, off, length, status), status

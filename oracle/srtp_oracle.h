@@ -1,0 +1,124 @@
+/*
+ * srtp_oracle.h -- CPU restatement of libjitsi's SRTP/SRTCP hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker for the MI355X engine
+ * (libjitsi_amd).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  The product never links or calls it.
+ *
+ * It restates, with Java integer semantics (two's-complement i32/i64, JLS
+ * 15.19 shift-distance masking, signed bytes), the reference files:
+ *   srtp/SRTPCryptoContext.java:237-744   (auth, replay, IV, guessIndex, update)
+ *   srtp/SRTCPCryptoContext.java:106-451  (SRTCP replay, IV, protect/unprotect)
+ *   srtp/BaseSRTPCryptoContext.java:178-278 (key storage, authenticatePacketHMAC)
+ *   srtp/SRTPCipherCTR.java:68-121        (AES-CM keystream + XOR)
+ *   srtp/SRTPTransformer.java:100-219, srtp/SRTCPTransformer.java:92-207,
+ *   srtp/SRTPContextFactory.java:50-68    (per-transformer SSRC context map)
+ *   nm/RawPacket.java:203-220,463-614,723-839,885-909,988-999,1284-1292
+ *   tf/SinglePacketTransformer.java:121-216 (array loop, rethrow aborts batch)
+ * where srtp/ = src/org/jitsi/impl/neomedia/transform/srtp/ and
+ * nm/ = src/org/jitsi/impl/neomedia/, tf/ = .../neomedia/transform/.
+ *
+ * Primitives (AES-128 block, HMAC-SHA1) come from OpenSSL 3 libcrypto, the
+ * same library family the reference's JNI backend binds
+ * (src/native/openssl/BlockCipher.c, HMAC.c).  Parity pinning: FIPS-197,
+ * RFC 2202, RFC 3711 App. B.2/B.3 known-answer tests (the reference ships no
+ * SRTP test vectors); see tests/test_oracle_kat.py.
+ *
+ * Packet model: packet i lives in seg[off[i] .. off[i]+cap[i]); this region is
+ * the Java RawPacket buffer with offset 0 and buffer.length == cap[i].  len[i]
+ * is RawPacket.length (updated in place).  A reallocating RawPacket.append /
+ * grow is modelled as "fits in cap"; a packet whose cap is too small is
+ * rejected up front with ORC_ERR_CAPACITY and leaves no trace.
+ */
+#ifndef SRTP_ORACLE_H
+#define SRTP_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* SRTPPolicy constants, srtp/SRTPPolicy.java:29-63 */
+enum { ORC_NULL_ENCRYPTION = 0, ORC_AESCM_ENCRYPTION = 1, ORC_AESF8_ENCRYPTION = 2,
+       ORC_TWOFISH_ENCRYPTION = 3, ORC_TWOFISHF8_ENCRYPTION = 4 };
+enum { ORC_NULL_AUTHENTICATION = 0, ORC_HMACSHA1_AUTHENTICATION = 1,
+       ORC_SKEIN_AUTHENTICATION = 2 };
+
+/* Per-packet status (same numbering as include/srtp_mi355x.h). */
+enum {
+    ORC_OK = 0,
+    ORC_DROP_REPLAY = 1,     /* checkReplay false -> null */
+    ORC_DROP_AUTH = 2,       /* authenticatePacket false -> null */
+    ORC_DROP_VERSION = 3,    /* SRTPTransformer.reverseTransform version check */
+    ORC_DROP_NO_CONTEXT = 4, /* factory closed -> getContext null */
+    ORC_ERR_CAPACITY = 5,    /* cap too small for the in-place append */
+    ORC_ERR_MALFORMED = 6,   /* reference throws (AIOOBE / IOOBE) */
+    ORC_DROP_INVALID = 7,    /* RawPacket.isInvalid (length < 12) */
+    ORC_NOT_PROCESSED = 8,   /* after a throw: rest of the array aborted */
+    ORC_SKIPPED = 9          /* null element / predicate mismatch */
+};
+
+/* Packet flags (javax.media.Buffer values used by SRTPCryptoContext:609-611) */
+enum { ORC_FLAG_DISCARD = 0x2, ORC_FLAG_SILENCE = 0x4, ORC_FLAG_SKIP = (int)0x80000000u };
+
+enum { ORC_KIND_RTP = 0, ORC_KIND_RTCP = 1 };
+/* MODE_REF: the reference call structure (one 16-B AES-ECB call per keystream
+ * block + tail block, HMAC re-keyed per packet).  MODE_TUNED: one
+ * EVP_aes_128_ctr call per packet, pre-keyed HMAC context copied per packet. */
+enum { ORC_MODE_REF = 0, ORC_MODE_TUNED = 1 };
+
+typedef struct {
+    int32_t enc_type, enc_key_len, auth_type, auth_key_len, auth_tag_len, salt_key_len;
+} orc_policy;
+
+typedef struct orc_factory orc_factory;
+typedef struct orc_transformer orc_transformer;
+
+/* SRTPContextFactory(sender, masterKey, masterSalt, srtpPolicy, srtcpPolicy).
+ * Returns NULL if the policy is outside the restated profiles. */
+orc_factory *orc_factory_new(int sender, const uint8_t *master_key, int key_len,
+                             const uint8_t *master_salt, int salt_len,
+                             const orc_policy *srtp, const orc_policy *srtcp, int mode);
+void orc_factory_close(orc_factory *f);
+
+/* new SRTPTransformer(fwd, rev) / new SRTCPTransformer(fwd, rev) */
+orc_transformer *orc_transformer_new(int kind, orc_factory *fwd, orc_factory *rev);
+/* setContextFactory / updateFactory: closes the replaced factory, keeps contexts */
+void orc_transformer_set_factory(orc_transformer *t, orc_factory *f, int forward);
+/* close(): closes both factories, drops all contexts */
+void orc_transformer_close(orc_transformer *t);
+void orc_transformer_free(orc_transformer *t);
+/* SRTPCryptoContext.checkReplay property (SRTP only; SRTCP always checks). */
+void orc_set_check_replay(int enabled);
+
+/* transform(RawPacket[]) (reverse=0) / reverseTransform(RawPacket[]) (reverse=1).
+ * ts[i] is packet i's transformer (a bundle may span transformers; abort on a
+ * throw is scoped to that transformer's packets, like one transform() call per
+ * transformer).  If ts_stride == 0 every packet uses ts[0]. */
+int orc_process(orc_transformer *const *ts, int ts_stride, int reverse,
+                uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
+                const uint32_t *flags, int32_t *status, uint32_t n, int abort_on_error);
+
+/* Context state snapshot for parity tests. Returns 0 if the SSRC has no context. */
+typedef struct {
+    int32_t roc, s_l, seq_num_set, guessed_roc;   /* SRTP */
+    int32_t sent_index, received_index;           /* SRTCP */
+    uint64_t replay_window;
+} orc_ctx_state;
+int orc_get_state(orc_transformer *t, uint32_t ssrc, orc_ctx_state *out);
+uint32_t orc_num_contexts(orc_transformer *t);
+
+/* Primitive helpers exposed for the KAT tests. */
+void orc_aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]);
+void orc_hmac_sha1(const uint8_t *key, int key_len, const uint8_t *msg, size_t n, uint8_t out[20]);
+/* RFC 3711 4.3 PRF exactly as SRTPCryptoContext.deriveSrtpKeys (labels 0/1/2)
+ * or SRTCPCryptoContext.deriveSrtcpKeys (labels 3/4/5). */
+void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp,
+                     uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
