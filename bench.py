@@ -68,7 +68,7 @@ def cpu_baseline(seconds: float, threads: int, pkt_len: int, ssrcs: int):
         fs = O.Factory(True, k, s, pol, pol, O.MODE_REF)
         fr = O.Factory(False, k, s, pol, pol, O.MODE_REF)
         ts, tr = O.Transformer(O.KIND_RTP, fs, fs), O.Transformer(O.KIND_RTP, fr, fr)
-        step = n // per_thread_ssrc
+        step = -(-n // per_thread_ssrc)
         o = b.off.astype(np.int64)
         seg = b.seg.copy()
         while not stop[0]:
@@ -141,7 +141,9 @@ def main():
     torch.cuda.synchronize(dev)
     bad = int((st != 0).sum())
     if bad:
-        raise SystemExit(f"rank {rank}: {bad} packets not accepted after warmup")
+        hist = torch.bincount(st.to(torch.int64), minlength=10).tolist()
+        raise SystemExit(f"rank {rank}: {bad} packets not accepted after warmup; status "
+                         f"histogram {hist}")
     if world > 1:
         dist.barrier()
     eng.set_timing(True)

@@ -43,7 +43,7 @@
  * Ownership: the caller owns every buffer; the engine owns contexts, session
  * keys and device scratch, and zeroes keys when factories are closed.
  * Threading: calls on one engine are serialised internally; work is enqueued
- * on the given HIP stream (NULL = the engine's own stream), so bundles that
+ * on the given HIP stream (NULL = the default stream), so bundles that
  * touch the same transformer must be submitted on one stream (submission order
  * == processing order, as the reference's `synchronized` contexts give).
  */
@@ -136,7 +136,7 @@ int srtp_transformer_set_factory(srtp_engine *e, int32_t transformer, int32_t fa
 int srtp_transformer_close(srtp_engine *e, int32_t transformer);
 
 /* Process one bundle whose buffers are device (HBM) pointers; asynchronous on
- * `stream` (a hipStream_t, NULL = engine stream).  tids == NULL means every
+ * `stream` (a hipStream_t, NULL = the default stream).  tids == NULL means every
  * packet belongs to `tid`; otherwise tids[i] (device array) names packet i's
  * transformer.  flags may be NULL.  reverse = 0: transform (protect),
  * reverse = 1: reverseTransform (unprotect). */

@@ -450,7 +450,7 @@ int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, 
                           const uint32_t *flags, int32_t *status, uint32_t n, void *stream) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    hipStream_t s = (hipStream_t)stream; // NULL = the default (null) stream
     return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s);
 }
 
@@ -504,7 +504,7 @@ int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, in
 
 int srtp_engine_sync(srtp_engine *e, void *stream) {
     if (!e) return SRTP_EINVAL;
-    HIPCHK(e, hipStreamSynchronize(stream ? (hipStream_t)stream : e->stream));
+    HIPCHK(e, hipStreamSynchronize((hipStream_t)stream));
     return SRTP_OK;
 }
 

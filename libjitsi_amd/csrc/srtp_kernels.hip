@@ -57,56 +57,139 @@ __device__ __forceinline__ int64_t java_lshl(int64_t v, int64_t n) {
 }
 
 // ----------------------------------------------------------------- AES-128
-// T-table lookup for byte value x: lane l reads copy (l & 31), i.e. LDS
-// byte address x*128 + 4*(l & 31) -> bank (l & 31).
-#define TE(x) te[(x) << 5]
+// LDS image of the four AES T-tables T_r = rotl(T0, 8r), 32 lane copies each,
+// 128 KB.  Byte address of entry x of table t for a lane with copy c = lane & 31:
+//     (t >> 1) << 16 | x << 8 | (t & 1) << 7 | c << 2
+// so a ds_read_b32 wave instruction hits bank c for every lane (conflict-free:
+// lanes l and l+32 sit in different halves of the wave's LDS access), and the
+// address is one v_perm_b32 of the state word and a per-lane base
+// (byte 1 <- state byte k, bytes 0 and 2 <- base).
+constexpr int kTeWords = 32768;  // 128 KB
+constexpr int kAesBlock = 1024;  // threads per workgroup of the AES kernels (1 WG per CU)
 
-__device__ __forceinline__ void fill_te(uint32_t *s_te) {
-    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) s_te[i] = d_te0[i >> 5];
+__device__ __forceinline__ void fill_te4(uint32_t *s_te) {
+    for (int i = threadIdx.x; i < kTeWords; i += blockDim.x) {
+        const int t = ((i >> 14) << 1) | ((i >> 5) & 1);
+        const uint32_t v = d_te0[(i >> 6) & 255];
+        s_te[i] = t ? rotl(v, 8u * (uint32_t)t) : v;
+    }
     __syncthreads();
+}
+
+struct TeBase {
+    uint32_t b[4]; // per-lane byte base of table t (bytes 0 and 2 of the address)
+};
+
+__device__ __forceinline__ TeBase te_base() {
+    TeBase tb;
+    const uint32_t c4 = (threadIdx.x & 31u) << 2;
+#pragma unroll
+    for (int t = 0; t < 4; t++) tb.b[t] = (uint32_t)((t >> 1) << 16) | (uint32_t)((t & 1) << 7) | c4;
+    return tb;
+}
+
+// entry (byte k of s) of table t
+#define TL(s, k, t)                                                                     \
+    (*reinterpret_cast<const uint32_t *>(                                               \
+        lds + __builtin_amdgcn_perm((s), tb.b[t], 0x0c020000u | ((4u + (k)) << 8))))
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
 struct RoundKeys {
     uint32_t k[44];
 };
 
-// FIPS-197 AES-128 encryption of one block held as four little-endian column
-// words (byte r of word j = state row r, column j).  Row r of output column j
-// comes from input column j+r (ShiftRows); T_r = rotl(T_0, 8r).
-__device__ __forceinline__ void aes_encrypt(const uint32_t *__restrict__ te, const RoundKeys &rk,
-                                            uint32_t &s0, uint32_t &s1, uint32_t &s2,
-                                            uint32_t &s3) {
-    s0 ^= rk.k[0]; s1 ^= rk.k[1]; s2 ^= rk.k[2]; s3 ^= rk.k[3];
+// FIPS-197 AES-128 on two independent blocks (interleaved for ILP), each held
+// as four little-endian column words (byte r of word j = state row r, column
+// j).  Output column j, row r comes from input column j+r (ShiftRows), looked
+// up in T_r (MixColumns coefficients rotated by row).
+__device__ __forceinline__ void aes_encrypt2(const char *__restrict__ lds, const TeBase &tb,
+                                             const RoundKeys &rk, uint32_t a[4], uint32_t b[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) { a[j] ^= rk.k[j]; b[j] ^= rk.k[j]; }
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        uint32_t t0 = TE(s0 & 0xff) ^ rotl(TE((s1 >> 8) & 0xff), 8) ^
-                      rotl(TE((s2 >> 16) & 0xff), 16) ^ rotl(TE(s3 >> 24), 24) ^ rk.k[4 * r];
-        uint32_t t1 = TE(s1 & 0xff) ^ rotl(TE((s2 >> 8) & 0xff), 8) ^
-                      rotl(TE((s3 >> 16) & 0xff), 16) ^ rotl(TE(s0 >> 24), 24) ^ rk.k[4 * r + 1];
-        uint32_t t2 = TE(s2 & 0xff) ^ rotl(TE((s3 >> 8) & 0xff), 8) ^
-                      rotl(TE((s0 >> 16) & 0xff), 16) ^ rotl(TE(s1 >> 24), 24) ^ rk.k[4 * r + 2];
-        uint32_t t3 = TE(s3 & 0xff) ^ rotl(TE((s0 >> 8) & 0xff), 8) ^
-                      rotl(TE((s1 >> 16) & 0xff), 16) ^ rotl(TE(s2 >> 24), 24) ^ rk.k[4 * r + 3];
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        uint32_t ta[4], tbk[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            ta[j] = xor3(xor3(TL(a[j], 0, 0), TL(a[(j + 1) & 3], 1, 1), TL(a[(j + 2) & 3], 2, 2)),
+                         TL(a[(j + 3) & 3], 3, 3), rk.k[4 * r + j]);
+            tbk[j] = xor3(xor3(TL(b[j], 0, 0), TL(b[(j + 1) & 3], 1, 1), TL(b[(j + 2) & 3], 2, 2)),
+                          TL(b[(j + 3) & 3], 3, 3), rk.k[4 * r + j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
     }
-    // last round: S(x) is byte 1 of T0[x] (T0 = 2s | s<<8 | s<<16 | 3s<<24)
-    uint32_t t0 = ((TE(s0 & 0xff) >> 8) & 0xffu) | (TE((s1 >> 8) & 0xff) & 0xff00u) |
-                  (TE((s2 >> 16) & 0xff) & 0xff0000u) | ((TE(s3 >> 24) << 8) & 0xff000000u);
-    uint32_t t1 = ((TE(s1 & 0xff) >> 8) & 0xffu) | (TE((s2 >> 8) & 0xff) & 0xff00u) |
-                  (TE((s3 >> 16) & 0xff) & 0xff0000u) | ((TE(s0 >> 24) << 8) & 0xff000000u);
-    uint32_t t2 = ((TE(s2 & 0xff) >> 8) & 0xffu) | (TE((s3 >> 8) & 0xff) & 0xff00u) |
-                  (TE((s0 >> 16) & 0xff) & 0xff0000u) | ((TE(s1 >> 24) << 8) & 0xff000000u);
-    uint32_t t3 = ((TE(s3 & 0xff) >> 8) & 0xffu) | (TE((s0 >> 8) & 0xff) & 0xff00u) |
-                  (TE((s1 >> 16) & 0xff) & 0xff0000u) | ((TE(s2 >> 24) << 8) & 0xff000000u);
-    s0 = t0 ^ rk.k[40]; s1 = t1 ^ rk.k[41]; s2 = t2 ^ rk.k[42]; s3 = t3 ^ rk.k[43];
+    // Last round (no MixColumns): S(x) sits in byte 1 of T0, 2 of T1, 0 of T2,
+    // 0 of T3; two v_perm_b32 gather the four S-box bytes of a column.
+    uint32_t ta[4], tbk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t lo_a = __builtin_amdgcn_perm(TL(a[(j + 1) & 3], 1, 1), TL(a[j], 0, 0), 0x0c0c0601u);
+        const uint32_t hi_a = __builtin_amdgcn_perm(TL(a[(j + 3) & 3], 3, 3), TL(a[(j + 2) & 3], 2, 2), 0x04000c0cu);
+        ta[j] = xor3(lo_a, hi_a, rk.k[40 + j]);
+        const uint32_t lo_b = __builtin_amdgcn_perm(TL(b[(j + 1) & 3], 1, 1), TL(b[j], 0, 0), 0x0c0c0601u);
+        const uint32_t hi_b = __builtin_amdgcn_perm(TL(b[(j + 3) & 3], 3, 3), TL(b[(j + 2) & 3], 2, 2), 0x04000c0cu);
+        tbk[j] = xor3(lo_b, hi_b, rk.k[40 + j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
 }
 
-// SRTPCipherCTR keystream block j: AES(iv[0..13] || u16_be(j))  (:77-84)
-__device__ __forceinline__ void ctr_block(const uint32_t *__restrict__ te, const RoundKeys &rk,
-                                          const uint32_t iv[4], uint32_t j, uint32_t out[4]) {
+// AES-CM state of one packet (SRTPCipherCTR.getCipherStream :68-92): keystream
+// block j = AES(iv[0..13] || u16_be(j)), XORed over packet bytes [off, end).
+struct Ctr {
+    uint32_t iv[4];
+    int off, end;
+    uint32_t carry[4]; // keystream block preceding the current 64-B chunk
+};
+
+__device__ __forceinline__ void ctr_input(const uint32_t iv[4], int j, uint32_t out[4]) {
     out[0] = iv[0]; out[1] = iv[1]; out[2] = iv[2];
-    out[3] = iv[3] | (((j >> 8) & 0xffu) << 16) | ((j & 0xffu) << 24);
-    aes_encrypt(te, rk, out[0], out[1], out[2], out[3]);
+    out[3] = iv[3] | ((((uint32_t)j >> 8) & 0xffu) << 16) | (((uint32_t)j & 0xffu) << 24);
+}
+
+// XOR the keystream into the 16 LE words d[] of packet chunk c (bytes 64c ..
+// 64c+63).  Payload word i uses keystream word i; the payload starts `off`
+// bytes into the packet (a multiple of 4), so chunk word 4m+k takes keystream
+// word 16c + 4m + k - off/4, i.e. blocks 4c - off/16 - 1 .. 4c - off/16 + 3.
+// Computes four new blocks (two interleaved pairs, one AES code site).
+__device__ __forceinline__ void ctr_chunk(const char *__restrict__ lds, const TeBase &tb,
+                                          const RoundKeys &rk, Ctr &cs, int c, uint32_t d[16]) {
+    const int hq = cs.off >> 4, s = (cs.off >> 2) & 3;
+    const int j0 = 4 * c - hq;
+    uint32_t K[16];
+#pragma unroll 1
+    for (int pr = 0; pr < 2; pr++) {
+        uint32_t x[4], y[4];
+        ctr_input(cs.iv, j0 + 2 * pr, x);
+        ctr_input(cs.iv, j0 + 2 * pr + 1, y);
+        aes_encrypt2(lds, tb, rk, x, y);
+#pragma unroll
+        for (int k = 0; k < 8; k++) K[k] = K[k + 8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { K[8 + k] = x[k]; K[12 + k] = y[k]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        // keystream word for chunk word i: concat(carry, K)[4 + i - s]
+        const uint32_t a0 = K[i];
+        const uint32_t a1 = i >= 1 ? K[i - 1] : cs.carry[3 + i];
+        const uint32_t a2 = i >= 2 ? K[i - 2] : cs.carry[2 + i];
+        const uint32_t a3 = i >= 3 ? K[i - 3] : cs.carry[1 + i];
+        const uint32_t ksw = (s & 2) ? ((s & 1) ? a3 : a2) : ((s & 1) ? a1 : a0);
+        const int pos = 64 * c + 4 * i;
+        uint32_t m = 0u;
+        if (pos >= cs.off && pos < cs.end) {
+            const int rem = cs.end - pos;
+            m = rem >= 4 ? 0xffffffffu : ((1u << (8 * rem)) - 1u);
+        }
+        d[i] ^= ksw & m;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs.carry[k] = K[12 + k];
 }
 
 // ----------------------------------------------------------------- SHA-1
@@ -172,21 +255,43 @@ __device__ __forceinline__ void inner_words(uint32_t w[16], int b, int mac_len, 
     }
 }
 
-// HMAC outer block: opad midstate || inner digest.
-__device__ __forceinline__ void outer_words(uint32_t w[16], const uint32_t inner[5]) {
+// HMAC outer block: w = inner digest || padding, h = opad midstate.
+__device__ __forceinline__ void outer_words(uint32_t w[16], uint32_t h[5], const KeySet *ks) {
 #pragma unroll
-    for (int k = 0; k < 5; k++) w[k] = inner[k];
+    for (int k = 0; k < 5; k++) { w[k] = h[k]; h[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ks->opad[k]); }
     w[5] = 0x80000000u;
 #pragma unroll
     for (int k = 6; k < 15; k++) w[k] = 0u;
     w[15] = (64 + 20) * 8;
 }
 
-__device__ __forceinline__ uint32_t tag_byte(const uint32_t h[5], int i) {
-    uint32_t wv = h[0];
+// The first T (<= 12) bytes of the big-endian digest h, as stored / compared
+// at p (byte accesses: tags sit at arbitrary alignment).  Fully unrolled so h
+// stays in registers.
+__device__ __forceinline__ bool tag_matches(const uint32_t h[5], const uint8_t *p, int T) {
+    bool ok = true;
 #pragma unroll
-    for (int k = 1; k < 5; k++) if ((i >> 2) == k) wv = h[k];
-    return (wv >> (24 - 8 * (i & 3))) & 0xffu;
+    for (int k = 0; k < 3; k++) {
+        uint32_t got = 0u, mask = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int idx = 4 * k + i;
+            if (idx < T) {
+                got |= ld_u8(p + idx) << (24 - 8 * i);
+                mask |= 0xffu << (24 - 8 * i);
+            }
+        }
+        ok &= ((got ^ h[k]) & mask) == 0u;
+    }
+    return ok;
+}
+
+__device__ __forceinline__ void tag_write(const uint32_t h[5], uint8_t *p, int T) {
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (4 * k + i < T) p[4 * k + i] = (uint8_t)(h[k] >> (24 - 8 * i));
 }
 
 // ------------------------------------------------------- RawPacket helpers
@@ -403,7 +508,7 @@ __device__ __forceinline__ void verify_one(const BundleArgs &a, const KeySet *__
         mac_len = io;
     }
     if (mac_len < 0) mac_len = 0;
-    uint32_t h[5], inner[5] = {0, 0, 0, 0, 0};
+    uint32_t h[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
     const int nb_full = mac_len >> 6;
@@ -431,16 +536,11 @@ __device__ __forceinline__ void verify_one(const BundleArgs &a, const KeySet *__
         if (b < nb_inner) {
             inner_words(w, b, mac_len, suffix);
         } else {
-#pragma unroll
-            for (int k = 0; k < 5; k++) { inner[k] = h[k]; h[k] = sgpr(ks->opad[k]); }
-            outer_words(w, inner);
+            outer_words(w, h, ks);
         }
         sha1_compress(h, w);
     }
-    const uint8_t *tp = pkt + (L - T);
-    bool ok = true;
-    for (int i = 0; i < T; i++) ok &= (ld_u8(tp + i) == tag_byte(h, i));
-    a.auth_ok[p] = ok ? 1u : 0u;
+    a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kBlock, 4) void k_verify(BundleArgs a) {
@@ -461,7 +561,7 @@ __device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks,
     int mac_len = L - T;
     if (mac_len < 0) mac_len = 0;
     const uint8_t *pkt = a.seg + a.off[p];
-    uint32_t h[5], inner[5] = {0, 0, 0, 0, 0};
+    uint32_t h[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) h[k] = a.mid[5 * (size_t)p + k];
     const int nb_full = mac_len >> 6;
@@ -477,15 +577,11 @@ __device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks,
         if (b < nb_inner) {
             inner_words(w, b, mac_len, (uint32_t)g);
         } else {
-#pragma unroll
-            for (int k = 0; k < 5; k++) { inner[k] = h[k]; h[k] = ks->opad[k]; }
-            outer_words(w, inner);
+            outer_words(w, h, ks);
         }
         sha1_compress(h, w);
     }
-    bool ok = true;
-    for (int i = 0; i < T; i++) ok &= (ld_u8(pkt + mac_len + i) == tag_byte(h, i));
-    return ok;
+    return tag_matches(h, pkt + mac_len, T);
 }
 
 // ============================================================== k_walk
@@ -646,41 +742,6 @@ __device__ __forceinline__ int32_t finish_status(const BundleArgs &a, uint32_t p
     return st;
 }
 
-// Keystream word k of a data quad when payload words are shifted by s words
-// against the 16-B quad grid: concat(prev, cur)[4 - s + k].
-__device__ __forceinline__ uint32_t ks_word(int s, const uint32_t prev[4], const uint32_t cur[4],
-                                            int k) {
-    const uint32_t a0 = cur[k];
-    const uint32_t a1 = k >= 1 ? cur[k - 1] : prev[3 + k];
-    const uint32_t a2 = k >= 2 ? cur[k - 2] : prev[2 + k];
-    const uint32_t a3 = k >= 3 ? cur[k - 3] : prev[1 + k];
-    return (s & 2) ? ((s & 1) ? a3 : a2) : ((s & 1) ? a1 : a0);
-}
-
-// XOR the AES-CM keystream into data quad q (bytes 16q..16q+15) over
-// [enc_off, enc_end); keystream block j covers bytes enc_off + 16j ...
-__device__ __forceinline__ void ctr_quad(const uint32_t *__restrict__ te, const RoundKeys &rk,
-                                         const uint32_t iv[4], int q, int enc_off, int enc_end,
-                                         uint32_t prev[4], uint32_t cur[4], uint4 &v) {
-    const int hq = enc_off >> 4, s = (enc_off >> 2) & 3;
-#pragma unroll
-    for (int k = 0; k < 4; k++) prev[k] = cur[k];
-    ctr_block(te, rk, iv, (uint32_t)(q - hq), cur);
-    uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int pos = 16 * q + 4 * k;
-        const uint32_t ksw = ks_word(s, prev, cur, k);
-        uint32_t m = 0u;
-        if (pos >= enc_off && pos < enc_end) {
-            const int rem = enc_end - pos;
-            m = rem >= 4 ? 0xffffffffu : ((1u << (8 * rem)) - 1u);
-        }
-        d[k] ^= ksw & m;
-    }
-    v = make_uint4(d[0], d[1], d[2], d[3]);
-}
-
 __device__ __forceinline__ void make_iv_rtp(const KeySet *ks, const uint4 &hdr, uint32_t roc,
                                             uint32_t iv[4]) {
     // processPacketAESCM :482-525: salt ^ (0, SSRC, ROC, SEQ, 0)
@@ -704,7 +765,8 @@ __device__ __forceinline__ void make_iv_rtcp(const KeySet *ks, const uint4 &hdr,
 // :94-121) + HMAC-SHA1 over the ciphertext (authenticatePacketHMAC :269-278)
 // + trailer (RawPacket.append :203-220).  Packet bytes: one read, one write.
 __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
-                                            const uint32_t *__restrict__ te, uint32_t p) {
+                                            const char *__restrict__ lds, const TeBase &tb,
+                                            uint32_t p) {
     uint8_t *pkt = a.seg + a.off[p];
     const bool do_enc = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
     const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
@@ -713,59 +775,56 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     const int L = (int)a.w_len[p] - (do_mac ? (T + (rtcp ? 4 : 0)) : 0);
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
     const uint32_t cw = a.w_cw[p];
-    uint32_t iv[4];
-    int enc_off;
+    Ctr cs;
     uint32_t suffix;
     if (!rtcp) {
-        enc_off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-        make_iv_rtp(ks, hdr, cw, iv);
+        cs.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        make_iv_rtp(ks, hdr, cw, cs.iv);
         suffix = cw;
     } else {
-        enc_off = 8;
-        make_iv_rtcp(ks, hdr, cw, iv);
+        cs.off = 8;
+        make_iv_rtcp(ks, hdr, cw, cs.iv);
         suffix = do_enc ? (cw | 0x80000000u) : 0u;
     }
+    cs.end = L;
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
     RoundKeys rk;
     load_round_keys_uniform(ks, rk);
-    uint32_t prev[4] = {0, 0, 0, 0}, cur[4] = {0, 0, 0, 0};
-    uint32_t h[5], inner[5] = {0, 0, 0, 0, 0};
+    uint32_t h[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
     const int nb_data = (L + 63) >> 6;
     const int nb_inner = do_mac ? ((L + 12) >> 6) + 1 : 0;
     const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
-    // One AES site and one SHA-1 site: block b gathers its four 16-B quads
-    // (encrypting them in place), then runs one compression (inner blocks,
-    // then the outer block).
+    // One AES site and one SHA-1 site: 64-B chunk b is loaded, encrypted in
+    // place, stored, then hashed (inner blocks, then the outer block).
     for (int b = 0; b < n_blocks; b++) {
         uint32_t w[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) w[k] = 0u;
+        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
         if (b < nb_data) {
-#pragma unroll 1
-            for (int m = 0; m < 4; m++) {
-                const int q = 4 * b + m;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (16 * q < L) {
-                    uint4 *qp = reinterpret_cast<uint4 *>(pkt + 16 * q);
-                    v = *qp;
-                    if (do_enc && 16 * q + 16 > enc_off) {
-                        ctr_quad(te, rk, iv, q, enc_off, L, prev, cur, v);
-                        *qp = v;
-                    }
-                }
 #pragma unroll
-                for (int k = 0; k < 12; k++) w[k] = w[k + 4];
-                w[12] = v.x; w[13] = v.y; w[14] = v.z; w[15] = v.w;
+            for (int m = 0; m < 4; m++) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (64 * b + 16 * m < L) v = qp[m];
+                w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
             }
+            if (do_enc && 64 * b + 64 > cs.off) {
+                ctr_chunk(lds, tb, rk, cs, b, w);
+#pragma unroll
+                for (int m = 0; m < 4; m++)
+                    if (64 * b + 16 * m < L && 64 * b + 16 * m + 16 > cs.off)
+                        qp[m] = make_uint4(w[4 * m], w[4 * m + 1], w[4 * m + 2], w[4 * m + 3]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = 0u;
         }
         if (!do_mac) continue;
         if (b < nb_inner) {
             inner_words(w, b, L, suffix);
         } else {
-#pragma unroll
-            for (int k = 0; k < 5; k++) { inner[k] = h[k]; h[k] = sgpr(ks->opad[k]); }
-            outer_words(w, inner);
+            outer_words(w, h, ks);
         }
         sha1_compress(h, w);
     }
@@ -776,53 +835,64 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
         o += 4;
     }
-    for (int i = 0; i < T; i++) pkt[o + i] = (uint8_t)tag_byte(h, i);
+    tag_write(h, pkt + o, T);
 }
 
-__global__ __launch_bounds__(kBlock, 4) void k_protect(BundleArgs a) {
-    __shared__ uint32_t s_te[256 * 32];
-    fill_te(s_te);
+__global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
+    __shared__ uint32_t s_te[kTeWords];
+    fill_te4(s_te);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
     const bool todo = finish_status(a, p) == SRTP_STATUS_OK;
     const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
-    const uint32_t *te = s_te + (threadIdx.x & 31);
-    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { protect_one(a, a.keysets + ks_u, te, p); });
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s_te);
+    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { protect_one(a, a.keysets + ks_u, lds, tb, p); });
 }
 
 // ============================================================== k_decrypt
 // AES-CM decryption of accepted packets (SRTPCryptoContext :609-627,
 // SRTCPCryptoContext :355-370).
 __device__ __forceinline__ void decrypt_one(const BundleArgs &a, const KeySet *__restrict__ ks,
-                                            const uint32_t *__restrict__ te, uint32_t p) {
+                                            const char *__restrict__ lds, const TeBase &tb,
+                                            uint32_t p) {
     uint8_t *pkt = a.seg + a.off[p];
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
     const uint32_t cw = a.w_cw[p];
-    const int L = (int)a.w_len[p];
-    uint32_t iv[4];
-    int enc_off;
+    Ctr cs;
     if (sgpr(ks->kind) == SRTP_KIND_RTP) {
-        enc_off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-        make_iv_rtp(ks, hdr, cw, iv);
+        cs.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        make_iv_rtp(ks, hdr, cw, cs.iv);
     } else {
-        enc_off = 8;
-        make_iv_rtcp(ks, hdr, cw & 0x7FFFFFFFu, iv);
+        cs.off = 8;
+        make_iv_rtcp(ks, hdr, cw & 0x7FFFFFFFu, cs.iv);
     }
-    if (L - enc_off <= 0) return;
+    cs.end = (int)a.w_len[p];
+    if (cs.end - cs.off <= 0) return;
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
     RoundKeys rk;
     load_round_keys_uniform(ks, rk);
-    uint32_t prev[4] = {0, 0, 0, 0}, cur[4] = {0, 0, 0, 0};
-    for (int q = enc_off >> 4; 16 * q < L; q++) {
-        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 16 * q);
-        uint4 v = *qp;
-        ctr_quad(te, rk, iv, q, enc_off, L, prev, cur, v);
-        *qp = v;
+    for (int c = cs.off >> 6; 64 * c < cs.end; c++) {
+        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * c);
+        uint32_t w[16];
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (64 * c + 16 * m < cs.end) v = qp[m];
+            w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+        }
+        ctr_chunk(lds, tb, rk, cs, c, w);
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+            if (64 * c + 16 * m < cs.end && 64 * c + 16 * m + 16 > cs.off)
+                qp[m] = make_uint4(w[4 * m], w[4 * m + 1], w[4 * m + 2], w[4 * m + 3]);
     }
 }
 
-__global__ __launch_bounds__(kBlock, 4) void k_decrypt(BundleArgs a) {
-    __shared__ uint32_t s_te[256 * 32];
-    fill_te(s_te);
+__global__ __launch_bounds__(kAesBlock) void k_decrypt(BundleArgs a) {
+    __shared__ uint32_t s_te[kTeWords];
+    fill_te4(s_te);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
     bool todo = finish_status(a, p) == SRTP_STATUS_OK;
@@ -838,8 +908,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_decrypt(BundleArgs a) {
             todo = false; // E flag clear: sent unencrypted
         }
     }
-    const uint32_t *te = s_te + (threadIdx.x & 31);
-    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { decrypt_one(a, a.keysets + ks_u, te, p); });
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s_te);
+    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { decrypt_one(a, a.keysets + ks_u, lds, tb, p); });
 }
 
 // ============================================================== maintenance
@@ -877,11 +948,11 @@ hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_protect, grid_for(a.n), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_protect, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_decrypt(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_decrypt, grid_for(a.n), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_decrypt, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,

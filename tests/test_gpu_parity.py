@@ -397,6 +397,36 @@ def test_many_transformers_one_bundle(twin):
     twin.run([ts[i] for i in perm], False, sb.seg, sb.off, sb.length, sb.cap)
 
 
+def reseq(b, step):
+    o = b.off.astype(np.int64)
+    q = ((b.seg[o + 2].astype(np.int64) << 8) | b.seg[o + 3]) + step
+    b.seg[o + 2] = ((q >> 8) & 0xFF).astype(np.uint8)
+    b.seg[o + 3] = (q & 0xFF).astype(np.uint8)
+
+
+def test_bench_loop_multi_step(twin):
+    """bench.py's step at reduced size: protect -> unprotect -> advance every
+    packet's seq by the packets per SSRC, repeated; includes SSRCs that wrap."""
+    n, nssrc = 6000, 700
+    rng = np.random.default_rng(77)
+    seq0 = rng.integers(0, 65536, nssrc).astype(np.uint32)
+    seq0[:20] = 65536 - rng.integers(1, 60, 20)
+    b = synth.rtp_bundle(n, nssrc, 1200, seed=synth.SEED_BASE + 2, seq0=seq0)
+    (k, s), = synth.keys(2, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    step = -(-n // nssrc)
+    cur = b.copy()
+    for it in range(6):
+        seg, ln, st = twin.run(snd, False, cur.seg, cur.off, cur.length, cur.cap,
+                               check_state=(it % 2 == 0))
+        assert (st == 0).all(), np.bincount(st)
+        seg2, ln2, st2 = twin.run(rcv, True, seg, cur.off, ln, cur.cap, check_state=(it % 2 == 0))
+        assert (st2 == 0).all(), np.bincount(st2)
+        cur.seg, cur.length = seg2, ln2
+        reseq(cur, step)
+
+
 def test_full_size_round_trip_properties(engine_factory):
     """BASELINE config 2 at full bundle size (2^18 x 1200 B, 10k SSRCs) on the
     device path: protect then unprotect restores every byte, all tags verify,
@@ -437,7 +467,11 @@ def test_full_size_round_trip_properties(engine_factory):
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
     assert int((ln != 1200).sum()) == 0
-    assert np.array_equal(seg.cpu().numpy(), b.seg)
+    dec = seg.cpu().numpy()
+    keep = np.ones(len(b.seg), bool)  # bytes past the shrunk length keep the old tag
+    for j in range(10):
+        keep[o + 1200 + j] = False
+    assert np.array_equal(dec[keep], b.seg[keep])
     seg2 = torch.from_numpy(b.seg).to(dev)
     ln2 = torch.from_numpy(b.length.view(np.int32)).to(dev)
     eng.transform_device(False, snd.tid, seg2, off, ln2, cap, st, stream=stream)
