@@ -143,9 +143,9 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     uint32_t m = std::max<uint32_t>(n, 1024);
     HIPCHK(e, dalloc(&e->p_slot, m));
     HIPCHK(e, dalloc(&e->sk_in, m));
-    HIPCHK(e, dalloc(&e->sk_out, m));
+    HIPCHK(e, dalloc(&e->sk_out, m + 8)); // k_walk reads batches of 4 past a segment end
     HIPCHK(e, dalloc(&e->sv_in, m));
-    HIPCHK(e, dalloc(&e->sv_out, m));
+    HIPCHK(e, dalloc(&e->sv_out, m + 8));
     HIPCHK(e, dalloc(&e->w_status, m));
     HIPCHK(e, dalloc(&e->w_cw, m));
     HIPCHK(e, dalloc(&e->w_len, m));

@@ -585,7 +585,130 @@ __device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks,
 }
 
 // ============================================================== k_walk
-// One lane per context: the packets of the context in array order.
+// One lane per context: the serial state machine over the context's packets in
+// array order.  Records come from the sorted array four at a time (one memory
+// round trip per four packets, verify results prefetched with them).
+struct WalkCtx {
+    int enc, auth, T, kind;
+    bool check_replay, reverse;
+};
+
+// Processes one packet; returns false when the rest of the context's packets
+// are aborted (a throw with abort_on_error).
+__device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, const WalkCtx &c,
+                                         CtxState &st, const WalkRec &rec, uint32_t g0,
+                                         uint32_t auth_ok, bool dry, int32_t tid) {
+    const uint32_t p = rec.p & kRecIdxMask;
+    const int L = (int)(rec.lc & 0xffffu), C = (int)(rec.lc >> 16);
+    const int T = c.T;
+    bool threw = false;
+    if (c.kind == SRTP_KIND_RTP) {
+        const int seq = (int)rec.word;
+        if (!c.reverse) {
+            const int Tt = (c.auth != SRTP_NULL_AUTHENTICATION) ? T : 0;
+            if (L + Tt > C) { a.w_status[p] = SRTP_STATUS_ERR_CAPACITY; return true; }
+        }
+        if (!(st.flags & 1u)) { st.flags |= 1u; st.b = seq; } // seqNumSet (:587-591, :662-666)
+        // guessIndex :457-475
+        int32_t g;
+        if (st.b < 32768) g = (seq - st.b > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
+        else g = (st.b - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
+        st.g = g;
+        const int64_t gi = java_lshl((int64_t)g, 16) | seq;
+        const int64_t local = java_lshl((int64_t)st.a, 16) | st.b;
+        const int64_t delta = gi - local;
+        // checkReplay :279-323
+        if (c.check_replay && delta <= 0) {
+            if (-delta > 64 || (((uint64_t)st.window >> ((-delta) & 63)) & 1u)) {
+                a.w_status[p] = SRTP_STATUS_DROP_REPLAY;
+                return true;
+            }
+        }
+        int newL = L;
+        if (c.reverse) {
+            if (c.auth != SRTP_NULL_AUTHENTICATION) {
+                newL = L - T > 0 ? L - T : 0;
+                a.w_len[p] = (uint32_t)newL;
+                bool ok;
+                if ((uint32_t)g == g0) {
+                    ok = auth_ok != 0;
+                } else {
+                    ok = reverify_rtp(a, ks, p, L, g);
+                    atomicAdd(&a.ctl->n_mismatch, 1u);
+                }
+                if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
+            }
+            if (c.enc == SRTP_AESCM_ENCRYPTION && !(rec.p & kRecSkipDec))
+                threw = ctr_would_throw(rec.h, newL - rec.h);
+        } else {
+            if (c.enc == SRTP_AESCM_ENCRYPTION) threw = ctr_would_throw(rec.h, L - rec.h);
+            if (!threw && c.auth != SRTP_NULL_AUTHENTICATION) newL = L + T;
+        }
+        if (!threw) {
+            a.w_cw[p] = (uint32_t)g;
+            a.w_len[p] = (uint32_t)newL;
+            // update :719-744
+            if (delta > 0) st.window = (uint64_t)java_lshl((int64_t)st.window, delta) | 1ull;
+            else st.window |= (uint64_t)(int64_t)java_ishl1((int32_t)(-delta));
+            if (g == st.a) {
+                if (seq > st.b) st.b = seq & 0xffff;
+            } else if (g == (int32_t)((uint32_t)st.a + 1u)) {
+                st.b = seq & 0xffff;
+                st.a = g;
+            }
+        }
+    } else if (!c.reverse) {
+        // SRTCPCryptoContext.transformPacket :391-427
+        const int trailer = (c.auth != SRTP_NULL_AUTHENTICATION) ? 4 + T : 0;
+        if (L + trailer > C) { a.w_status[p] = SRTP_STATUS_ERR_CAPACITY; return true; }
+        a.w_cw[p] = (uint32_t)st.a;
+        a.w_len[p] = (uint32_t)(L + trailer);
+        st.a = (int32_t)(((uint32_t)st.a + 1u) & 0x7FFFFFFFu);
+    } else {
+        // SRTCPCryptoContext.reverseTransformPacket :315-374
+        const int io = L - 4 - T;
+        if (io < 0) {
+            threw = true;
+        } else {
+            uint32_t word = rec.word;
+            if (rec.h != T) word = ld_be32(a.seg + a.off[p] + io);
+            const int32_t index = (int32_t)(word & 0x7FFFFFFFu);
+            const bool decrypt = (word & 0x80000000u) != 0;
+            const int64_t delta = (int64_t)(int32_t)((uint32_t)index - (uint32_t)st.b);
+            // SRTCP checkReplay (:106-120) is not config-gated
+            if (delta <= 0 && (-delta > 64 || (((uint64_t)st.window >> ((-delta) & 63)) & 1u))) {
+                a.w_status[p] = SRTP_STATUS_DROP_REPLAY;
+                return true;
+            }
+            int newL = L;
+            if (c.auth != SRTP_NULL_AUTHENTICATION) {
+                newL = L - T - 4 > 0 ? L - T - 4 : 0;
+                a.w_len[p] = (uint32_t)newL;
+                if (!auth_ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
+            }
+            if (decrypt && c.enc == SRTP_AESCM_ENCRYPTION && newL - 8 < 0) threw = true;
+            if (!threw) {
+                a.w_cw[p] = word;
+                // update :435-451 (reversed delta)
+                const int32_t d2 = (int32_t)((uint32_t)st.b - (uint32_t)index);
+                if (d2 > 0) st.window = (uint64_t)java_lshl((int64_t)st.window, d2) | 1ull;
+                else st.window |= (uint64_t)(int64_t)java_ishl1(d2);
+                st.b = index;
+            }
+        }
+    }
+    if (threw) {
+        a.w_status[p] = SRTP_STATUS_ERR_MALFORMED;
+        if (a.abort_on_error) {
+            if (dry) atomicMin(&a.e_min[tid], (int32_t)p);
+            return false; // the rest of this transformer's array is aborted
+        }
+        return true;
+    }
+    a.w_status[p] = SRTP_STATUS_OK;
+    return true;
+}
+
 __global__ __launch_bounds__(kBlock) void k_walk(BundleArgs a, int limit_pass) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const BundleCtl ctl = *a.ctl;
@@ -598,127 +721,46 @@ __global__ __launch_bounds__(kBlock) void k_walk(BundleArgs a, int limit_pass) {
     const uint32_t slot = key;
     CtxState st = a.ctx[slot];
     const KeySet *ks = a.keysets + st.ks;
-    const int enc = ks->enc_type, auth = ks->auth_type, T = ks->tag_len, kind = ks->kind;
+    WalkCtx c;
+    c.enc = ks->enc_type; c.auth = ks->auth_type; c.T = ks->tag_len; c.kind = ks->kind;
+    c.check_replay = a.check_replay != 0;
+    c.reverse = a.reverse != 0;
+    const bool need_auth = c.reverse && c.auth != SRTP_NULL_AUTHENTICATION;
     const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
     const bool dry = two_pass && !limit_pass;
     const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
-    const bool check_replay = a.check_replay != 0;
     const uint32_t first_p = a.sv_out[i].p & kRecIdxMask;
 
-    for (uint32_t j = i; j < a.n && a.sk_out[j] == key; j++) {
-        const WalkRec rec = a.sv_out[j];
-        const uint32_t p = rec.p & kRecIdxMask;
-        if (limit_pass && (int32_t)p > E) break; // aborted (k_protect/k_decrypt label them)
-        const int L = (int)(rec.lc & 0xffffu), C = (int)(rec.lc >> 16);
-        bool threw = false;
-        if (kind == SRTP_KIND_RTP) {
-            const int seq = (int)rec.word;
-            if (!a.reverse) {
-                const int Tt = (auth != SRTP_NULL_AUTHENTICATION) ? T : 0;
-                if (L + Tt > C) { a.w_status[p] = SRTP_STATUS_ERR_CAPACITY; continue; }
-            }
-            if (!(st.flags & 1u)) { st.flags |= 1u; st.b = seq; } // seqNumSet (:587-591, :662-666)
-            // guessIndex :457-475
-            int32_t g;
-            if (st.b < 32768) g = (seq - st.b > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
-            else g = (st.b - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
-            st.g = g;
-            const int64_t gi = java_lshl((int64_t)g, 16) | seq;
-            const int64_t local = java_lshl((int64_t)st.a, 16) | st.b;
-            const int64_t delta = gi - local;
-            // checkReplay :279-323
-            bool replay_ok = true;
-            if (check_replay && delta <= 0) {
-                if (-delta > 64) replay_ok = false;
-                else if (((uint64_t)st.window >> ((-delta) & 63)) & 1u) replay_ok = false;
-            }
-            if (!replay_ok) { a.w_status[p] = SRTP_STATUS_DROP_REPLAY; continue; }
-            int newL = L;
-            if (a.reverse) {
-                if (auth != SRTP_NULL_AUTHENTICATION) {
-                    newL = L - T > 0 ? L - T : 0;
-                    a.w_len[p] = (uint32_t)newL;
-                    bool ok;
-                    if ((uint32_t)g == a.g0[p]) {
-                        ok = a.auth_ok[p] != 0;
-                    } else {
-                        ok = reverify_rtp(a, ks, p, L, g);
-                        atomicAdd(&a.ctl->n_mismatch, 1u);
-                    }
-                    if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; continue; }
-                }
-                if (enc == SRTP_AESCM_ENCRYPTION && !(rec.p & kRecSkipDec))
-                    threw = ctr_would_throw(rec.h, newL - rec.h);
-            } else {
-                if (enc == SRTP_AESCM_ENCRYPTION) threw = ctr_would_throw(rec.h, L - rec.h);
-                if (!threw && auth != SRTP_NULL_AUTHENTICATION) newL = L + T;
-            }
-            if (!threw) {
-                a.w_cw[p] = (uint32_t)g;
-                a.w_len[p] = (uint32_t)newL;
-                // update :719-744
-                if (delta > 0) {
-                    st.window = (uint64_t)java_lshl((int64_t)st.window, delta) | 1ull;
-                } else {
-                    st.window |= (uint64_t)(int64_t)java_ishl1((int32_t)(-delta));
-                }
-                if (g == st.a) {
-                    if (seq > st.b) st.b = seq & 0xffff;
-                } else if (g == (int32_t)((uint32_t)st.a + 1u)) {
-                    st.b = seq & 0xffff;
-                    st.a = g;
-                }
-            }
-        } else if (!a.reverse) {
-            // SRTCPCryptoContext.transformPacket :391-427
-            const int trailer = (auth != SRTP_NULL_AUTHENTICATION) ? 4 + T : 0;
-            if (L + trailer > C) { a.w_status[p] = SRTP_STATUS_ERR_CAPACITY; continue; }
-            a.w_cw[p] = (uint32_t)st.a;
-            a.w_len[p] = (uint32_t)(L + trailer);
-            st.a = (int32_t)(((uint32_t)st.a + 1u) & 0x7FFFFFFFu);
-        } else {
-            // SRTCPCryptoContext.reverseTransformPacket :315-374
-            const int io = L - 4 - T;
-            if (io < 0) {
-                threw = true;
-            } else {
-                uint32_t word = rec.word;
-                if (rec.h != T) word = ld_be32(a.seg + a.off[p] + io);
-                const int32_t index = (int32_t)(word & 0x7FFFFFFFu);
-                const bool decrypt = (word & 0x80000000u) != 0;
-                const int64_t delta = (int64_t)(int32_t)((uint32_t)index - (uint32_t)st.b);
-                bool replay_ok = true; // SRTCP checkReplay (:106-120) is not config-gated
-                if (delta <= 0) {
-                    if (-delta > 64) replay_ok = false;
-                    else if (((uint64_t)st.window >> ((-delta) & 63)) & 1u) replay_ok = false;
-                }
-                if (!replay_ok) { a.w_status[p] = SRTP_STATUS_DROP_REPLAY; continue; }
-                int newL = L;
-                if (auth != SRTP_NULL_AUTHENTICATION) {
-                    newL = L - T - 4 > 0 ? L - T - 4 : 0;
-                    a.w_len[p] = (uint32_t)newL;
-                    if (!a.auth_ok[p]) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; continue; }
-                }
-                if (decrypt && enc == SRTP_AESCM_ENCRYPTION && newL - 8 < 0) threw = true;
-                if (!threw) {
-                    a.w_cw[p] = word;
-                    // update :435-451 (reversed delta)
-                    const int32_t d2 = (int32_t)((uint32_t)st.b - (uint32_t)index);
-                    if (d2 > 0) st.window = (uint64_t)java_lshl((int64_t)st.window, d2) | 1ull;
-                    else st.window |= (uint64_t)(int64_t)java_ishl1(d2);
-                    st.b = index;
+    // Scratch arrays carry 8 entries of slack, so the batch loads never leave them.
+    bool live = true;
+    for (uint32_t j = i; live; j += 4) {
+        WalkRec r[4];
+        uint32_t g0[4] = {0, 0, 0, 0}, ok[4] = {0, 0, 0, 0};
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool mine = (j + q < a.n) && a.sk_out[j + q] == key;
+            r[q] = a.sv_out[j + q];
+            cnt += (mine && cnt == q) ? 1 : 0;
+        }
+        if (need_auth) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (q < cnt) {
+                    const uint32_t p = r[q].p & kRecIdxMask;
+                    if (c.kind == SRTP_KIND_RTP) g0[q] = a.g0[p];
+                    ok[q] = a.auth_ok[p];
                 }
             }
         }
-        if (threw) {
-            a.w_status[p] = SRTP_STATUS_ERR_MALFORMED;
-            if (a.abort_on_error) {
-                if (dry) atomicMin(&a.e_min[tid], (int32_t)p);
-                break; // the rest of this transformer's array is aborted
-            }
-            continue;
+#pragma unroll 1
+        for (int q = 0; q < cnt; q++) {
+            if (limit_pass && (int32_t)(r[0].p & kRecIdxMask) > E) { live = false; break; }
+            if (!walk_one(a, ks, c, st, r[0], g0[0], ok[0], dry, tid)) { live = false; break; }
+#pragma unroll
+            for (int k = 0; k < 3; k++) { r[k] = r[k + 1]; g0[k] = g0[k + 1]; ok[k] = ok[k + 1]; }
         }
-        a.w_status[p] = SRTP_STATUS_OK;
+        if (cnt < 4) break;
     }
     if (dry) return; // first of two passes: state is committed by the limit pass
     if (limit_pass && st.birth == a.serial && (int32_t)first_p > E) {
