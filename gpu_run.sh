@@ -21,6 +21,12 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --steps 20 --warmup 3
 fi
+if [ "$MODE" = one ]; then
+  step pytest_one 600 python -m pytest tests -m gpu -q -x --timeout 300 -p no:cacheprovider -k "${2:-malformed}"
+fi
+if [ "$MODE" = diag2 ]; then
+  step diag2 300 python tools_diag2.py
+fi
 if [ "$MODE" = diag ]; then
   step diag 600 python tools_diag.py
 fi

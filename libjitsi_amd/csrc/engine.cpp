@@ -41,6 +41,7 @@ struct srtp_engine {
     WalkRec *sv_in = nullptr, *sv_out = nullptr;
     int32_t *w_status = nullptr;
     uint32_t *w_cw = nullptr, *w_len = nullptr, *g0 = nullptr, *auth_ok = nullptr, *mid = nullptr;
+    uint32_t *tailc = nullptr, *spec = nullptr;
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     int32_t *e_min = nullptr;
@@ -127,12 +128,12 @@ uint32_t next_pow2(uint64_t x) {
 
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
-                    e->w_len, e->g0, e->auth_ok, e->mid, e->sort_temp};
+                    e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
     e->w_status = nullptr;
-    e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = nullptr;
+    e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
     e->sort_temp = nullptr;
     e->scratch_n = 0;
 }
@@ -152,6 +153,8 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->g0, m));
     HIPCHK(e, dalloc(&e->auth_ok, m));
     HIPCHK(e, dalloc(&e->mid, (size_t)5 * m));
+    HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
+    HIPCHK(e, dalloc(&e->spec, m));
     e->sort_temp_bytes = sort_temp_bytes(m);
     HIPCHK(e, hipMalloc(&e->sort_temp, std::max<size_t>(e->sort_temp_bytes, 16)));
     e->scratch_n = m;
@@ -414,6 +417,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
     a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
+    a.tailc = e->tailc; a.spec = e->spec;
     a.e_min = e->e_min; a.ctl = e->ctl;
     HIPCHK(e, hipMemsetAsync(e->ctl, 0, sizeof(BundleCtl), s));
     if (a.abort_on_error)
@@ -428,7 +432,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);
-        HIPCHK(e, launch_verify(a, s));
+        HIPCHK(e, launch_unprotect(a, s));
     }
     {
         StageTimer t(e, s, SRTP_STAGE_WALK);
@@ -437,7 +441,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
-        HIPCHK(e, launch_decrypt(a, s));
+        HIPCHK(e, launch_unprotect_fix(a, s));
     } else {
         StageTimer t(e, s, SRTP_STAGE_PROTECT);
         HIPCHK(e, launch_protect(a, s));

@@ -42,6 +42,8 @@ struct BundleArgs {
     uint32_t *g0;          // [n] unprotect: ROC the verify pass assumed
     uint32_t *auth_ok;     // [n] unprotect: tag matched under g0
     uint32_t *mid;         // [5n] unprotect: inner SHA-1 state before the ROC block
+    uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
+    uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl;
 };
@@ -50,10 +52,12 @@ hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n_max);
 hipError_t launch_sort(const BundleArgs &a, void *temp, size_t temp_bytes, int end_bit,
                        hipStream_t s);
-hipError_t launch_verify(const BundleArgs &a, hipStream_t s);
+// unprotect: fused tag check + speculative in-place decryption (before the walk)
+hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s);
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
-hipError_t launch_decrypt(const BundleArgs &a, hipStream_t s);
+// unprotect: statuses/lengths out; undo/redo the rare speculation misses (after the walk)
+hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 hipError_t launch_remove_transformer(uint64_t *ctx_keys, CtxState *ctx, uint32_t cap,
                                      uint32_t tid, hipStream_t s);
 hipError_t launch_count_contexts(const uint64_t *ctx_keys, uint32_t cap, unsigned long long *out,

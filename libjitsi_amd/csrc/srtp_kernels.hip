@@ -6,9 +6,10 @@
 //              (SRTPTransformer.getContext :152-175, lazily derived contexts),
 //              emits a 16-B walk record keyed by slot.
 //   radix sort (hipcub) by slot, stable -> each context's packets in array order.
-//   k_verify   [unprotect] one lane per packet: HMAC-SHA1 tag check under the ROC
-//              guessed from the context state at bundle start; keeps the inner
-//              SHA-1 midstate before the ROC-carrying block.
+//   k_unprotect [unprotect] one lane per packet: HMAC-SHA1 tag check and
+//              speculative in-place AES-CM decryption under the ROC guessed from
+//              the context state at bundle start; keeps the inner SHA-1 midstate
+//              and ciphertext of the ROC-carrying block for re-checks.
 //   k_walk     one lane per context segment: the serial integer state machine of
 //              SRTPCryptoContext (guessIndex :457-475, checkReplay :279-323,
 //              update :719-744) / SRTCPCryptoContext (:106-120, :435-451), in
@@ -16,7 +17,8 @@
 //              "limit" pass reproduces SinglePacketTransformer's abort-on-throw.
 //   k_protect  [protect] one lane per packet: fused AES-CM keystream + XOR +
 //              HMAC-SHA1 (one read and one write of the packet bytes).
-//   k_decrypt  [unprotect] one lane per packet: AES-CM over accepted packets.
+//   k_unprotect_fix [unprotect] statuses/lengths out; undoes/redoes the rare
+//              packets whose speculation the walk overturned.
 //
 // AES uses one little-endian T-table, replicated 32x in LDS so that lane l
 // only ever touches LDS bank (l & 31): 32 KB, conflict-free ds_read_b32.
@@ -477,82 +479,6 @@ __device__ __forceinline__ void load_round_keys_uniform(const KeySet *__restrict
     }
 }
 
-// ============================================================== k_verify
-// Unprotect, one lane per packet: tag check of SRTPCryptoContext.authenticatePacket
-// (:237-266) / SRTCPCryptoContext (:333-353) under the ROC guessed from the
-// context state at bundle start (exact unless the bundle itself moves s_l by
-// more than 2^15 or forged packets change the guess; k_walk re-checks those).
-__device__ __forceinline__ void verify_one(const BundleArgs &a, const KeySet *__restrict__ ks,
-                                           uint32_t p, const CtxState &st) {
-    const int L = (int)a.len[p];
-    const int T = ks->tag_len;
-    const uint8_t *pkt = a.seg + a.off[p];
-    int mac_len;
-    uint32_t suffix;
-    const bool rtp = ks->kind == SRTP_KIND_RTP;
-    if (rtp) {
-        const int32_t seq = (int32_t)((pkt[2] << 8) | pkt[3]);
-        int32_t g = st.a;
-        if (st.flags & 1u) { // guessIndex :457-475
-            const int32_t s_l = st.b;
-            if (s_l < 32768) g = (seq - s_l > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
-            else g = (s_l - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
-        }
-        a.g0[p] = (uint32_t)g;
-        mac_len = L - T;
-        suffix = (uint32_t)g;
-    } else {
-        const int io = L - 4 - T;
-        if (io < 0) return; // the reference throws here (k_walk)
-        suffix = ld_be32(pkt + io);
-        mac_len = io;
-    }
-    if (mac_len < 0) mac_len = 0;
-    uint32_t h[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
-    const int nb_full = mac_len >> 6;
-    const int nb_data = (mac_len + 63) >> 6;
-    const int nb_inner = ((mac_len + 12) >> 6) + 1;
-    for (int b = 0; b <= nb_inner; b++) {
-        uint32_t w[16];
-        if (b < nb_data) {
-            const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (64 * b + 16 * m < mac_len) v = qp[m];
-                w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; k++) w[k] = 0u;
-        }
-        if (b == nb_full && rtp) { // midstate before the ROC-carrying block
-            uint32_t *mp = a.mid + 5 * (size_t)p;
-#pragma unroll
-            for (int k = 0; k < 5; k++) mp[k] = h[k];
-        }
-        if (b < nb_inner) {
-            inner_words(w, b, mac_len, suffix);
-        } else {
-            outer_words(w, h, ks);
-        }
-        sha1_compress(h, w);
-    }
-    a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(kBlock, 4) void k_verify(BundleArgs a) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.n) return;
-    const uint32_t slot = a.p_slot[p];
-    if (slot == kNoSlot) return;
-    const CtxState st = a.ctx[slot];
-    const bool todo = a.keysets[st.ks].auth_type != SRTP_NULL_AUTHENTICATION;
-    for_each_keyset(todo, st.ks, [&](uint32_t ks_u) { verify_one(a, a.keysets + ks_u, p, st); });
-}
-
 // Re-check one SRTP tag under another ROC from the verify pass's midstate
 // (only the block(s) carrying the ROC are re-hashed).
 __device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks, uint32_t p, int L,
@@ -566,12 +492,16 @@ __device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks,
     for (int k = 0; k < 5; k++) h[k] = a.mid[5 * (size_t)p + k];
     const int nb_full = mac_len >> 6;
     const int nb_inner = ((mac_len + 12) >> 6) + 1;
+    const bool sp = a.spec[p] != 0; // packet now holds plaintext: use the saved ciphertext
     for (int b = nb_full; b <= nb_inner; b++) {
         uint32_t w[16];
+        const uint4 *src = (sp && b == nb_full)
+                               ? reinterpret_cast<const uint4 *>(a.tailc + 16 * (size_t)p)
+                               : reinterpret_cast<const uint4 *>(pkt + 64 * b);
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (64 * b + 16 * m < mac_len) v = reinterpret_cast<const uint4 *>(pkt + 64 * b)[m];
+            if (64 * b + 16 * m < mac_len) v = src[m];
             w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
         }
         if (b < nb_inner) {
@@ -787,19 +717,19 @@ __device__ __forceinline__ int32_t finish_status(const BundleArgs &a, uint32_t p
 __device__ __forceinline__ void make_iv_rtp(const KeySet *ks, const uint4 &hdr, uint32_t roc,
                                             uint32_t iv[4]) {
     // processPacketAESCM :482-525: salt ^ (0, SSRC, ROC, SEQ, 0)
-    iv[0] = sgpr(ks->salt[0]);
-    iv[1] = sgpr(ks->salt[1]) ^ hdr.z;        // bytes 8..11 = SSRC (BE in memory)
-    iv[2] = sgpr(ks->salt[2]) ^ bswap(roc);
-    iv[3] = sgpr(ks->salt[3]) ^ (hdr.x >> 16); // bytes 2..3 = SEQ
+    iv[0] = ks->salt[0];
+    iv[1] = ks->salt[1] ^ hdr.z;        // bytes 8..11 = SSRC (BE in memory)
+    iv[2] = ks->salt[2] ^ bswap(roc);
+    iv[3] = ks->salt[3] ^ (hdr.x >> 16); // bytes 2..3 = SEQ
 }
 
 __device__ __forceinline__ void make_iv_rtcp(const KeySet *ks, const uint4 &hdr, uint32_t index,
                                              uint32_t iv[4]) {
     // SRTCPCryptoContext.processPacketAESCM :218-260: salt ^ (0, SSRC, 0, index, 0)
-    iv[0] = sgpr(ks->salt[0]);
-    iv[1] = sgpr(ks->salt[1]) ^ hdr.y;        // bytes 4..7 = RTCP SSRC
-    iv[2] = sgpr(ks->salt[2]) ^ ((((index >> 24) & 0xffu) << 16) | (((index >> 16) & 0xffu) << 24));
-    iv[3] = sgpr(ks->salt[3]) ^ (((index >> 8) & 0xffu) | ((index & 0xffu) << 8));
+    iv[0] = ks->salt[0];
+    iv[1] = ks->salt[1] ^ hdr.y;        // bytes 4..7 = RTCP SSRC
+    iv[2] = ks->salt[2] ^ ((((index >> 24) & 0xffu) << 16) | (((index >> 16) & 0xffu) << 24));
+    iv[3] = ks->salt[3] ^ (((index >> 8) & 0xffu) | ((index & 0xffu) << 8));
 }
 
 // ============================================================== k_protect
@@ -892,67 +822,229 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { protect_one(a, a.keysets + ks_u, lds, tb, p); });
 }
 
-// ============================================================== k_decrypt
-// AES-CM decryption of accepted packets (SRTPCryptoContext :609-627,
-// SRTCPCryptoContext :355-370).
-__device__ __forceinline__ void decrypt_one(const BundleArgs &a, const KeySet *__restrict__ ks,
-                                            const char *__restrict__ lds, const TeBase &tb,
-                                            uint32_t p) {
+// ============================================================== k_unprotect
+// Unprotect, one lane per packet, before the walk: HMAC-SHA1 over the
+// ciphertext (SRTPCryptoContext.authenticatePacket :237-266 /
+// SRTCPCryptoContext :333-353) and, in the same pass, speculative in-place
+// AES-CM decryption (:609-627 / :355-370) under the ROC guessed from the
+// context state at bundle start.  Keeps the inner SHA-1 midstate before the
+// ROC-carrying block and that block's ciphertext, so the walk can re-check a
+// tag under another ROC cheaply; k_unprotect_fix repairs the rare packets the
+// walk rejects or guesses differently.
+__device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
+                                              const char *__restrict__ lds, const TeBase &tb,
+                                              uint32_t p, const CtxState &st) {
     uint8_t *pkt = a.seg + a.off[p];
+    const int L = (int)a.len[p];
+    const int T = (int)sgpr(ks->tag_len);
+    const bool rtp = sgpr(ks->kind) == SRTP_KIND_RTP;
+    const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    const bool aes = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
-    const uint32_t cw = a.w_cw[p];
     Ctr cs;
-    if (sgpr(ks->kind) == SRTP_KIND_RTP) {
-        cs.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-        make_iv_rtp(ks, hdr, cw, cs.iv);
+    int end;       // bytes covered by the MAC and the decryption: [0, end) / [off, end)
+    uint32_t suffix;
+    bool spec = false;
+    if (rtp) {
+        const int32_t seq = (int32_t)(bswap(hdr.x) & 0xffffu);
+        int32_t g = st.a;
+        if (st.flags & 1u) { // guessIndex :457-475 on the bundle-start state
+            const int32_t s_l = st.b;
+            if (s_l < 32768) g = (seq - s_l > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
+            else g = (s_l - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
+        }
+        a.g0[p] = (uint32_t)g;
+        end = do_mac ? (L - T > 0 ? L - T : 0) : L;
+        suffix = (uint32_t)g;
+        const uint32_t fl = a.flags ? a.flags[p] : 0u;
+        if (aes && !(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE))) {
+            cs.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+            // Speculate only when the header fields the IV and the header length
+            // are read from (SSRC, SEQ, CC, X, extension length) lie before the
+            // decrypted region; a negative extension length can put them inside
+            // it, and k_unprotect_fix must then still see the original bytes.
+            const uint32_t b0 = hdr.x & 0xffu;
+            const int fixed = 12 + 4 * (int)(b0 & 0x0fu) + ((b0 & 0x10u) ? 4 : 0);
+            spec = cs.off >= fixed && !ctr_would_throw(cs.off, end - cs.off) && end - cs.off > 0;
+            if (spec) make_iv_rtp(ks, hdr, (uint32_t)g, cs.iv);
+        }
     } else {
-        cs.off = 8;
-        make_iv_rtcp(ks, hdr, cw & 0x7FFFFFFFu, cs.iv);
+        const int io = L - 4 - T;
+        if (io < 0) { a.spec[p] = 0u; return; } // the reference throws here (k_walk)
+        suffix = ld_be32(pkt + io);
+        end = do_mac ? (io > 0 ? io : 0) : L;
+        if (aes && (suffix & 0x80000000u) && end - 8 > 0) {
+            cs.off = 8;
+            make_iv_rtcp(ks, hdr, suffix & 0x7FFFFFFFu, cs.iv);
+            spec = true;
+        }
     }
-    cs.end = (int)a.w_len[p];
-    if (cs.end - cs.off <= 0) return;
+    a.spec[p] = spec ? 1u : 0u;
+    if (!do_mac && !spec) return;
+    cs.end = end;
 #pragma unroll
     for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
     RoundKeys rk;
-    load_round_keys_uniform(ks, rk);
-    for (int c = cs.off >> 6; 64 * c < cs.end; c++) {
-        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * c);
-        uint32_t w[16];
+    if (spec) load_round_keys_uniform(ks, rk);
+    uint32_t h[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
+    const int nb_full = end >> 6;
+    const int nb_data = (end + 63) >> 6;
+    const int nb_inner = ((end + 12) >> 6) + 1;
+    const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
+    for (int b = 0; b < n_blocks; b++) {
+        uint32_t d[16];
+        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
 #pragma unroll
         for (int m = 0; m < 4; m++) {
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (64 * c + 16 * m < cs.end) v = qp[m];
-            w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+            if (b < nb_data && 64 * b + 16 * m < end) v = qp[m];
+            d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
         }
-        ctr_chunk(lds, tb, rk, cs, c, w);
+        if (do_mac) {
+            if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
+                uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
-        for (int m = 0; m < 4; m++)
-            if (64 * c + 16 * m < cs.end && 64 * c + 16 * m + 16 > cs.off)
-                qp[m] = make_uint4(w[4 * m], w[4 * m + 1], w[4 * m + 2], w[4 * m + 3]);
+                for (int k = 0; k < 5; k++) mp[k] = h[k];
+                if (spec) {
+                    uint4 *tp = reinterpret_cast<uint4 *>(a.tailc + 16 * (size_t)p);
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+                        tp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+                }
+            }
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = d[k];
+            if (b < nb_inner) inner_words(w, b, end, suffix);
+            else outer_words(w, h, ks);
+            sha1_compress(h, w);
+        }
+        if (spec && b < nb_data && 64 * b + 64 > cs.off) {
+            if (do_mac) {
+                // re-read the chunk (L1/L2-hot) rather than keep 16 words live across SHA-1
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    uint4 v = make_uint4(0, 0, 0, 0);
+                    if (64 * b + 16 * m < end) v = qp[m];
+                    d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
+                }
+            }
+            ctr_chunk(lds, tb, rk, cs, b, d);
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+                if (64 * b + 16 * m < end && 64 * b + 16 * m + 16 > cs.off)
+                    qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+        }
     }
+    if (do_mac) a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(kAesBlock) void k_decrypt(BundleArgs a) {
+__global__ __launch_bounds__(kAesBlock) void k_unprotect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords];
     fill_te4(s_te);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
-    bool todo = finish_status(a, p) == SRTP_STATUS_OK;
-    uint32_t ks_id = 0;
-    if (todo) {
-        ks_id = a.ctx[a.p_slot[p]].ks;
-        const KeySet *ks = a.keysets + ks_id;
-        if (ks->enc_type != SRTP_AESCM_ENCRYPTION) todo = false;
-        else if (ks->kind == SRTP_KIND_RTP) {
-            const uint32_t fl = a.flags ? a.flags[p] : 0u;
-            if (fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) todo = false; // :609-611
-        } else if (!(a.w_cw[p] & 0x80000000u)) {
-            todo = false; // E flag clear: sent unencrypted
-        }
-    }
+    const uint32_t slot = a.p_slot[p];
+    const bool todo = slot != kNoSlot;
+    CtxState st = {};
+    if (todo) st = a.ctx[slot];
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
-    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { decrypt_one(a, a.keysets + ks_u, lds, tb, p); });
+    for_each_keyset(todo, st.ks, [&](uint32_t ks_u) { unprotect_one(a, a.keysets + ks_u, lds, tb, p, st); });
+}
+
+// ============================================================== k_unprotect_fix
+// AES-128 with the T-table read from global memory (rare repair path only).
+__device__ void aes_encrypt_global(const KeySet *ks, uint32_t s[4]) {
+    uint32_t x0 = s[0] ^ ks->rk[0], x1 = s[1] ^ ks->rk[1], x2 = s[2] ^ ks->rk[2], x3 = s[3] ^ ks->rk[3];
+#pragma unroll 1
+    for (int r = 1; r < 10; r++) {
+        const uint32_t t0 = d_te0[x0 & 0xff] ^ rotl(d_te0[(x1 >> 8) & 0xff], 8) ^
+                            rotl(d_te0[(x2 >> 16) & 0xff], 16) ^ rotl(d_te0[x3 >> 24], 24) ^ ks->rk[4 * r];
+        const uint32_t t1 = d_te0[x1 & 0xff] ^ rotl(d_te0[(x2 >> 8) & 0xff], 8) ^
+                            rotl(d_te0[(x3 >> 16) & 0xff], 16) ^ rotl(d_te0[x0 >> 24], 24) ^ ks->rk[4 * r + 1];
+        const uint32_t t2 = d_te0[x2 & 0xff] ^ rotl(d_te0[(x3 >> 8) & 0xff], 8) ^
+                            rotl(d_te0[(x0 >> 16) & 0xff], 16) ^ rotl(d_te0[x1 >> 24], 24) ^ ks->rk[4 * r + 2];
+        const uint32_t t3 = d_te0[x3 & 0xff] ^ rotl(d_te0[(x0 >> 8) & 0xff], 8) ^
+                            rotl(d_te0[(x1 >> 16) & 0xff], 16) ^ rotl(d_te0[x2 >> 24], 24) ^ ks->rk[4 * r + 3];
+        x0 = t0; x1 = t1; x2 = t2; x3 = t3;
+    }
+#define SB(x) ((d_te0[(x)] >> 8) & 0xffu)
+    s[0] = (SB(x0 & 0xff) | (SB((x1 >> 8) & 0xff) << 8) | (SB((x2 >> 16) & 0xff) << 16) | (SB(x3 >> 24) << 24)) ^ ks->rk[40];
+    s[1] = (SB(x1 & 0xff) | (SB((x2 >> 8) & 0xff) << 8) | (SB((x3 >> 16) & 0xff) << 16) | (SB(x0 >> 24) << 24)) ^ ks->rk[41];
+    s[2] = (SB(x2 & 0xff) | (SB((x3 >> 8) & 0xff) << 8) | (SB((x0 >> 16) & 0xff) << 16) | (SB(x1 >> 24) << 24)) ^ ks->rk[42];
+    s[3] = (SB(x3 & 0xff) | (SB((x0 >> 8) & 0xff) << 8) | (SB((x1 >> 16) & 0xff) << 16) | (SB(x2 >> 24) << 24)) ^ ks->rk[43];
+#undef SB
+}
+
+// XOR AES-CM keystream(s) for IV(s) into packet bytes [off, end), 4-B words.
+__device__ void ctr_xor_global(const KeySet *ks, uint8_t *pkt, int off, int end, const uint32_t *iv_a,
+                               const uint32_t *iv_b) {
+    for (int j = 0; off + 16 * j < end; j++) {
+        uint32_t ka[4] = {0, 0, 0, 0}, kb[4] = {0, 0, 0, 0};
+        if (iv_a) {
+            ctr_input(iv_a, j, ka);
+            aes_encrypt_global(ks, ka);
+        }
+        if (iv_b) {
+            ctr_input(iv_b, j, kb);
+            aes_encrypt_global(ks, kb);
+        }
+        for (int k = 0; k < 4; k++) {
+            const int pos = off + 16 * j + 4 * k;
+            if (pos >= end) break;
+            const uint32_t ksw = ka[k] ^ kb[k];
+            for (int i = 0; i < 4 && pos + i < end; i++) pkt[pos + i] ^= (uint8_t)(ksw >> (8 * i));
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_unprotect_fix(BundleArgs a) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const int L0 = (int)a.len[p];
+    const int32_t st = finish_status(a, p);
+    const uint32_t slot = a.p_slot[p];
+    if (slot == kNoSlot) return;
+    const uint32_t did = a.spec[p];
+    const KeySet *ks = a.keysets + a.ctx[slot].ks;
+    const bool rtp = ks->kind == SRTP_KIND_RTP;
+    bool need = false;
+    if (st == SRTP_STATUS_OK && ks->enc_type == SRTP_AESCM_ENCRYPTION) {
+        if (rtp) {
+            const uint32_t fl = a.flags ? a.flags[p] : 0u;
+            need = !(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
+        } else {
+            need = (a.w_cw[p] & 0x80000000u) != 0;
+        }
+    }
+    if (!did && !need) return;
+    if (did && need && (!rtp || a.g0[p] == a.w_cw[p])) return; // speculation was right
+    // rare: undo the speculative keystream and/or apply the walk's
+    uint8_t *pkt = a.seg + a.off[p];
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const int T = ks->tag_len;
+    const bool mac = ks->auth_type != SRTP_NULL_AUTHENTICATION;
+    uint32_t iv_spec[4], iv_real[4];
+    int off, end;
+    if (rtp) {
+        off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        end = mac ? (L0 - T > 0 ? L0 - T : 0) : L0;
+        make_iv_rtp(ks, hdr, a.g0[p], iv_spec);
+        make_iv_rtp(ks, hdr, a.w_cw[p], iv_real);
+    } else {
+        off = 8;
+        end = mac ? (L0 - T - 4 > 0 ? L0 - T - 4 : 0) : L0;
+        const uint32_t idx = (a.w_cw[p] & 0x7FFFFFFFu);
+        const uint32_t sidx = ld_be32(pkt + L0 - 4 - T) & 0x7FFFFFFFu;
+        make_iv_rtcp(ks, hdr, sidx, iv_spec);
+        make_iv_rtcp(ks, hdr, idx, iv_real);
+    }
+    ctr_xor_global(ks, pkt, off, end, did ? iv_spec : nullptr, need ? iv_real : nullptr);
+    atomicAdd(&a.ctl->n_walk, 1u); // repaired packets (diagnostic)
 }
 
 // ============================================================== maintenance
@@ -981,8 +1073,8 @@ hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_parse, grid_for(a.n), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_verify(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_verify, grid_for(a.n), dim3(kBlock), 0, s, a);
+hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_unprotect, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
@@ -993,8 +1085,8 @@ hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_protect, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_decrypt(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_decrypt, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
+hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_unprotect_fix, grid_for(a.n), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,

@@ -90,8 +90,13 @@ class Twin:
         if not np.array_equal(seg_o, seg_e):
             diff = np.nonzero(seg_o != seg_e)[0]
             pk = np.searchsorted(off.astype(np.int64), diff[:5], side="right") - 1
-            raise AssertionError(f"segment bytes differ at {diff[:5].tolist()} (packets {pk.tolist()}, "
-                                 f"status {st_o[pk].tolist()}); {len(diff)} bytes in total")
+            p0 = int(pk[0])
+            o0, c0 = int(off[p0]), int(cap[p0])
+            raise AssertionError(
+                f"segment bytes differ at {diff[:5].tolist()} (packets {pk.tolist()}, status "
+                f"{st_o[pk].tolist()}); {len(diff)} bytes in total; reverse={reverse}; packet {p0} "
+                f"len in {int(length[p0])} out {int(len_o[p0])}\n in  {seg[o0:o0 + c0].tobytes().hex()}"
+                f"\n ora {seg_o[o0:o0 + c0].tobytes().hex()}\n eng {seg_e[o0:o0 + c0].tobytes().hex()}")
         if check_state:
             self.check_states(per_pkt, seg, off, length)
         return seg_e, len_e, st_e

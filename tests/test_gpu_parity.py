@@ -283,6 +283,28 @@ def twin_check_replay_sequences(twin, snd, rcv, b):
         sub = synth.select(b, np.array([i]))
 
 
+def test_roc_guess_overturned_by_walk(twin):
+    """Bundles whose in-bundle updates move s_l across the 2^15 guess
+    thresholds: the ROC the verify/speculative-decrypt pass guessed from the
+    bundle-start state (-1 for seq 60000, 0 for seq 10) differs from the walk's
+    (0, 1), forcing the midstate re-check and the fix-up re-decryption."""
+    (k, s), = synth.keys(31, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    for seqs in ([100], [30000, 60000, 10, 20, 40000, 70, 33000], [65000, 1000, 34000]):
+        b = synth.rtp_bundle(len(seqs), 1, 333, seed=len(seqs))
+        set_seqs(b, seqs)
+        seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+        seg2, ln2, st2 = twin.run(rcv, True, seg, b.off, ln, b.cap)
+        assert (st2 == st).all()
+
+
+def set_seqs(b, seqs):
+    for i, q in enumerate(seqs):
+        b.seg[b.off[i] + 2] = q >> 8
+        b.seg[b.off[i] + 3] = q & 0xFF
+
+
 def test_check_replay_disabled(engine_factory, oracle):
     eng = engine_factory(check_replay=False, max_contexts=1024, max_factories=64,
                          max_transformers=64)
