@@ -30,6 +30,9 @@ fi
 if [ "$MODE" = diag ]; then
   step diag 600 python tools_diag.py
 fi
+if [ "$MODE" = micro ] || [ "$MODE" = prof ]; then
+  step sort_bench 120 ./tools/sort_bench
+fi
 if [ "$MODE" = prof ]; then
   export TMPDIR=/tmp
   B="python3 bench.py --steps 5 --warmup 1 --no-cpu"

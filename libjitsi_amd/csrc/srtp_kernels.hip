@@ -20,9 +20,11 @@
 //   k_unprotect_fix [unprotect] statuses/lengths out; undoes/redoes the rare
 //              packets whose speculation the walk overturned.
 //
-// AES uses one little-endian T-table, replicated 32x in LDS so that lane l
-// only ever touches LDS bank (l & 31): 32 KB, conflict-free ds_read_b32.
-// Round keys live in VGPRs, SHA-1 runs per lane with v_alignbit rotates.
+// AES uses four little-endian T-tables replicated 32x in LDS (128 KB) so that
+// lane l only ever touches LDS bank (l & 31): conflict-free ds_read_b32 with a
+// single v_perm_b32 per lookup address and v_bitop3 XORs.  Round keys, salt
+// and HMAC midstates are wave-uniform SGPRs; SHA-1 runs per lane with
+// v_alignbit rotates.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -481,22 +483,26 @@ __device__ __forceinline__ void load_round_keys_uniform(const KeySet *__restrict
 
 // Re-check one SRTP tag under another ROC from the verify pass's midstate
 // (only the block(s) carrying the ROC are re-hashed).
-__device__ __noinline__ bool reverify_rtp(const BundleArgs &a, const KeySet *ks, uint32_t p, int L,
-                                          int32_t g) {
+struct ReverifyArgs { // by value: keeps the kernel arguments out of scratch
+    const uint8_t *pkt;
+    const uint32_t *mid;   // 5 words
+    const uint32_t *tailc; // 16 words, or null when the packet still holds ciphertext
+};
+
+__device__ __noinline__ bool reverify_rtp(ReverifyArgs r, const KeySet *ks, int L, int32_t g) {
     const int T = ks->tag_len;
     int mac_len = L - T;
     if (mac_len < 0) mac_len = 0;
-    const uint8_t *pkt = a.seg + a.off[p];
+    const uint8_t *pkt = r.pkt;
     uint32_t h[5];
 #pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = a.mid[5 * (size_t)p + k];
+    for (int k = 0; k < 5; k++) h[k] = r.mid[k];
     const int nb_full = mac_len >> 6;
     const int nb_inner = ((mac_len + 12) >> 6) + 1;
-    const bool sp = a.spec[p] != 0; // packet now holds plaintext: use the saved ciphertext
     for (int b = nb_full; b <= nb_inner; b++) {
         uint32_t w[16];
-        const uint4 *src = (sp && b == nb_full)
-                               ? reinterpret_cast<const uint4 *>(a.tailc + 16 * (size_t)p)
+        const uint4 *src = (r.tailc && b == nb_full) // packet holds plaintext: saved ciphertext
+                               ? reinterpret_cast<const uint4 *>(r.tailc)
                                : reinterpret_cast<const uint4 *>(pkt + 64 * b);
 #pragma unroll
         for (int m = 0; m < 4; m++) {
@@ -563,7 +569,11 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                 if ((uint32_t)g == g0) {
                     ok = auth_ok != 0;
                 } else {
-                    ok = reverify_rtp(a, ks, p, L, g);
+                    ReverifyArgs rv;
+                    rv.pkt = a.seg + a.off[p];
+                    rv.mid = a.mid + 5 * (size_t)p;
+                    rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
+                    ok = reverify_rtp(rv, ks, L, g);
                     atomicAdd(&a.ctl->n_mismatch, 1u);
                 }
                 if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
