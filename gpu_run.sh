@@ -33,6 +33,13 @@ fi
 if [ "$MODE" = micro ] || [ "$MODE" = prof ]; then
   step sort_bench 120 ./tools/sort_bench
 fi
+if [ "$MODE" = micro ]; then
+  export TMPDIR=/tmp
+  step calib 120 ./tools/pmc_calib
+  step calib_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/calib/trace -o run -- ./tools/pmc_calib
+  step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib/fetch -o run -- ./tools/pmc_calib
+  step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib/write -o run -- ./tools/pmc_calib
+fi
 if [ "$MODE" = prof ]; then
   export TMPDIR=/tmp
   B="python3 bench.py --steps 5 --warmup 1 --no-cpu"

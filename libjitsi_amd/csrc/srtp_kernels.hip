@@ -26,7 +26,9 @@
 // and HMAC midstates are wave-uniform SGPRs; SHA-1 runs per lane with
 // v_alignbit rotates.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+#include <rocprim/rocprim.hpp>
 
 #include "../../include/srtp_mi355x.h"
 #include "srtp_kernels.h"
@@ -217,6 +219,114 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
         e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// ------------------------------------------------- fused AES-CM + SHA-1 step
+// One SHA-1 round t (compile-time after unrolling) on working state v[0..4].
+template <int t>
+__device__ __forceinline__ void sha1_round(uint32_t v[5], uint32_t w[16]) {
+    uint32_t wt;
+    if (t < 16) {
+        wt = w[t];
+    } else {
+        wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+        w[t & 15] = wt;
+    }
+    const uint32_t b = v[1], c = v[2], d = v[3];
+    uint32_t f, k;
+    if (t < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
+    else if (t < 40) { f = xor3(b, c, d); k = 0x6ED9EBA1u; }
+    else if (t < 60) { f = (b & c) | (d & (b | c)); k = 0x8F1BBCDCu; }
+    else { f = xor3(b, c, d); k = 0xCA62C1D6u; }
+    const uint32_t tmp = rotl(v[0], 5) + f + v[4] + k + wt;
+    v[4] = d; v[3] = c; v[2] = rotl(b, 30); v[1] = v[0]; v[0] = tmp;
+}
+
+template <int t0>
+__device__ __forceinline__ void sha1_rounds4(uint32_t v[5], uint32_t w[16]) {
+    sha1_round<t0>(v, w); sha1_round<t0 + 1>(v, w);
+    sha1_round<t0 + 2>(v, w); sha1_round<t0 + 3>(v, w);
+}
+
+// One middle AES round (1..9) on two interleaved blocks.
+__device__ __forceinline__ void aes_round2(const char *__restrict__ lds, const TeBase &tb,
+                                           const uint32_t *rkr, uint32_t a[4], uint32_t b[4]) {
+    uint32_t ta[4], tbk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        ta[j] = xor3(xor3(TL(a[j], 0, 0), TL(a[(j + 1) & 3], 1, 1), TL(a[(j + 2) & 3], 2, 2)),
+                     TL(a[(j + 3) & 3], 3, 3), rkr[j]);
+        tbk[j] = xor3(xor3(TL(b[j], 0, 0), TL(b[(j + 1) & 3], 1, 1), TL(b[(j + 2) & 3], 2, 2)),
+                      TL(b[(j + 3) & 3], 3, 3), rkr[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
+}
+
+__device__ __forceinline__ void aes_last2(const char *__restrict__ lds, const TeBase &tb,
+                                          const uint32_t *rkr, uint32_t a[4], uint32_t b[4]) {
+    uint32_t ta[4], tbk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t lo_a = __builtin_amdgcn_perm(TL(a[(j + 1) & 3], 1, 1), TL(a[j], 0, 0), 0x0c0c0601u);
+        const uint32_t hi_a = __builtin_amdgcn_perm(TL(a[(j + 3) & 3], 3, 3), TL(a[(j + 2) & 3], 2, 2), 0x04000c0cu);
+        ta[j] = xor3(lo_a, hi_a, rkr[j]);
+        const uint32_t lo_b = __builtin_amdgcn_perm(TL(b[(j + 1) & 3], 1, 1), TL(b[j], 0, 0), 0x0c0c0601u);
+        const uint32_t hi_b = __builtin_amdgcn_perm(TL(b[(j + 3) & 3], 3, 3), TL(b[(j + 2) & 3], 2, 2), 0x04000c0cu);
+        tbk[j] = xor3(lo_b, hi_b, rkr[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
+}
+
+// Half P (0/1) of the interleaved chunk step: keystream blocks j0+2P, j0+2P+1
+// into K8[8] and SHA-1 rounds 40P .. 40P+39 on v / w.  After each AES round
+// of the block pair come four SHA-1 rounds, so the VALU work of the hash fills
+// the LDS latency of the table lookups.  Straight-line code, no branches.
+template <int P>
+__device__ __forceinline__ void ks_sha_half(const char *__restrict__ lds, const TeBase &tb,
+                                            const RoundKeys &rk, const uint32_t iv[4], int j0,
+                                            uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
+    uint32_t x[4], y[4];
+    ctr_input(iv, j0 + 2 * P, x); ctr_input(iv, j0 + 2 * P + 1, y);
+#pragma unroll
+    for (int j = 0; j < 4; j++) { x[j] ^= rk.k[j]; y[j] ^= rk.k[j]; }
+    constexpr int t = 40 * P;
+    aes_round2(lds, tb, rk.k + 4, x, y); sha1_rounds4<t + 0>(v, w);
+    aes_round2(lds, tb, rk.k + 8, x, y); sha1_rounds4<t + 4>(v, w);
+    aes_round2(lds, tb, rk.k + 12, x, y); sha1_rounds4<t + 8>(v, w);
+    aes_round2(lds, tb, rk.k + 16, x, y); sha1_rounds4<t + 12>(v, w);
+    aes_round2(lds, tb, rk.k + 20, x, y); sha1_rounds4<t + 16>(v, w);
+    aes_round2(lds, tb, rk.k + 24, x, y); sha1_rounds4<t + 20>(v, w);
+    aes_round2(lds, tb, rk.k + 28, x, y); sha1_rounds4<t + 24>(v, w);
+    aes_round2(lds, tb, rk.k + 32, x, y); sha1_rounds4<t + 28>(v, w);
+    aes_round2(lds, tb, rk.k + 36, x, y); sha1_rounds4<t + 32>(v, w);
+    aes_last2(lds, tb, rk.k + 40, x, y); sha1_rounds4<t + 36>(v, w);
+#pragma unroll
+    for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
+}
+
+// XOR keystream K (blocks 4c - off/16 .. +3, see ctr_chunk) into the chunk
+// words d[] of chunk c, within [off, end); advances the carry.
+__device__ __forceinline__ void ctr_apply(Ctr &cs, int c, const uint32_t K[16], uint32_t d[16]) {
+    const int s = (cs.off >> 2) & 3;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t a0 = K[i];
+        const uint32_t a1 = i >= 1 ? K[i - 1] : cs.carry[3 + i];
+        const uint32_t a2 = i >= 2 ? K[i - 2] : cs.carry[2 + i];
+        const uint32_t a3 = i >= 3 ? K[i - 3] : cs.carry[1 + i];
+        const uint32_t ksw = (s & 2) ? ((s & 1) ? a3 : a2) : ((s & 1) ? a1 : a0);
+        // branch-free byte mask of [off, end) over this word (off is a multiple
+        // of 4): keeps the loop body one basic block
+        const int pos = 64 * c + 4 * i;
+        const int valid = min(max(cs.end - pos, 0), 4);
+        uint32_t m = (uint32_t)((1ull << (8 * valid)) - 1ull);
+        m = pos >= cs.off ? m : 0u;
+        d[i] ^= ksw & m;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs.carry[k] = K[12 + k];
 }
 
 // Message word (big-endian) at byte position pos of the HMAC inner stream
@@ -432,17 +542,25 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
 }
 
 // ============================================================== sort
+// Stable radix sort of the walk records by context slot.  rocPRIM picks its
+// merge sort below 1M keys of more than 2 bytes; that path is ~1.5x slower here
+// and launches ~10 kernels per bundle, so the config forces the onesweep radix
+// path (MergeSortLimit = 0): one histogram pass + one pass per 8-bit digit.
+using SlotSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                  rocprim::default_config, 0>;
+
 size_t sort_temp_bytes(uint32_t n_max) {
     size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                       (WalkRec *)nullptr, (WalkRec *)nullptr, (int)n_max, 0, 32);
+    (void)rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, bytes, (uint32_t *)nullptr,
+                                                    (uint32_t *)nullptr, (WalkRec *)nullptr,
+                                                    (WalkRec *)nullptr, (size_t)n_max, 0, 32);
     return bytes;
 }
 
 hipError_t launch_sort(const BundleArgs &a, void *temp, size_t temp_bytes, int end_bit,
                        hipStream_t s) {
-    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, a.sk_in, a.sk_out, a.sv_in,
-                                              a.sv_out, (int)a.n, 0, end_bit, s);
+    return rocprim::radix_sort_pairs<SlotSortConfig>(temp, temp_bytes, a.sk_in, a.sk_out, a.sv_in,
+                                                     a.sv_out, (size_t)a.n, 0, (unsigned)end_bit, s);
 }
 
 // Runs body(ks) once per distinct session-key set among this wave's lanes with
@@ -742,13 +860,48 @@ __device__ __forceinline__ void make_iv_rtcp(const KeySet *ks, const uint4 &hdr,
     iv[3] = ks->salt[3] ^ (((index >> 8) & 0xffu) | ((index & 0xffu) << 8));
 }
 
+__device__ __forceinline__ void load_chunk(const uint8_t *pkt, int b, int lim, uint32_t d[16]) {
+    const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (64 * b + 16 * m < lim) v = qp[m];
+        d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
+    }
+}
+
+// Whole 64-B chunk b (inside the packet: no bounds checks, no branches).
+__device__ __forceinline__ void load_chunk_full(const uint8_t *pkt, int b, uint32_t d[16]) {
+    const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const uint4 v = qp[m];
+        d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint32_t d[16]) {
+    uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
+#pragma unroll
+    for (int m = 0; m < 4; m++) qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+}
+
+// Store the 16-B pieces of chunk b that overlap the ciphered range [off, end).
+__device__ __forceinline__ void store_chunk(uint8_t *pkt, int b, const Ctr &cs, const uint32_t d[16]) {
+    uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+        if (64 * b + 16 * m < cs.end && 64 * b + 16 * m + 16 > cs.off)
+            qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+}
+
 // ============================================================== k_protect
 // Fused protect, one lane per packet: AES-CM in place (SRTPCipherCTR.process
 // :94-121) + HMAC-SHA1 over the ciphertext (authenticatePacketHMAC :269-278)
 // + trailer (RawPacket.append :203-220).  Packet bytes: one read, one write.
 __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                             const char *__restrict__ lds, const TeBase &tb,
-                                            uint32_t p) {
+                                            uint32_t p, bool fused) {
     uint8_t *pkt = a.seg + a.off[p];
     const bool do_enc = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
     const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
@@ -779,9 +932,42 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     const int nb_data = (L + 63) >> 6;
     const int nb_inner = do_mac ? ((L + 12) >> 6) + 1 : 0;
     const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
+    int b = 0;
+    // Steady state (AES-CM + HMAC, wave-uniform): iteration b encrypts chunk b
+    // and hashes block b-1 -- a full data block, whose ciphertext c[] the
+    // previous iteration produced -- in one interleaved step.  Chunks 0..B-1
+    // are encrypted and blocks 0..B-2 hashed when it ends; block B-1 and the
+    // rest go through the generic loop below.
+    // (Chunks 1..B-1 lie wholly inside the packet: unconditional 64-B loads and
+    // stores; bytes outside [off, end) are written back unchanged.)
+    const int B = L >> 6;
+    if (fused && B >= 2) {
+        uint32_t c[16];
+        load_chunk(pkt, 0, L, c);
+        ctr_chunk(lds, tb, rk, cs, 0, c);
+        store_chunk(pkt, 0, cs, c);
+        const int hq = cs.off >> 4;
+        for (b = 1; b < B; b++) {
+            uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
+            uint32_t K[16], d[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
+            ks_sha_half<0>(lds, tb, rk, cs.iv, 4 * b - hq, K, v, c);
+            load_chunk_full(pkt, b, d);
+            ks_sha_half<1>(lds, tb, rk, cs.iv, 4 * b - hq, K + 8, v, c);
+#pragma unroll
+            for (int k = 0; k < 5; k++) h[k] += v[k];
+            ctr_apply(cs, b, K, d);
+            store_chunk_full(pkt, b, d);
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = d[k];
+        }
+        inner_words(c, B - 1, L, suffix); // block B-1 (may carry the suffix)
+        sha1_compress(h, c);
+    }
     // One AES site and one SHA-1 site: 64-B chunk b is loaded, encrypted in
     // place, stored, then hashed (inner blocks, then the outer block).
-    for (int b = 0; b < n_blocks; b++) {
+    for (; b < n_blocks; b++) {
         uint32_t w[16];
         uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
         if (b < nb_data) {
@@ -829,7 +1015,12 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
-    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) { protect_one(a, a.keysets + ks_u, lds, tb, p); });
+    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) {
+        const KeySet *ks = a.keysets + ks_u;
+        protect_one(a, ks, lds, tb, p,
+                    sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
+                        sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
+    });
 }
 
 // ============================================================== k_unprotect
@@ -843,7 +1034,7 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
 // walk rejects or guesses differently.
 __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                               const char *__restrict__ lds, const TeBase &tb,
-                                              uint32_t p, const CtxState &st) {
+                                              uint32_t p, const CtxState &st, bool fused) {
     uint8_t *pkt = a.seg + a.off[p];
     const int L = (int)a.len[p];
     const int T = (int)sgpr(ks->tag_len);
@@ -852,6 +1043,8 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     const bool aes = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
     Ctr cs;
+    cs.off = 0;
+    cs.iv[0] = cs.iv[1] = cs.iv[2] = cs.iv[3] = 0u;
     int end;       // bytes covered by the MAC and the decryption: [0, end) / [off, end)
     uint32_t suffix;
     bool spec = false;
@@ -891,11 +1084,11 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     }
     a.spec[p] = spec ? 1u : 0u;
     if (!do_mac && !spec) return;
-    cs.end = end;
+    cs.end = spec ? end : 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
     RoundKeys rk;
-    if (spec) load_round_keys_uniform(ks, rk);
+    load_round_keys_uniform(ks, rk);
     uint32_t h[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
@@ -903,7 +1096,24 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     const int nb_data = (end + 63) >> 6;
     const int nb_inner = ((end + 12) >> 6) + 1;
     const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
-    for (int b = 0; b < n_blocks; b++) {
+    int b = 0;
+    if (fused) { // AES-CM + HMAC, wave-uniform: full blocks before the ROC-carrying one
+        const int hq = cs.off >> 4;
+        for (; b < nb_full; b++) {
+            uint32_t d[16], w[16], K[16];
+            load_chunk_full(pkt, b, d);
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = bswap(d[k]);
+            uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
+            ks_sha_half<0>(lds, tb, rk, cs.iv, 4 * b - hq, K, v, w);
+            ks_sha_half<1>(lds, tb, rk, cs.iv, 4 * b - hq, K + 8, v, w);
+#pragma unroll
+            for (int k = 0; k < 5; k++) h[k] += v[k];
+            ctr_apply(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
+            store_chunk_full(pkt, b, d);
+        }
+    }
+    for (; b < n_blocks; b++) {
         uint32_t d[16];
         uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
 #pragma unroll
@@ -963,7 +1173,12 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect(BundleArgs a) {
     if (todo) st = a.ctx[slot];
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
-    for_each_keyset(todo, st.ks, [&](uint32_t ks_u) { unprotect_one(a, a.keysets + ks_u, lds, tb, p, st); });
+    for_each_keyset(todo, st.ks, [&](uint32_t ks_u) {
+        const KeySet *ks = a.keysets + ks_u;
+        unprotect_one(a, ks, lds, tb, p, st,
+                      sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
+                          sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
+    });
 }
 
 // ============================================================== k_unprotect_fix
