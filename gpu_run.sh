@@ -15,7 +15,7 @@ step() {  # step <name> <timeout-s> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ] || [ "$MODE" = diag ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
@@ -30,7 +30,7 @@ fi
 if [ "$MODE" = diag ]; then
   step diag 600 python tools_diag.py
 fi
-if [ "$MODE" = micro ] || [ "$MODE" = prof ]; then
+if [ "$MODE" = micro ]; then
   step sort_bench 120 ./tools/sort_bench
 fi
 if [ "$MODE" = micro ]; then
