@@ -21,6 +21,18 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --steps 20 --warmup 3
 fi
+if [ "$MODE" = quick ]; then
+  step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
+  step bench 300 python bench.py --steps 20 --warmup 3 --no-cpu
+  export TMPDIR=/tmp
+  step rocprof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+fi
+if [ "$MODE" = valu ]; then
+  step valu_bench 120 ./tools/valu_bench
+fi
+if [ "$MODE" = probe ]; then
+  step probe 300 python tools/walk_probe.py
+fi
 if [ "$MODE" = one ]; then
   step pytest_one 600 python -m pytest tests -m gpu -q -x --timeout 300 -p no:cacheprovider -k "${2:-malformed}"
 fi

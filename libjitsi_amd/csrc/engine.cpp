@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/srtp_mi355x.h"
@@ -413,6 +414,8 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.check_replay = e->opts.check_replay;
     a.abort_on_error = e->opts.abort_on_error;
     a.serial = e->serial++;
+    static const int debug_mode = getenv("SRTP_DEBUG") ? atoi(getenv("SRTP_DEBUG")) : 0;
+    a.debug = debug_mode;
     a.p_slot = e->p_slot; a.sk_in = e->sk_in; a.sk_out = e->sk_out;
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;

@@ -32,6 +32,7 @@ struct BundleArgs {
     int32_t check_replay;
     int32_t abort_on_error;
     uint32_t serial;       // bundle serial (context birth stamp)
+    int32_t debug;         // diagnostics only (SRTP_DEBUG env): 0 in production
     // per-bundle scratch
     uint32_t *p_slot;      // [n] context slot of packet p
     uint32_t *sk_in, *sk_out; // [n] sort keys (slot)

@@ -80,6 +80,9 @@ __device__ __forceinline__ void fill_te4(uint32_t *s_te) {
         s_te[i] = t ? rotl(v, 8u * (uint32_t)t) : v;
     }
     __syncthreads();
+    // The table is read only by inline asm (aes_rounds_asm.inc): let the
+    // pointer escape so the LDS image and the stores above are kept.
+    asm volatile("" ::"s"(s_te) : "memory");
 }
 
 struct TeBase {
@@ -107,42 +110,8 @@ struct RoundKeys {
     uint32_t k[44];
 };
 
-// FIPS-197 AES-128 on two independent blocks (interleaved for ILP), each held
-// as four little-endian column words (byte r of word j = state row r, column
-// j).  Output column j, row r comes from input column j+r (ShiftRows), looked
-// up in T_r (MixColumns coefficients rotated by row).
 __device__ __forceinline__ void aes_encrypt2(const char *__restrict__ lds, const TeBase &tb,
-                                             const RoundKeys &rk, uint32_t a[4], uint32_t b[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) { a[j] ^= rk.k[j]; b[j] ^= rk.k[j]; }
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        uint32_t ta[4], tbk[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            ta[j] = xor3(xor3(TL(a[j], 0, 0), TL(a[(j + 1) & 3], 1, 1), TL(a[(j + 2) & 3], 2, 2)),
-                         TL(a[(j + 3) & 3], 3, 3), rk.k[4 * r + j]);
-            tbk[j] = xor3(xor3(TL(b[j], 0, 0), TL(b[(j + 1) & 3], 1, 1), TL(b[(j + 2) & 3], 2, 2)),
-                          TL(b[(j + 3) & 3], 3, 3), rk.k[4 * r + j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
-    }
-    // Last round (no MixColumns): S(x) sits in byte 1 of T0, 2 of T1, 0 of T2,
-    // 0 of T3; two v_perm_b32 gather the four S-box bytes of a column.
-    uint32_t ta[4], tbk[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t lo_a = __builtin_amdgcn_perm(TL(a[(j + 1) & 3], 1, 1), TL(a[j], 0, 0), 0x0c0c0601u);
-        const uint32_t hi_a = __builtin_amdgcn_perm(TL(a[(j + 3) & 3], 3, 3), TL(a[(j + 2) & 3], 2, 2), 0x04000c0cu);
-        ta[j] = xor3(lo_a, hi_a, rk.k[40 + j]);
-        const uint32_t lo_b = __builtin_amdgcn_perm(TL(b[(j + 1) & 3], 1, 1), TL(b[j], 0, 0), 0x0c0c0601u);
-        const uint32_t hi_b = __builtin_amdgcn_perm(TL(b[(j + 3) & 3], 3, 3), TL(b[(j + 2) & 3], 2, 2), 0x04000c0cu);
-        tbk[j] = xor3(lo_b, hi_b, rk.k[40 + j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
-}
+                                             const RoundKeys &rk, uint32_t a[4], uint32_t b[4]);
 
 // AES-CM state of one packet (SRTPCipherCTR.getCipherStream :68-92): keystream
 // block j = AES(iv[0..13] || u16_be(j)), XORed over packet bytes [off, end).
@@ -248,35 +217,35 @@ __device__ __forceinline__ void sha1_rounds4(uint32_t v[5], uint32_t w[16]) {
     sha1_round<t0 + 2>(v, w); sha1_round<t0 + 3>(v, w);
 }
 
-// One middle AES round (1..9) on two interleaved blocks.
+// One middle AES round (1..9) / the last round on two interleaved blocks:
+// hand-scheduled asm (aes_rounds_asm.inc, generated by tools/gen_aes_asm.py),
+// which needs the T-table image at LDS address 0 -- s_te is the only LDS
+// object of the AES kernels.
+#include "aes_rounds_asm.inc"
+
 __device__ __forceinline__ void aes_round2(const char *__restrict__ lds, const TeBase &tb,
                                            const uint32_t *rkr, uint32_t a[4], uint32_t b[4]) {
-    uint32_t ta[4], tbk[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        ta[j] = xor3(xor3(TL(a[j], 0, 0), TL(a[(j + 1) & 3], 1, 1), TL(a[(j + 2) & 3], 2, 2)),
-                     TL(a[(j + 3) & 3], 3, 3), rkr[j]);
-        tbk[j] = xor3(xor3(TL(b[j], 0, 0), TL(b[(j + 1) & 3], 1, 1), TL(b[(j + 2) & 3], 2, 2)),
-                      TL(b[(j + 3) & 3], 3, 3), rkr[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
+    (void)lds;
+    aes_round2_asm(a, b, tb.b, rkr);
 }
 
 __device__ __forceinline__ void aes_last2(const char *__restrict__ lds, const TeBase &tb,
                                           const uint32_t *rkr, uint32_t a[4], uint32_t b[4]) {
-    uint32_t ta[4], tbk[4];
+    (void)lds;
+    aes_last2_asm(a, b, tb.b, rkr);
+}
+
+// FIPS-197 AES-128 on two independent blocks (interleaved for ILP), each held
+// as four little-endian column words (byte r of word j = state row r, column
+// j).  Output column j, row r comes from input column j+r (ShiftRows), looked
+// up in T_r (MixColumns coefficients rotated by row).
+__device__ __forceinline__ void aes_encrypt2(const char *__restrict__ lds, const TeBase &tb,
+                                             const RoundKeys &rk, uint32_t a[4], uint32_t b[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t lo_a = __builtin_amdgcn_perm(TL(a[(j + 1) & 3], 1, 1), TL(a[j], 0, 0), 0x0c0c0601u);
-        const uint32_t hi_a = __builtin_amdgcn_perm(TL(a[(j + 3) & 3], 3, 3), TL(a[(j + 2) & 3], 2, 2), 0x04000c0cu);
-        ta[j] = xor3(lo_a, hi_a, rkr[j]);
-        const uint32_t lo_b = __builtin_amdgcn_perm(TL(b[(j + 1) & 3], 1, 1), TL(b[j], 0, 0), 0x0c0c0601u);
-        const uint32_t hi_b = __builtin_amdgcn_perm(TL(b[(j + 3) & 3], 3, 3), TL(b[(j + 2) & 3], 2, 2), 0x04000c0cu);
-        tbk[j] = xor3(lo_b, hi_b, rkr[j]);
-    }
+    for (int j = 0; j < 4; j++) { a[j] ^= rk.k[j]; b[j] ^= rk.k[j]; }
 #pragma unroll
-    for (int j = 0; j < 4; j++) { a[j] = ta[j]; b[j] = tbk[j]; }
+    for (int r = 1; r < 10; r++) aes_round2(lds, tb, rk.k + 4 * r, a, b);
+    aes_last2(lds, tb, rk.k + 40, a, b);
 }
 
 // Half P (0/1) of the interleaved chunk step: keystream blocks j0+2P, j0+2P+1
@@ -607,7 +576,7 @@ struct ReverifyArgs { // by value: keeps the kernel arguments out of scratch
     const uint32_t *tailc; // 16 words, or null when the packet still holds ciphertext
 };
 
-__device__ __noinline__ bool reverify_rtp(ReverifyArgs r, const KeySet *ks, int L, int32_t g) {
+__device__ __forceinline__ bool reverify_rtp(ReverifyArgs r, const KeySet *ks, int L, int32_t g) {
     const int T = ks->tag_len;
     int mac_len = L - T;
     if (mac_len < 0) mac_len = 0;
@@ -640,8 +609,7 @@ __device__ __noinline__ bool reverify_rtp(ReverifyArgs r, const KeySet *ks, int 
 
 // ============================================================== k_walk
 // One lane per context: the serial state machine over the context's packets in
-// array order.  Records come from the sorted array four at a time (one memory
-// round trip per four packets, verify results prefetched with them).
+// array order (records sorted by context slot, stable).
 struct WalkCtx {
     int enc, auth, T, kind;
     bool check_replay, reverse;
@@ -767,66 +735,102 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
     return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_walk(BundleArgs a, int limit_pass) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const BundleCtl ctl = *a.ctl;
-    const bool two_pass = a.abort_on_error && ctl.any_throw;
-    if (limit_pass && !two_pass) return;
-    if (i >= a.n) return;
-    const uint32_t key = a.sk_out[i];
-    if (key > a.ctx_mask) return;
-    if (i > 0 && a.sk_out[i - 1] == key) return;
-    const uint32_t slot = key;
-    CtxState st = a.ctx[slot];
-    const KeySet *ks = a.keysets + st.ks;
-    WalkCtx c;
-    c.enc = ks->enc_type; c.auth = ks->auth_type; c.T = ks->tag_len; c.kind = ks->kind;
-    c.check_replay = a.check_replay != 0;
-    c.reverse = a.reverse != 0;
-    const bool need_auth = c.reverse && c.auth != SRTP_NULL_AUTHENTICATION;
-    const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
-    const bool dry = two_pass && !limit_pass;
-    const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
-    const uint32_t first_p = a.sv_out[i].p & kRecIdxMask;
+// One wave per workgroup stages kWalkSpan consecutive sorted records in LDS
+// with one coalesced pass (plus, for unprotect, the verify pass's g0/auth_ok of
+// each record, gathered in parallel), compacts the segment starts of the span,
+// and lane l walks the l-th segment: the per-context chain reads LDS (tens of
+// cycles per record) instead of dependent HBM round trips.  The rare segment
+// that runs past the span reads its tail from global memory.
+constexpr int kWalkBlock = 64;
+constexpr int kWalkPer = 4;
+constexpr int kWalkSpan = kWalkBlock * kWalkPer;
 
-    // Scratch arrays carry 8 entries of slack, so the batch loads never leave them.
-    bool live = true;
-    for (uint32_t j = i; live; j += 4) {
-        WalkRec r[4];
-        uint32_t g0[4] = {0, 0, 0, 0}, ok[4] = {0, 0, 0, 0};
-        int cnt = 0;
+template <bool REV>
+__global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pass) {
+    __shared__ WalkRec s_rec[kWalkSpan];
+    __shared__ uint32_t s_key[kWalkSpan];
+    __shared__ uint32_t s_g0[REV ? kWalkSpan : 1];
+    __shared__ uint32_t s_ok[REV ? kWalkSpan : 1];
+    __shared__ uint32_t s_start[kWalkSpan];
+    __shared__ uint32_t s_nstart;
+    const bool two_pass = a.abort_on_error && a.ctl->any_throw;
+    if (limit_pass && !two_pass) return;
+    const uint32_t base = blockIdx.x * kWalkSpan;
+    if (base >= a.n) return;
+    const uint32_t span = min((uint32_t)kWalkSpan, a.n - base);
+    if (threadIdx.x == 0) s_nstart = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const bool mine = (j + q < a.n) && a.sk_out[j + q] == key;
-            r[q] = a.sv_out[j + q];
-            cnt += (mine && cnt == q) ? 1 : 0;
-        }
-        if (need_auth) {
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (q < cnt) {
-                    const uint32_t p = r[q].p & kRecIdxMask;
-                    if (c.kind == SRTP_KIND_RTP) g0[q] = a.g0[p];
-                    ok[q] = a.auth_ok[p];
-                }
+    for (int k = 0; k < kWalkPer; k++) {
+        const uint32_t j = threadIdx.x + k * kWalkBlock;
+        if (j < span) {
+            const WalkRec r = a.sv_out[base + j];
+            s_rec[j] = r;
+            s_key[j] = a.sk_out[base + j];
+            if (REV) {
+                const uint32_t p = r.p & kRecIdxMask;
+                s_g0[j] = a.g0[p];
+                s_ok[j] = a.auth_ok[p];
             }
         }
-#pragma unroll 1
-        for (int q = 0; q < cnt; q++) {
-            if (limit_pass && (int32_t)(r[0].p & kRecIdxMask) > E) { live = false; break; }
-            if (!walk_one(a, ks, c, st, r[0], g0[0], ok[0], dry, tid)) { live = false; break; }
+    }
+    __syncthreads();
+    if (a.debug == 1) return;
+    const uint32_t prev_key = base ? a.sk_out[base - 1] : ~0u;
 #pragma unroll
-            for (int k = 0; k < 3; k++) { r[k] = r[k + 1]; g0[k] = g0[k + 1]; ok[k] = ok[k + 1]; }
+    for (int k = 0; k < kWalkPer; k++) {
+        const uint32_t j = threadIdx.x + k * kWalkBlock;
+        if (j < span) {
+            const uint32_t key = s_key[j];
+            if (key <= a.ctx_mask && (j ? s_key[j - 1] : prev_key) != key)
+                s_start[atomicAdd(&s_nstart, 1u)] = j;
         }
-        if (cnt < 4) break;
     }
-    if (dry) return; // first of two passes: state is committed by the limit pass
-    if (limit_pass && st.birth == a.serial && (int32_t)first_p > E) {
-        // derived for a packet the reference never reached: forget it again
-        __hip_atomic_store(&a.ctx_keys[slot], kTombKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
+    __syncthreads();
+    const uint32_t nstart = s_nstart;
+    const bool dry = two_pass && !limit_pass;
+#pragma unroll 1
+    for (uint32_t q = threadIdx.x; q < nstart; q += kWalkBlock) {
+        const uint32_t j = s_start[q];
+        const uint32_t key = s_key[j];
+        const uint32_t slot = key;
+        CtxState st = a.ctx[slot];
+        const KeySet *ks = a.keysets + st.ks;
+        WalkCtx c;
+        c.enc = ks->enc_type; c.auth = ks->auth_type; c.T = ks->tag_len; c.kind = ks->kind;
+        c.check_replay = a.check_replay != 0;
+        c.reverse = REV;
+        const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
+        const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
+        const uint32_t first_p = s_rec[j].p & kRecIdxMask;
+#pragma unroll 1
+        for (uint32_t i = base + j; i < a.n; i++) {
+            const uint32_t jj = i - base;
+            WalkRec r;
+            uint32_t g0 = 0u, ok = 0u;
+            if (jj < span) {
+                if (s_key[jj] != key) break;
+                r = s_rec[jj];
+                if (REV) { g0 = s_g0[jj]; ok = s_ok[jj]; }
+            } else {
+                if (a.sk_out[i] != key) break;
+                r = a.sv_out[i];
+                if (REV) {
+                    const uint32_t p = r.p & kRecIdxMask;
+                    g0 = a.g0[p]; ok = a.auth_ok[p];
+                }
+            }
+            if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) break;
+            if (a.debug == 2) { st.window += r.p ^ g0 ^ ok; continue; }
+            if (!walk_one(a, ks, c, st, r, g0, ok, dry, tid)) break;
+        }
+        if (dry) continue; // first of two passes: state is committed by the limit pass
+        if (limit_pass && st.birth == a.serial && (int32_t)first_p > E) {
+            // derived for a packet the reference never reached: forget it again
+            __hip_atomic_store(&a.ctx_keys[slot], kTombKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        a.ctx[slot] = st;
     }
-    a.ctx[slot] = st;
 }
 
 // ====================================================== final status helper
@@ -1303,7 +1307,11 @@ hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
-    hipLaunchKernelGGL(k_walk, grid_for(a.n), dim3(kBlock), 0, s, a, limit_pass);
+    const dim3 grid((a.n + kWalkSpan - 1) / kWalkSpan);
+    if (a.reverse)
+        hipLaunchKernelGGL(k_walk<true>, grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+    else
+        hipLaunchKernelGGL(k_walk<false>, grid, dim3(kWalkBlock), 0, s, a, limit_pass);
     return hipGetLastError();
 }
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
