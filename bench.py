@@ -48,6 +48,9 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--policy", default="AES_CM_128_HMAC_SHA1_80",
+                    help="protection profile; 'AES_CM_128_NULL_AUTH' (cipher only) is a "
+                         "diagnostic split of the fused kernel, not the headline metric")
     return ap.parse_args()
 
 
@@ -117,7 +120,11 @@ def main():
     eng = SRTPEngine(device=local_rank, max_contexts=max(1 << 16, 4 * nssrc), max_factories=64,
                      max_transformers=64, max_batch=n)
     (k, s), = synth.keys(2 + rank, 1)
-    pols = profile_policies("AES_CM_128_HMAC_SHA1_80")
+    if args.policy == "AES_CM_128_NULL_AUTH":
+        from libjitsi_amd import SRTPPolicy as P
+        pols = (P(1, 16, 0, 0, 0, 14),) * 2
+    else:
+        pols = profile_policies(args.policy)
     snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
     rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng))
 
@@ -193,7 +200,7 @@ def main():
 
     total_pkts = n * args.steps * world
     pps = total_pkts / dt_max
-    T = 10
+    T = pols[0].authTagLength
     alg_bytes_rt = 2 * (L + (L + T))  # protect L + (L+T), unprotect (L+T) + L
     gbs = pps * alg_bytes_rt / 1e9
     prot_ms, prot_cnt = timing["protect"]

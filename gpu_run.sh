@@ -52,14 +52,23 @@ if [ "$MODE" = micro ]; then
   step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib/fetch -o run -- ./tools/pmc_calib
   step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib/write -o run -- ./tools/pmc_calib
 fi
-if [ "$MODE" = prof ]; then
+if [ "$MODE" = prof ] || [ "$MODE" = profall ]; then
   export TMPDIR=/tmp
   B="python3 bench.py --steps 5 --warmup 1 --no-cpu"
-  step rocprof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- $B
-  step rocprof_list 120 rocprofv3 -L
-  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/fetch -o run -- $B
-  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write -o run -- $B
-  step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d gpurun_out/prof/sq -o run -- $B
-  step pmc_sq2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d gpurun_out/prof/sq2 -o run -- $B
+  P=gpurun_out/prof
+  step rocprof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run -- $B
+  step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/fetch -o run -- $B
+  step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -o run -- $B
+  step pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $P/sq -o run -- $B
+  step pmc_sq2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $P/sq2 -o run -- $B
+fi
+if [ "$MODE" = profall ]; then
+  step calib 120 ./tools/pmc_calib
+  step calib_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/calib/trace -o run -- ./tools/pmc_calib
+  step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib/fetch -o run -- ./tools/pmc_calib
+  step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib/write -o run -- ./tools/pmc_calib
+fi
+if [ "$MODE" = golden ]; then
+  step pytest_golden 600 python -u -m pytest tests/test_golden.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 fi
 exit 0

@@ -1,0 +1,118 @@
+"""gfx950 AES-128 T-table round generator shared by tools/gen_aes_asm.py (the
+product's aes_rounds_asm.inc) and tools/aes_bench (the variant micro-benchmark).
+
+A round over B interleaved blocks (state words %[<z>0..3] for z in blocks):
+  * every lookup address is one v_perm_b32 of a state word and a per-lane
+    table base (see TL() in srtp_kernels.hip);
+  * the ds_read_b32 of all blocks are streamed, keeping up to 15 in flight (the
+    4-bit lgkmcnt limit), and each output column is folded as soon as its four
+    lookups are known to have landed (LDS returns in order).
+tables=4: T0..T3 in LDS; column j = T0 ^ T1 ^ T2 ^ T3 ^ rk[j] (2 v_bitop3).
+tables=2: T0, T1 in LDS; T2 = rotl16(T0), T3 = rotl16(T1), so column j =
+  T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk[j])) (2 v_bitop3 + 1 v_alignbit),
+  half the LDS image.
+"""
+
+MAX_LGKM = 15
+
+
+def lookups(z, tb, tables):
+    out = []
+    for j in range(4):
+        for t in range(4):
+            base = t if tables == 4 else (t & 1)  # table; t is also the state byte
+            out.append((f"%[t{tb + 4 * j + t}]", f"%[{z}{(j + t) & 3}]", base, t))
+    return out
+
+
+def consume(z, tb, j, last, tables):
+    a, b, c, d = (f"%[t{tb + 4 * j + t}]" for t in range(4))
+    if last:
+        # S(x): byte 1 of T0 / byte 2 of T1 (tables 2: rotl16 of T0/T1 puts it
+        # at byte 3 / byte 0 -- same selectors after the table swap below)
+        if tables == 4:
+            return [f"v_perm_b32 {a}, {b}, {a}, %[s4]",
+                    f"v_perm_b32 {c}, {d}, {c}, %[s5]",
+                    f"v_bitop3_b32 %[{z}{j}], {a}, {c}, %[k{j}] bitop3:0x96"]
+        return [f"v_perm_b32 {a}, {b}, {a}, %[s4]",
+                f"v_perm_b32 {c}, {d}, {c}, %[s6]",
+                f"v_bitop3_b32 %[{z}{j}], {a}, {c}, %[k{j}] bitop3:0x96"]
+    if tables == 4:
+        return [f"v_bitop3_b32 {a}, {a}, {b}, {c} bitop3:0x96",
+                f"v_bitop3_b32 %[{z}{j}], {a}, {d}, %[k{j}] bitop3:0x96"]
+    return [f"v_bitop3_b32 {c}, {c}, {d}, %[r{j}] bitop3:0x96",
+            f"v_alignbit_b32 {c}, {c}, {c}, 16",
+            f"v_bitop3_b32 %[{z}{j}], {a}, {b}, {c} bitop3:0x96"]
+
+
+def round_body(blocks, last, tables=4):
+    L = []
+    per = [lookups(z, 16 * i, tables) for i, z in enumerate(blocks)]
+    reads = [dst for lk in per for dst, _, _, _ in lk]
+    cols = [(z, 16 * i, j) for i, z in enumerate(blocks) for j in range(4)]
+    # perms of block 0, its first reads, then the perms of each later block
+    # interleaved with the remaining reads (one per lgkmcnt(14) wait)
+    pending_perms = []
+    for i, lk in enumerate(per):
+        pending_perms.append([f"v_perm_b32 {dst}, {src}, %[b{t}], %[s{k}]" for dst, src, t, k in lk])
+    L += pending_perms[0]
+    nread = 0
+    for i in range(min(MAX_LGKM, 16)):
+        L.append(f"ds_read_b32 {reads[nread]}, {reads[nread]}")
+        nread += 1
+    for blk in range(1, len(blocks)):
+        L += pending_perms[blk]
+        # reads of this block become issuable now
+    done, nxt = -1, 0
+    while nread < len(reads):
+        if nread >= MAX_LGKM:
+            L.append(f"s_waitcnt lgkmcnt({MAX_LGKM - 1})")
+            done = nread - MAX_LGKM
+        L.append(f"ds_read_b32 {reads[nread]}, {reads[nread]}")
+        nread += 1
+        while nxt < len(cols) and 4 * nxt + 3 <= done:
+            L.extend(consume(*cols[nxt], last, tables))
+            nxt += 1
+    L.append("s_waitcnt lgkmcnt(0)")
+    while nxt < len(cols):
+        L.extend(consume(*cols[nxt], last, tables))
+        nxt += 1
+    return L
+
+
+SEL4 = ["0x0c020400u", "0x0c020500u", "0x0c020600u", "0x0c020700u"]
+SEL2 = ["0x0c0c0400u", "0x0c0c0500u", "0x0c0c0600u", "0x0c0c0700u"]
+
+
+def emit(name, blocks, last, tables=4):
+    """A __device__ function running one (middle or last) round on the blocks."""
+    body = round_body(blocks, last, tables)
+    nb = len(blocks)
+    args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
+    s = [f"__device__ __forceinline__ void {name}({args}, const uint32_t bs[4],",
+         "                                       const uint32_t *__restrict__ rkr) {",
+         f"    uint32_t t[{16 * nb}];"]
+    if tables == 2 and not last:
+        s.append("    uint32_t r16[4];")
+        s.append("#pragma unroll")
+        s.append("    for (int j = 0; j < 4; j++) r16[j] = __builtin_amdgcn_alignbit(rkr[j], rkr[j], 16);")
+    s.append("    asm volatile(")
+    for ln in body:
+        s.append(f'        "{ln}\\n"')
+    outs = [f'[{z}{i}] "+v"({z}[{i}])' for z in blocks for i in range(4)]
+    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(16 * nb)]
+    ins = [f'[b{i}] "v"(bs[{i}])' for i in range(4)]
+    sels = SEL4 if tables == 4 else SEL2
+    ins += [f'[s{i}] "s"({sels[i]})' for i in range(4)]
+    if last:
+        ins += ['[s4] "s"(0x0c0c0601u)', '[s5] "s"(0x04000c0cu)']
+        if tables == 2:
+            ins += ['[s6] "s"(0x06010c0cu)']
+    if tables == 2 and not last:
+        ins += [f'[r{i}] "s"(r16[{i}])' for i in range(4)]
+    ins += [f'[k{i}] "s"(rkr[{i}])' for i in range(4)]
+    s.append("        : " + ",\n          ".join(outs))
+    s.append("        : " + ",\n          ".join(ins))
+    s.append('        : "memory");')
+    s.append("}")
+    return "\n".join(s)
