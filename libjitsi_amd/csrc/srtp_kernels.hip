@@ -248,21 +248,69 @@ __device__ __forceinline__ void aes_encrypt2(const char *__restrict__ lds, const
     aes_last2(lds, tb, rk.k + 40, a, b);
 }
 
+// ------------------------------------------- AES-CM rounds 1-2, precomputed
+// Counter blocks of one packet differ only in IV bytes 14-15, and for block
+// index j < 256 only in byte 15 (row 3 of column 3).  After AddRoundKey and
+// round 1 that byte reaches output column 0 alone (through T3); in round 2
+// that column reaches each output column through exactly one lookup.  So per
+// packet: p0 = the constant part of round-1 column 0, r[0..3] = the constant
+// parts of the round-2 columns (27 lookups once), and per block only
+//     u0 = p0 ^ T3[j ^ kb];   s = (r0 ^ T0[u0.b0], r1 ^ T3[u0.b3],
+//                                 r2 ^ T2[u0.b2], r3 ^ T1[u0.b1])
+// -- 5 lookups instead of 32 for rounds 1-2 (133 instead of 160 per block).
+struct CtrPre {
+    uint32_t p0, r[4], kb;
+};
+
+__device__ __forceinline__ void ctr_precompute(const char *__restrict__ lds, const TeBase &tb,
+                                               const RoundKeys &rk, const uint32_t iv[4],
+                                               CtrPre &cp) {
+    const uint32_t w0 = iv[0] ^ rk.k[0], w1 = iv[1] ^ rk.k[1], w2 = iv[2] ^ rk.k[2];
+    const uint32_t w3 = iv[3] ^ rk.k[3]; // bytes 14-15 of iv are zero (counter slot)
+    cp.kb = w3 >> 24;
+    cp.p0 = xor3(TL(w0, 0, 0), TL(w1, 1, 1), TL(w2, 2, 2)) ^ rk.k[4];
+    const uint32_t u1 = xor3(TL(w1, 0, 0), TL(w2, 1, 1), TL(w3, 2, 2)) ^ TL(w0, 3, 3) ^ rk.k[5];
+    const uint32_t u2 = xor3(TL(w2, 0, 0), TL(w3, 1, 1), TL(w0, 2, 2)) ^ TL(w1, 3, 3) ^ rk.k[6];
+    const uint32_t u3 = xor3(TL(w3, 0, 0), TL(w0, 1, 1), TL(w1, 2, 2)) ^ TL(w2, 3, 3) ^ rk.k[7];
+    cp.r[0] = xor3(TL(u1, 1, 1), TL(u2, 2, 2), TL(u3, 3, 3)) ^ rk.k[8];
+    cp.r[1] = xor3(TL(u1, 0, 0), TL(u2, 1, 1), TL(u3, 2, 2)) ^ rk.k[9];
+    cp.r[2] = xor3(TL(u2, 0, 0), TL(u3, 1, 1), TL(u1, 3, 3)) ^ rk.k[10];
+    cp.r[3] = xor3(TL(u3, 0, 0), TL(u1, 2, 2), TL(u2, 3, 3)) ^ rk.k[11];
+}
+
+// State after round 2 (round key 2 included) of counter blocks ja and jb
+// (both < 256).
+__device__ __forceinline__ void ctr_first2(const char *__restrict__ lds, const TeBase &tb,
+                                           const CtrPre &cp, int ja, int jb, uint32_t a[4],
+                                           uint32_t b[4]) {
+    const uint32_t xa = (uint32_t)ja ^ cp.kb, xb = (uint32_t)jb ^ cp.kb;
+    const uint32_t ua = cp.p0 ^ TL(xa, 0, 3), ub = cp.p0 ^ TL(xb, 0, 3);
+    a[0] = cp.r[0] ^ TL(ua, 0, 0); b[0] = cp.r[0] ^ TL(ub, 0, 0);
+    a[1] = cp.r[1] ^ TL(ua, 3, 3); b[1] = cp.r[1] ^ TL(ub, 3, 3);
+    a[2] = cp.r[2] ^ TL(ua, 2, 2); b[2] = cp.r[2] ^ TL(ub, 2, 2);
+    a[3] = cp.r[3] ^ TL(ua, 1, 1); b[3] = cp.r[3] ^ TL(ub, 1, 1);
+}
+
+// True when a counter block of this chunk step could reach index 256 (IV
+// byte 14 no longer zero: the precompute does not apply), on any active lane.
+__device__ __forceinline__ bool ctr_pre_exhausted(int j0) {
+    return __ballot(j0 + 3 >= 256) != 0ull;
+}
+
 // Half P (0/1) of the interleaved chunk step: keystream blocks j0+2P, j0+2P+1
-// into K8[8] and SHA-1 rounds 40P .. 40P+39 on v / w.  After each AES round
-// of the block pair come four SHA-1 rounds, so the VALU work of the hash fills
-// the LDS latency of the table lookups.  Straight-line code, no branches.
+// into K8[8] and SHA-1 rounds 40P .. 40P+39 on v / w.  Rounds 1-2 come from
+// the counter precompute (8 SHA-1 rounds beside them), then after each
+// remaining AES round of the block pair come four SHA-1 rounds, so the VALU
+// work of the hash fills the LDS latency of the table lookups.  Straight-line
+// code, no branches.
 template <int P>
 __device__ __forceinline__ void ks_sha_half(const char *__restrict__ lds, const TeBase &tb,
-                                            const RoundKeys &rk, const uint32_t iv[4], int j0,
+                                            const RoundKeys &rk, const CtrPre &cp, int j0,
                                             uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
     uint32_t x[4], y[4];
-    ctr_input(iv, j0 + 2 * P, x); ctr_input(iv, j0 + 2 * P + 1, y);
-#pragma unroll
-    for (int j = 0; j < 4; j++) { x[j] ^= rk.k[j]; y[j] ^= rk.k[j]; }
+    ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
     constexpr int t = 40 * P;
-    aes_round2(lds, tb, rk.k + 4, x, y); sha1_rounds4<t + 0>(v, w);
-    aes_round2(lds, tb, rk.k + 8, x, y); sha1_rounds4<t + 4>(v, w);
+    sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
     aes_round2(lds, tb, rk.k + 12, x, y); sha1_rounds4<t + 8>(v, w);
     aes_round2(lds, tb, rk.k + 16, x, y); sha1_rounds4<t + 12>(v, w);
     aes_round2(lds, tb, rk.k + 20, x, y); sha1_rounds4<t + 16>(v, w);
@@ -338,10 +386,17 @@ __device__ __forceinline__ void inner_words(uint32_t w[16], int b, int mac_len, 
     }
 }
 
-// HMAC outer block: w = inner digest || padding, h = opad midstate.
+// HMAC outer block: w = inner digest || padding, h = opad midstate.  UNIFORM:
+// ks is the same for every active lane (the packet kernels, which loop over
+// the wave's key sets), so the midstate is read into SGPRs; otherwise (k_walk's
+// re-check, one context per lane) each lane reads its own key set's.
+template <bool UNIFORM = true>
 __device__ __forceinline__ void outer_words(uint32_t w[16], uint32_t h[5], const KeySet *ks) {
 #pragma unroll
-    for (int k = 0; k < 5; k++) { w[k] = h[k]; h[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ks->opad[k]); }
+    for (int k = 0; k < 5; k++) {
+        w[k] = h[k];
+        h[k] = UNIFORM ? (uint32_t)__builtin_amdgcn_readfirstlane((int)ks->opad[k]) : ks->opad[k];
+    }
     w[5] = 0x80000000u;
 #pragma unroll
     for (int k = 6; k < 15; k++) w[k] = 0u;
@@ -600,7 +655,7 @@ __device__ __forceinline__ bool reverify_rtp(ReverifyArgs r, const KeySet *ks, i
         if (b < nb_inner) {
             inner_words(w, b, mac_len, (uint32_t)g);
         } else {
-            outer_words(w, h, ks);
+            outer_words<false>(w, h, ks); // ks varies across the walk's lanes
         }
         sha1_compress(h, w);
     }
@@ -951,14 +1006,18 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         ctr_chunk(lds, tb, rk, cs, 0, c);
         store_chunk(pkt, 0, cs, c);
         const int hq = cs.off >> 4;
+        CtrPre cp;
+        ctr_precompute(lds, tb, rk, cs.iv, cp);
         for (b = 1; b < B; b++) {
+            // packets past ~4 KB: the generic loop below finishes them
+            if (ctr_pre_exhausted(4 * b - hq)) break;
             uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
             uint32_t K[16], d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
-            ks_sha_half<0>(lds, tb, rk, cs.iv, 4 * b - hq, K, v, c);
+            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
             load_chunk_full(pkt, b, d);
-            ks_sha_half<1>(lds, tb, rk, cs.iv, 4 * b - hq, K + 8, v, c);
+            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
             ctr_apply(cs, b, K, d);
@@ -966,7 +1025,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k];
         }
-        inner_words(c, B - 1, L, suffix); // block B-1 (may carry the suffix)
+        inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
         sha1_compress(h, c);
     }
     // One AES site and one SHA-1 site: 64-B chunk b is loaded, encrypted in
@@ -1103,14 +1162,17 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     int b = 0;
     if (fused) { // AES-CM + HMAC, wave-uniform: full blocks before the ROC-carrying one
         const int hq = cs.off >> 4;
+        CtrPre cp;
+        ctr_precompute(lds, tb, rk, cs.iv, cp);
         for (; b < nb_full; b++) {
+            if (ctr_pre_exhausted(4 * b - hq)) break; // generic loop finishes
             uint32_t d[16], w[16], K[16];
             load_chunk_full(pkt, b, d);
 #pragma unroll
             for (int k = 0; k < 16; k++) w[k] = bswap(d[k]);
             uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-            ks_sha_half<0>(lds, tb, rk, cs.iv, 4 * b - hq, K, v, w);
-            ks_sha_half<1>(lds, tb, rk, cs.iv, 4 * b - hq, K + 8, v, w);
+            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, w);
+            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, w);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
             ctr_apply(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
