@@ -198,7 +198,7 @@ __device__ __forceinline__ void sha1_round(uint32_t v[5], uint32_t w[16]) {
     if (t < 16) {
         wt = w[t];
     } else {
-        wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+        wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
         w[t & 15] = wt;
     }
     const uint32_t b = v[1], c = v[2], d = v[3];
@@ -344,6 +344,33 @@ __device__ __forceinline__ void ctr_apply(Ctr &cs, int c, const uint32_t K[16], 
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) cs.carry[k] = K[12 + k];
+}
+
+// ctr_apply for a chunk wholly inside the ciphered range (64c >= off and
+// 64c + 64 <= end) with the keystream shift S = (off >> 2) & 3 known: one XOR
+// per word, no byte masks or shift selects.
+template <int S>
+__device__ __forceinline__ void ctr_apply_full(Ctr &cs, const uint32_t K[16], uint32_t d[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) d[i] ^= (i >= S) ? K[i - S] : cs.carry[4 + i - S];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cs.carry[k] = K[12 + k];
+}
+
+// ctr_apply with the unmasked form when the whole wave allows it (the steady
+// state of the fused loops: headers of one length class, interior chunks).
+__device__ __forceinline__ void ctr_apply_wave(Ctr &cs, int c, const uint32_t K[16], uint32_t d[16]) {
+    const int s = (cs.off >> 2) & 3;
+    const int su = (int)__builtin_amdgcn_readfirstlane(s);
+    const bool odd = s != su || 64 * c < cs.off || 64 * c + 64 > cs.end;
+    if (__ballot(odd) == 0ull) {
+        if (su == 0) ctr_apply_full<0>(cs, K, d);
+        else if (su == 1) ctr_apply_full<1>(cs, K, d);
+        else if (su == 2) ctr_apply_full<2>(cs, K, d);
+        else ctr_apply_full<3>(cs, K, d);
+    } else {
+        ctr_apply(cs, c, K, d);
+    }
 }
 
 // Message word (big-endian) at byte position pos of the HMAC inner stream
@@ -1020,7 +1047,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
             ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-            ctr_apply(cs, b, K, d);
+            ctr_apply_wave(cs, b, K, d);
             store_chunk_full(pkt, b, d);
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k];
@@ -1175,7 +1202,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, w);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-            ctr_apply(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
+            ctr_apply_wave(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
             store_chunk_full(pkt, b, d);
         }
     }
