@@ -817,22 +817,25 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
     return true;
 }
 
-// One wave per workgroup stages kWalkSpan consecutive sorted records in LDS
-// with one coalesced pass (plus, for unprotect, the verify pass's g0/auth_ok of
-// each record, gathered in parallel), compacts the segment starts of the span,
-// and lane l walks the l-th segment: the per-context chain reads LDS (tens of
-// cycles per record) instead of dependent HBM round trips.  The rare segment
-// that runs past the span reads its tail from global memory.
+// One wave per workgroup owns the context segments that START among kWalkSpan
+// consecutive sorted records, and stages those records plus a look-ahead of
+// kWalkAhead more in LDS with one coalesced pass (plus, for unprotect, the
+// verify pass's g0/auth_ok of each record, gathered in parallel); it compacts
+// the segment starts and lane l walks the l-th segment: the per-context chain
+// reads LDS (tens of cycles per record) instead of dependent HBM round trips.
+// Only a segment longer than the look-ahead reads its tail from global memory.
 constexpr int kWalkBlock = 64;
 constexpr int kWalkPer = 4;
 constexpr int kWalkSpan = kWalkBlock * kWalkPer;
+constexpr int kWalkAhead = 256;
+constexpr int kWalkWin = kWalkSpan + kWalkAhead;
 
 template <bool REV>
 __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pass) {
-    __shared__ WalkRec s_rec[kWalkSpan];
-    __shared__ uint32_t s_key[kWalkSpan];
-    __shared__ uint32_t s_g0[REV ? kWalkSpan : 1];
-    __shared__ uint32_t s_ok[REV ? kWalkSpan : 1];
+    __shared__ WalkRec s_rec[kWalkWin];
+    __shared__ uint32_t s_key[kWalkWin];
+    __shared__ uint32_t s_g0[REV ? kWalkWin : 1];
+    __shared__ uint32_t s_ok[REV ? kWalkWin : 1];
     __shared__ uint32_t s_start[kWalkSpan];
     __shared__ uint32_t s_nstart;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
@@ -840,11 +843,12 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
     const uint32_t base = blockIdx.x * kWalkSpan;
     if (base >= a.n) return;
     const uint32_t span = min((uint32_t)kWalkSpan, a.n - base);
+    const uint32_t win = min((uint32_t)kWalkWin, a.n - base);
     if (threadIdx.x == 0) s_nstart = 0;
 #pragma unroll
-    for (int k = 0; k < kWalkPer; k++) {
+    for (int k = 0; k < kWalkWin / kWalkBlock; k++) {
         const uint32_t j = threadIdx.x + k * kWalkBlock;
-        if (j < span) {
+        if (j < win) {
             const WalkRec r = a.sv_out[base + j];
             s_rec[j] = r;
             s_key[j] = a.sk_out[base + j];
@@ -889,7 +893,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
             const uint32_t jj = i - base;
             WalkRec r;
             uint32_t g0 = 0u, ok = 0u;
-            if (jj < span) {
+            if (jj < win) {
                 if (s_key[jj] != key) break;
                 r = s_rec[jj];
                 if (REV) { g0 = s_g0[jj]; ok = s_ok[jj]; }
