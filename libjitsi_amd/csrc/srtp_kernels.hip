@@ -311,14 +311,16 @@ __device__ __forceinline__ void ks_sha_half(const char *__restrict__ lds, const 
     ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
     constexpr int t = 40 * P;
     sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
-    aes_round2(lds, tb, rk.k + 12, x, y); sha1_rounds4<t + 8>(v, w);
-    aes_round2(lds, tb, rk.k + 16, x, y); sha1_rounds4<t + 12>(v, w);
-    aes_round2(lds, tb, rk.k + 20, x, y); sha1_rounds4<t + 16>(v, w);
-    aes_round2(lds, tb, rk.k + 24, x, y); sha1_rounds4<t + 20>(v, w);
-    aes_round2(lds, tb, rk.k + 28, x, y); sha1_rounds4<t + 24>(v, w);
-    aes_round2(lds, tb, rk.k + 32, x, y); sha1_rounds4<t + 28>(v, w);
-    aes_round2(lds, tb, rk.k + 36, x, y); sha1_rounds4<t + 32>(v, w);
-    aes_last2(lds, tb, rk.k + 40, x, y); sha1_rounds4<t + 36>(v, w);
+    // rounds 3..10: SHA-1 rounds t+8 .. t+39 inside the round asm, at its LDS
+    // wait points (aes_rounds_asm.inc)
+    aes_round2_sha<t + 8>(x, y, tb.b, rk.k + 12, v, w);
+    aes_round2_sha<t + 12>(x, y, tb.b, rk.k + 16, v, w);
+    aes_round2_sha<t + 16>(x, y, tb.b, rk.k + 20, v, w);
+    aes_round2_sha<t + 20>(x, y, tb.b, rk.k + 24, v, w);
+    aes_round2_sha<t + 24>(x, y, tb.b, rk.k + 28, v, w);
+    aes_round2_sha<t + 28>(x, y, tb.b, rk.k + 32, v, w);
+    aes_round2_sha<t + 32>(x, y, tb.b, rk.k + 36, v, w);
+    aes_last2_sha<t + 36>(x, y, tb.b, rk.k + 40, v, w);
 #pragma unroll
     for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
 }

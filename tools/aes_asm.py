@@ -116,3 +116,85 @@ def emit(name, blocks, last, tables=4):
     s.append('        : "memory");')
     s.append("}")
     return "\n".join(s)
+
+
+# ---------------------------------------------------------------- SHA-1 inside
+SHA_K = [0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xCA62C1D6]
+
+
+def sha_rounds(t0, n=4):
+    """gfx950 instructions of SHA-1 rounds t0 .. t0+n-1 on the role registers
+    %[ha]..%[he] (a..e on entry) and the 16-word schedule %[w0..15]; the
+    working variable that becomes the new `a` is written in place of `e`,
+    rotl(b, 30) in place of `b`, so after n rounds role r sits in operand
+    (r + n) mod 5 (the caller rotates its array)."""
+    regs = ["%[ha]", "%[hb]", "%[hc]", "%[hd]", "%[he]"]
+    L = []
+    for t in range(t0, t0 + n):
+        a, b, c, d, e = regs
+        w0 = f"%[w{t & 15}]"
+        if t >= 16:
+            w3, w8, w14 = (f"%[w{(t - k) & 15}]" for k in (3, 8, 14))
+            L.append(f"v_bitop3_b32 %[sx], {w3}, {w8}, {w14} bitop3:0x96")
+            L.append(f"v_xor_b32 %[sx], %[sx], {w0}")
+            L.append(f"v_alignbit_b32 {w0}, %[sx], %[sx], 31")
+        op = 0xCA if t < 20 else 0x96 if t < 40 else 0xE8 if t < 60 else 0x96
+        L.append(f"v_bitop3_b32 %[sf], {b}, {c}, {d} bitop3:{op:#x}")
+        L.append(f"v_alignbit_b32 %[sr], {a}, {a}, 27")
+        L.append(f"v_add3_u32 {e}, {e}, %[sf], %[sr]")
+        L.append(f"v_add3_u32 {e}, {e}, %[sk], {w0}")
+        L.append(f"v_alignbit_b32 {b}, {b}, {b}, 2")
+        regs = [e, a, b, c, d]
+    return L
+
+
+def merge_sha(aes, sha):
+    """Spread the SHA-1 instructions over the LDS wait points of an AES round
+    (before each s_waitcnt), so the wave computes the hash while its table
+    lookups are in flight."""
+    waits = [i for i, ln in enumerate(aes) if ln.startswith("s_waitcnt")]
+    slots = len(waits)
+    out, k = [], 0
+    for i, ln in enumerate(aes):
+        if i in waits:
+            w = waits.index(i)
+            take = (len(sha) * (w + 1)) // slots - k
+            out += sha[k:k + take]
+            k += take
+        out.append(ln)
+    out += sha[k:]
+    return out
+
+
+def emit_sha(name, blocks, last, t0, tables=4):
+    """One AES round on the block pair with SHA-1 rounds t0..t0+3 interleaved;
+    v[5]/w[16] are the hash's working variables and schedule."""
+    body = merge_sha(round_body(blocks, last, tables), sha_rounds(t0))
+    nb = len(blocks)
+    args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
+    s = [f"template <> __device__ __forceinline__ void {name}<{t0}>({args}, const uint32_t bs[4],",
+         "        const uint32_t *__restrict__ rkr, uint32_t v[5], uint32_t w[16]) {",
+         f"    uint32_t t[{16 * nb}], sf, sr, sx;"]
+    s.append("    asm volatile(")
+    for ln in body:
+        s.append(f'        "{ln}\\n"')
+    outs = [f'[{z}{i}] "+v"({z}[{i}])' for z in blocks for i in range(4)]
+    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(16 * nb)]
+    outs += [f'[h{r}] "+v"(v[{i}])' for i, r in enumerate("abcde")]
+    outs += [f'[w{i}] "+v"(w[{i}])' for i in range(16)]
+    outs += ['[sf] "=&v"(sf)', '[sr] "=&v"(sr)', '[sx] "=&v"(sx)']
+    ins = [f'[b{i}] "v"(bs[{i}])' for i in range(4)]
+    sels = SEL4 if tables == 4 else SEL2
+    ins += [f'[s{i}] "s"({sels[i]})' for i in range(4)]
+    if last:
+        ins += ['[s4] "s"(0x0c0c0601u)', '[s5] "s"(0x04000c0cu)']
+    ins += [f'[k{i}] "s"(rkr[{i}])' for i in range(4)]
+    ins += [f'[sk] "s"({SHA_K[t0 // 20]:#010x}u)']
+    s.append("        : " + ",\n          ".join(outs))
+    s.append("        : " + ",\n          ".join(ins))
+    s.append('        : "memory");')
+    # roles after 4 rounds: a in v[1], b in v[2], c in v[3], d in v[4], e in v[0]
+    s.append("    const uint32_t e_ = v[0];")
+    s.append("    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4]; v[4] = e_;")
+    s.append("}")
+    return "\n".join(s)

@@ -77,6 +77,91 @@ __global__ __launch_bounds__(THREADS, MINW) void k_aes(uint32_t *out, const uint
     for (int k = 0; k < 4; k++) out[4 * gid + k] = acc[k];
 }
 
+// ---------------------------------------------------------------- AES + SHA-1 mix
+__device__ __forceinline__ void sha1c(uint32_t h[5], uint32_t w[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; t++) {
+        uint32_t wt;
+        if (t < 16) wt = w[t];
+        else { wt = rotl(__builtin_amdgcn_bitop3_b32(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15], 0x96) ^ w[t & 15], 1); w[t & 15] = wt; }
+        uint32_t f, k;
+        if (t < 20) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA); k = 0x5A827999u; }
+        else if (t < 40) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0x6ED9EBA1u; }
+        else if (t < 60) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8); k = 0x8F1BBCDCu; }
+        else { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0xCA62C1D6u; }
+        uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+        e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// MODE 0: every wave per step: 4 AES blocks then 1 SHA-1 compression.
+// MODE 1: waves in two groups ((wave >> 2) & 1), two phases per step with a
+//         workgroup barrier between: a group does its 4 AES blocks while the
+//         other does its SHA-1 compression, then they swap.
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_mix(uint32_t *out, const uint32_t *rkg, int steps) {
+    __shared__ uint32_t s_te[32768];
+    for (int i = threadIdx.x; i < 32768; i += 1024) {
+        const int t = ((i >> 14) << 1) | ((i >> 5) & 1);
+        s_te[i] = rotl(d_te0[(i >> 6) & 255], 8u * (uint32_t)t);
+    }
+    __syncthreads();
+    asm volatile("" ::"s"(s_te) : "memory");
+    const uint32_t c4 = (threadIdx.x & 31u) << 2;
+    uint32_t bs[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) bs[t] = (uint32_t)((t >> 1) << 16) | (uint32_t)((t & 1) << 7) | c4;
+    uint32_t rk[44];
+#pragma unroll
+    for (int i = 0; i < 44; i++) rk[i] = sgpr(rkg[i]);
+    const uint32_t gid = blockIdx.x * 1024 + threadIdx.x;
+    const uint32_t iv[4] = {gid, 0x01234567u, 0x89abcdefu ^ (gid * 3u), 0x0000a5a5u};
+    uint32_t acc[4] = {0, 0, 0, 0}, h[5] = {gid, 1, 2, 3, 4}, w[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = gid * 7u + k;
+    const int grp = (threadIdx.x >> 8) & 1;
+    auto aes4 = [&](int j) {
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++) {
+            uint32_t s[2][4];
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+                const uint32_t c = (uint32_t)(j + 2 * pr + b);
+                s[b][0] = iv[0] ^ rk[0]; s[b][1] = iv[1] ^ rk[1]; s[b][2] = iv[2] ^ rk[2];
+                s[b][3] = (iv[3] | (((c >> 8) & 0xffu) << 16) | ((c & 0xffu) << 24)) ^ rk[3];
+            }
+#pragma unroll
+            for (int r = 1; r < 10; r++) mid<2, 4>(s, bs, rk + 4 * r);
+            last<2, 4>(s, bs, rk + 40);
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int k = 0; k < 4; k++) acc[k] ^= s[b][k];
+        }
+    };
+    auto sha = [&]() {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] ^= acc[k & 3];
+        sha1c(h, w);
+    };
+#pragma unroll 1
+    for (int st = 0; st < steps; st++) {
+        if (MODE == 0) {
+            aes4(4 * st);
+            sha();
+        } else {
+            if (grp == 0) aes4(4 * st); else sha();
+            __syncthreads();
+            if (grp == 0) sha(); else aes4(4 * st);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) out[4 * gid + k] = acc[k] ^ h[k] ^ h[4];
+}
+
 // ---------------------------------------------------------------- host AES
 static uint8_t SB[256];
 static uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
@@ -157,6 +242,10 @@ int main() {
         V("n2_t2_512_4w", 2, 2, 512, 4),
         V("n4_t2_1024_6w", 4, 2, 1024, 5),
         V("n2_t2_768_6w", 2, 2, 768, 6),
+        V("n2_t4_768", 2, 4, 768, 1),
+        V("n2_t4_512", 2, 4, 512, 1),
+        V("n4_t4_768", 4, 4, 768, 1),
+        V("n4_t4_512", 4, 4, 512, 1),
     };
     const int nv = sizeof vs / sizeof vs[0];
     uint32_t *d_rk, *d_out;
@@ -206,6 +295,22 @@ int main() {
         printf("%-24s wg/CU %d  %8.3f ms  %7.1f Gblk/s  %6.3f ns/blk/CU (%5.2f cyc @2.1GHz)  %s\n",
                vs[v].name, per_cu, best, blocks / best / 1e6, ns_per_block_cu, ns_per_block_cu * 2.1,
                bad ? "MISMATCH" : "ok");
+    }
+    for (int mode = 0; mode < 2; mode++) {
+        const int steps = 152;
+        float best = 1e30f;
+        for (int rep = 0; rep < 4; rep++) {
+            CHECK(hipEventRecord(e0));
+            if (mode == 0) hipLaunchKernelGGL(k_mix<0>, dim3(cus), dim3(1024), 0, 0, d_out, d_rk, steps);
+            else hipLaunchKernelGGL(k_mix<1>, dim3(cus), dim3(1024), 0, 0, d_out, d_rk, steps);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < best) best = ms;
+        }
+        const double blocks = (double)cus * 1024 * steps * 4;
+        printf("mix %s: %.3f ms  %.3f ns/blk/CU (4 AES blocks + 1 SHA-1 compression per lane-step)\n",
+               mode ? "phase-split" : "fused      ", best, best * 1e6 / (blocks / cus));
     }
     return 0;
 }
