@@ -1281,93 +1281,83 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect(BundleArgs a) {
 }
 
 // ============================================================== k_unprotect_fix
-// AES-128 with the T-table read from global memory (rare repair path only).
-__device__ void aes_encrypt_global(const KeySet *ks, uint32_t s[4]) {
-    uint32_t x0 = s[0] ^ ks->rk[0], x1 = s[1] ^ ks->rk[1], x2 = s[2] ^ ks->rk[2], x3 = s[3] ^ ks->rk[3];
-#pragma unroll 1
-    for (int r = 1; r < 10; r++) {
-        const uint32_t t0 = d_te0[x0 & 0xff] ^ rotl(d_te0[(x1 >> 8) & 0xff], 8) ^
-                            rotl(d_te0[(x2 >> 16) & 0xff], 16) ^ rotl(d_te0[x3 >> 24], 24) ^ ks->rk[4 * r];
-        const uint32_t t1 = d_te0[x1 & 0xff] ^ rotl(d_te0[(x2 >> 8) & 0xff], 8) ^
-                            rotl(d_te0[(x3 >> 16) & 0xff], 16) ^ rotl(d_te0[x0 >> 24], 24) ^ ks->rk[4 * r + 1];
-        const uint32_t t2 = d_te0[x2 & 0xff] ^ rotl(d_te0[(x3 >> 8) & 0xff], 8) ^
-                            rotl(d_te0[(x0 >> 16) & 0xff], 16) ^ rotl(d_te0[x1 >> 24], 24) ^ ks->rk[4 * r + 2];
-        const uint32_t t3 = d_te0[x3 & 0xff] ^ rotl(d_te0[(x0 >> 8) & 0xff], 8) ^
-                            rotl(d_te0[(x1 >> 16) & 0xff], 16) ^ rotl(d_te0[x2 >> 24], 24) ^ ks->rk[4 * r + 3];
-        x0 = t0; x1 = t1; x2 = t2; x3 = t3;
-    }
-#define SB(x) ((d_te0[(x)] >> 8) & 0xffu)
-    s[0] = (SB(x0 & 0xff) | (SB((x1 >> 8) & 0xff) << 8) | (SB((x2 >> 16) & 0xff) << 16) | (SB(x3 >> 24) << 24)) ^ ks->rk[40];
-    s[1] = (SB(x1 & 0xff) | (SB((x2 >> 8) & 0xff) << 8) | (SB((x3 >> 16) & 0xff) << 16) | (SB(x0 >> 24) << 24)) ^ ks->rk[41];
-    s[2] = (SB(x2 & 0xff) | (SB((x3 >> 8) & 0xff) << 8) | (SB((x0 >> 16) & 0xff) << 16) | (SB(x1 >> 24) << 24)) ^ ks->rk[42];
-    s[3] = (SB(x3 & 0xff) | (SB((x0 >> 8) & 0xff) << 8) | (SB((x1 >> 16) & 0xff) << 16) | (SB(x2 >> 24) << 24)) ^ ks->rk[43];
-#undef SB
-}
-
-// XOR AES-CM keystream(s) for IV(s) into packet bytes [off, end), 4-B words.
-__device__ void ctr_xor_global(const KeySet *ks, uint8_t *pkt, int off, int end, const uint32_t *iv_a,
-                               const uint32_t *iv_b) {
-    for (int j = 0; off + 16 * j < end; j++) {
-        uint32_t ka[4] = {0, 0, 0, 0}, kb[4] = {0, 0, 0, 0};
-        if (iv_a) {
-            ctr_input(iv_a, j, ka);
-            aes_encrypt_global(ks, ka);
-        }
-        if (iv_b) {
-            ctr_input(iv_b, j, kb);
-            aes_encrypt_global(ks, kb);
-        }
-        for (int k = 0; k < 4; k++) {
-            const int pos = off + 16 * j + 4 * k;
-            if (pos >= end) break;
-            const uint32_t ksw = ka[k] ^ kb[k];
-            for (int i = 0; i < 4 && pos + i < end; i++) pkt[pos + i] ^= (uint8_t)(ksw >> (8 * i));
-        }
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_unprotect_fix(BundleArgs a) {
+// Final statuses/lengths of an unprotect bundle, and the repair of packets
+// whose speculative decryption the walk overturned: undo the keystream of the
+// guessed ROC (or of the SRTCP trailer's index) and/or apply the walk's.
+// Usually nothing needs repair and a workgroup exits after its statuses; when
+// some do (replays, forged tags, ROC guesses overturned in-bundle -- a flood of
+// them must not cost more than a decryption), the workgroup builds the LDS
+// T-tables and repairs at full AES speed.
+__global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
+    __shared__ uint32_t s_te[kTeWords];
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.n) return;
-    const int L0 = (int)a.len[p];
-    const int32_t st = finish_status(a, p);
-    const uint32_t slot = a.p_slot[p];
-    if (slot == kNoSlot) return;
-    const uint32_t did = a.spec[p];
-    const KeySet *ks = a.keysets + a.ctx[slot].ks;
-    const bool rtp = ks->kind == SRTP_KIND_RTP;
-    bool need = false;
-    if (st == SRTP_STATUS_OK && ks->enc_type == SRTP_AESCM_ENCRYPTION) {
-        if (rtp) {
-            const uint32_t fl = a.flags ? a.flags[p] : 0u;
-            need = !(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
-        } else {
-            need = (a.w_cw[p] & 0x80000000u) != 0;
+    bool repair = false, did = false, need = false;
+    uint32_t ks_id = 0;
+    int L0 = 0;
+    if (p < a.n) {
+        L0 = (int)a.len[p];
+        const int32_t st = finish_status(a, p);
+        const uint32_t slot = a.p_slot[p];
+        if (slot != kNoSlot) {
+            did = a.spec[p] != 0u;
+            ks_id = a.ctx[slot].ks;
+            const KeySet *ks = a.keysets + ks_id;
+            const bool rtp = ks->kind == SRTP_KIND_RTP;
+            if (st == SRTP_STATUS_OK && ks->enc_type == SRTP_AESCM_ENCRYPTION) {
+                if (rtp) {
+                    const uint32_t fl = a.flags ? a.flags[p] : 0u;
+                    need = !(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
+                } else {
+                    need = (a.w_cw[p] & 0x80000000u) != 0;
+                }
+            }
+            repair = (did || need) && !(did && need && (!rtp || a.g0[p] == a.w_cw[p]));
         }
     }
-    if (!did && !need) return;
-    if (did && need && (!rtp || a.g0[p] == a.w_cw[p])) return; // speculation was right
-    // rare: undo the speculative keystream and/or apply the walk's
-    uint8_t *pkt = a.seg + a.off[p];
-    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
-    const int T = ks->tag_len;
-    const bool mac = ks->auth_type != SRTP_NULL_AUTHENTICATION;
-    uint32_t iv_spec[4], iv_real[4];
-    int off, end;
-    if (rtp) {
-        off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-        end = mac ? (L0 - T > 0 ? L0 - T : 0) : L0;
-        make_iv_rtp(ks, hdr, a.g0[p], iv_spec);
-        make_iv_rtp(ks, hdr, a.w_cw[p], iv_real);
-    } else {
-        off = 8;
-        end = mac ? (L0 - T - 4 > 0 ? L0 - T - 4 : 0) : L0;
-        const uint32_t idx = (a.w_cw[p] & 0x7FFFFFFFu);
-        const uint32_t sidx = ld_be32(pkt + L0 - 4 - T) & 0x7FFFFFFFu;
-        make_iv_rtcp(ks, hdr, sidx, iv_spec);
-        make_iv_rtcp(ks, hdr, idx, iv_real);
-    }
-    ctr_xor_global(ks, pkt, off, end, did ? iv_spec : nullptr, need ? iv_real : nullptr);
+    if (!__syncthreads_or(repair)) return; // the common case: speculation was right
+    fill_te4(s_te);
+    if (!repair) return;
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s_te);
+    for_each_keyset(true, ks_id, [&](uint32_t ks_u) {
+        const KeySet *ks = a.keysets + ks_u;
+        RoundKeys rk;
+        load_round_keys_uniform(ks, rk);
+        uint8_t *pkt = a.seg + a.off[p];
+        const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+        const int T = ks->tag_len;
+        const bool mac = ks->auth_type != SRTP_NULL_AUTHENTICATION;
+        Ctr spec, real;
+        if (ks->kind == SRTP_KIND_RTP) {
+            real.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+            real.end = mac ? (L0 - T > 0 ? L0 - T : 0) : L0;
+            make_iv_rtp(ks, hdr, a.g0[p], spec.iv);
+            make_iv_rtp(ks, hdr, a.w_cw[p], real.iv);
+        } else {
+            real.off = 8;
+            real.end = mac ? (L0 - T - 4 > 0 ? L0 - T - 4 : 0) : L0;
+            const uint32_t sidx = ld_be32(pkt + L0 - 4 - T) & 0x7FFFFFFFu;
+            make_iv_rtcp(ks, hdr, sidx, spec.iv);
+            make_iv_rtcp(ks, hdr, a.w_cw[p] & 0x7FFFFFFFu, real.iv);
+        }
+        spec.off = real.off;
+        spec.end = did ? real.end : 0;
+        const int end = real.end;
+        if (!need) real.end = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) spec.carry[k] = real.carry[k] = 0u;
+        Ctr span = real;
+        span.end = end;
+        // chunks from the one holding `off` (words before it are masked, so
+        // the keystream carry may start at zero there)
+        for (int c = span.off >> 6; 64 * c < end; c++) {
+            uint32_t d[16];
+            load_chunk(pkt, c, end, d);
+            if (did) ctr_chunk(lds, tb, rk, spec, c, d);
+            if (need) ctr_chunk(lds, tb, rk, real, c, d);
+            store_chunk(pkt, c, span, d);
+        }
+    });
     atomicAdd(&a.ctl->n_walk, 1u); // repaired packets (diagnostic)
 }
 
@@ -1414,7 +1404,7 @@ hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_unprotect_fix, grid_for(a.n), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_unprotect_fix, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,
