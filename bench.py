@@ -40,8 +40,8 @@ METRIC = "SRTP protect+unprotect packets/s + GB/s, 1200B AES_CM_128_HMAC_SHA1_80
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=1 << 18, help="bundle size per GPU")
     ap.add_argument("--ssrcs", type=int, default=10000, help="concurrent SSRCs per GPU")
     ap.add_argument("--len", type=int, default=1200, help="RTP packet length")
@@ -229,6 +229,25 @@ def main():
         except Exception:
             traffic = None
 
+    # achievable HBM bandwidth on this device (plain device-to-device copy of
+    # 512 MiB, read + write bytes), reported beside the 8 TB/s spec peak
+    copy_gbs = None
+    try:
+        src = torch.empty(1 << 29, dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dst.copy_(src)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        copy_gbs = round(5 * 2 * src.numel() / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+        del src, dst
+    except Exception:
+        copy_gbs = None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -266,6 +285,9 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE per k_protect launch, "
+                                           "profiles/pmc_traffic.json" if traffic else None,
+                         "copy_measured_gbps": copy_gbs,
                          "algorithmic_bytes_per_launch": n * (L + L + T)},
             "cpu_baseline": cpu,
         }
