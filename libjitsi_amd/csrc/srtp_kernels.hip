@@ -1193,24 +1193,42 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     const int nb_inner = ((end + 12) >> 6) + 1;
     const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
     int b = 0;
-    if (fused) { // AES-CM + HMAC, wave-uniform: full blocks before the ROC-carrying one
+    if (fused && nb_full >= 2) {
+        // AES-CM + HMAC, wave-uniform, over the full blocks before the
+        // ROC-carrying one.  As in protect, iteration b computes the keystream
+        // of chunk b beside the hash of block b-1 (loaded the iteration
+        // before), so chunk b's load has half a chunk step to land.
         const int hq = cs.off >> 4;
         CtrPre cp;
         ctr_precompute(lds, tb, rk, cs.iv, cp);
-        for (; b < nb_full; b++) {
-            if (ctr_pre_exhausted(4 * b - hq)) break; // generic loop finishes
-            uint32_t d[16], w[16], K[16];
-            load_chunk_full(pkt, b, d);
+        uint32_t c[16];
+        load_chunk_full(pkt, 0, c);
+        {   // chunk 0 holds the header: generic keystream, masked below off
+            uint32_t d[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) w[k] = bswap(d[k]);
+            for (int k = 0; k < 16; k++) d[k] = c[k];
+            ctr_chunk(lds, tb, rk, cs, 0, d);
+            store_chunk(pkt, 0, cs, d); // cs.end = 0 without speculation: no store
+        }
+        for (b = 1; b < nb_full; b++) {
+            if (ctr_pre_exhausted(4 * b - hq)) break; // generic loop finishes
             uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, w);
-            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, w);
+            uint32_t K[16], d[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
+            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+            load_chunk_full(pkt, b, d);
+            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = d[k]; // ciphertext of chunk b, hashed next
             ctr_apply_wave(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
             store_chunk_full(pkt, b, d);
         }
+#pragma unroll
+        for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
+        sha1_compress(h, c); // block b-1, a full block before the ROC-carrying one
     }
     for (; b < n_blocks; b++) {
         uint32_t d[16];
