@@ -158,6 +158,8 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->spec, m));
     e->sort_temp_bytes = sort_temp_bytes(m);
     HIPCHK(e, hipMalloc(&e->sort_temp, std::max<size_t>(e->sort_temp_bytes, 16)));
+    // per-tile digit counts start at zero (each scan re-zeroes what it read)
+    HIPCHK(e, hipMemset(e->sort_temp, 0, e->sort_temp_bytes));
     e->scratch_n = m;
     return SRTP_OK;
 }
@@ -422,6 +424,9 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
     a.tailc = e->tailc; a.spec = e->spec;
     a.e_min = e->e_min; a.ctl = e->ctl;
+    const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
+    a.sort_counts = ss.counts[0];
+    a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     HIPCHK(e, hipMemsetAsync(e->ctl, 0, sizeof(BundleCtl), s));
     if (a.abort_on_error)
         HIPCHK(e, hipMemsetAsync(e->e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
@@ -431,7 +436,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     }
     {
         StageTimer t(e, s, SRTP_STAGE_SORT);
-        HIPCHK(e, launch_sort(a, e->sort_temp, e->sort_temp_bytes, e->ctx_bits + 1, s));
+        HIPCHK(e, launch_sort(a, ss, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);

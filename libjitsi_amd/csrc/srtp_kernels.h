@@ -8,6 +8,8 @@
 
 namespace srtp {
 
+constexpr int kSortMaxPass = 4; // 8-bit digits: context tables up to 2^31 slots
+
 // Everything one bundle needs; passed by value to every kernel.
 struct BundleArgs {
     // engine tables (HBM resident)
@@ -47,12 +49,26 @@ struct BundleArgs {
     uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl;
+    // radix sort of the walk records (srtp_kernels.hip "radix sort")
+    uint32_t *sort_counts; // [tiles][256] first-digit counts per 2048-record tile, by k_parse
+    int32_t sort_passes;   // 8-bit digits to sort (key width / 8, rounded up)
+};
+
+// Layout of the sort's scratch (one allocation of sort_temp_bytes(n_max)).
+struct SortScratch {
+    uint32_t *keys_tmp;
+    WalkRec *vals_tmp;
+    uint32_t *counts[kSortMaxPass]; // [tiles][256] digit counts per tile and pass (kept zero between uses)
+    uint32_t *offsets;              // [tiles][256] scatter base per tile and digit
+    uint32_t max_tiles;
 };
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n_max);
-hipError_t launch_sort(const BundleArgs &a, void *temp, size_t temp_bytes, int end_bit,
-                       hipStream_t s);
+SortScratch sort_scratch(void *temp, uint32_t n_max);
+// Stable LSD radix sort of (sk_in, sv_in) by key into (sk_out, sv_out),
+// a.sort_passes passes of 8 bits; zeroes the other parity's histograms.
+hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s);
 // unprotect: fused tag check + speculative in-place decryption (before the walk)
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s);

@@ -28,7 +28,6 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
-#include <rocprim/rocprim.hpp>
 
 #include "../../include/srtp_mi355x.h"
 #include "srtp_kernels.h"
@@ -516,9 +515,9 @@ __device__ uint32_t ctx_lookup_insert(const BundleArgs &a, uint64_t key, bool ma
 }
 
 // ============================================================== k_parse
-__global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
-    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.n) return;
+// Returns the packet's sort key: its context slot, or ctx_mask + 1 when the
+// packet is not walked (skipped, invalid, dropped before the state machine).
+__device__ __forceinline__ uint32_t parse_one(const BundleArgs &a, uint32_t p) {
     uint32_t invalid_key = a.ctx_mask + 1u;
     a.sk_in[p] = invalid_key;
     a.p_slot[p] = kNoSlot;
@@ -529,12 +528,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
     if ((fl & SRTP_PKT_FLAG_SKIP) || tid < 0 || (uint32_t)tid >= a.n_transformers ||
         !a.transformers[tid].alive) {
         a.w_status[p] = SRTP_STATUS_SKIPPED;
-        return;
+        return invalid_key;
     }
     uint32_t C = a.cap[p];
     if (L < 12 || L > C || C > 65535u) { // RawPacket.isInvalid :903-909
         a.w_status[p] = SRTP_STATUS_DROP_INVALID;
-        return;
+        return invalid_key;
     }
     const uint8_t *pkt = a.seg + a.off[p];
     uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
@@ -545,7 +544,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
         // SRTPTransformer.reverseTransform: RTP version 2 only (:189-190)
         if (a.reverse && (b0 & 0xC0u) != 0x80u) {
             a.w_status[p] = SRTP_STATUS_DROP_VERSION;
-            return;
+            return invalid_key;
         }
         ssrc = bswap(hdr.z);  // RawPacket.getSSRC :839
     } else {
@@ -562,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
     if (slot == kNoSlot) {
         if (may_create) atomicOr(&a.ctl->overflow, 1u);
         a.w_status[p] = SRTP_STATUS_DROP_NO_CONTEXT;
-        return;
+        return invalid_key;
     }
     a.p_slot[p] = slot;
     WalkRec rec;
@@ -592,28 +591,190 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
     a.sk_in[p] = slot;
     a.sv_in[p] = rec;
     a.w_status[p] = kStPending;
+    return slot;
 }
 
-// ============================================================== sort
-// Stable radix sort of the walk records by context slot.  rocPRIM picks its
-// merge sort below 1M keys of more than 2 bytes; that path is ~1.5x slower here
-// and launches ~10 kernels per bundle, so the config forces the onesweep radix
-// path (MergeSortLimit = 0): one histogram pass + one pass per 8-bit digit.
-using SlotSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                  rocprim::default_config, 0>;
+// One lane per packet; the block also counts the first sort digit of its
+// packets' keys into their 2048-record tile (the radix sort's first pass).
+__global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
+    __shared__ uint32_t s_hist[256];
+    s_hist[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < a.n) atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
+    __syncthreads();
+    const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kBlock
+    if (s_hist[threadIdx.x]) atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
+}
+
+// ============================================================== radix sort
+// Stable LSD radix sort of the walk records by context slot, 8-bit digits,
+// reduce-then-scan per digit: the digit counts of every 2048-record tile
+// (k_parse for the first digit, the previous pass's scatter for the next),
+// one small scan kernel turning them into per-tile scatter bases, and a
+// scatter kernel that ranks each tile's digits stably in LDS.  Five launches
+// for a two-digit sort and no memsets: each scan zeroes the counts it read.
+constexpr int kSortThreads = 256, kSortItems = 8, kSortTile = kSortThreads * kSortItems;
+static_assert(kSortTile == 2048 && kSortTile % kBlock == 0, "k_parse tiles");
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t sort_temp_bytes(uint32_t n_max) {
-    size_t bytes = 0;
-    (void)rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, bytes, (uint32_t *)nullptr,
-                                                    (uint32_t *)nullptr, (WalkRec *)nullptr,
-                                                    (WalkRec *)nullptr, (size_t)n_max, 0, 32);
-    return bytes;
+    const size_t tiles = (n_max + kSortTile - 1) / kSortTile;
+    return align256((size_t)n_max * 4) + align256((size_t)n_max * sizeof(WalkRec)) +
+           (kSortMaxPass + 1) * align256(tiles * 256 * 4);
 }
 
-hipError_t launch_sort(const BundleArgs &a, void *temp, size_t temp_bytes, int end_bit,
-                       hipStream_t s) {
-    return rocprim::radix_sort_pairs<SlotSortConfig>(temp, temp_bytes, a.sk_in, a.sk_out, a.sv_in,
-                                                     a.sv_out, (size_t)a.n, 0, (unsigned)end_bit, s);
+SortScratch sort_scratch(void *temp, uint32_t n_max) {
+    SortScratch ss;
+    char *p = reinterpret_cast<char *>(temp);
+    ss.max_tiles = (n_max + kSortTile - 1) / kSortTile;
+    const size_t cb = align256((size_t)ss.max_tiles * 256 * 4);
+    ss.keys_tmp = reinterpret_cast<uint32_t *>(p); p += align256((size_t)n_max * 4);
+    ss.vals_tmp = reinterpret_cast<WalkRec *>(p); p += align256((size_t)n_max * sizeof(WalkRec));
+    for (int q = 0; q < kSortMaxPass; q++) { ss.counts[q] = reinterpret_cast<uint32_t *>(p); p += cb; }
+    ss.offsets = reinterpret_cast<uint32_t *>(p);
+    return ss;
+}
+
+// One block of 1024: offsets[t][d] = (records with a smaller digit) +
+// (records with digit d in tiles before t); then zeroes the counts for the next
+// bundle.  Thread (g, d) covers digit d over a quarter of the tiles, reading
+// them 8 at a time so the loads overlap.
+constexpr int kScanGroups = 4;
+__global__ __launch_bounds__(256 * kScanGroups) void k_sort_scan(uint32_t *counts, uint32_t *offsets,
+                                                                 uint32_t tiles) {
+    __shared__ uint32_t s_part[kScanGroups][256], s_tot[256];
+    const int d = threadIdx.x & 255, g = threadIdx.x >> 8;
+    const uint32_t per = (tiles + kScanGroups - 1) / kScanGroups;
+    const uint32_t t0 = min(tiles, g * per), t1 = min(tiles, t0 + per);
+    uint32_t sum = 0u;
+    for (uint32_t t = t0; t < t1; t += 8) {
+        uint32_t c[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += c[k];
+    }
+    s_part[g][d] = sum;
+    __syncthreads();
+    if (g == 0) {
+        uint32_t tot = 0u;
+#pragma unroll
+        for (int k = 0; k < kScanGroups; k++) tot += s_part[k][d];
+        s_tot[d] = tot;
+    }
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) { // inclusive scan of the digit totals
+        uint32_t x = 0u;
+        if (g == 0 && d >= o) x = s_tot[d - o];
+        __syncthreads();
+        if (g == 0) s_tot[d] += x;
+        __syncthreads();
+    }
+    uint32_t run = 0u;
+    for (int k = 0; k < kScanGroups; k++) run += s_part[k][d];
+    run = s_tot[d] - run; // records with a smaller digit
+    for (int k = 0; k < g; k++) run += s_part[k][d];
+    for (uint32_t t = t0; t < t1; t += 8) {
+        uint32_t c[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (t + k < t1) {
+                offsets[(t + k) * 256 + d] = run;
+                counts[(t + k) * 256 + d] = 0u;
+            }
+            run += c[k];
+        }
+    }
+}
+
+struct SortPass {
+    const uint32_t *sk;
+    const WalkRec *sv;
+    uint32_t *dk;
+    WalkRec *dv;
+    uint32_t n, shift;
+    const uint32_t *offsets;  // [tiles][256]
+    uint32_t *next_counts;    // next pass's [tiles][256] counts, or null on the last pass
+};
+
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
+    __shared__ uint32_t s_base[256], s_run[256], s_wcnt[kSortThreads / 64][256];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t tile = blockIdx.x, base = tile * kSortTile;
+    s_base[t] = sp.offsets[tile * 256 + t];
+    s_run[t] = 0u;
+#pragma unroll
+    for (int k = 0; k < kSortThreads / 64; k++) s_wcnt[k][t] = 0u;
+    uint32_t key[kSortItems], loc[kSortItems];
+    WalkRec val[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < sp.n) { key[r] = sp.sk[i]; val[r] = sp.sv[i]; }
+    }
+    __syncthreads();
+    // stable local ranks: items in order r-major, t-minor (= index order)
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const bool valid = base + r * kSortThreads + t < sp.n;
+        const uint32_t d = valid ? (key[r] >> sp.shift) & 255u : 0u;
+        unsigned long long m = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const unsigned long long b = __ballot((d >> bit) & 1u);
+            m &= ((d >> bit) & 1u) ? b : ~b;
+        }
+        const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (valid && below == 0u) s_wcnt[w][d] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = s_run[d];
+            for (int k = 0; k < w; k++) pre += s_wcnt[k][d];
+            loc[r] = pre + below;
+        }
+        __syncthreads();
+        uint32_t add = 0u;
+#pragma unroll
+        for (int k = 0; k < kSortThreads / 64; k++) { add += s_wcnt[k][t]; s_wcnt[k][t] = 0u; }
+        s_run[t] += add;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        if (base + r * kSortThreads + t < sp.n) {
+            const uint32_t pos = s_base[(key[r] >> sp.shift) & 255u] + loc[r];
+            sp.dk[pos] = key[r];
+            sp.dv[pos] = val[r];
+            if (sp.next_counts)
+                atomicAdd(&sp.next_counts[(pos / kSortTile) * 256 + ((key[r] >> (sp.shift + 8)) & 255u)], 1u);
+        }
+    }
+}
+
+hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s) {
+    const uint32_t tiles = (a.n + kSortTile - 1) / kSortTile;
+    const int P = a.sort_passes;
+    for (int q = 0; q < P; q++) {
+        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(256 * kScanGroups), 0, s, ss.counts[q], ss.offsets,
+                           tiles);
+        SortPass sp;
+        // ping-pong: in -> tmp -> (out | in) -> (out | tmp) -> out
+        const bool last = q == P - 1;
+        sp.sk = q == 0 ? a.sk_in : (q & 1) ? ss.keys_tmp : a.sk_in;
+        sp.sv = q == 0 ? a.sv_in : (q & 1) ? ss.vals_tmp : a.sv_in;
+        sp.dk = last ? a.sk_out : (q & 1) ? a.sk_in : ss.keys_tmp;
+        sp.dv = last ? a.sv_out : (q & 1) ? a.sv_in : ss.vals_tmp;
+        sp.n = a.n;
+        sp.shift = 8u * (uint32_t)q;
+        sp.offsets = ss.offsets;
+        sp.next_counts = last ? nullptr : ss.counts[q + 1];
+        hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
+    }
+    return hipGetLastError();
 }
 
 // Runs body(ks) once per distinct session-key set among this wave's lanes with
