@@ -296,6 +296,34 @@ __device__ __forceinline__ bool ctr_pre_exhausted(int j0) {
     return __ballot(j0 + 3 >= 256) != 0ull;
 }
 
+__device__ __forceinline__ void ctr_apply(Ctr &cs, int c, const uint32_t K[16], uint32_t d[16]);
+
+// ctr_chunk with rounds 1-2 from the counter precompute when no active lane's
+// blocks of chunk c reach index 256 (otherwise the full rounds).
+__device__ __forceinline__ void ctr_chunk_pre(const char *__restrict__ lds, const TeBase &tb,
+                                              const RoundKeys &rk, const CtrPre &cp, Ctr &cs, int c,
+                                              uint32_t d[16]) {
+    const int j0 = 4 * c - (cs.off >> 4);
+    if (ctr_pre_exhausted(j0)) {
+        ctr_chunk(lds, tb, rk, cs, c, d);
+        return;
+    }
+    uint32_t K[16];
+#pragma unroll 1
+    for (int pr = 0; pr < 2; pr++) {
+        uint32_t x[4], y[4];
+        ctr_first2(lds, tb, cp, j0 + 2 * pr, j0 + 2 * pr + 1, x, y);
+#pragma unroll
+        for (int r = 3; r < 10; r++) aes_round2(lds, tb, rk.k + 4 * r, x, y);
+        aes_last2(lds, tb, rk.k + 40, x, y);
+#pragma unroll
+        for (int k = 0; k < 8; k++) K[k] = K[k + 8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { K[8 + k] = x[k]; K[12 + k] = y[k]; }
+    }
+    ctr_apply(cs, c, K, d);
+}
+
 // Half P (0/1) of the interleaved chunk step: keystream blocks j0+2P, j0+2P+1
 // into K8[8] and SHA-1 rounds 40P .. 40P+39 on v / w.  Rounds 1-2 come from
 // the counter precompute (8 SHA-1 rounds beside them), then after each
@@ -1194,14 +1222,14 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     // (Chunks 1..B-1 lie wholly inside the packet: unconditional 64-B loads and
     // stores; bytes outside [off, end) are written back unchanged.)
     const int B = L >> 6;
+    CtrPre cp; // AES-CM rounds 1-2 of this packet's counter blocks
+    if (do_enc) ctr_precompute(lds, tb, rk, cs.iv, cp);
     if (fused && B >= 2) {
         uint32_t c[16];
         load_chunk(pkt, 0, L, c);
-        ctr_chunk(lds, tb, rk, cs, 0, c);
+        ctr_chunk_pre(lds, tb, rk, cp, cs, 0, c);
         store_chunk(pkt, 0, cs, c);
         const int hq = cs.off >> 4;
-        CtrPre cp;
-        ctr_precompute(lds, tb, rk, cs.iv, cp);
         for (b = 1; b < B; b++) {
             // packets past ~4 KB: the generic loop below finishes them
             if (ctr_pre_exhausted(4 * b - hq)) break;
@@ -1235,7 +1263,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
                 w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
             }
             if (do_enc && 64 * b + 64 > cs.off) {
-                ctr_chunk(lds, tb, rk, cs, b, w);
+                ctr_chunk_pre(lds, tb, rk, cp, cs, b, w);
 #pragma unroll
                 for (int m = 0; m < 4; m++)
                     if (64 * b + 16 * m < L && 64 * b + 16 * m + 16 > cs.off)
@@ -1368,7 +1396,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             uint32_t d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) d[k] = c[k];
-            ctr_chunk(lds, tb, rk, cs, 0, d);
+            ctr_chunk_pre(lds, tb, rk, cp, cs, 0, d);
             store_chunk(pkt, 0, cs, d); // cs.end = 0 without speculation: no store
         }
         for (b = 1; b < nb_full; b++) {

@@ -8,7 +8,10 @@
 #include <stdint.h>
 #include <vector>
 
-constexpr int kN = 262144, kLen = 1200, kStride = 1216;
+#ifndef STRIDE
+#define STRIDE 1216
+#endif
+constexpr int kN = 262144, kLen = 1200, kStride = STRIDE;
 
 __global__ void k_stream_rd(const uint4 *src, size_t n16, uint32_t *out) {
     uint32_t acc = 0;
