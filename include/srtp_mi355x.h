@@ -157,6 +157,24 @@ int srtp_get_context_state(srtp_engine *e, int32_t transformer, uint32_t ssrc,
 /* number of live contexts in the engine's table */
 int64_t srtp_engine_num_contexts(srtp_engine *e);
 
+/* Context-state export / import: lets a stream's ROC, s_l,
+ * replay window and SRTCP indices follow it to another engine or GPU (SSRC
+ * re-sharding, failover) or survive a transformer rebuild.  The reference keeps
+ * this state inside SRTPCryptoContext (srtp/SRTPCryptoContext.java:96-135) with
+ * no API for it; DtlsPacketTransformer rebuilds contexts from scratch on rekey
+ * (tf/dtls/DtlsPacketTransformer.java:614-642).
+ *
+ * srtp_export_contexts writes up to `max` (ssrc, state) pairs of the
+ * transformer's contexts and sets *count to the number it has (which may
+ * exceed max).  srtp_set_context_state creates or overwrites the transformer's
+ * context for ssrc with *st (key_set ignored); its session keys are those of
+ * the transformer's forward (forward = 1) or reverse factory, which must be
+ * open.  Both synchronise the engine's device. */
+int srtp_export_contexts(srtp_engine *e, int32_t transformer, uint32_t *ssrcs,
+                         srtp_ctx_state *states, uint32_t max, uint32_t *count);
+int srtp_set_context_state(srtp_engine *e, int32_t transformer, uint32_t ssrc, int32_t forward,
+                           const srtp_ctx_state *st);
+
 /* Per-stage kernel timing with HIP events recorded on the bundle's stream
  * (measurement hook for bench.py; off by default). */
 #define SRTP_STAGE_PARSE 0

@@ -32,7 +32,8 @@ EXPORTED = [
     "srtp_transformer_create", "srtp_transformer_set_factory", "srtp_transformer_close",
     "srtp_transform_device", "srtp_transform_host", "srtp_engine_sync",
     "srtp_get_context_state", "srtp_engine_num_contexts", "srtp_engine_set_timing",
-    "srtp_engine_read_timing", "srtp_derive_session_keys",
+    "srtp_engine_read_timing", "srtp_derive_session_keys", "srtp_export_contexts",
+    "srtp_set_context_state",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -95,6 +96,8 @@ def lib() -> C.CDLL:
     L.srtp_engine_set_timing.argtypes = [vp, i32]
     L.srtp_engine_read_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.srtp_derive_session_keys.argtypes = [pu8, pu8, i32, pu8, pu8, pu8]
+    L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
+    L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     _lib = L
     return L
 

@@ -551,6 +551,81 @@ int srtp_get_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, srtp_ctx_st
     return 0;
 }
 
+static void fill_state(const CtxState &s, const KeySet &ks, srtp_ctx_state *out) {
+    memset(out, 0, sizeof *out);
+    out->key_set = s.ks;
+    out->replay_window = s.window;
+    if (ks.kind == SRTP_KIND_RTP) {
+        out->roc = s.a; out->s_l = s.b; out->seq_num_set = (int32_t)(s.flags & 1u);
+        out->guessed_roc = s.g;
+    } else {
+        out->sent_index = s.a; out->received_index = s.b;
+    }
+}
+
+int srtp_export_contexts(srtp_engine *e, int32_t t, uint32_t *ssrcs, srtp_ctx_state *states,
+                         uint32_t max, uint32_t *count) {
+    if (!e || !count || (max && (!ssrcs || !states))) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (t < 0 || (size_t)t >= e->transformers.size()) return fail(e, SRTP_EINVAL, "bad transformer id");
+    HIPCHK(e, hipDeviceSynchronize());
+    std::vector<uint64_t> keys(e->ctx_cap);
+    std::vector<CtxState> ctx(e->ctx_cap);
+    HIPCHK(e, hipMemcpy(keys.data(), e->d_ctx_keys, keys.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(ctx.data(), e->d_ctx, ctx.size() * sizeof(CtxState), hipMemcpyDeviceToHost));
+    std::vector<KeySet> ks(e->n_keysets);
+    if (!ks.empty())
+        HIPCHK(e, hipMemcpy(ks.data(), e->d_keysets, ks.size() * sizeof(KeySet), hipMemcpyDeviceToHost));
+    uint32_t n = 0;
+    for (uint32_t h = 0; h < e->ctx_cap; h++) {
+        const uint64_t k = keys[h];
+        if (k == kEmptyKey || k == kTombKey || (int32_t)(k >> 32) != t) continue;
+        if (n < max) {
+            ssrcs[n] = (uint32_t)k;
+            fill_state(ctx[h], ks[ctx[h].ks], &states[n]);
+        }
+        n++;
+    }
+    for (auto &x : ks) memset(&x, 0, sizeof x);
+    *count = n;
+    return SRTP_OK;
+}
+
+int srtp_set_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, int32_t forward,
+                           const srtp_ctx_state *st) {
+    if (!e || !st) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (t < 0 || (size_t)t >= e->transformers.size()) return fail(e, SRTP_EINVAL, "bad transformer id");
+    const TransformerRec &tr = e->transformers[t];
+    if (!tr.alive) return fail(e, SRTP_EINVAL, "transformer closed");
+    const int32_t f = forward ? tr.fwd : tr.rev;
+    if (f < 0 || !e->factories[f].open) return fail(e, SRTP_EPOLICY, "factory closed");
+    CtxState s{};
+    s.ks = (uint32_t)(tr.kind == SRTP_KIND_RTP ? e->factories[f].ks_rtp : e->factories[f].ks_rtcp);
+    s.window = st->replay_window;
+    if (tr.kind == SRTP_KIND_RTP) {
+        s.a = st->roc; s.b = st->s_l; s.g = st->guessed_roc; s.flags = st->seq_num_set ? 1u : 0u;
+    } else {
+        s.a = st->sent_index; s.b = st->received_index;
+    }
+    s.birth = 0;
+    HIPCHK(e, hipDeviceSynchronize());
+    const uint64_t key = ((uint64_t)(uint32_t)t << 32) | ssrc;
+    const uint32_t mask = e->ctx_cap - 1;
+    uint32_t h = (uint32_t)mix64_host(key) & mask, free_slot = kNoSlot;
+    for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        uint64_t k;
+        HIPCHK(e, hipMemcpy(&k, e->d_ctx_keys + h, 8, hipMemcpyDeviceToHost));
+        if (k == key) { free_slot = h; break; }
+        if (k == kTombKey && free_slot == kNoSlot) free_slot = h; // reuse, but keep probing for key
+        if (k == kEmptyKey) { if (free_slot == kNoSlot) free_slot = h; break; }
+    }
+    if (free_slot == kNoSlot) return fail(e, SRTP_EFULL, "context table full");
+    HIPCHK(e, hipMemcpy(e->d_ctx + free_slot, &s, sizeof s, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_ctx_keys + free_slot, &key, 8, hipMemcpyHostToDevice));
+    return SRTP_OK;
+}
+
 int64_t srtp_engine_num_contexts(srtp_engine *e) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);

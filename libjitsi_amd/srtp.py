@@ -148,6 +148,30 @@ class SRTPEngine:
             return None
         return {k: getattr(st, k) for k, _ in N.CtxState._fields_}
 
+    def export_contexts(self, transformer: "_SRTPBase") -> dict:
+        """{ssrc: state} of every context the transformer holds:
+        ROC / s_l / replay window / SRTCP indices, to move a stream to another
+        engine or GPU with srtp_set_context_state."""
+        L = N.lib()
+        cnt = C.c_uint32()
+        N.check(L.srtp_export_contexts(self.h, transformer.tid, None, None, 0, C.byref(cnt)), self.h,
+                "export_contexts")
+        n = cnt.value
+        ssrcs = (C.c_uint32 * max(n, 1))()
+        states = (N.CtxState * max(n, 1))()
+        N.check(L.srtp_export_contexts(self.h, transformer.tid, ssrcs, states, n, C.byref(cnt)),
+                self.h, "export_contexts")
+        return {int(ssrcs[i]): {k: getattr(states[i], k) for k, _ in N.CtxState._fields_}
+                for i in range(min(n, cnt.value))}
+
+    def import_context(self, transformer: "_SRTPBase", ssrc: int, state: dict,
+                       forward: bool) -> None:
+        """Create or overwrite the transformer's context for ssrc with an
+        exported state, keyed by its forward or reverse factory."""
+        st = N.CtxState(**{k: state.get(k, 0) for k, _ in N.CtxState._fields_})
+        N.check(N.lib().srtp_set_context_state(self.h, transformer.tid, ssrc & 0xFFFFFFFF,
+                                               int(forward), C.byref(st)), self.h, "import_context")
+
     # -- bundle entry points -------------------------------------------------
     def transform_host(self, reverse: bool, tid, seg: np.ndarray, off: np.ndarray,
                        length: np.ndarray, cap: np.ndarray, flags=None) -> np.ndarray:
