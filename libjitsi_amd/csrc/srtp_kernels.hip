@@ -1079,26 +1079,31 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
         const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
         const uint32_t first_p = s_rec[j].p & kRecIdxMask;
-#pragma unroll 1
-        for (uint32_t i = base + j; i < a.n; i++) {
-            const uint32_t jj = i - base;
-            WalkRec r;
+        // One record of the chain; false ends it.
+        auto step = [&](const WalkRec &r, uint32_t g0, uint32_t ok) -> bool {
+            if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) return false;
+            if (a.debug == 2) { st.window += r.p ^ g0 ^ ok; return true; }
+            return walk_one(a, ks, c, st, r, g0, ok, dry, tid);
+        };
+        // The staged window, from LDS only: no global load in this loop, so
+        // nothing waits on vmcnt -- which would also wait for walk_one's
+        // status stores of earlier records.
+        uint32_t jj = j;
+        bool more = true;
+        for (; jj < win; jj++) {
+            if (s_key[jj] != key) { more = false; break; }
+            if (!step(s_rec[jj], REV ? s_g0[jj] : 0u, REV ? s_ok[jj] : 0u)) { more = false; break; }
+        }
+        // A chain longer than the look-ahead continues from global memory.
+        for (uint32_t i = base + jj; more && i < a.n; i++) {
+            if (a.sk_out[i] != key) break;
+            const WalkRec r = a.sv_out[i];
             uint32_t g0 = 0u, ok = 0u;
-            if (jj < win) {
-                if (s_key[jj] != key) break;
-                r = s_rec[jj];
-                if (REV) { g0 = s_g0[jj]; ok = s_ok[jj]; }
-            } else {
-                if (a.sk_out[i] != key) break;
-                r = a.sv_out[i];
-                if (REV) {
-                    const uint32_t p = r.p & kRecIdxMask;
-                    g0 = a.g0[p]; ok = a.auth_ok[p];
-                }
+            if (REV) {
+                const uint32_t p = r.p & kRecIdxMask;
+                g0 = a.g0[p]; ok = a.auth_ok[p];
             }
-            if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) break;
-            if (a.debug == 2) { st.window += r.p ^ g0 ^ ok; continue; }
-            if (!walk_one(a, ks, c, st, r, g0, ok, dry, tid)) break;
+            if (!step(r, g0, ok)) break;
         }
         if (dry) continue; // first of two passes: state is committed by the limit pass
         if (limit_pass && st.birth == a.serial && (int32_t)first_p > E) {
