@@ -642,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
 // one small scan kernel turning them into per-tile scatter bases, and a
 // scatter kernel that ranks each tile's digits stably in LDS.  Five launches
 // for a two-digit sort and no memsets: each scan zeroes the counts it read.
-constexpr int kSortThreads = 256, kSortItems = 8, kSortTile = kSortThreads * kSortItems;
+constexpr int kSortThreads = 512, kSortItems = 4, kSortTile = kSortThreads * kSortItems;
 static_assert(kSortTile == 2048 && kSortTile % kBlock == 0, "k_parse tiles");
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -668,7 +668,7 @@ SortScratch sort_scratch(void *temp, uint32_t n_max) {
 // One block of 1024: offsets[t][d] = (records with a smaller digit) +
 // (records with digit d in tiles before t); then zeroes the counts for the next
 // bundle.  Thread (g, d) covers digit d over a quarter of the tiles, reading
-// them 8 at a time so the loads overlap.
+// them 32 at a time so the loads overlap.
 constexpr int kScanGroups = 4;
 __global__ __launch_bounds__(256 * kScanGroups) void k_sort_scan(uint32_t *counts, uint32_t *offsets,
                                                                  uint32_t tiles) {
@@ -677,12 +677,12 @@ __global__ __launch_bounds__(256 * kScanGroups) void k_sort_scan(uint32_t *count
     const uint32_t per = (tiles + kScanGroups - 1) / kScanGroups;
     const uint32_t t0 = min(tiles, g * per), t1 = min(tiles, t0 + per);
     uint32_t sum = 0u;
-    for (uint32_t t = t0; t < t1; t += 8) {
-        uint32_t c[8];
+    for (uint32_t t = t0; t < t1; t += 32) {
+        uint32_t c[32];
 #pragma unroll
-        for (int k = 0; k < 8; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
+        for (int k = 0; k < 32; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
 #pragma unroll
-        for (int k = 0; k < 8; k++) sum += c[k];
+        for (int k = 0; k < 32; k++) sum += c[k];
     }
     s_part[g][d] = sum;
     __syncthreads();
@@ -704,12 +704,12 @@ __global__ __launch_bounds__(256 * kScanGroups) void k_sort_scan(uint32_t *count
     for (int k = 0; k < kScanGroups; k++) run += s_part[k][d];
     run = s_tot[d] - run; // records with a smaller digit
     for (int k = 0; k < g; k++) run += s_part[k][d];
-    for (uint32_t t = t0; t < t1; t += 8) {
-        uint32_t c[8];
+    for (uint32_t t = t0; t < t1; t += 32) {
+        uint32_t c[32];
 #pragma unroll
-        for (int k = 0; k < 8; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
+        for (int k = 0; k < 32; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < 32; k++) {
             if (t + k < t1) {
                 offsets[(t + k) * 256 + d] = run;
                 counts[(t + k) * 256 + d] = 0u;
@@ -733,10 +733,12 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
     __shared__ uint32_t s_base[256], s_run[256], s_wcnt[kSortThreads / 64][256];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t tile = blockIdx.x, base = tile * kSortTile;
-    s_base[t] = sp.offsets[tile * 256 + t];
-    s_run[t] = 0u;
+    if (t < 256) {
+        s_base[t] = sp.offsets[tile * 256 + t];
+        s_run[t] = 0u;
 #pragma unroll
-    for (int k = 0; k < kSortThreads / 64; k++) s_wcnt[k][t] = 0u;
+        for (int k = 0; k < kSortThreads / 64; k++) s_wcnt[k][t] = 0u;
+    }
     uint32_t key[kSortItems], loc[kSortItems];
     WalkRec val[kSortItems];
 #pragma unroll
@@ -765,10 +767,12 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
             loc[r] = pre + below;
         }
         __syncthreads();
-        uint32_t add = 0u;
+        if (t < 256) {
+            uint32_t add = 0u;
 #pragma unroll
-        for (int k = 0; k < kSortThreads / 64; k++) { add += s_wcnt[k][t]; s_wcnt[k][t] = 0u; }
-        s_run[t] += add;
+            for (int k = 0; k < kSortThreads / 64; k++) { add += s_wcnt[k][t]; s_wcnt[k][t] = 0u; }
+            s_run[t] += add;
+        }
         __syncthreads();
     }
 #pragma unroll
