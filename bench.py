@@ -48,6 +48,9 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the receiver on the sender's stream (no overlap between "
+                         "step i's unprotect and step i+1's protect)")
     ap.add_argument("--policy", default="AES_CM_128_HMAC_SHA1_80",
                     help="protection profile; 'AES_CM_128_NULL_AUTH' (cipher only) is a "
                          "diagnostic split of the fused kernel, not the headline metric")
@@ -120,8 +123,16 @@ def main():
     # context table: >= 1.6x the SSRCs (load <= 0.31 at 10k); its size sets the
     # sort's key width (2^15 slots + the invalid key: 16 bits = two radix passes)
     max_ctx = 1 << max(12, (int(1.6 * nssrc) - 1).bit_length())
+    # The sender and the receiver side each get an engine of their own (its own
+    # scratch, context table and bundle stream), as a send thread and a receive
+    # thread would: step i's unprotect (receiver stream, after step i's protect)
+    # overlaps step i+1's protect (sender stream).  --serial: one engine, one
+    # stream, every kernel in order.
     eng = SRTPEngine(device=local_rank, max_contexts=max_ctx, max_factories=64,
                      max_transformers=64, max_batch=n)
+    eng_r = eng if args.serial else SRTPEngine(device=local_rank, max_contexts=max_ctx,
+                                               max_factories=64, max_transformers=64,
+                                               max_batch=n)
     (k, s), = synth.keys(2 + rank, 1)
     if args.policy == "AES_CM_128_NULL_AUTH":
         from libjitsi_amd import SRTPPolicy as P
@@ -129,14 +140,16 @@ def main():
     else:
         pols = profile_policies(args.policy)
     snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
-    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng))
+    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng_r))
 
     off = torch.from_numpy(b.off.view(np.int32)).to(dev)
     cap = torch.from_numpy(b.cap.view(np.int32)).to(dev)
-    st = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)      # sender statuses
+    st_r = torch.empty(n, dtype=torch.int32, device=dev)    # receiver statuses
     off64 = off.to(torch.int64)
     seq_step = -(-n // nssrc)  # packets per SSRC per bundle
     stream = torch.cuda.current_stream(dev)
+    stream_r = stream if args.serial else torch.cuda.Stream(dev)
 
     def advance_seq(seg, k):
         """Advance every packet's RTP sequence number by k bundles' worth."""
@@ -164,19 +177,31 @@ def main():
     del base
     torch.cuda.synchronize(dev)
 
-    def step(i):
+    protected = [torch.cuda.Event() for _ in range(ring)]
+    received = [None] * ring
+
+    def step(i, serial=args.serial):
         j = i % ring
         if i >= ring:
+            if received[j] is not None:
+                stream.wait_event(received[j])  # unprotect of step i - ring is done
             advance_seq(segs[j], ring)
         eng.transform_device(False, snd.tid, segs[j], off, lens[j], cap, st, stream=stream)
-        eng.transform_device(True, rcv.tid, segs[j], off, lens[j], cap, st, stream=stream)
+        rs = stream if serial else stream_r
+        if rs is not stream:
+            protected[j].record(stream)
+            rs.wait_event(protected[j])
+        eng_r.transform_device(True, rcv.tid, segs[j], off, lens[j], cap, st_r, stream=rs)
+        if rs is not stream:
+            received[j] = torch.cuda.Event()
+            received[j].record(rs)
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    bad = int((st != 0).sum())
+    bad = int((st != 0).sum()) + int((st_r != 0).sum())
     if bad:
-        hist = torch.bincount(st.to(torch.int64), minlength=10).tolist()
+        hist = torch.bincount(torch.cat([st, st_r]).to(torch.int64), minlength=10).tolist()
         raise SystemExit(f"rank {rank}: {bad} packets not accepted after warmup; status "
                          f"histogram {hist}")
     if world > 1:
@@ -191,18 +216,26 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ok = int((st != 0).sum()) == 0 and all(int((x != L).sum()) == 0 for x in lens)
+    ok = (int((st != 0).sum()) == 0 and int((st_r != 0).sum()) == 0
+          and all(int((x != L).sum()) == 0 for x in lens))
     # Per-stage HIP-event timing (k_protect's launch duration for the roofline)
-    # in a separate, untimed pass: the event records would otherwise sit
+    # in a separate, untimed pass, serial (one stream, so no stage shares the
+    # GPU with the other direction): the event records would otherwise sit
     # between the kernels of the timed steps.
-    eng.set_timing(True)
-    eng.read_timing()
+    engines = [eng] if eng_r is eng else [eng, eng_r]
+    for e in engines:
+        e.set_timing(True)
+        e.read_timing()
     for i in range(total, total + min(args.steps, 10)):
-        step(i)
+        step(i, serial=True)
     torch.cuda.synchronize(dev)
-    timing = eng.read_timing()
-    eng.set_timing(False)
-    ok = ok and int((st != 0).sum()) == 0
+    timing = {}
+    for e in engines:
+        for key, (ms, cnt) in e.read_timing().items():
+            m0, c0 = timing.get(key, (0.0, 0))
+            timing[key] = (m0 + ms, c0 + cnt)
+        e.set_timing(False)
+    ok = ok and int((st != 0).sum()) == 0 and int((st_r != 0).sum()) == 0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -276,7 +309,9 @@ def main():
             "config": {"workload": "configs[1]: 10k concurrent SSRCs x 1200-B RTP, "
                                    "AES_CM_128_HMAC_SHA1_80, protect then unprotect",
                        "packets_per_gpu_per_step": n, "ssrcs_per_gpu": nssrc, "pkt_len": L,
-                       "parallelism": f"ssrc-sharded x{world}"},
+                       "parallelism": f"ssrc-sharded x{world}",
+                       "streams": "serial" if args.serial else
+                                  "sender + receiver engine, one stream each"},
             "gbps": round(gbs, 2),
             "goodput_gbps": round(pps * L * 2 / 1e9, 2),
             "all_accepted": ok,

@@ -425,8 +425,10 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.tailc = e->tailc; a.spec = e->spec;
     a.e_min = e->e_min; a.ctl = e->ctl;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
-    a.sort_counts = ss.counts[0];
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
+    a.sort_counts = ss.counts[0];
+    a.sort_zero = ss.counts[a.sort_passes - 1];
+    a.sort_zero_words = ((n + 2047u) / 2048u) * 256u; // tiles of this bundle x 256 digits
     HIPCHK(e, hipMemsetAsync(e->ctl, 0, sizeof(BundleCtl), s));
     if (a.abort_on_error)
         HIPCHK(e, hipMemsetAsync(e->e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));

@@ -52,6 +52,8 @@ struct BundleArgs {
     // radix sort of the walk records (srtp_kernels.hip "radix sort")
     uint32_t *sort_counts; // [tiles][256] first-digit counts per 2048-record tile, by k_parse
     int32_t sort_passes;   // 8-bit digits to sort (key width / 8, rounded up)
+    uint32_t *sort_zero;   // the last pass's digit counts, re-zeroed by k_walk
+    uint32_t sort_zero_words;
 };
 
 // Layout of the sort's scratch (one allocation of sort_temp_bytes(n_max)).
@@ -59,7 +61,6 @@ struct SortScratch {
     uint32_t *keys_tmp;
     WalkRec *vals_tmp;
     uint32_t *counts[kSortMaxPass]; // [tiles][256] digit counts per tile and pass (kept zero between uses)
-    uint32_t *offsets;              // [tiles][256] scatter base per tile and digit
     uint32_t max_tiles;
 };
 

@@ -639,9 +639,10 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
 // Stable LSD radix sort of the walk records by context slot, 8-bit digits,
 // reduce-then-scan per digit: the digit counts of every 2048-record tile
 // (k_parse for the first digit, the previous pass's scatter for the next),
-// one small scan kernel turning them into per-tile scatter bases, and a
-// scatter kernel that ranks each tile's digits stably in LDS.  Five launches
-// for a two-digit sort and no memsets: each scan zeroes the counts it read.
+// and one scatter kernel per digit that turns them into its tile's scatter
+// bases and ranks the tile's digits stably in LDS.  Two launches for a
+// two-digit sort and no memsets: pass q re-zeroes pass q-1's counts, k_walk
+// the last pass's.
 constexpr int kSortThreads = 512, kSortItems = 4, kSortTile = kSortThreads * kSortItems;
 static_assert(kSortTile == 2048 && kSortTile % kBlock == 0, "k_parse tiles");
 
@@ -650,7 +651,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t sort_temp_bytes(uint32_t n_max) {
     const size_t tiles = (n_max + kSortTile - 1) / kSortTile;
     return align256((size_t)n_max * 4) + align256((size_t)n_max * sizeof(WalkRec)) +
-           (kSortMaxPass + 1) * align256(tiles * 256 * 4);
+           kSortMaxPass * align256(tiles * 256 * 4);
 }
 
 SortScratch sort_scratch(void *temp, uint32_t n_max) {
@@ -661,62 +662,7 @@ SortScratch sort_scratch(void *temp, uint32_t n_max) {
     ss.keys_tmp = reinterpret_cast<uint32_t *>(p); p += align256((size_t)n_max * 4);
     ss.vals_tmp = reinterpret_cast<WalkRec *>(p); p += align256((size_t)n_max * sizeof(WalkRec));
     for (int q = 0; q < kSortMaxPass; q++) { ss.counts[q] = reinterpret_cast<uint32_t *>(p); p += cb; }
-    ss.offsets = reinterpret_cast<uint32_t *>(p);
     return ss;
-}
-
-// One block of 1024: offsets[t][d] = (records with a smaller digit) +
-// (records with digit d in tiles before t); then zeroes the counts for the next
-// bundle.  Thread (g, d) covers digit d over a quarter of the tiles, reading
-// them 32 at a time so the loads overlap.
-constexpr int kScanGroups = 4;
-__global__ __launch_bounds__(256 * kScanGroups) void k_sort_scan(uint32_t *counts, uint32_t *offsets,
-                                                                 uint32_t tiles) {
-    __shared__ uint32_t s_part[kScanGroups][256], s_tot[256];
-    const int d = threadIdx.x & 255, g = threadIdx.x >> 8;
-    const uint32_t per = (tiles + kScanGroups - 1) / kScanGroups;
-    const uint32_t t0 = min(tiles, g * per), t1 = min(tiles, t0 + per);
-    uint32_t sum = 0u;
-    for (uint32_t t = t0; t < t1; t += 32) {
-        uint32_t c[32];
-#pragma unroll
-        for (int k = 0; k < 32; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
-#pragma unroll
-        for (int k = 0; k < 32; k++) sum += c[k];
-    }
-    s_part[g][d] = sum;
-    __syncthreads();
-    if (g == 0) {
-        uint32_t tot = 0u;
-#pragma unroll
-        for (int k = 0; k < kScanGroups; k++) tot += s_part[k][d];
-        s_tot[d] = tot;
-    }
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) { // inclusive scan of the digit totals
-        uint32_t x = 0u;
-        if (g == 0 && d >= o) x = s_tot[d - o];
-        __syncthreads();
-        if (g == 0) s_tot[d] += x;
-        __syncthreads();
-    }
-    uint32_t run = 0u;
-    for (int k = 0; k < kScanGroups; k++) run += s_part[k][d];
-    run = s_tot[d] - run; // records with a smaller digit
-    for (int k = 0; k < g; k++) run += s_part[k][d];
-    for (uint32_t t = t0; t < t1; t += 32) {
-        uint32_t c[32];
-#pragma unroll
-        for (int k = 0; k < 32; k++) c[k] = t + k < t1 ? counts[(t + k) * 256 + d] : 0u;
-#pragma unroll
-        for (int k = 0; k < 32; k++) {
-            if (t + k < t1) {
-                offsets[(t + k) * 256 + d] = run;
-                counts[(t + k) * 256 + d] = 0u;
-            }
-            run += c[k];
-        }
-    }
 }
 
 struct SortPass {
@@ -724,20 +670,57 @@ struct SortPass {
     const WalkRec *sv;
     uint32_t *dk;
     WalkRec *dv;
-    uint32_t n, shift;
-    const uint32_t *offsets;  // [tiles][256]
+    uint32_t n, shift, tiles;
+    const uint32_t *counts;   // this pass's [tiles][256] digit counts
     uint32_t *next_counts;    // next pass's [tiles][256] counts, or null on the last pass
+    uint32_t *zero;           // the previous pass's counts (this tile's row is re-zeroed), or null
 };
 
 __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
     __shared__ uint32_t s_base[256], s_run[256], s_wcnt[kSortThreads / 64][256];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t tile = blockIdx.x, base = tile * kSortTile;
-    if (t < 256) {
-        s_base[t] = sp.offsets[tile * 256 + t];
-        s_run[t] = 0u;
+    {
+        // scatter base of digit d in this tile = (records with a smaller digit)
+        // + (records with digit d in earlier tiles).  Every tile re-reads the
+        // whole [tiles][256] count table (128 KB at 2^18 records, L2-resident),
+        // which costs less than a separate scan launch.  Thread (g, d) sums
+        // digit d over every other tile, 16 loads in flight.
+        const int d = t & 255, g = t >> 8;
+        uint32_t before = 0u, total = 0u;
+        for (uint32_t u0 = (uint32_t)g; u0 < sp.tiles; u0 += 32u) {
+            uint32_t c[16];
 #pragma unroll
-        for (int k = 0; k < kSortThreads / 64; k++) s_wcnt[k][t] = 0u;
+            for (int k = 0; k < 16; k++) {
+                const uint32_t u = u0 + 2u * k;
+                c[k] = u < sp.tiles ? sp.counts[u * 256u + d] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                total += c[k];
+                before += u0 + 2u * k < tile ? c[k] : 0u;
+            }
+        }
+        s_wcnt[g][d] = total;
+        s_wcnt[2 + g][d] = before;
+        if (sp.zero && g == 0) sp.zero[tile * 256u + d] = 0u;
+        __syncthreads();
+        uint32_t x = 0u;
+        if (g == 0) { x = s_wcnt[0][d] + s_wcnt[1][d]; s_run[d] = x; }
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) { // inclusive scan of the digit totals
+            const uint32_t y = (g == 0 && d >= o) ? s_run[d - o] : 0u;
+            __syncthreads();
+            if (g == 0) s_run[d] += y;
+            __syncthreads();
+        }
+        if (g == 0) s_base[d] = s_run[d] - x + s_wcnt[2][d] + s_wcnt[3][d];
+        __syncthreads();
+        if (t < 256) {
+            s_run[t] = 0u;
+#pragma unroll
+            for (int k = 0; k < kSortThreads / 64; k++) s_wcnt[k][t] = 0u;
+        }
     }
     uint32_t key[kSortItems], loc[kSortItems];
     WalkRec val[kSortItems];
@@ -791,8 +774,6 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
     const uint32_t tiles = (a.n + kSortTile - 1) / kSortTile;
     const int P = a.sort_passes;
     for (int q = 0; q < P; q++) {
-        hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(256 * kScanGroups), 0, s, ss.counts[q], ss.offsets,
-                           tiles);
         SortPass sp;
         // ping-pong: in -> tmp -> (out | in) -> (out | tmp) -> out
         const bool last = q == P - 1;
@@ -802,8 +783,12 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
         sp.dv = last ? a.sv_out : (q & 1) ? a.sv_in : ss.vals_tmp;
         sp.n = a.n;
         sp.shift = 8u * (uint32_t)q;
-        sp.offsets = ss.offsets;
+        sp.tiles = tiles;
+        sp.counts = ss.counts[q];
         sp.next_counts = last ? nullptr : ss.counts[q + 1];
+        // pass q re-zeroes pass q-1's counts (read by all of pass q-1); the last
+        // pass's are re-zeroed by the walk (BundleArgs::sort_zero)
+        sp.zero = q ? ss.counts[q - 1] : nullptr;
         hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
     }
     return hipGetLastError();
@@ -1035,6 +1020,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
     __shared__ uint32_t s_nstart;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
     if (limit_pass && !two_pass) return;
+    if (!limit_pass) // the sort's last digit counts, zero again for the next bundle
+        for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words;
+             i += gridDim.x * kWalkBlock)
+            a.sort_zero[i] = 0u;
     const uint32_t base = blockIdx.x * kWalkSpan;
     if (base >= a.n) return;
     const uint32_t span = min((uint32_t)kWalkSpan, a.n - base);
