@@ -46,6 +46,10 @@
  * on the given HIP stream (NULL = the default stream), so bundles that
  * touch the same transformer must be submitted on one stream (submission order
  * == processing order, as the reference's `synchronized` contexts give).
+ * Bundles of one engine share its device scratch: a bundle submitted on a
+ * different stream than the engine's previous one first waits (host-side) for
+ * that stream.  Independent directions that should overlap on the device use
+ * one engine each (e.g. a send-side and a receive-side engine).
  */
 #ifndef SRTP_MI355X_H
 #define SRTP_MI355X_H

@@ -45,8 +45,19 @@ struct srtp_engine {
     uint32_t *tailc = nullptr, *spec = nullptr;
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
-    int32_t *e_min = nullptr;
-    BundleCtl *ctl = nullptr;
+    // Two control blocks (BundleCtl + e_min row), alternating per bundle: each
+    // bundle's k_parse resets the other one for the next bundle, so the common
+    // case needs no memset launch.  ctl_clean / emin_filled track what is known
+    // reset on the device (emin_filled = leading e_min entries at 0x7f7f7f7f).
+    int32_t *e_min = nullptr; // [2][max_transformers]
+    BundleCtl *ctl = nullptr; // [2]
+    int ctl_cur = 0;
+    bool ctl_clean[2] = {false, false};
+    uint32_t emin_filled[2] = {0u, 0u};
+    // stream of the previous bundle: a bundle on another stream first waits
+    // for it (bundles of one engine share its scratch)
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
     unsigned long long *d_count = nullptr;
     uint32_t serial = 1;
 
@@ -263,8 +274,8 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
             dalloc(&e->d_transformers, o.max_transformers) != hipSuccess ||
             dalloc(&e->d_ctx_keys, e->ctx_cap) != hipSuccess ||
             dalloc(&e->d_ctx, e->ctx_cap) != hipSuccess ||
-            dalloc(&e->e_min, o.max_transformers) != hipSuccess ||
-            dalloc(&e->ctl, 1) != hipSuccess || dalloc(&e->d_count, 1) != hipSuccess) {
+            dalloc(&e->e_min, 2 * (size_t)o.max_transformers) != hipSuccess ||
+            dalloc(&e->ctl, 2) != hipSuccess || dalloc(&e->d_count, 1) != hipSuccess) {
             rc = SRTP_ENOMEM;
             break;
         }
@@ -402,6 +413,10 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         return fail(e, SRTP_EINVAL, "bad transformer id");
     int rc = ensure_scratch(e, n);
     if (rc != SRTP_OK) return rc;
+    if (e->have_last && e->last_stream != s) // scratch still in use on the other stream
+        HIPCHK(e, hipStreamSynchronize(e->last_stream));
+    e->last_stream = s;
+    e->have_last = true;
     BundleArgs a{};
     a.keysets = e->d_keysets;
     a.factories = e->d_factories;
@@ -423,19 +438,30 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
     a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
     a.tailc = e->tailc; a.spec = e->spec;
-    a.e_min = e->e_min; a.ctl = e->ctl;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     a.sort_counts = ss.counts[0];
     a.sort_zero = ss.counts[a.sort_passes - 1];
     a.sort_zero_words = ((n + 2047u) / 2048u) * 256u; // tiles of this bundle x 256 digits
-    HIPCHK(e, hipMemsetAsync(e->ctl, 0, sizeof(BundleCtl), s));
-    if (a.abort_on_error)
-        HIPCHK(e, hipMemsetAsync(e->e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
+    const int c = e->ctl_cur;
+    const size_t nt_max = e->opts.max_transformers;
+    a.ctl = e->ctl + c;
+    a.e_min = e->e_min + c * nt_max;
+    a.ctl_next = e->ctl + (c ^ 1);
+    a.e_min_next = e->e_min + (c ^ 1) * nt_max;
+    const bool need_ctl = !e->ctl_clean[c];
+    const bool need_emin = a.abort_on_error && e->emin_filled[c] < a.n_transformers;
+    e->ctl_clean[c] = false; // this bundle's atomics dirty it
+    e->emin_filled[c] = 0u;
+    if (need_ctl) HIPCHK(e, hipMemsetAsync(a.ctl, 0, sizeof(BundleCtl), s));
+    if (need_emin) HIPCHK(e, hipMemsetAsync(a.e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
     {
         StageTimer t(e, s, SRTP_STAGE_PARSE);
-        HIPCHK(e, launch_parse(a, s));
+        HIPCHK(e, launch_parse(a, s)); // also resets control block c ^ 1
     }
+    e->ctl_clean[c ^ 1] = true;
+    e->emin_filled[c ^ 1] = a.n_transformers;
+    e->ctl_cur = c ^ 1;
     {
         StageTimer t(e, s, SRTP_STAGE_SORT);
         HIPCHK(e, launch_sort(a, ss, s));

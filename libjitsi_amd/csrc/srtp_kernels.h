@@ -48,6 +48,8 @@ struct BundleArgs {
     uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
     uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
+    BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse
+    int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse
     BundleCtl *ctl;
     // radix sort of the walk records (srtp_kernels.hip "radix sort")
     uint32_t *sort_counts; // [tiles][256] first-digit counts per 2048-record tile, by k_parse

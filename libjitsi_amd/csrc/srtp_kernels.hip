@@ -5,7 +5,8 @@
 //              (transformer, SSRC) -> context slot in an HBM hash table
 //              (SRTPTransformer.getContext :152-175, lazily derived contexts),
 //              emits a 16-B walk record keyed by slot.
-//   radix sort (hipcub) by slot, stable -> each context's packets in array order.
+//   radix sort (own LSD, 8-bit digits) by slot, stable -> each context's
+//              packets in array order.
 //   k_unprotect [unprotect] one lane per packet: HMAC-SHA1 tag check and
 //              speculative in-place AES-CM decryption under the ROC guessed from
 //              the context state at bundle start; keeps the inner SHA-1 midstate
@@ -629,6 +630,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
     s_hist[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    // reset the next bundle's control block (the previous bundle, which used
+    // it, completed before this kernel started)
+    if (p == 0) *a.ctl_next = BundleCtl{};
+    if (a.abort_on_error)
+        for (uint32_t i = p; i < a.n_transformers; i += gridDim.x * blockDim.x)
+            a.e_min_next[i] = 0x7f7f7f7f;
     if (p < a.n) atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
     __syncthreads();
     const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kBlock
