@@ -19,7 +19,7 @@ if [ "$MODE" = all ] || [ "$MODE" = test ] || [ "$MODE" = diag ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 600 python bench.py --steps 20 --warmup 3
+  step bench 600 python bench.py
 fi
 if [ "$MODE" = quick ]; then
   step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
