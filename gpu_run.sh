@@ -23,7 +23,7 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = quick ]; then
   step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider
-  step bench 300 python bench.py --steps 20 --warmup 3 --no-cpu
+  step bench 300 python bench.py --no-cpu
   export TMPDIR=/tmp
   step rocprof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
 fi

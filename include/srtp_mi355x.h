@@ -66,6 +66,7 @@ extern "C" {
 /* SRTPPolicy constants (transform/srtp/SRTPPolicy.java:29-63) */
 #define SRTP_NULL_ENCRYPTION 0
 #define SRTP_AESCM_ENCRYPTION 1
+#define SRTP_AESF8_ENCRYPTION 2 /* SRTPCipherF8 (SDES F8_128_HMAC_SHA1_80) */
 #define SRTP_NULL_AUTHENTICATION 0
 #define SRTP_HMACSHA1_AUTHENTICATION 1
 

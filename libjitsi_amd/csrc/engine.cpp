@@ -26,6 +26,8 @@ struct srtp_engine {
     std::string last_error;
 
     KeySet *d_keysets = nullptr;
+    F8Keys *d_f8keys = nullptr; // IV' keys of AES-F8 key sets (same index)
+    uint32_t n_f8 = 0;          // AES-F8 key sets created: k_f8 runs only when > 0
     uint32_t n_keysets = 0, max_keysets = 0;
     FactoryRec *d_factories = nullptr;
     std::vector<FactoryRec> factories;
@@ -101,10 +103,17 @@ void dfree(void *p) {
 // auth (SRTPPolicy.java; profile tables DtlsPacketTransformer.java:574-612,
 // SDesTransformEngine.java:129-147).  Tag length <= 12 keeps the reference's
 // readRegionToBuff in range for every packet of >= 12 bytes.
-bool policy_ok(const srtp_policy *p) {
+bool policy_ok(const srtp_policy *p, bool rtcp) {
     if (!p) return false;
-    if (p->enc_type != SRTP_NULL_ENCRYPTION && p->enc_type != SRTP_AESCM_ENCRYPTION) return false;
-    if (p->enc_type == SRTP_AESCM_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+    if (p->enc_type != SRTP_NULL_ENCRYPTION && p->enc_type != SRTP_AESCM_ENCRYPTION &&
+        p->enc_type != SRTP_AESF8_ENCRYPTION)
+        return false;
+    if (p->enc_type != SRTP_NULL_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+        return false;
+    // SRTCP F8 ciphers [8, 8 + length - 4 - tag) (SRTCPCryptoContext :285-291):
+    // inside the packet only with an HMAC trailer of >= 4 tag bytes after it
+    if (rtcp && p->enc_type == SRTP_AESF8_ENCRYPTION &&
+        (p->auth_type == SRTP_NULL_AUTHENTICATION || p->auth_tag_len < 4))
         return false;
     if (p->auth_type != SRTP_NULL_AUTHENTICATION && p->auth_type != SRTP_HMACSHA1_AUTHENTICATION)
         return false;
@@ -114,11 +123,18 @@ bool policy_ok(const srtp_policy *p) {
 }
 
 void build_keyset(const uint8_t mk[16], const uint8_t ms[14], bool rtcp, const srtp_policy *pol,
-                  KeySet *ks) {
+                  KeySet *ks, F8Keys *f8) {
     memset(ks, 0, sizeof *ks);
+    memset(f8, 0, sizeof *f8);
     uint8_t enc[16], auth[20], salt[16] = {0};
     derive_session_keys(mk, ms, rtcp, enc, auth, salt);
     aes128_expand_le(enc, ks->rk);
+    if (pol->enc_type == SRTP_AESF8_ENCRYPTION) { // SRTPCipherF8.deriveForIV :66-95
+        uint8_t m[16];
+        for (int i = 0; i < 16; i++) m[i] = (uint8_t)(enc[i] ^ (i < 14 ? salt[i] : 0x55));
+        aes128_expand_le(m, f8->rk);
+        memset(m, 0, sizeof m);
+    }
     hmac_sha1_midstates(auth, ks->ipad, ks->opad);
     for (int i = 0; i < 4; i++)
         ks->salt[i] = (uint32_t)salt[4 * i] | ((uint32_t)salt[4 * i + 1] << 8) |
@@ -270,6 +286,7 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
         e->ctx_bits = 0;
         while ((1u << e->ctx_bits) < e->ctx_cap) e->ctx_bits++;
         if (dalloc(&e->d_keysets, e->max_keysets) != hipSuccess ||
+            dalloc(&e->d_f8keys, e->max_keysets) != hipSuccess ||
             dalloc(&e->d_factories, o.max_factories) != hipSuccess ||
             dalloc(&e->d_transformers, o.max_transformers) != hipSuccess ||
             dalloc(&e->d_ctx_keys, e->ctx_cap) != hipSuccess ||
@@ -299,13 +316,15 @@ void srtp_engine_destroy(srtp_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->d_keysets) // zero session keys before release
         (void)hipMemset(e->d_keysets, 0, (size_t)e->max_keysets * sizeof(KeySet));
+    if (e->d_f8keys)
+        (void)hipMemset(e->d_f8keys, 0, (size_t)e->max_keysets * sizeof(F8Keys));
     free_scratch(e);
     for (auto &m : e->marks) {
         (void)hipEventDestroy(m.a);
         (void)hipEventDestroy(m.b);
     }
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
-    void *ptrs[] = {e->d_keysets, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
+    void *ptrs[] = {e->d_keysets, e->d_f8keys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
                     e->e_min, e->ctl, e->d_count, e->h_seg, e->h_off, e->h_len, e->h_cap,
                     e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
@@ -322,15 +341,20 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
     std::lock_guard<std::mutex> g(e->mu);
     // NULL-cipher profiles keep a 16-B master key + 14-B salt for the RFC 3711
     // 4.3 PRF (the reference throws there: SURVEY Q15) -- parity unpinned.
-    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp_pol) || !policy_ok(srtcp_pol))
+    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp_pol, false) || !policy_ok(srtcp_pol, true))
         return fail(e, SRTP_EPOLICY, "unsupported SRTP policy");
     if (e->factories.size() >= e->opts.max_factories || e->n_keysets + 2 > e->max_keysets)
         return fail(e, SRTP_EFULL, "factory table full");
     KeySet ks[2];
-    build_keyset(mk, ms, false, srtp_pol, &ks[0]);
-    build_keyset(mk, ms, true, srtcp_pol, &ks[1]);
+    F8Keys f8[2];
+    build_keyset(mk, ms, false, srtp_pol, &ks[0], &f8[0]);
+    build_keyset(mk, ms, true, srtcp_pol, &ks[1], &f8[1]);
     HIPCHK(e, hipMemcpy(e->d_keysets + e->n_keysets, ks, sizeof ks, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_f8keys + e->n_keysets, f8, sizeof f8, hipMemcpyHostToDevice));
     memset(ks, 0, sizeof ks);
+    memset(f8, 0, sizeof f8);
+    e->n_f8 += (srtp_pol->enc_type == SRTP_AESF8_ENCRYPTION) +
+               (srtcp_pol->enc_type == SRTP_AESF8_ENCRYPTION);
     FactoryRec f;
     f.open = 1;
     f.ks_rtp = (int32_t)e->n_keysets;
@@ -419,6 +443,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     e->have_last = true;
     BundleArgs a{};
     a.keysets = e->d_keysets;
+    a.f8keys = e->d_f8keys;
     a.factories = e->d_factories;
     a.transformers = e->d_transformers;
     a.ctx_keys = e->d_ctx_keys;
@@ -478,9 +503,11 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
         HIPCHK(e, launch_unprotect_fix(a, s));
+        if (e->n_f8) HIPCHK(e, launch_f8(a, s));
     } else {
         StageTimer t(e, s, SRTP_STAGE_PROTECT);
         HIPCHK(e, launch_protect(a, s));
+        if (e->n_f8) HIPCHK(e, launch_f8(a, s));
     }
     return SRTP_OK;
 }

@@ -14,6 +14,7 @@ constexpr int kSortMaxPass = 4; // 8-bit digits: context tables up to 2^31 slots
 struct BundleArgs {
     // engine tables (HBM resident)
     const KeySet *keysets;
+    const F8Keys *f8keys;  // [keysets] IV' keys of the AES-F8 key sets
     const FactoryRec *factories;
     const TransformerRec *transformers;
     uint64_t *ctx_keys;
@@ -78,6 +79,9 @@ hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s);
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
 // unprotect: statuses/lengths out; undo/redo the rare speculation misses (after the walk)
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
+// AES-F8 packets after the final statuses: protect (F8 + HMAC + trailer) or
+// decryption of the accepted unprotected packets.
+hipError_t launch_f8(const BundleArgs &a, hipStream_t s);
 hipError_t launch_remove_transformer(uint64_t *ctx_keys, CtxState *ctx, uint32_t cap,
                                      uint32_t tid, hipStream_t s);
 hipError_t launch_count_contexts(const uint64_t *ctx_keys, uint32_t cap, unsigned long long *out,

@@ -511,6 +511,16 @@ __device__ __forceinline__ bool ctr_would_throw(int32_t h, int plen) {
     return plen > 0 && h < 0;
 }
 
+// The cipher of policy `enc` would throw on region [h, h+plen): AES-CM as
+// above; AES-F8 (SRTPCipherF8.process :97-128) only when the header length
+// throws or a block is XORed at a negative offset (a negative length ciphers
+// nothing and a non-negative offset stays inside the packet).
+__device__ __forceinline__ bool enc_would_throw(int enc, int32_t h, int plen) {
+    if (enc == SRTP_AESCM_ENCRYPTION) return ctr_would_throw(h, plen);
+    if (enc == SRTP_AESF8_ENCRYPTION) return h == kHdrThrow || (plen > 0 && h < 0);
+    return false;
+}
+
 __device__ __forceinline__ int32_t packet_tid(const BundleArgs &a, uint32_t p) {
     return a.tids ? a.tids[p] : a.tid;
 }
@@ -933,10 +943,9 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                 }
                 if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
             }
-            if (c.enc == SRTP_AESCM_ENCRYPTION && !(rec.p & kRecSkipDec))
-                threw = ctr_would_throw(rec.h, newL - rec.h);
+            if (!(rec.p & kRecSkipDec)) threw = enc_would_throw(c.enc, rec.h, newL - rec.h);
         } else {
-            if (c.enc == SRTP_AESCM_ENCRYPTION) threw = ctr_would_throw(rec.h, L - rec.h);
+            threw = enc_would_throw(c.enc, rec.h, L - rec.h);
             if (!threw && c.auth != SRTP_NULL_AUTHENTICATION) newL = L + T;
         }
         if (!threw) {
@@ -1307,6 +1316,7 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     const char *lds = reinterpret_cast<const char *>(s_te);
     for_each_keyset(todo, ks_id, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
+        if (sgpr(ks->enc_type) == SRTP_AESF8_ENCRYPTION) return; // k_f8
         protect_one(a, ks, lds, tb, p,
                     sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
                         sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
@@ -1573,6 +1583,148 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     atomicAdd(&a.ctl->n_walk, 1u); // repaired packets (diagnostic)
 }
 
+// ============================================================== k_f8
+// AES-F8 packets (SRTPCipherF8; SDES F8_128_HMAC_SHA1_80), after the final
+// statuses of k_protect / k_unprotect_fix.  Protect: F8 encryption, then the
+// HMAC over the ciphertext and the trailer.  Unprotect: k_unprotect already
+// checked the tag (HMAC is over the ciphertext, independent of the cipher) and
+// did not speculate, so only the accepted packets are deciphered here.  The F8
+// keystream is a chain, S(j) = E(k_e, IV' ^ S(j-1) ^ j), so a lane walks its
+// packet block by block.
+
+// Round keys at p (wave-uniform) into SGPRs.
+__device__ __forceinline__ void load_rk_uniform(const uint32_t *__restrict__ p, RoundKeys &rk) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        const uint4 v = q[i];
+        rk.k[4 * i] = sgpr(v.x); rk.k[4 * i + 1] = sgpr(v.y);
+        rk.k[4 * i + 2] = sgpr(v.z); rk.k[4 * i + 3] = sgpr(v.w);
+    }
+}
+
+// SRTPCipherF8.process :97-128 + processBlock :145-183 over packet bytes
+// [off, off + len) (off a multiple of 4; len <= 0 ciphers nothing).
+__device__ void f8_region(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
+                          const F8Keys *f8, uint8_t *pkt, int off, int len, const uint32_t iv[4]) {
+    uint32_t ivp[4] = {iv[0], iv[1], iv[2], iv[3]};
+    {
+        RoundKeys rkf; // IV' = E(k_e ^ (k_s || 0x55..), IV)
+        load_rk_uniform(f8->rk, rkf);
+        uint32_t z[4] = {0u, 0u, 0u, 0u};
+        aes_encrypt2(lds, tb, rkf, ivp, z);
+    }
+    if (len <= 0) return;
+    RoundKeys rk;
+    load_round_keys_uniform(ks, rk);
+    uint32_t S[4] = {0u, 0u, 0u, 0u};
+    const int end = off + len;
+    for (int j = 0; off + 16 * j < end; j++) {
+        uint32_t x[4], y[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[k] = S[k] ^ ivp[k];
+        x[3] ^= bswap((uint32_t)j); // the counter j into bytes 12..15, big-endian
+        aes_encrypt2(lds, tb, rk, x, y);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            S[k] = x[k];
+            const int pos = off + 16 * j + 4 * k;
+            if (pos < end) {
+                const int rem = end - pos;
+                const uint32_t m = rem >= 4 ? ~0u : ((1u << (8 * rem)) - 1u);
+                uint32_t *w = reinterpret_cast<uint32_t *>(pkt + pos);
+                *w ^= x[k] & m;
+            }
+        }
+    }
+}
+
+// HMAC-SHA1 tag of packet bytes [0, L) || suffix (authenticatePacketHMAC :269-278).
+__device__ void hmac_packet(const KeySet *ks, const uint8_t *pkt, int L, uint32_t suffix,
+                            uint32_t h[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
+    const int nb_data = (L + 63) >> 6;
+    const int nb_inner = ((L + 12) >> 6) + 1;
+    for (int b = 0; b <= nb_inner; b++) {
+        uint32_t w[16];
+        const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (b < nb_data && 64 * b + 16 * m < L) v = qp[m];
+            w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+        }
+        if (b < nb_inner) inner_words(w, b, L, suffix);
+        else outer_words(w, h, ks);
+        sha1_compress(h, w);
+    }
+}
+
+__global__ __launch_bounds__(kAesBlock) void k_f8(BundleArgs a) {
+    __shared__ uint32_t s_te[kTeWords];
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    bool todo = false;
+    uint32_t ks_id = 0;
+    if (p < a.n && a.status[p] == SRTP_STATUS_OK) {
+        const uint32_t slot = a.p_slot[p];
+        if (slot != kNoSlot) {
+            ks_id = a.ctx[slot].ks;
+            const KeySet *ks = a.keysets + ks_id;
+            if (ks->enc_type == SRTP_AESF8_ENCRYPTION) {
+                if (!a.reverse) todo = true;
+                else if (ks->kind == SRTP_KIND_RTP)
+                    todo = !((a.flags ? a.flags[p] : 0u) &
+                             (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
+                else todo = (a.w_cw[p] & 0x80000000u) != 0; // E flag
+            }
+        }
+    }
+    if (!__syncthreads_or(todo)) return;
+    fill_te4(s_te);
+    if (!todo) return;
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s_te);
+    for_each_keyset(true, ks_id, [&](uint32_t ks_u) {
+        const KeySet *ks = a.keysets + ks_u;
+        const F8Keys *f8 = a.f8keys + ks_u;
+        uint8_t *pkt = a.seg + a.off[p];
+        const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+        const int T = (int)sgpr(ks->tag_len);
+        const bool mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+        const uint32_t cw = a.w_cw[p];
+        uint32_t iv[4];
+        if (sgpr(ks->kind) == SRTP_KIND_RTP) {
+            // processPacketAESF8 :532-555: IV = 0 || header[1..11] || ROC_be
+            iv[0] = hdr.x & 0xffffff00u; iv[1] = hdr.y; iv[2] = hdr.z; iv[3] = bswap(cw);
+            const int L = (int)a.len[p] - (!a.reverse && mac ? T : 0);
+            const int h = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+            f8_region(lds, tb, ks, f8, pkt, h, L - h, iv);
+            if (!a.reverse && mac) {
+                uint32_t hh[5];
+                hmac_packet(ks, pkt, L, cw, hh);
+                tag_write(hh, pkt + L, T);
+            }
+        } else {
+            // SRTCPCryptoContext.processPacketAESF8 :267-298: IV = 0^4 ||
+            // (index | E)_be || header[0..7]; ciphers [8, 8 + length - 4 - tag)
+            // of the length at the call (protect: before the trailer; unprotect:
+            // after shrinking it).
+            const uint32_t ie = cw | 0x80000000u;
+            iv[0] = 0u; iv[1] = bswap(ie); iv[2] = hdr.x; iv[3] = hdr.y;
+            const int L = (int)a.len[p] - (a.reverse ? 0 : 4 + T);
+            f8_region(lds, tb, ks, f8, pkt, 8, L - 4 - T, iv);
+            if (!a.reverse) { // the policy check guarantees an HMAC trailer
+                uint32_t hh[5];
+                hmac_packet(ks, pkt, L, ie, hh);
+                pkt[L] = (uint8_t)(ie >> 24); pkt[L + 1] = (uint8_t)(ie >> 16);
+                pkt[L + 2] = (uint8_t)(ie >> 8); pkt[L + 3] = (uint8_t)ie;
+                tag_write(hh, pkt + L + 4, T);
+            }
+        }
+    });
+}
+
 // ============================================================== maintenance
 __global__ void k_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1617,6 +1769,10 @@ hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
 }
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_unprotect_fix, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_f8(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_f8, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,

@@ -29,6 +29,14 @@ struct alignas(256) KeySet {
 };
 static_assert(sizeof(KeySet) == 256, "KeySet is one 256-B record");
 
+// AES-F8 IV' key of a key set (SRTPCipherF8.deriveForIV :66-95: the session
+// key ^ (session salt || 0x55 0x55)), kept beside KeySet, indexed by key-set id.
+struct alignas(64) F8Keys {
+    uint32_t rk[4 * (kAesRounds + 1)]; // round keys, little-endian column words
+    uint32_t pad[4];
+};
+static_assert(sizeof(F8Keys) == 192, "F8Keys is 192 B");
+
 struct FactoryRec {      // SRTPContextFactory
     int32_t open;        // 0 after close(): getDefaultContext() == null
     int32_t ks_rtp;      // key set of its default SRTPCryptoContext

@@ -73,13 +73,15 @@ class SRTPPolicy:
 def profile_policies(profile: str):
     """(srtpPolicy, srtcpPolicy) of a DTLS-SRTP protection profile, as the table
     in transform/dtls/DtlsPacketTransformer.java:574-612 builds them (note the
-    10-byte SRTCP tag of the _32 profiles)."""
+    10-byte SRTCP tag of the _32 profiles), or of the SDES F8 crypto suite
+    (transform/sdes/SDesTransformEngine.java:129-176: AES-F8, 10-byte tags)."""
     P = SRTPPolicy
     table = {
         "AES_CM_128_HMAC_SHA1_80": (P.AESCM_ENCRYPTION, 16, 14, 10, 10),
         "AES_CM_128_HMAC_SHA1_32": (P.AESCM_ENCRYPTION, 16, 14, 4, 10),
         "NULL_HMAC_SHA1_80": (P.NULL_ENCRYPTION, 0, 0, 10, 10),
         "NULL_HMAC_SHA1_32": (P.NULL_ENCRYPTION, 0, 0, 4, 10),
+        "F8_128_HMAC_SHA1_80": (P.AESF8_ENCRYPTION, 16, 14, 10, 10),
     }
     enc, klen, slen, rtp_tag, rtcp_tag = table[profile]
     return (P(enc, klen, P.HMACSHA1_AUTHENTICATION, 20, rtp_tag, slen),

@@ -74,6 +74,7 @@ def lib():
         L.orc_aes128_encrypt_block.argtypes = [u8p, u8p, u8p]
         L.orc_hmac_sha1.argtypes = [u8p, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_derive_keys.argtypes = [u8p, u8p, C.c_int, u8p, u8p, u8p]
+        L.orc_aes_f8.argtypes = [u8p, u8p, C.c_int, u8p, u8p, C.c_int]
         _lib = L
     return _lib
 
@@ -107,6 +108,16 @@ def derive_keys(master_key: bytes, master_salt: bytes, rtcp: bool = False):
     lib().orc_derive_keys(kp, sp, int(rtcp), enc.ctypes.data_as(P), auth.ctypes.data_as(P),
                           salt.ctypes.data_as(P))
     return enc.tobytes(), auth.tobytes(), salt.tobytes()
+
+
+def aes_f8(key: bytes, salt: bytes, iv: bytes, data: bytes) -> bytes:
+    """SRTPCipherF8 (deriveForIV + process) over `data` with IV `iv`."""
+    k, kp = _u8(key)
+    s, sp = _u8(salt)
+    i, ip = _u8(iv)
+    d, dp = _u8(data if data else b"\0")
+    lib().orc_aes_f8(kp, sp, len(salt), ip, dp, len(data))
+    return d.tobytes()[:len(data)]
 
 
 def set_check_replay(enabled: bool) -> None:

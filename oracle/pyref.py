@@ -6,7 +6,8 @@ implemented here from FIPS-197, HMAC-SHA1 comes from Python's hashlib/hmac,
 and the context state machine is restated directly from
 
   srtp/SRTPCryptoContext.java:237-744, srtp/SRTCPCryptoContext.java:106-451,
-  srtp/SRTPCipherCTR.java:68-121, srtp/BaseSRTPCryptoContext.java:269-278,
+  srtp/SRTPCipherCTR.java:68-121, srtp/SRTPCipherF8.java:66-183,
+  srtp/BaseSRTPCryptoContext.java:269-278,
   srtp/SRTPTransformer.java:100-219, srtp/SRTCPTransformer.java:92-207,
   nm/RawPacket.java, tf/SinglePacketTransformer.java:121-216
 
@@ -126,6 +127,31 @@ def ctr_process(rks, buf: bytearray, buflen, off, length, iv):
         buf[i + off] ^= ks[i]
 
 
+def f8_process(rks, f8rks, buf: bytearray, off, length, iv):
+    """SRTPCipherF8.process :97-128 / processBlock :145-183: IV' = E(k_e ^ m, IV),
+    S(j) = E(k_e, IV' ^ S(j-1) ^ j), S(-1) = 0, j big-endian in bytes 12..15."""
+    ivp = aes_block(f8rks, bytes(iv))
+    s = bytes(16)
+    j = pos = 0
+    while pos < length:
+        n = min(16, length - pos)
+        x = bytearray(a ^ b for a, b in zip(s, ivp))
+        for k in range(4):
+            x[12 + k] ^= (j >> (24 - 8 * k)) & 0xFF
+        s = aes_block(rks, bytes(x))
+        j += 1
+        if off < 0:
+            raise Throw("AIOOBE")
+        for i in range(n):
+            buf[off + pos + i] ^= s[i]
+        pos += n
+
+
+def f8_key_mask(key, salt):
+    """SRTPCipherF8.deriveForIV :66-95: key ^ (salt || 0x55..)."""
+    return bytes(k ^ (salt[i] if i < len(salt) else 0x55) for i, k in enumerate(key))
+
+
 def derive(mk, ms, rtcp):
     """RFC 3711 4.3 with kdr = 0 (computeIv label << 48 -> byte 7)."""
     rks = expand_key(mk)
@@ -143,6 +169,7 @@ class Ctx:
         self.policy = policy  # (enc, enc_len, auth, auth_len, tag, salt_len)
         enc, auth, salt = derive(mk, ms, rtcp)
         self.rks = expand_key(enc)
+        self.f8rks = expand_key(f8_key_mask(enc, salt)) if policy[0] == 2 else None
         self.auth = auth
         self.salt = salt
         self.roc = self.s_l = self.guessed = 0
@@ -247,6 +274,16 @@ def rtp_iv(c, buf):
                  [ib[k] ^ c.salt[8 + k] for k in range(6)] + [0, 0])
 
 
+def rtp_f8_iv(c, buf):
+    """SRTPCryptoContext.processPacketAESF8 :532-555: 0 || header[1..11] || ROC."""
+    return bytes([0]) + bytes(buf[1:12]) + (c.guessed & M32).to_bytes(4, "big")
+
+
+def rtcp_f8_iv(buf, index):
+    """SRTCPCryptoContext.processPacketAESF8 :267-298: 0^4 || E|index || header[0..7]."""
+    return bytes(4) + ((index | 0x80000000) & M32).to_bytes(4, "big") + bytes(buf[0:8])
+
+
 def rtcp_iv(c, buf, index):
     ib = (index & M32).to_bytes(4, "big")
     return bytes(list(c.salt[:4]) + [buf[4 + k] ^ c.salt[4 + k] for k in range(4)] +
@@ -273,10 +310,13 @@ def process_one(t, reverse, buf: bytearray, L, cap, flags):
             gi = guess(c, seq)
             if not replay_ok(c, gi):
                 return 1, L
-            if enc == 1:
+            if enc in (1, 2):
                 try:
                     h = header_len(buf, cap)
-                    ctr_process(c.rks, buf, cap, h, L - h, rtp_iv(c, buf))
+                    if enc == 1:
+                        ctr_process(c.rks, buf, cap, h, L - h, rtp_iv(c, buf))
+                    else:
+                        f8_process(c.rks, c.f8rks, buf, h, L - h, rtp_f8_iv(c, buf))
                 except Throw:
                     return 6, L
             if auth:
@@ -295,10 +335,13 @@ def process_one(t, reverse, buf: bytearray, L, cap, flags):
             L = max(0, L - T) if T > 0 else L
             if c.mac(bytes(buf[:L]), c.guessed)[:T] != got:
                 return 2, L
-        if not (flags & 0x6) and enc == 1:
+        if not (flags & 0x6) and enc in (1, 2):
             try:
                 h = header_len(buf, cap)
-                ctr_process(c.rks, buf, cap, h, L - h, rtp_iv(c, buf))
+                if enc == 1:
+                    ctr_process(c.rks, buf, cap, h, L - h, rtp_iv(c, buf))
+                else:
+                    f8_process(c.rks, c.f8rks, buf, h, L - h, rtp_f8_iv(c, buf))
             except Throw:
                 return 6, L
         update(c, seq, gi)
@@ -313,7 +356,9 @@ def process_one(t, reverse, buf: bytearray, L, cap, flags):
             return 5, L
         if enc == 1:
             ctr_process(c.rks, buf, cap, 8, L - 8, rtcp_iv(c, buf, c.sent))
-        index = (c.sent | 0x80000000) if enc == 1 else 0
+        elif enc == 2:
+            f8_process(c.rks, c.f8rks, buf, 8, L - 4 - T, rtcp_f8_iv(buf, c.sent))
+        index = (c.sent | 0x80000000) if enc in (1, 2) else 0
         if auth:
             tag = c.mac(bytes(buf[:L]), index)[:T]
             buf[L:L + 4] = (index & M32).to_bytes(4, "big")
@@ -340,6 +385,8 @@ def process_one(t, reverse, buf: bytearray, L, cap, flags):
             ctr_process(c.rks, buf, cap, 8, L - 8, rtcp_iv(c, buf, index))
         except Throw:
             return 6, L
+    if decrypt and enc == 2:
+        f8_process(c.rks, c.f8rks, buf, 8, L - 4 - T, rtcp_f8_iv(buf, index))
     d2 = i32(c.recv - index)
     if d2 > 0:
         c.window = lshl(c.window, d2) | 1

@@ -45,6 +45,7 @@ typedef struct orc_ctx {
     uint8_t enc_key[16], auth_key[20], salt_key[14];
     EVP_CIPHER_CTX *ecb;  /* AES-128 keyed with the session key */
     EVP_CIPHER_CTX *ctr;  /* tuned mode */
+    EVP_CIPHER_CTX *f8;   /* AES-F8: IV' cipher keyed with encKey ^ (salt || 0x55..) */
     HMAC_CTX *hmac;       /* ref: re-keyed per packet; tuned: pre-keyed template */
     HMAC_CTX *hmac_work;
     /* SRTPCryptoContext state (:130-164) */
@@ -144,6 +145,52 @@ static int cipher_ctr_process(orc_ctx *x, uint8_t *data, int buf_len, int off, i
     if (stream != sbuf)
         free(stream);
     return 0;
+}
+
+/* SRTPCipherF8.deriveForIV, SRTPCipherF8.java:66-95: the IV' cipher is keyed
+ * with key ^ (salt || 0x55 0x55 ..) (the salt copied, the rest 0x55). */
+static EVP_CIPHER_CTX *f8_iv_cipher_new(const uint8_t key[16], const uint8_t *salt, int salt_len) {
+    uint8_t mk[16];
+    for (int i = 0; i < 16; i++)
+        mk[i] = (uint8_t)(key[i] ^ (i < salt_len ? salt[i] : 0x55));
+    EVP_CIPHER_CTX *c = aes_ecb_new(mk);
+    memset(mk, 0, sizeof mk);
+    return c;
+}
+
+/* SRTPCipherF8.process :97-128 and processBlock :145-183: IV' = E(k_e ^ m, IV);
+ * S(j) = E(k_e, IV' ^ S(j-1) ^ j) with S(-1) = 0 and j (a long) XORed into
+ * bytes 12..15 big-endian; data[off + 16j + i] ^= S(j)[i].  The XOR loop
+ * throws (AIOOBE) at a negative offset before touching the block; a negative
+ * length processes nothing. */
+static int cipher_f8_process(EVP_CIPHER_CTX *c, EVP_CIPHER_CTX *f8c, uint8_t *data, int off,
+                             int len, const uint8_t iv[16]) {
+    uint8_t ivp[16], S[16];
+    aes_block(f8c, iv, ivp);
+    memset(S, 0, sizeof S);
+    int64_t J = 0;
+    int in_len = len;
+    while (in_len > 0) {
+        int n = in_len >= 16 ? 16 : in_len;
+        for (int i = 0; i < 16; i++) S[i] ^= ivp[i];
+        S[12] ^= (uint8_t)(J >> 24); S[13] ^= (uint8_t)(J >> 16);
+        S[14] ^= (uint8_t)(J >> 8);  S[15] ^= (uint8_t)J;
+        J++;
+        aes_block(c, S, S);
+        if (off < 0) return THROW;
+        for (int i = 0; i < n; i++) data[off + i] ^= S[i];
+        in_len -= n;
+        off += n;
+    }
+    return 0;
+}
+
+void orc_aes_f8(const uint8_t key[16], const uint8_t *salt, int salt_len, const uint8_t iv[16],
+                uint8_t *data, int len) {
+    EVP_CIPHER_CTX *c = aes_ecb_new(key), *f = f8_iv_cipher_new(key, salt, salt_len);
+    cipher_f8_process(c, f, data, 0, len, iv);
+    EVP_CIPHER_CTX_free(c);
+    EVP_CIPHER_CTX_free(f);
 }
 
 /* BaseSRTPCryptoContext.authenticatePacketHMAC, :269-278: tag_store =
@@ -257,6 +304,7 @@ static void ctx_free(orc_ctx *x) {
     if (!x) return;
     if (x->ecb) EVP_CIPHER_CTX_free(x->ecb);
     if (x->ctr) EVP_CIPHER_CTX_free(x->ctr);
+    if (x->f8) EVP_CIPHER_CTX_free(x->f8);
     if (x->hmac) HMAC_CTX_free(x->hmac);
     if (x->hmac_work) HMAC_CTX_free(x->hmac_work);
     memset(x, 0, sizeof *x);
@@ -272,9 +320,16 @@ static void map_clear(ctx_map *m) {
 }
 
 /* ---------- factory / transformer -------------------------------------- */
-static int policy_ok(const orc_policy *p) {
-    if (p->enc_type != ORC_NULL_ENCRYPTION && p->enc_type != ORC_AESCM_ENCRYPTION) return 0;
-    if (p->enc_type == ORC_AESCM_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+static int policy_ok(const orc_policy *p, int rtcp) {
+    if (p->enc_type != ORC_NULL_ENCRYPTION && p->enc_type != ORC_AESCM_ENCRYPTION &&
+        p->enc_type != ORC_AESF8_ENCRYPTION)
+        return 0;
+    if (p->enc_type != ORC_NULL_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+        return 0;
+    /* SRTCP F8 ciphers [8, 8 + length - 4 - tag) (SRTCPCryptoContext :285-291),
+     * which leaves the packet unless an HMAC trailer of >= 4 tag bytes follows */
+    if (rtcp && p->enc_type == ORC_AESF8_ENCRYPTION &&
+        (p->auth_type == ORC_NULL_AUTHENTICATION || p->auth_tag_len < 4))
         return 0;
     if (p->auth_type != ORC_NULL_AUTHENTICATION && p->auth_type != ORC_HMACSHA1_AUTHENTICATION)
         return 0;
@@ -290,7 +345,7 @@ orc_factory *orc_factory_new(int sender, const uint8_t *mk, int key_len, const u
     /* NULL-cipher profiles: the reference throws in key derivation;
      * here they keep a 16-B master key + 14-B salt for the AES-CM PRF, as RFC 3711
      * 4.3 prescribes -- behaviour "parity unpinned". */
-    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp) || !policy_ok(srtcp)) return NULL;
+    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp, 0) || !policy_ok(srtcp, 1)) return NULL;
     orc_factory *f = (orc_factory *)calloc(1, sizeof *f);
     f->sender = sender; f->mode = mode;
     memcpy(f->master_key, mk, 16);
@@ -348,6 +403,8 @@ static orc_ctx *get_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) {
     orc_derive_keys(f->master_key, f->master_salt, t->kind == ORC_KIND_RTCP, x->enc_key,
                     x->auth_key, x->salt_key);
     x->ecb = aes_ecb_new(x->enc_key);
+    if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) /* deriveSrtpKeys :443-444 */
+        x->f8 = f8_iv_cipher_new(x->enc_key, x->salt_key, 14);
     if (x->mode == ORC_MODE_TUNED) {
         x->ctr = EVP_CIPHER_CTX_new();
         EVP_EncryptInit_ex(x->ctr, EVP_aes_128_ctr(), NULL, x->enc_key, NULL);
@@ -414,6 +471,25 @@ static int srtp_process_aescm(orc_ctx *x, uint8_t *b, int len, int cap) {
     return cipher_ctr_process(x, b, cap, h, payload_len, iv);
 }
 
+/* processPacketAESF8 :532-555: IV = 0x00 || header bytes 1..11 || ROC_be. */
+static int srtp_process_aesf8(orc_ctx *x, uint8_t *b, int len, int cap) {
+    uint8_t iv[16];
+    memcpy(iv, b, 12);
+    iv[0] = 0;
+    int32_t roc = x->guessed_roc;
+    iv[12] = (uint8_t)(roc >> 24); iv[13] = (uint8_t)(roc >> 16);
+    iv[14] = (uint8_t)(roc >> 8);  iv[15] = (uint8_t)roc;
+    int h;
+    if (header_length(b, cap, &h) == THROW) return THROW;
+    return cipher_f8_process(x->ecb, x->f8, b, h, len - h, iv);
+}
+
+static int srtp_encrypt(orc_ctx *x, uint8_t *b, int len, int cap) {
+    if (x->policy.enc_type == ORC_AESCM_ENCRYPTION) return srtp_process_aescm(x, b, len, cap);
+    if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) return srtp_process_aesf8(x, b, len, cap);
+    return 0;
+}
+
 /* transformPacket :658-705 */
 static int srtp_transform(orc_ctx *x, uint8_t *b, uint32_t *len, int cap) {
     int L = (int)*len;
@@ -421,8 +497,7 @@ static int srtp_transform(orc_ctx *x, uint8_t *b, uint32_t *len, int cap) {
     if (!x->seq_num_set) { x->seq_num_set = 1; x->s_l = seq; }
     int64_t gi = guess_index(x, seq);
     if (!srtp_check_replay(x, gi)) return ORC_DROP_REPLAY;
-    if (x->policy.enc_type == ORC_AESCM_ENCRYPTION)
-        if (srtp_process_aescm(x, b, L, cap) == THROW) return ORC_ERR_MALFORMED;
+    if (srtp_encrypt(x, b, L, cap) == THROW) return ORC_ERR_MALFORMED;
     if (x->policy.auth_type != ORC_NULL_AUTHENTICATION) {
         authenticate_packet_hmac(x, b, L, x->guessed_roc);
         int T = x->policy.auth_tag_len;
@@ -458,8 +533,7 @@ static int srtp_reverse(orc_ctx *x, uint8_t *b, uint32_t *len, int cap, uint32_t
     *len = (uint32_t)L;
     if (!ok) return ORC_DROP_AUTH;
     if ((flags & (ORC_FLAG_DISCARD | ORC_FLAG_SILENCE)) == 0)
-        if (x->policy.enc_type == ORC_AESCM_ENCRYPTION)
-            if (srtp_process_aescm(x, b, L, cap) == THROW) return ORC_ERR_MALFORMED;
+        if (srtp_encrypt(x, b, L, cap) == THROW) return ORC_ERR_MALFORMED;
     srtp_update(x, seq, gi);
     return ORC_OK;
 }
@@ -505,12 +579,27 @@ static int srtcp_process_aescm(orc_ctx *x, uint8_t *b, int L, int cap, int32_t i
     return cipher_ctr_process(x, b, cap, 8, L - 8, iv);
 }
 
+/* processPacketAESF8 :267-298: IV = 0 (4 B) || (index | E)_be || packet bytes
+ * 0..7; ciphers [8, 8 + length - (4 + tag)) of the length at the call (before
+ * the trailer on protect, after shrinking it on unprotect). */
+static int srtcp_process_aesf8(orc_ctx *x, uint8_t *b, int L, int32_t index) {
+    uint8_t iv[16] = {0};
+    uint32_t ie = (uint32_t)index | 0x80000000u;
+    iv[4] = (uint8_t)(ie >> 24); iv[5] = (uint8_t)(ie >> 16);
+    iv[6] = (uint8_t)(ie >> 8);  iv[7] = (uint8_t)ie;
+    memcpy(iv + 8, b, 8);
+    return cipher_f8_process(x->ecb, x->f8, b, 8, L - (4 + x->policy.auth_tag_len), iv);
+}
+
 /* transformPacket :391-427 */
 static int srtcp_transform(orc_ctx *x, uint8_t *b, uint32_t *len, int cap) {
     int L = (int)*len;
     int encrypt = 0;
     if (x->policy.enc_type == ORC_AESCM_ENCRYPTION) {
         if (srtcp_process_aescm(x, b, L, cap, x->sent_index) == THROW) return ORC_ERR_MALFORMED;
+        encrypt = 1;
+    } else if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) {
+        if (srtcp_process_aesf8(x, b, L, x->sent_index) == THROW) return ORC_ERR_MALFORMED;
         encrypt = 1;
     }
     int32_t index = encrypt ? (int32_t)((uint32_t)x->sent_index | 0x80000000u) : 0;
@@ -551,6 +640,8 @@ static int srtcp_reverse(orc_ctx *x, uint8_t *b, uint32_t *len, int cap) {
     }
     if (decrypt && x->policy.enc_type == ORC_AESCM_ENCRYPTION)
         if (srtcp_process_aescm(x, b, L, cap, index) == THROW) return ORC_ERR_MALFORMED;
+    if (decrypt && x->policy.enc_type == ORC_AESF8_ENCRYPTION)
+        if (srtcp_process_aesf8(x, b, L, index) == THROW) return ORC_ERR_MALFORMED;
     srtcp_update(x, index);
     return ORC_OK;
 }

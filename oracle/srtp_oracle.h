@@ -11,6 +11,7 @@
  *   srtp/SRTCPCryptoContext.java:106-451  (SRTCP replay, IV, protect/unprotect)
  *   srtp/BaseSRTPCryptoContext.java:178-278 (key storage, authenticatePacketHMAC)
  *   srtp/SRTPCipherCTR.java:68-121        (AES-CM keystream + XOR)
+ *   srtp/SRTPCipherF8.java:66-183         (AES-F8 IV' key, keystream chain)
  *   srtp/SRTPTransformer.java:100-219, srtp/SRTCPTransformer.java:92-207,
  *   srtp/SRTPContextFactory.java:50-68    (per-transformer SSRC context map)
  *   nm/RawPacket.java:203-220,463-614,723-839,885-909,988-999,1284-1292
@@ -115,6 +116,9 @@ void orc_aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8
 void orc_hmac_sha1(const uint8_t *key, int key_len, const uint8_t *msg, size_t n, uint8_t out[20]);
 /* RFC 3711 4.3 PRF exactly as SRTPCryptoContext.deriveSrtpKeys (labels 0/1/2)
  * or SRTCPCryptoContext.deriveSrtcpKeys (labels 3/4/5). */
+/* AES-F8 (SRTPCipherF8.deriveForIV + process) over data[0..len) with IV iv. */
+void orc_aes_f8(const uint8_t key[16], const uint8_t *salt, int salt_len, const uint8_t iv[16],
+                uint8_t *data, int len);
 void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp,
                      uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]);
 

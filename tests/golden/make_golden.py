@@ -49,6 +49,7 @@ PROFILES = {
     "AES_CM_128_HMAC_SHA1_32": ((1, 16, 1, 20, 4, 14), (1, 16, 1, 20, 10, 14)),
     "NULL_HMAC_SHA1_80": ((0, 0, 1, 20, 10, 0), (0, 0, 1, 20, 10, 0)),
     "NULL_HMAC_SHA1_32": ((0, 0, 1, 20, 4, 0), (0, 0, 1, 20, 10, 0)),
+    "F8_128_HMAC_SHA1_80": ((2, 16, 1, 20, 10, 14), (2, 16, 1, 20, 10, 14)),
 }
 STATE_KEYS = ("roc", "s_l", "seq_num_set", "guessed_roc", "sent_index", "received_index",
               "replay_window")
@@ -528,12 +529,71 @@ def null_profiles():
     r.save()
 
 
+def sdes_f8():
+    r = Recorder("sdes_f8", "SDES F8_128_HMAC_SHA1_80 (AES-F8, SRTPCipherF8; its IV' key and "
+                 "keystream chain pinned by RFC 3711 B.1): SRTP + SRTCP round trips across a "
+                 "seq wrap with header extensions and 8-KiB packets, tamper/replay faults, "
+                 "DISCARD/SILENCE flags, ROC guesses overturned in-bundle, malformed "
+                 "extension headers, an SDES-style rekey; SRTCP ciphers only [8, 8 + len - 4 - "
+                 "tag) (SRTCPCryptoContext.processPacketAESF8 :285-291)")
+    rng = np.random.default_rng(synth.SEED_BASE + 8)
+    keys = synth.keys(8, 2)
+    (k, s) = keys[0]
+    fs, fr = r.factory(True, k, s, "F8_128_HMAC_SHA1_80"), r.factory(False, k, s, "F8_128_HMAC_SHA1_80")
+    snd, rcv = r.transformer(O.KIND_RTP, fs), r.transformer(O.KIND_RTP, fr)
+    cs, cr = r.transformer(O.KIND_RTCP, fs), r.transformer(O.KIND_RTCP, fr)
+    for step in range(3):
+        if step == 2:  # SDES-style rekey: contexts keep their keys (Q16)
+            k2, s2 = keys[1]
+            nfs = r.factory(True, k2, s2, "F8_128_HMAC_SHA1_80")
+            nfr = r.factory(False, k2, s2, "F8_128_HMAC_SHA1_80")
+            r.set_factory(snd, nfs, True)
+            r.set_factory(rcv, nfr, False)
+        n_ssrc = 4 + step
+        b = synth.rtp_bundle(60, n_ssrc, (12, 1400), seed=800 + step, ext_frac=0.2,
+                             ssrcs=np.arange(n_ssrc, dtype=np.uint32) + 500,
+                             seq0=np.full(n_ssrc, (65520 + 15 * step) & 0xFFFF, np.uint32))
+        pb, st = r.bundle(snd, False, b)
+        assert (st == 0).all()
+        fb = inject_faults(pb, rng)
+        flags = np.zeros(fb.n, np.uint32)
+        flags[::9] = O.FLAG_SILENCE
+        flags[4::13] = O.FLAG_DISCARD
+        r.bundle(rcv, True, fb, flags=flags)
+        cb = synth.rtcp_bundle(12, 3, (12, 200), seed=820 + step,
+                               ssrcs=np.arange(3, dtype=np.uint32) + 500)
+        pc, st = r.bundle(cs, False, cb)
+        assert (st == 0).all()
+        r.bundle(cr, True, synth.select(pc, np.array([0, 2, 1, 2, 3, 4, 5, 11, 6, 7, 8, 9, 10])))
+    # ROC guesses overturned in-bundle, one SSRC
+    (k3, s3), = synth.keys(81, 1)
+    f3s, f3r = r.factory(True, k3, s3, "F8_128_HMAC_SHA1_80"), r.factory(False, k3, s3, "F8_128_HMAC_SHA1_80")
+    t3s, t3r = r.transformer(O.KIND_RTP, f3s), r.transformer(O.KIND_RTP, f3r)
+    for seqs in ([30000, 60000, 10, 20, 40000, 70, 33000], [20000, 52000, 52001, 100, 65535, 5]):
+        b = synth.rtp_bundle(len(seqs), 1, 333, seed=len(seqs) + 80)
+        set_seqs(b, seqs)
+        pb, _ = r.bundle(t3s, False, b)
+        r.bundle(t3r, True, pb)
+    # large packets and malformed headers (the F8 path throws only on the header)
+    r.bundle(t3s, False, synth.rtp_bundle(3, 2, 8000, seed=83))
+    mb = synth.rtp_bundle(30, 3, (12, 200), seed=84)
+    for i in range(mb.n):
+        mb.seg[mb.off[i]] = int(rng.integers(0, 256)) | 0x80
+        if rng.random() < 0.4:
+            mb.seg[mb.off[i] + 14] = int(rng.integers(0, 256))
+    r.bundle(t3r, True, mb)
+    r.bundle(t3s, False, mb)
+    r.save()
+
+
 SCENARIOS = [libsrtp_kat, c1_opus160_wrap, c2_video1200, c3_mixed_faults, c4_srtp_srtcp_rekey,
              edge_replay_quirks, edge_roc_overturn, lambda: edge_malformed(True),
              lambda: edge_malformed(False), edge_flags_lifecycle, edge_check_replay_off,
-             null_profiles]
+             null_profiles, sdes_f8]
 
 if __name__ == "__main__":
     O.build()
+    only = set(sys.argv[1:])  # scenario function names; none = all
     for sc in SCENARIOS:
-        sc()
+        if not only or getattr(sc, "__name__", "") in only:
+            sc()

@@ -21,7 +21,7 @@ def test_fixture_set_complete():
     for need in ("libsrtp_kat", "c1_opus160_wrap", "c2_video1200", "c3_mixed_faults",
                  "c4_srtp_srtcp_rekey", "edge_replay_quirks", "edge_roc_overturn",
                  "edge_malformed_abort", "edge_malformed_noabort", "edge_flags_lifecycle",
-                 "edge_check_replay_off", "null_profiles"):
+                 "edge_check_replay_off", "null_profiles", "sdes_f8"):
         assert need in names, need
 
 

@@ -21,6 +21,7 @@ P80 = profile_policies("AES_CM_128_HMAC_SHA1_80")
 P32 = profile_policies("AES_CM_128_HMAC_SHA1_32")
 PNULL80 = profile_policies("NULL_HMAC_SHA1_80")
 PNULL32 = profile_policies("NULL_HMAC_SHA1_32")
+PF8 = profile_policies("F8_128_HMAC_SHA1_80")
 LIBSRTP_KEY = bytes.fromhex("E1F97A0D3E018BE0D64FA32C06DE4139")
 LIBSRTP_SALT = bytes.fromhex("0EC675AD498AFEEBB6960B3AABE6")
 
@@ -97,7 +98,7 @@ def test_config2_video_1200B(twin):
     round_trip(twin, P80, b, [4096, 4096], key_seed=2)
 
 
-@pytest.mark.parametrize("pols", [P32, PNULL80, PNULL32], ids=["_32", "NULL_80", "NULL_32"])
+@pytest.mark.parametrize("pols", [P32, PNULL80, PNULL32, PF8], ids=["_32", "NULL_80", "NULL_32", "F8_80"])
 def test_profiles_round_trip(twin, pols):
     b = synth.rtp_bundle(3000, 37, (60, 1400), seed=synth.SEED_BASE + 4, ext_frac=0.1)
     round_trip(twin, pols, b, [1000, 2000], key_seed=4)
@@ -243,6 +244,45 @@ def test_config4_srtp_srtcp_mixed_rekey(twin):
         b, ts_s, ts_r = bundle(step)
         seg, ln, st = twin.run(ts_s, False, b.seg, b.off, b.length, b.cap)
         seg2, ln2, st2 = twin.run(ts_r, True, seg, b.off, ln, b.cap)
+
+
+def test_aes_f8_srtp_srtcp(twin):
+    """SDES F8_128_HMAC_SHA1_80 (SRTPCipherF8): C3 faults on F8 SRTP, DISCARD /
+    SILENCE flags, F8 SRTCP with replays, and one bundle mixing F8 and AES-CM
+    transformers (the CM packets take the fused kernels, the F8 ones k_f8)."""
+    rng = np.random.default_rng(synth.SEED_BASE + 8)
+    (k, s), (k2, s2) = synth.keys(8, 2)
+    fs, fr = twin.factory(True, k, s, *PF8), twin.factory(False, k, s, *PF8)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    seq0 = np.full(40, 65500, np.uint32)
+    b = synth.rtp_bundle(3000, 40, (12, 1400), seed=81, ext_frac=0.1, seq0=seq0)
+    seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+    assert (st == 0).all()
+    pb = b.copy()
+    pb.seg, pb.length = seg, ln
+    fb = inject_faults(pb, rng)
+    flags = np.zeros(fb.n, np.uint32)
+    flags[::9] = N.PKT_FLAG_SILENCE
+    flags[4::13] = N.PKT_FLAG_DISCARD
+    _, _, st = twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap, flags=flags)
+    assert (st == N.STATUS_OK).sum() > 0.9 * fb.n and (st == N.STATUS_DROP_AUTH).any()
+    cs, cr = twin.transformer(O.KIND_RTCP, fs), twin.transformer(O.KIND_RTCP, fr)
+    cb = synth.rtcp_bundle(300, 7, (12, 200), seed=82)
+    seg, ln, st = twin.run(cs, False, cb.seg, cb.off, cb.length, cb.cap)
+    pc = cb.copy()
+    pc.seg, pc.length = seg, ln
+    rb = synth.select(pc, np.r_[0:300, 5:40])  # + replays
+    twin.run(cr, True, rb.seg, rb.off, rb.length, rb.cap)
+    # mixed F8 + AES-CM bundle
+    gs = twin.factory(True, k2, s2, *P80)
+    t80 = twin.transformer(O.KIND_RTP, gs)
+    b1 = synth.rtp_bundle(500, 9, (60, 1400), seed=83, ssrcs=np.arange(9, dtype=np.uint32) + 7)
+    b2 = synth.rtp_bundle(500, 9, (60, 1400), seed=84, ssrcs=np.arange(9, dtype=np.uint32) + 7)
+    mb = synth.concat([b1, b2])
+    perm = rng.permutation(mb.n)
+    ts = [snd] * b1.n + [t80] * b2.n
+    mb = synth.select(mb, perm)
+    twin.run([ts[i] for i in perm], False, mb.seg, mb.off, mb.length, mb.cap)
 
 
 def test_replay_window_quirks_q6_q7_q13(twin):

@@ -134,3 +134,50 @@ def test_malformed(oracle, abort):
         P.run(r, True, pb, abort=abort)
         cb = synth.rtcp_bundle(20, 3, (12, 40), seed=60 + rep)
         P.run(tc, True, cb, abort=abort)
+
+
+def test_aes_f8_profiles(oracle):
+    """AES-F8 (SDES F8_128_HMAC_SHA1_80, SRTPCipherF8) for SRTP and SRTCP:
+    protect, tampering, replays, a ROC wrap, extension headers, and the SRTCP
+    quirk of ciphering only [8, 8 + length - 4 - tag)."""
+    P = Pair(oracle)
+    (k, s), = synth.keys(7, 1)
+    for tags in ((10, 10), (4, 4), (4, 10)):
+        f, fr = P.factory(True, k, s, *pols(*tags, enc=2)), P.factory(False, k, s, *pols(*tags, enc=2))
+        t, r = P.transformer(0, f), P.transformer(0, fr)
+        tc, rc = P.transformer(1, f), P.transformer(1, fr)
+        for rep in range(3):
+            b = synth.rtp_bundle(40, 3, (12, 300), seed=70 + rep, ext_frac=0.3,
+                                 ssrcs=np.arange(3, dtype=np.uint32) + 9,
+                                 seq0=np.full(3, (65525 + 40 * rep) & 0xFFFF, np.uint32))
+            pb, st = P.run(t, False, b)
+            assert (st == 0).all()
+            pb.seg[pb.off[5] + 13] ^= 4  # tamper
+            ub, st = P.run(r, True, synth.concat([pb, synth.select(pb, np.arange(3))]))  # + replays
+            assert st[5] == 2 and (st[40:] == 1).all()
+            for i in range(40):  # accepted packets come back as the original RTP
+                if i != 5:
+                    o = b.off[i]
+                    assert st[i] == 0 and ub.length[i] == b.length[i]
+                    assert np.array_equal(ub.seg[o:o + b.length[i]], b.seg[o:o + b.length[i]])
+            cb = synth.rtcp_bundle(20, 3, (12, 120), seed=80 + rep,
+                                   ssrcs=np.arange(3, dtype=np.uint32) + 9)
+            pcb, st = P.run(tc, False, cb)
+            assert (st == 0).all()
+            ucb, st = P.run(rc, True, pcb)
+            assert (st == 0).all()
+            for i in range(cb.n):
+                o = cb.off[i]
+                assert np.array_equal(ucb.seg[o:o + cb.length[i]], cb.seg[o:o + cb.length[i]])
+
+
+def test_f8_policy_bounds(oracle):
+    """SRTCP F8 ciphers [8, 8 + length - 4 - tag): outside the packet without an
+    HMAC trailer of >= 4 tag bytes, so such SRTCP policies are refused (the
+    SRTP side of the same factory may use any tag length)."""
+    (k, s), = synth.keys(9, 1)
+    with pytest.raises(ValueError):
+        oracle.Factory(True, k, s, oracle.Policy(2, 16, 1, 20, 10, 14), oracle.Policy(2, 16, 0, 0, 0, 14))
+    with pytest.raises(ValueError):
+        oracle.Factory(True, k, s, oracle.Policy(2, 16, 1, 20, 10, 14), oracle.Policy(2, 16, 1, 20, 2, 14))
+    oracle.Factory(True, k, s, oracle.Policy(2, 16, 0, 0, 0, 14), oracle.Policy(2, 16, 1, 20, 4, 14))

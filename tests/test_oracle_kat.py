@@ -49,6 +49,30 @@ def test_rfc3711_b2_keystream(oracle):
                                 "41E95B3BB0A2E8DD477901E4FCA894C0")
 
 
+# RFC 3711 App. B.1: AES-f8 (IV' = E(k_e ^ (k_s || 0x55..), IV), chained S(j))
+B1_KEY = bytes.fromhex("234829008467be186c3de14aae72d62c")
+B1_SALT = bytes.fromhex("32f2870d")
+B1_IV = bytes.fromhex("006e5cba50681de55c621599d462564a")  # 0 || RTP header[1..11] || ROC
+B1_PT = b"pseudorandomness is the next best thing"
+B1_CT = ("019ce7a26e7854014a6366aa95d4eefd" "1ad4172a14f9faf455b7f1d4b62bd08f" "562c0eef7c4802")
+
+
+def test_rfc3711_b1_aes_f8(oracle):
+    mask = bytes(k ^ (B1_SALT[i] if i < 4 else 0x55) for i, k in enumerate(B1_KEY))
+    assert oracle.aes128_block(mask, B1_IV).hex() == "595b699bbd3bc0df26062093c1ad8f73"  # IV'
+    assert oracle.aes_f8(B1_KEY, B1_SALT, B1_IV, B1_PT).hex() == B1_CT
+    # F8 is an involution on the same IV
+    assert oracle.aes_f8(B1_KEY, B1_SALT, B1_IV, bytes.fromhex(B1_CT)) == B1_PT
+
+
+def test_rfc3711_b1_aes_f8_pyref():
+    from oracle import pyref as R
+    buf = bytearray(B1_PT)
+    R.f8_process(R.expand_key(B1_KEY), R.expand_key(R.f8_key_mask(B1_KEY, B1_SALT)), buf, 0,
+                 len(buf), B1_IV)
+    assert buf.hex() == B1_CT
+
+
 def test_rfc3711_b3_key_derivation(oracle):
     enc, auth, salt = oracle.derive_keys(B3_KEY, B3_SALT)
     assert enc.hex().upper() == "C61E7A93744F39EE10734AFE3FF7A087"
