@@ -48,6 +48,8 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the pinned-host end-to-end leg")
+    ap.add_argument("--e2e-bundles", type=int, default=24)
     ap.add_argument("--serial", action="store_true",
                     help="run the receiver on the sender's stream (no overlap between "
                          "step i's unprotect and step i+1's protect)")
@@ -100,6 +102,59 @@ def cpu_baseline(seconds: float, threads: int, pkt_len: int, ssrcs: int):
         th.join()
     dt = time.perf_counter() - t0
     return sum(counts) / dt, sum(counts), dt
+
+
+def e2e_leg(b, pols, keys, n, L, local_rank, bundles, depth=3):
+    """End-to-end through PCIe (SURVEY.md 8d "end-to-end: pinned host buffers,
+    H2D + kernels + D2H"): the same workload's bundles held in pinned host
+    slots of an SRTPPipeline, each bundle copied to HBM, processed, copied
+    back.  Each slot alternates protect (sender) and unprotect (receiver) of
+    its bundle, so its content returns to the original RTP every two bundles;
+    the engine runs with checkReplay off (SRTPCryptoContext's config flag) so
+    the repeated sequence numbers are processed in full, not dropped.
+    Returns directional packets/s (one bundle = one direction) and PCIe GB/s."""
+    from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPPipeline, SRTPTransformer
+    eng = SRTPEngine(device=local_rank, check_replay=False, max_contexts=1 << 15,
+                     max_factories=8, max_transformers=8, max_batch=n)
+    k, s = keys
+    snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
+    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng))
+    nb = len(b.seg)
+    pl = SRTPPipeline(eng, max_packets=n, max_seg_bytes=nb, depth=depth)
+    for j in range(depth):
+        sl = pl.slot(j)
+        sl["seg"][:nb] = b.seg
+        sl["off"][:n] = b.off
+        sl["len"][:n] = b.length
+        sl["cap"][:n] = b.cap
+    use = [0] * depth
+
+    def submit(i):
+        j = i % depth
+        rev = use[j] % 2 == 1
+        pl.submit(j, rev, n, nb, tid=(rcv if rev else snd).tid)
+        use[j] += 1
+
+    warm = 2 * depth
+    for i in range(warm):
+        submit(i)
+    for j in range(depth):
+        pl.wait(j)
+    t0 = time.perf_counter()
+    for i in range(warm, warm + bundles):
+        submit(i)
+    for j in range(depth):
+        pl.wait(j)
+    dt = time.perf_counter() - t0
+    ok = all(int((pl.slot(j)["status"][:n] != 0).sum()) == 0 for j in range(depth))
+    pps = bundles * n / dt
+    pcie = bundles * 2 * nb / dt / 1e9
+    pl.close()
+    return {"directional_pps": round(pps, 1), "round_trip_pps": round(pps / 2, 1),
+            "pcie_gbps_h2d_plus_d2h": round(pcie, 2), "bundles": bundles, "depth": depth,
+            "all_accepted": ok,
+            "note": "pinned host slots -> H2D -> protect or unprotect -> D2H, bundles of the "
+                    "same workload; checkReplay off so repeated bundles are processed in full"}
 
 
 def main():
@@ -292,6 +347,12 @@ def main():
                          f"4096-packet bundles, {nssrc} SSRCs split across threads",
                "gbps": round(v * alg_bytes_rt / 1e9, 3)}
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        del segs, lens
+        torch.cuda.empty_cache()
+        e2e = e2e_leg(b, pols, (k, s), n, L, local_rank, args.e2e_bundles)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -325,6 +386,7 @@ def main():
                          "copy_measured_gbps": copy_gbs,
                          "algorithmic_bytes_per_launch": n * (L + L + T)},
             "cpu_baseline": cpu,
+            "e2e": e2e,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

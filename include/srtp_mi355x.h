@@ -194,6 +194,40 @@ int srtp_engine_set_timing(srtp_engine *e, int32_t enable);
  * bundle count since the last read into ms[] / count[], and resets. */
 int srtp_engine_read_timing(srtp_engine *e, double *ms, uint64_t *count);
 
+/* Host bundle pipeline (SURVEY.md 8d end-to-end timing, 8f.2 bundle former):
+ * `depth` slots of pinned host memory the caller packs bundles into directly
+ * (the RawPacket[] -> packed-segment marshalling a JNI shim does; see
+ * INTEGRATION.md), each moved H2D on a copy stream, processed by the engine on
+ * its stream in submission order, and moved D2H on a second copy stream, so
+ * slot i's copies overlap slot j's kernels.  Replaces the reference's
+ * per-packet calls through PacketTransformer.transform/reverseTransform
+ * (transform/PacketTransformer.java:28-53) fed 1-element arrays by
+ * RTPConnectorInputStream.java:425-452 / RTPConnectorOutputStream.java:268-300.
+ *
+ * srtp_pipeline_slot_get returns slot i's pinned arrays (seg holds seg_cap
+ * bytes; the per-packet arrays hold max_packets entries).  srtp_pipeline_submit
+ * enqueues slot i's first n packets (seg_bytes of segment) as one bundle for
+ * transformer `tid`, or per packet from slot.tids when use_tids != 0; flags
+ * are passed when use_flags != 0.  It first waits for the slot's previous
+ * bundle.  srtp_pipeline_wait blocks until slot i's results (seg, len, status)
+ * are back in its pinned arrays.  Packet regions are validated as in
+ * srtp_transform_host. */
+typedef struct srtp_pipeline srtp_pipeline;
+typedef struct {
+    uint8_t *seg;
+    size_t seg_cap;
+    uint32_t *off, *len, *cap, *flags;
+    int32_t *tids, *status;
+    uint32_t max_packets;
+} srtp_pipeline_slot;
+int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes,
+                         int32_t depth, srtp_pipeline **out);
+void srtp_pipeline_destroy(srtp_pipeline *pl);
+int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *out);
+int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                         int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes);
+int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
+
 /* Control-plane crypto without a GPU (used by CPU-side tests): RFC 3711 4.3
  * session keys exactly as SRTPCryptoContext.deriveSrtpKeys (rtcp = 0) /
  * SRTCPCryptoContext.deriveSrtcpKeys (rtcp = 1). */

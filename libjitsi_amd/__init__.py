@@ -1,15 +1,16 @@
 """libjitsi_amd -- MI355X-native SRTP/SRTCP packet-crypto engine.
 
 A drop-in for the per-packet hot path of libjitsi's SRTPTransformer /
-SRTCPTransformer (AES_CM_128_HMAC_SHA1_80/_32 and NULL-cipher profiles):
+SRTCPTransformer (AES_CM_128_HMAC_SHA1_80/_32, F8_128_HMAC_SHA1_80 and NULL-cipher
+profiles):
 bundles of packets from many SSRC contexts are protected/unprotected by
 hand-written gfx950 kernels behind the C ABI in include/srtp_mi355x.h.
 """
 from .srtp import (PacketTransformer, RawPacket, SRTCPTransformer, SRTPContextFactory,  # noqa: F401
-                   SRTPEngine, SRTPPolicy, SRTPTransformer, SRTPTransformException, pack,
+                   SRTPEngine, SRTPPipeline, SRTPPolicy, SRTPTransformer, SRTPTransformException, pack,
                    profile_policies, transform_bundle)
 from . import _native  # noqa: F401
 
 __all__ = ["PacketTransformer", "RawPacket", "SRTCPTransformer", "SRTPContextFactory", "SRTPEngine",
-           "SRTPPolicy", "SRTPTransformer", "SRTPTransformException", "pack", "profile_policies",
+           "SRTPPipeline", "SRTPPolicy", "SRTPTransformer", "SRTPTransformException", "pack", "profile_policies",
            "transform_bundle"]

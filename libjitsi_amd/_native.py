@@ -33,7 +33,8 @@ EXPORTED = [
     "srtp_transform_device", "srtp_transform_host", "srtp_engine_sync",
     "srtp_get_context_state", "srtp_engine_num_contexts", "srtp_engine_set_timing",
     "srtp_engine_read_timing", "srtp_derive_session_keys", "srtp_export_contexts",
-    "srtp_set_context_state",
+    "srtp_set_context_state", "srtp_pipeline_create", "srtp_pipeline_destroy",
+    "srtp_pipeline_slot_get", "srtp_pipeline_submit", "srtp_pipeline_wait",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -59,6 +60,12 @@ class CtxState(C.Structure):
                 ("guessed_roc", C.c_int32), ("sent_index", C.c_int32),
                 ("received_index", C.c_int32), ("replay_window", C.c_uint64),
                 ("key_set", C.c_uint32)]
+
+
+class PipelineSlot(C.Structure):
+    _fields_ = [("seg", C.c_void_p), ("seg_cap", C.c_size_t), ("off", C.c_void_p),
+                ("len", C.c_void_p), ("cap", C.c_void_p), ("flags", C.c_void_p),
+                ("tids", C.c_void_p), ("status", C.c_void_p), ("max_packets", C.c_uint32)]
 
 
 _lib = None
@@ -98,6 +105,12 @@ def lib() -> C.CDLL:
     L.srtp_derive_session_keys.argtypes = [pu8, pu8, i32, pu8, pu8, pu8]
     L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
     L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
+    L.srtp_pipeline_create.argtypes = [vp, u32, C.c_size_t, i32, C.POINTER(vp)]
+    L.srtp_pipeline_destroy.argtypes = [vp]
+    L.srtp_pipeline_destroy.restype = None
+    L.srtp_pipeline_slot_get.argtypes = [vp, i32, C.POINTER(PipelineSlot)]
+    L.srtp_pipeline_submit.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t]
+    L.srtp_pipeline_wait.argtypes = [vp, i32]
     _lib = L
     return L
 

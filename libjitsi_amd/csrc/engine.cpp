@@ -521,6 +521,19 @@ int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, 
     return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s);
 }
 
+// Every packet region [off, off + cap rounded to 16) inside the segment,
+// 16-B aligned, cap <= 65535 (the kernels' 16-bit length fields).
+static int validate_regions(srtp_engine *e, const uint32_t *off, const uint32_t *cap, uint32_t n,
+                            size_t seg_bytes) {
+    for (uint32_t i = 0; i < n; i++) {
+        if (off[i] % 16 != 0) return fail(e, SRTP_EINVAL, "off[i] must be 16-byte aligned");
+        uint64_t end = (uint64_t)off[i] + ((cap[i] + 15u) & ~15u);
+        if (cap[i] > 65535u || end > seg_bytes)
+            return fail(e, SRTP_EINVAL, "packet region outside the segment");
+    }
+    return SRTP_OK;
+}
+
 int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
                         uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
                         const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n) {
@@ -528,12 +541,8 @@ int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, in
     std::lock_guard<std::mutex> g(e->mu);
     if (n == 0) return SRTP_OK;
     if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
-    for (uint32_t i = 0; i < n; i++) {
-        if (off[i] % 16 != 0) return fail(e, SRTP_EINVAL, "off[i] must be 16-byte aligned");
-        uint64_t end = (uint64_t)off[i] + ((cap[i] + 15u) & ~15u);
-        if (cap[i] > 65535u || end > seg_bytes)
-            return fail(e, SRTP_EINVAL, "packet region outside the segment");
-    }
+    int vr = validate_regions(e, off, cap, n, seg_bytes);
+    if (vr != SRTP_OK) return vr;
     hipStream_t s = e->stream;
     size_t need = (seg_bytes + 15) & ~(size_t)15;
     if (need > e->h_seg_bytes) {
@@ -726,3 +735,142 @@ int srtp_derive_session_keys(const uint8_t mk[16], const uint8_t ms[14], int32_t
 }
 
 } // extern "C"
+
+// ------------------------------------------------------------ host pipeline
+struct srtp_pipeline {
+    srtp_engine *e = nullptr;
+    uint32_t max_n = 0;
+    size_t max_seg = 0;
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    std::mutex mu;
+    struct Slot {
+        srtp_pipeline_slot h{};     // pinned host arrays
+        uint8_t *d_seg = nullptr;   // device copies
+        uint32_t *d_off = nullptr, *d_len = nullptr, *d_cap = nullptr, *d_flags = nullptr;
+        int32_t *d_tids = nullptr, *d_status = nullptr;
+        hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out = nullptr;
+        bool busy = false;
+        int rc = SRTP_OK;           // engine return code of the last submit
+    };
+    std::vector<Slot> slots;
+};
+
+static void pipeline_free(srtp_pipeline *pl) {
+    for (auto &sl : pl->slots) {
+        if (sl.busy && sl.ev_out) (void)hipEventSynchronize(sl.ev_out);
+        void *hp[] = {sl.h.seg, sl.h.off, sl.h.len, sl.h.cap, sl.h.flags, sl.h.tids, sl.h.status};
+        for (void *p : hp)
+            if (p) (void)hipHostFree(p);
+        void *dp[] = {sl.d_seg, sl.d_off, sl.d_len, sl.d_cap, sl.d_flags, sl.d_tids, sl.d_status};
+        for (void *p : dp) dfree(p);
+        hipEvent_t ev[] = {sl.ev_in, sl.ev_done, sl.ev_out};
+        for (auto x : ev)
+            if (x) (void)hipEventDestroy(x);
+    }
+    if (pl->s_in) (void)hipStreamDestroy(pl->s_in);
+    if (pl->s_out) (void)hipStreamDestroy(pl->s_out);
+    delete pl;
+}
+
+template <class T> static hipError_t halloc(T **p, size_t count) {
+    return hipHostMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+}
+
+int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes,
+                         int32_t depth, srtp_pipeline **out) {
+    if (!e || !out || depth < 1 || depth > 16 || max_packets == 0 || max_packets > kRecIdxMask)
+        return SRTP_EINVAL;
+    *out = nullptr;
+    srtp_pipeline *pl = new (std::nothrow) srtp_pipeline();
+    if (!pl) return SRTP_ENOMEM;
+    pl->e = e;
+    pl->max_n = max_packets;
+    pl->max_seg = (max_seg_bytes + 15) & ~(size_t)15;
+    pl->slots.resize((size_t)depth);
+    bool ok = hipSetDevice(e->opts.device) == hipSuccess &&
+              hipStreamCreateWithFlags(&pl->s_in, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&pl->s_out, hipStreamNonBlocking) == hipSuccess;
+    for (auto &sl : pl->slots) {
+        if (!ok) break;
+        const size_t n = max_packets;
+        ok = halloc(&sl.h.seg, pl->max_seg) == hipSuccess && halloc(&sl.h.off, n) == hipSuccess &&
+             halloc(&sl.h.len, n) == hipSuccess && halloc(&sl.h.cap, n) == hipSuccess &&
+             halloc(&sl.h.flags, n) == hipSuccess && halloc(&sl.h.tids, n) == hipSuccess &&
+             halloc(&sl.h.status, n) == hipSuccess &&
+             dalloc(&sl.d_seg, pl->max_seg) == hipSuccess && dalloc(&sl.d_off, n) == hipSuccess &&
+             dalloc(&sl.d_len, n) == hipSuccess && dalloc(&sl.d_cap, n) == hipSuccess &&
+             dalloc(&sl.d_flags, n) == hipSuccess && dalloc(&sl.d_tids, n) == hipSuccess &&
+             dalloc(&sl.d_status, n) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&sl.ev_out, hipEventDisableTiming) == hipSuccess;
+        sl.h.seg_cap = pl->max_seg;
+        sl.h.max_packets = max_packets;
+    }
+    if (!ok) {
+        pipeline_free(pl);
+        return SRTP_ENOMEM;
+    }
+    *out = pl;
+    return SRTP_OK;
+}
+
+void srtp_pipeline_destroy(srtp_pipeline *pl) {
+    if (pl) pipeline_free(pl);
+}
+
+int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *out) {
+    if (!pl || !out || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
+    *out = pl->slots[(size_t)slot].h;
+    return SRTP_OK;
+}
+
+static int pipeline_wait_locked(srtp_pipeline *pl, srtp_pipeline::Slot &sl) {
+    if (!sl.busy) return SRTP_OK;
+    sl.busy = false;
+    if (hipEventSynchronize(sl.ev_out) != hipSuccess) return fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
+    return sl.rc;
+}
+
+int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                         int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes) {
+    if (!pl || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> gp(pl->mu);
+    srtp_pipeline::Slot &sl = pl->slots[(size_t)slot];
+    srtp_engine *e = pl->e;
+    (void)pipeline_wait_locked(pl, sl); // the slot's previous bundle (its status is the caller's)
+    if (n > pl->max_n || seg_bytes > pl->max_seg) return fail(e, SRTP_EINVAL, "bundle exceeds the slot");
+    if (n == 0) return SRTP_OK;
+    seg_bytes = (seg_bytes + 15) & ~(size_t)15;
+    std::lock_guard<std::mutex> g(e->mu);
+    int rc = validate_regions(e, sl.h.off, sl.h.cap, n, seg_bytes);
+    if (rc != SRTP_OK) return rc;
+    if (!use_tids && (tid < 0 || (size_t)tid >= e->transformers.size()))
+        return fail(e, SRTP_EINVAL, "bad transformer id");
+    hipStream_t si = pl->s_in, so = pl->s_out, s = e->stream;
+    HIPCHK(e, hipMemcpyAsync(sl.d_seg, sl.h.seg, seg_bytes, hipMemcpyHostToDevice, si));
+    HIPCHK(e, hipMemcpyAsync(sl.d_off, sl.h.off, n * 4ull, hipMemcpyHostToDevice, si));
+    HIPCHK(e, hipMemcpyAsync(sl.d_len, sl.h.len, n * 4ull, hipMemcpyHostToDevice, si));
+    HIPCHK(e, hipMemcpyAsync(sl.d_cap, sl.h.cap, n * 4ull, hipMemcpyHostToDevice, si));
+    if (use_flags) HIPCHK(e, hipMemcpyAsync(sl.d_flags, sl.h.flags, n * 4ull, hipMemcpyHostToDevice, si));
+    if (use_tids) HIPCHK(e, hipMemcpyAsync(sl.d_tids, sl.h.tids, n * 4ull, hipMemcpyHostToDevice, si));
+    HIPCHK(e, hipEventRecord(sl.ev_in, si));
+    HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+    sl.rc = transform_locked(e, reverse, use_tids ? sl.d_tids : nullptr, tid, sl.d_seg, sl.d_off,
+                             sl.d_len, sl.d_cap, use_flags ? sl.d_flags : nullptr, sl.d_status, n, s);
+    if (sl.rc != SRTP_OK) return sl.rc;
+    HIPCHK(e, hipEventRecord(sl.ev_done, s));
+    HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+    HIPCHK(e, hipMemcpyAsync(sl.h.seg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
+    HIPCHK(e, hipMemcpyAsync(sl.h.len, sl.d_len, n * 4ull, hipMemcpyDeviceToHost, so));
+    HIPCHK(e, hipMemcpyAsync(sl.h.status, sl.d_status, n * 4ull, hipMemcpyDeviceToHost, so));
+    HIPCHK(e, hipEventRecord(sl.ev_out, so));
+    sl.busy = true;
+    return SRTP_OK;
+}
+
+int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot) {
+    if (!pl || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> gp(pl->mu);
+    return pipeline_wait_locked(pl, pl->slots[(size_t)slot]);
+}

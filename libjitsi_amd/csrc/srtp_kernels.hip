@@ -1434,16 +1434,21 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
         sha1_compress(h, c); // block b-1, a full block before the ROC-carrying one
     }
-    for (; b < n_blocks; b++) {
-        uint32_t d[16];
-        uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
+    // The blocks left after the fused loop: first the MAC over their
+    // ciphertext, then their decryption -- two loops, so that no AES state
+    // (round keys, counter, keystream carry) is live across SHA-1 and nothing
+    // spills to scratch; the round keys are reloaded for the second loop.
+    const int b_tail = b;
+    if (do_mac) {
+        for (; b < n_blocks; b++) {
+            uint32_t d[16];
+            const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
 #pragma unroll
-        for (int m = 0; m < 4; m++) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (b < nb_data && 64 * b + 16 * m < end) v = qp[m];
-            d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
-        }
-        if (do_mac) {
+            for (int m = 0; m < 4; m++) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (b < nb_data && 64 * b + 16 * m < end) v = qp[m];
+                d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
+            }
             if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
@@ -1455,32 +1460,33 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                         tp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
                 }
             }
-            uint32_t w[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) w[k] = d[k];
-            if (b < nb_inner) inner_words(w, b, end, suffix);
-            else outer_words(w, h, ks);
-            sha1_compress(h, w);
+            if (b < nb_inner) inner_words(d, b, end, suffix);
+            else outer_words(d, h, ks);
+            sha1_compress(h, d);
         }
-        if (spec && b < nb_data && 64 * b + 64 > cs.off) {
-            if (do_mac) {
-                // re-read the chunk (L1/L2-hot) rather than keep 16 words live across SHA-1
-                asm volatile("" ::: "memory");
+        a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+    }
+    if (spec) {
+        asm volatile("" ::: "memory"); // reload the round keys below, do not keep them live
+        RoundKeys rk2;
+        load_round_keys_uniform(ks, rk2);
+        for (int c = b_tail; c < nb_data; c++) {
+            if (64 * c + 64 <= cs.off) continue;
+            uint32_t d[16];
+            uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * c);
 #pragma unroll
-                for (int m = 0; m < 4; m++) {
-                    uint4 v = make_uint4(0, 0, 0, 0);
-                    if (64 * b + 16 * m < end) v = qp[m];
-                    d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
-                }
+            for (int m = 0; m < 4; m++) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (64 * c + 16 * m < end) v = qp[m];
+                d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
             }
-            ctr_chunk(lds, tb, rk, cs, b, d);
+            ctr_chunk(lds, tb, rk2, cs, c, d);
 #pragma unroll
             for (int m = 0; m < 4; m++)
-                if (64 * b + 16 * m < end && 64 * b + 16 * m + 16 > cs.off)
+                if (64 * c + 16 * m < end && 64 * c + 16 * m + 16 > cs.off)
                     qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
         }
     }
-    if (do_mac) a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kAesBlock) void k_unprotect(BundleArgs a) {

@@ -70,6 +70,66 @@ class SRTPPolicy:
                 f"{self.authKeyLength}, tag={self.authTagLength}, salt={self.saltKeyLength})")
 
 
+class SRTPPipeline:
+    """Pinned-host bundle pipeline over one engine (srtp_pipeline_*, C ABI).
+
+    ``depth`` slots of pinned host memory; a caller packs a bundle straight
+    into a slot's arrays (``slot(i)``: numpy views ``seg``, ``off``, ``len``,
+    ``cap``, ``flags``, ``tids``, ``status``), ``submit``s it (H2D on a copy
+    stream, the engine's kernels, D2H on a second copy stream) and ``wait``s
+    for the results in the same arrays.  Bundles run in submission order;
+    while slot i's kernels run, slot j's copies proceed.  This is the bundle
+    former the reference lacks (its I/O layer hands 1-element RawPacket[]
+    arrays to PacketTransformer.transform, RTPConnectorOutputStream.java:268-300)."""
+
+    def __init__(self, engine: "SRTPEngine", max_packets: int, max_seg_bytes: int, depth: int = 3):
+        self.engine = engine
+        h = C.c_void_p()
+        N.check(N.lib().srtp_pipeline_create(engine.h, max_packets, max_seg_bytes, depth,
+                                             C.byref(h)), engine.h, "srtp_pipeline_create")
+        self.h = h
+        self.depth = depth
+        self._slots = []
+        for i in range(depth):
+            sl = N.PipelineSlot()
+            N.check(N.lib().srtp_pipeline_slot_get(self.h, i, C.byref(sl)), engine.h, "slot_get")
+            m = sl.max_packets
+
+            def view(ptr, ct, count):
+                return np.ctypeslib.as_array((ct * count).from_address(ptr))
+            self._slots.append(dict(
+                seg=view(sl.seg, C.c_uint8, sl.seg_cap), off=view(sl.off, C.c_uint32, m),
+                len=view(sl.len, C.c_uint32, m), cap=view(sl.cap, C.c_uint32, m),
+                flags=view(sl.flags, C.c_uint32, m), tids=view(sl.tids, C.c_int32, m),
+                status=view(sl.status, C.c_int32, m)))
+
+    def slot(self, i: int) -> dict:
+        return self._slots[i]
+
+    def submit(self, i: int, reverse: bool, n: int, seg_bytes: int, tid=None,
+               use_flags: bool = False) -> None:
+        """Enqueue slot i's first n packets; ``tid`` = one transformer id, or
+        None to use the slot's per-packet ``tids``."""
+        N.check(N.lib().srtp_pipeline_submit(self.h, i, int(reverse), int(tid is None),
+                                             -1 if tid is None else int(tid), int(use_flags),
+                                             n, seg_bytes), self.engine.h, "srtp_pipeline_submit")
+
+    def wait(self, i: int) -> None:
+        N.check(N.lib().srtp_pipeline_wait(self.h, i), self.engine.h, "srtp_pipeline_wait")
+
+    def close(self) -> None:
+        if self.h:
+            self._slots = []
+            N.lib().srtp_pipeline_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def profile_policies(profile: str):
     """(srtpPolicy, srtcpPolicy) of a DTLS-SRTP protection profile, as the table
     in transform/dtls/DtlsPacketTransformer.java:574-612 builds them (note the
