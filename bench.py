@@ -50,6 +50,8 @@ def parse_args():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned-host end-to-end leg")
     ap.add_argument("--e2e-bundles", type=int, default=24)
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for the barrier/timing reduction (nccl = RCCL)")
     ap.add_argument("--serial", action="store_true",
                     help="run the receiver on the sender's stream (no overlap between "
                          "step i's unprotect and step i+1's protect)")
@@ -165,9 +167,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # SRTP_BENCH_ONE_DEVICE=1 puts every rank on device 0: a rehearsal of the
+    # N-rank path on a 1-GPU box (with --backend gloo; RCCL wants distinct GPUs)
+    if os.environ.get("SRTP_BENCH_ONE_DEVICE") == "1":
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local_rank)
 
     from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPTransformer, profile_policies, synth
@@ -293,6 +302,8 @@ def main():
     ok = ok and int((st != 0).sum()) == 0 and int((st_r != 0).sum()) == 0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
+        if args.backend != "nccl":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = float(t.item())
 
