@@ -1382,6 +1382,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             spec = true;
         }
     }
+    if (a.debug == 5) spec = false; // diagnostics: MAC only (results wrong by design)
     a.spec[p] = spec ? 1u : 0u;
     if (!do_mac && !spec) return;
     cs.end = spec ? end : 0;
@@ -1449,7 +1450,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 if (b < nb_data && 64 * b + 16 * m < end) v = qp[m];
                 d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
             }
-            if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
+            if (b == nb_full && rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
