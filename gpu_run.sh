@@ -37,10 +37,10 @@ if [ "$MODE" = one ]; then
   step pytest_one 600 python -m pytest tests -m gpu -q -x --timeout 300 -p no:cacheprovider -k "${2:-malformed}"
 fi
 if [ "$MODE" = diag2 ]; then
-  step diag2 300 python tools_diag2.py
+  step diag2 300 python tools/twin_diag.py
 fi
 if [ "$MODE" = diag ]; then
-  step diag 600 python tools_diag.py
+  step diag 600 python tools/bench_loop_diag.py
 fi
 if [ "$MODE" = micro ]; then
   step sort_bench 120 ./tools/sort_bench

@@ -1,6 +1,6 @@
 """GPU diagnostic for the bench loop: per-step status histograms + oracle twin."""
 import sys, numpy as np, torch
-sys.path.insert(0, '.')
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPTransformer, profile_policies, synth
 from oracle import oracle as O
 n, nssrc, L = 1 << 18, 10000, 1200

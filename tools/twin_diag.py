@@ -1,4 +1,4 @@
-import sys; sys.path.insert(0, '.'); sys.path.insert(0, 'tests')
+import os, sys; R = os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path.insert(0, R); sys.path.insert(0, os.path.join(R, 'tests'))
 import numpy as np
 from libjitsi_amd import SRTPEngine, profile_policies, synth
 from harness import Twin
