@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsrtp_mi355x.so")
+# SRTP_MI355X_LIB: another in-tree build of the same ABI (diagnostic variants)
+LIB_PATH = os.environ.get("SRTP_MI355X_LIB") or os.path.join(_HERE, "libsrtp_mi355x.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "srtp_mi355x.h")
 
 # include/srtp_mi355x.h
