@@ -1610,39 +1610,93 @@ __device__ __forceinline__ void load_rk_uniform(const uint32_t *__restrict__ p, 
     }
 }
 
-// SRTPCipherF8.process :97-128 + processBlock :145-183 over packet bytes
-// [off, off + len) (off a multiple of 4; len <= 0 ciphers nothing).
-__device__ void f8_region(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
-                          const F8Keys *f8, uint8_t *pkt, int off, int len, const uint32_t iv[4]) {
-    uint32_t ivp[4] = {iv[0], iv[1], iv[2], iv[3]};
-    {
-        RoundKeys rkf; // IV' = E(k_e ^ (k_s || 0x55..), IV)
-        load_rk_uniform(f8->rk, rkf);
-        uint32_t z[4] = {0u, 0u, 0u, 0u};
-        aes_encrypt2(lds, tb, rkf, ivp, z);
+// One packet's AES-F8 work: IV, ciphered region [off, off + len), and for
+// protect the HMAC trailer.
+struct F8Job {
+    uint8_t *pkt;
+    int off, len;   // ciphered region (off a multiple of 4; len <= 0: none)
+    uint32_t iv[4]; // IV, little-endian words
+    int L;          // protect: MAC length (the packet before its trailer)
+    uint32_t suffix;
+    bool rtcp;
+};
+
+__device__ __forceinline__ F8Job f8_job(const BundleArgs &a, const KeySet *ks, uint32_t p) {
+    F8Job j;
+    j.pkt = a.seg + a.off[p];
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(j.pkt);
+    const int T = (int)sgpr(ks->tag_len);
+    const bool mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    const uint32_t cw = a.w_cw[p];
+    j.rtcp = sgpr(ks->kind) == SRTP_KIND_RTCP;
+    if (!j.rtcp) {
+        // processPacketAESF8 :532-555: IV = 0 || header[1..11] || ROC_be
+        j.iv[0] = hdr.x & 0xffffff00u; j.iv[1] = hdr.y; j.iv[2] = hdr.z; j.iv[3] = bswap(cw);
+        j.L = (int)a.len[p] - (!a.reverse && mac ? T : 0);
+        j.off = rtp_header_len(j.pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        j.len = j.L - j.off;
+        j.suffix = cw;
+    } else {
+        // SRTCPCryptoContext.processPacketAESF8 :267-298: IV = 0^4 || (index |
+        // E)_be || header[0..7]; ciphers [8, 8 + length - 4 - tag) of the length
+        // at the call (protect: before the trailer; unprotect: after shrinking it)
+        j.suffix = cw | 0x80000000u;
+        j.iv[0] = 0u; j.iv[1] = bswap(j.suffix); j.iv[2] = hdr.x; j.iv[3] = hdr.y;
+        j.L = (int)a.len[p] - (a.reverse ? 0 : 4 + T);
+        j.off = 8;
+        j.len = j.L - 4 - T;
     }
-    if (len <= 0) return;
+    return j;
+}
+
+// XOR keystream block S into job bytes [off + 16 jb, ...) within its region.
+__device__ __forceinline__ void f8_xor_block(const F8Job &j, int jb, const uint32_t S[4]) {
+    const int end = j.off + j.len;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pos = j.off + 16 * jb + 4 * k;
+        if (pos < end) {
+            const int rem = end - pos;
+            const uint32_t m = rem >= 4 ? ~0u : ((1u << (8 * rem)) - 1u);
+            uint32_t *w = reinterpret_cast<uint32_t *>(j.pkt + pos);
+            *w ^= S[k] & m;
+        }
+    }
+}
+
+// SRTPCipherF8.process :97-128 + processBlock :145-183 for two packets of one
+// key set at once (the second may be absent: has1 false), so both blocks of
+// the two-block AES round code do useful work: IV' = E(k_e ^ (k_s || 0x55..),
+// IV), then S(j) = E(k_e, IV' ^ S(j-1) ^ j), S(-1) = 0, j big-endian in bytes
+// 12..15, XORed over each packet's region.
+__device__ void f8_pair(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
+                        const F8Keys *f8, const F8Job &j0, const F8Job &j1, bool has1) {
+    uint32_t p0[4], p1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { p0[k] = j0.iv[k]; p1[k] = has1 ? j1.iv[k] : 0u; }
+    {
+        RoundKeys rkf;
+        load_rk_uniform(f8->rk, rkf);
+        aes_encrypt2(lds, tb, rkf, p0, p1);
+    }
+    const int n0 = j0.len > 0 ? (j0.len + 15) >> 4 : 0;
+    const int n1 = has1 && j1.len > 0 ? (j1.len + 15) >> 4 : 0;
+    const int nb = max(n0, n1);
+    if (nb == 0) return;
     RoundKeys rk;
     load_round_keys_uniform(ks, rk);
-    uint32_t S[4] = {0u, 0u, 0u, 0u};
-    const int end = off + len;
-    for (int j = 0; off + 16 * j < end; j++) {
-        uint32_t x[4], y[4] = {0u, 0u, 0u, 0u};
+    uint32_t s0[4] = {0u, 0u, 0u, 0u}, s1[4] = {0u, 0u, 0u, 0u};
+    for (int jb = 0; jb < nb; jb++) {
+        uint32_t x[4], y[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = S[k] ^ ivp[k];
-        x[3] ^= bswap((uint32_t)j); // the counter j into bytes 12..15, big-endian
+        for (int k = 0; k < 4; k++) { x[k] = s0[k] ^ p0[k]; y[k] = s1[k] ^ p1[k]; }
+        x[3] ^= bswap((uint32_t)jb);
+        y[3] ^= bswap((uint32_t)jb);
         aes_encrypt2(lds, tb, rk, x, y);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            S[k] = x[k];
-            const int pos = off + 16 * j + 4 * k;
-            if (pos < end) {
-                const int rem = end - pos;
-                const uint32_t m = rem >= 4 ? ~0u : ((1u << (8 * rem)) - 1u);
-                uint32_t *w = reinterpret_cast<uint32_t *>(pkt + pos);
-                *w ^= x[k] & m;
-            }
-        }
+        for (int k = 0; k < 4; k++) { s0[k] = x[k]; s1[k] = y[k]; }
+        if (jb < n0) f8_xor_block(j0, jb, s0);
+        if (jb < n1) f8_xor_block(j1, jb, s1);
     }
 }
 
@@ -1668,67 +1722,77 @@ __device__ void hmac_packet(const KeySet *ks, const uint8_t *pkt, int L, uint32_
     }
 }
 
-__global__ __launch_bounds__(kAesBlock) void k_f8(BundleArgs a) {
-    __shared__ uint32_t s_te[kTeWords];
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    bool todo = false;
-    uint32_t ks_id = 0;
-    if (p < a.n && a.status[p] == SRTP_STATUS_OK) {
-        const uint32_t slot = a.p_slot[p];
-        if (slot != kNoSlot) {
-            ks_id = a.ctx[slot].ks;
-            const KeySet *ks = a.keysets + ks_id;
-            if (ks->enc_type == SRTP_AESF8_ENCRYPTION) {
-                if (!a.reverse) todo = true;
-                else if (ks->kind == SRTP_KIND_RTP)
-                    todo = !((a.flags ? a.flags[p] : 0u) &
-                             (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
-                else todo = (a.w_cw[p] & 0x80000000u) != 0; // E flag
-            }
-        }
+// Protect's trailer after the F8 pass: tag (SRTP) or E|index + tag (SRTCP;
+// the policy check guarantees an HMAC trailer there).
+__device__ __forceinline__ void f8_trailer(const KeySet *ks, const F8Job &j) {
+    if (sgpr(ks->auth_type) == SRTP_NULL_AUTHENTICATION) return;
+    const int T = (int)sgpr(ks->tag_len);
+    uint32_t hh[5];
+    hmac_packet(ks, j.pkt, j.L, j.suffix, hh);
+    int o = j.L;
+    if (j.rtcp) {
+        j.pkt[o] = (uint8_t)(j.suffix >> 24); j.pkt[o + 1] = (uint8_t)(j.suffix >> 16);
+        j.pkt[o + 2] = (uint8_t)(j.suffix >> 8); j.pkt[o + 3] = (uint8_t)j.suffix;
+        o += 4;
     }
-    if (!__syncthreads_or(todo)) return;
+    tag_write(hh, j.pkt + o, T);
+}
+
+// This packet needs k_f8: final status OK, AES-F8 key set, and for unprotect
+// decryption is due (SRTP: no DISCARD/SILENCE flag; SRTCP: the E flag).
+__device__ __forceinline__ bool f8_todo(const BundleArgs &a, uint32_t p, uint32_t *ks_id) {
+    if (p >= a.n || a.status[p] != SRTP_STATUS_OK) return false;
+    const uint32_t slot = a.p_slot[p];
+    if (slot == kNoSlot) return false;
+    *ks_id = a.ctx[slot].ks;
+    const KeySet *ks = a.keysets + *ks_id;
+    if (ks->enc_type != SRTP_AESF8_ENCRYPTION) return false;
+    if (!a.reverse) return true;
+    if (ks->kind == SRTP_KIND_RTP)
+        return !((a.flags ? a.flags[p] : 0u) & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
+    return (a.w_cw[p] & 0x80000000u) != 0;
+}
+
+// ============================================================== k_f8
+// AES-F8 packets (SRTPCipherF8; SDES F8_128_HMAC_SHA1_80), after the final
+// statuses of k_protect / k_unprotect_fix.  Protect: F8 encryption, then the
+// HMAC over the ciphertext and the trailer.  Unprotect: k_unprotect already
+// checked the tag (HMAC is over the ciphertext, independent of the cipher) and
+// did not speculate, so only the accepted packets are deciphered here.  The F8
+// keystream is a chain, so a lane walks packets block by block -- two packets
+// per lane (2g, 2g+1) through the two-block AES rounds when they share a key
+// set (packets of one transformer usually sit side by side), else one by one.
+constexpr int kF8Block = 512; // two packets per lane: 1024 packets per workgroup, one per CU
+
+__global__ __launch_bounds__(kF8Block) void k_f8(BundleArgs a) {
+    __shared__ uint32_t s_te[kTeWords];
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t q0 = 2 * g, q1 = 2 * g + 1;
+    uint32_t k0 = 0, k1 = 0;
+    const bool t0 = f8_todo(a, q0, &k0), t1 = f8_todo(a, q1, &k1);
+    if (!__syncthreads_or(t0 || t1)) return;
     fill_te4(s_te);
-    if (!todo) return;
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
-    for_each_keyset(true, ks_id, [&](uint32_t ks_u) {
+    const bool pair = t0 && t1 && k0 == k1;
+    bool one0 = t0 && !pair, one1 = t1 && !pair;
+    for_each_keyset(pair || one0, t0 ? k0 : k1, [&](uint32_t ks_u) {
+        // pairs, and lone first packets (which take their key set's pass)
         const KeySet *ks = a.keysets + ks_u;
-        const F8Keys *f8 = a.f8keys + ks_u;
-        uint8_t *pkt = a.seg + a.off[p];
-        const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
-        const int T = (int)sgpr(ks->tag_len);
-        const bool mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
-        const uint32_t cw = a.w_cw[p];
-        uint32_t iv[4];
-        if (sgpr(ks->kind) == SRTP_KIND_RTP) {
-            // processPacketAESF8 :532-555: IV = 0 || header[1..11] || ROC_be
-            iv[0] = hdr.x & 0xffffff00u; iv[1] = hdr.y; iv[2] = hdr.z; iv[3] = bswap(cw);
-            const int L = (int)a.len[p] - (!a.reverse && mac ? T : 0);
-            const int h = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-            f8_region(lds, tb, ks, f8, pkt, h, L - h, iv);
-            if (!a.reverse && mac) {
-                uint32_t hh[5];
-                hmac_packet(ks, pkt, L, cw, hh);
-                tag_write(hh, pkt + L, T);
-            }
-        } else {
-            // SRTCPCryptoContext.processPacketAESF8 :267-298: IV = 0^4 ||
-            // (index | E)_be || header[0..7]; ciphers [8, 8 + length - 4 - tag)
-            // of the length at the call (protect: before the trailer; unprotect:
-            // after shrinking it).
-            const uint32_t ie = cw | 0x80000000u;
-            iv[0] = 0u; iv[1] = bswap(ie); iv[2] = hdr.x; iv[3] = hdr.y;
-            const int L = (int)a.len[p] - (a.reverse ? 0 : 4 + T);
-            f8_region(lds, tb, ks, f8, pkt, 8, L - 4 - T, iv);
-            if (!a.reverse) { // the policy check guarantees an HMAC trailer
-                uint32_t hh[5];
-                hmac_packet(ks, pkt, L, ie, hh);
-                pkt[L] = (uint8_t)(ie >> 24); pkt[L + 1] = (uint8_t)(ie >> 16);
-                pkt[L + 2] = (uint8_t)(ie >> 8); pkt[L + 3] = (uint8_t)ie;
-                tag_write(hh, pkt + L + 4, T);
-            }
+        const F8Job j0 = f8_job(a, ks, pair || one0 ? q0 : q1);
+        F8Job j1 = j0;
+        if (pair) j1 = f8_job(a, ks, q1);
+        f8_pair(lds, tb, ks, a.f8keys + ks_u, j0, j1, pair);
+        if (!a.reverse) {
+            f8_trailer(ks, j0);
+            if (pair) f8_trailer(ks, j1);
         }
+    });
+    for_each_keyset(one1, k1, [&](uint32_t ks_u) { // lone second packets
+        const KeySet *ks = a.keysets + ks_u;
+        const F8Job j = f8_job(a, ks, q1);
+        f8_pair(lds, tb, ks, a.f8keys + ks_u, j, j, false);
+        if (!a.reverse) f8_trailer(ks, j);
     });
 }
 
@@ -1779,7 +1843,8 @@ hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_f8(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_f8, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
+    const uint32_t lanes = (a.n + 1) / 2; // two packets per lane
+    hipLaunchKernelGGL(k_f8, dim3((lanes + kF8Block - 1) / kF8Block), dim3(kF8Block), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,
