@@ -72,6 +72,10 @@ __device__ __forceinline__ int64_t java_lshl(int64_t v, int64_t n) {
 // (byte 1 <- state byte k, bytes 0 and 2 <- base).
 constexpr int kTeWords = 32768;  // 128 KB
 constexpr int kAesBlock = 1024;  // threads per workgroup of the AES kernels (1 WG per CU)
+#ifndef SRTP_UNPROTECT_BLOCK
+#define SRTP_UNPROTECT_BLOCK 1024
+#endif
+constexpr int kUnprotectBlock = SRTP_UNPROTECT_BLOCK; // k_unprotect's workgroup size
 
 __device__ __forceinline__ void fill_te4(uint32_t *s_te) {
     for (int i = threadIdx.x; i < kTeWords; i += blockDim.x) {
@@ -1468,9 +1472,13 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
     }
     if (spec) {
-        asm volatile("" ::: "memory"); // reload the round keys below, do not keep them live
+        // reload the round keys through an opaque copy of the key-set pointer:
+        // with the plain pointer the compiler keeps the first load's VGPR copies
+        // live across the MAC loop instead (44 VGPRs spilled to scratch)
+        const KeySet *ks2 = ks;
+        asm volatile("" : "+v"(ks2));
         RoundKeys rk2;
-        load_round_keys_uniform(ks, rk2);
+        load_round_keys_uniform(ks2, rk2);
         for (int c = b_tail; c < nb_data; c++) {
             if (64 * c + 64 <= cs.off) continue;
             uint32_t d[16];
@@ -1490,7 +1498,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     }
 }
 
-__global__ __launch_bounds__(kAesBlock) void k_unprotect(BundleArgs a) {
+__global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords];
     fill_te4(s_te);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1823,7 +1831,8 @@ hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_unprotect, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
+    hipLaunchKernelGGL(k_unprotect, dim3((a.n + kUnprotectBlock - 1) / kUnprotectBlock),
+                       dim3(kUnprotectBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {

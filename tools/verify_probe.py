@@ -9,6 +9,8 @@ import sys, json, numpy as np, torch
 sys.path.insert(0, %r)
 from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPTransformer, profile_policies, synth
 n, nssrc = 1 << 18, 10000
+import os
+TWO = os.environ.get('PROBE_TWO') == '1'
 res = {}
 for L in (160, 1200):
     b = synth.rtp_bundle(n, nssrc, L, seed=synth.SEED_BASE + 2)
@@ -24,8 +26,11 @@ for L in (160, 1200):
     r = {}
     seq_step = -(-n // nssrc)
     off64 = off.to(torch.int64)
+    eng2 = SRTPEngine(max_contexts=1 << 14, max_factories=64, max_transformers=64, max_batch=n) \
+        if TWO else eng
+    eng2.set_timing(True)
     snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
-    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng))
+    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng2))
     tp, tv = [], []
     for it in range(6):  # one sender / receiver pair, steady state as in bench.py
         seg, ln = seg0.clone(), ln0.clone()
@@ -33,19 +38,19 @@ for L in (160, 1200):
         q = ((hi << 8) | lo) + it * seq_step
         seg[off64 + 2] = ((q >> 8) & 0xFF).to(torch.uint8)
         seg[off64 + 3] = (q & 0xFF).to(torch.uint8)
-        torch.cuda.synchronize(); eng.read_timing()
+        torch.cuda.synchronize(); eng.read_timing(); eng2.read_timing()
         eng.transform_device(False, snd.tid, seg, off, ln, cap, st)
         torch.cuda.synchronize()
         tp.append(round(eng.read_timing()["protect"][0], 4))
-        eng.transform_device(True, rcv.tid, seg, off, ln, cap, st)
+        eng2.transform_device(True, rcv.tid, seg, off, ln, cap, st)
         torch.cuda.synchronize()
-        tv.append(round(eng.read_timing()["verify"][0], 4))
+        tv.append(round(eng2.read_timing()["verify"][0], 4))
         assert int((st != 0).sum()) == 0, "not all packets accepted"
     r = {"protect_ms": tp, "verify_ms": tv}
     res[L] = r
 print(json.dumps(res))
 ''' % ROOT
-for mode in ("0", "5"):
-    env = dict(os.environ, SRTP_DEBUG=mode)
+for mode, two in (("0", "0"), ("0", "1")):
+    env = dict(os.environ, SRTP_DEBUG=mode, PROBE_TWO=two)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
-    print("SRTP_DEBUG=%s" % mode, out.stdout.strip(), out.stderr.strip()[-300:] if out.returncode else "", flush=True)
+    print("SRTP_DEBUG=%s two_engines=%s" % (mode, two), out.stdout.strip(), out.stderr.strip()[-300:] if out.returncode else "", flush=True)
