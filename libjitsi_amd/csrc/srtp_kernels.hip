@@ -1025,7 +1025,10 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
 // reads LDS (tens of cycles per record) instead of dependent HBM round trips.
 // Only a segment longer than the look-ahead reads its tail from global memory.
 constexpr int kWalkBlock = 64;
-constexpr int kWalkPer = 4;
+#ifndef SRTP_WALK_PER
+#define SRTP_WALK_PER 4
+#endif
+constexpr int kWalkPer = SRTP_WALK_PER; // records per lane of a span
 constexpr int kWalkSpan = kWalkBlock * kWalkPer;
 constexpr int kWalkAhead = 256;
 constexpr int kWalkWin = kWalkSpan + kWalkAhead;
