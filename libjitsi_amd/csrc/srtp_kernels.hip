@@ -562,25 +562,33 @@ __device__ uint32_t ctx_lookup_insert(const BundleArgs &a, uint64_t key, bool ma
 // packet is not walked (skipped, invalid, dropped before the state machine).
 __device__ __forceinline__ uint32_t parse_one(const BundleArgs &a, uint32_t p) {
     uint32_t invalid_key = a.ctx_mask + 1u;
+    // the per-packet words first, all in flight together; then the transformer
+    // record and the header (when the packet has a valid region) together
+    const uint32_t L = a.len[p];
+    const uint32_t fl = a.flags ? a.flags[p] : 0u;
+    const int32_t tid = packet_tid(a, p);
+    const uint32_t C = a.cap[p];
+    const uint32_t o = a.off[p];
     a.sk_in[p] = invalid_key;
     a.p_slot[p] = kNoSlot;
-    uint32_t L = a.len[p];
     a.w_len[p] = L;
-    uint32_t fl = a.flags ? a.flags[p] : 0u;
-    int32_t tid = packet_tid(a, p);
-    if ((fl & SRTP_PKT_FLAG_SKIP) || tid < 0 || (uint32_t)tid >= a.n_transformers ||
-        !a.transformers[tid].alive) {
+    if ((fl & SRTP_PKT_FLAG_SKIP) || tid < 0 || (uint32_t)tid >= a.n_transformers) {
         a.w_status[p] = SRTP_STATUS_SKIPPED;
         return invalid_key;
     }
-    uint32_t C = a.cap[p];
-    if (L < 12 || L > C || C > 65535u) { // RawPacket.isInvalid :903-909
+    const bool bad_len = L < 12 || L > C || C > 65535u; // RawPacket.isInvalid :903-909
+    const uint8_t *pkt = a.seg + o;
+    uint4 hdr = make_uint4(0, 0, 0, 0);
+    if (!bad_len) hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const TransformerRec tr = a.transformers[tid];
+    if (!tr.alive) {
+        a.w_status[p] = SRTP_STATUS_SKIPPED;
+        return invalid_key;
+    }
+    if (bad_len) {
         a.w_status[p] = SRTP_STATUS_DROP_INVALID;
         return invalid_key;
     }
-    const uint8_t *pkt = a.seg + a.off[p];
-    uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
-    const TransformerRec tr = a.transformers[tid];
     uint32_t b0 = hdr.x & 0xffu;
     uint32_t ssrc;
     if (tr.kind == SRTP_KIND_RTP) {
