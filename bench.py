@@ -316,8 +316,11 @@ def main():
     avg_prot_s = prot_ms / 1e3 / max(prot_cnt, 1)
     achieved = n * (L + (L + T)) / avg_prot_s / 1e9
     stages = {k: (v[0] / max(v[1], 1)) for k, v in timing.items() if v[1]}
+    achieved_u = None
+    if "verify" in stages and stages["verify"] > 0:
+        achieved_u = n * (L + (L + T)) / (stages["verify"] / 1e3) / 1e9
 
-    traffic = None
+    traffic = traffic_u = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
@@ -325,6 +328,7 @@ def main():
                 pmc = json.load(f)
             if pmc.get("packets") == n and pmc.get("len") == L:
                 traffic = pmc.get("k_protect_bytes_per_launch")
+                traffic_u = pmc.get("k_unprotect_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -396,6 +400,11 @@ def main():
                                            "profiles/pmc_traffic.json" if traffic else None,
                          "copy_measured_gbps": copy_gbs,
                          "algorithmic_bytes_per_launch": n * (L + L + T)},
+            "roofline_k_unprotect": None if achieved_u is None else {
+                "bound": "hbm", "achieved": round(achieved_u, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved_u / HBM_PEAK_GBS, 4), "traffic": traffic_u,
+                "note": "the other dominant kernel (unprotect: tag check + speculative decryption), "
+                        "same algorithmic bytes per packet, HIP events of the same serial pass"},
             "cpu_baseline": cpu,
             "e2e": e2e,
         }

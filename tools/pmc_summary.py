@@ -139,6 +139,11 @@ def main():
                   "k_protect_bytes_per_launch": round(kp["hbm_bytes"]),
                   "k_protect_read_bytes": round(kp["hbm_read_bytes"]),
                   "k_protect_write_bytes": round(kp["hbm_write_bytes"])}
+            ku = derived.get("k_unprotect", {})
+            if "hbm_bytes" in ku:
+                js.update({"k_unprotect_bytes_per_launch": round(ku["hbm_bytes"]),
+                           "k_unprotect_read_bytes": round(ku["hbm_read_bytes"]),
+                           "k_unprotect_write_bytes": round(ku["hbm_write_bytes"])})
             root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
             with open(os.path.join(root, "profiles", "pmc_traffic.json"), "w") as f:
                 json.dump(js, f, indent=1)
