@@ -320,7 +320,7 @@ def main():
     if "verify" in stages and stages["verify"] > 0:
         achieved_u = n * (L + (L + T)) / (stages["verify"] / 1e3) / 1e9
 
-    traffic = traffic_u = None
+    traffic = traffic_u = util = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
@@ -329,6 +329,7 @@ def main():
             if pmc.get("packets") == n and pmc.get("len") == L:
                 traffic = pmc.get("k_protect_bytes_per_launch")
                 traffic_u = pmc.get("k_unprotect_bytes_per_launch")
+                util = pmc.get("k_protect_utilisation")
         except Exception:
             traffic = None
 
@@ -399,6 +400,7 @@ def main():
                          "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE per k_protect launch, "
                                            "profiles/pmc_traffic.json" if traffic else None,
                          "copy_measured_gbps": copy_gbs,
+                         "utilisation": util,
                          "algorithmic_bytes_per_launch": n * (L + L + T)},
             "roofline_k_unprotect": None if achieved_u is None else {
                 "bound": "hbm", "achieved": round(achieved_u, 1), "peak": HBM_PEAK_GBS,

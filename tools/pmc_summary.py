@@ -115,6 +115,10 @@ def main():
             d["lds_bank_conflict_frac"] = round(c["SQ_LDS_BANK_CONFLICT"] / max(1, c["SQ_LDS_IDX_ACTIVE"]), 4)
         if "GRBM_GUI_ACTIVE" in c:
             d["eff_clock_ghz"] = round(c["GRBM_GUI_ACTIVE"] / 8 / (avg_us * 1e3), 3)
+            if "SQ_INSTS_VALU" in c:
+                # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles; 1024 SIMDs
+                cyc = c["GRBM_GUI_ACTIVE"] / 8
+                d["valu_busy_frac"] = round(c["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 3)
         if "SQ_BUSY_CYCLES" in c:
             d["sq_busy_cycles"] = c["SQ_BUSY_CYCLES"]
         for name in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
@@ -139,6 +143,9 @@ def main():
                   "k_protect_bytes_per_launch": round(kp["hbm_bytes"]),
                   "k_protect_read_bytes": round(kp["hbm_read_bytes"]),
                   "k_protect_write_bytes": round(kp["hbm_write_bytes"])}
+            js["k_protect_utilisation"] = {
+                k: kp.get(k) for k in ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac",
+                                       "eff_clock_ghz")}
             ku = derived.get("k_unprotect", {})
             if "hbm_bytes" in ku:
                 js.update({"k_unprotect_bytes_per_launch": round(ku["hbm_bytes"]),
