@@ -14,6 +14,7 @@ import pytest
 
 from libjitsi_amd import profile_policies, synth
 from libjitsi_amd import _native as N
+from oracle import oracle as O
 from harness import Twin
 
 pytestmark = pytest.mark.gpu
@@ -58,11 +59,13 @@ def fault(b, rng, per_pkt_ts):
     return fb, ts
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_randomized_mixed_bundles(engine_factory, oracle, seed):
+@pytest.mark.parametrize("seed,abort,check_replay",
+                         [(1, True, True), (2, True, True), (3, True, True), (4, False, True),
+                          (5, True, False)])
+def test_randomized_mixed_bundles(engine_factory, oracle, seed, abort, check_replay):
     eng = engine_factory(max_contexts=1 << 14, max_factories=256, max_transformers=256,
-                         max_batch=1 << 14)
-    twin = Twin(eng)
+                         max_batch=1 << 14, abort_on_error=abort, check_replay=check_replay)
+    twin = Twin(eng, check_replay=check_replay)
     rng = np.random.default_rng(9000 + seed)
     pairs = [make_pair(twin, kind, prof, 900 + 10 * seed + j)
              for j, (kind, prof) in enumerate((k, p) for p in PROFILES for k in (0, 1))]
@@ -99,14 +102,18 @@ def test_randomized_mixed_bundles(engine_factory, oracle, seed):
         flags[rng.random(b.n) < 0.02] = N.PKT_FLAG_SKIP
         for i in np.nonzero(rng.random(b.n) < 0.01)[0]:
             ts_s[i] = None  # null elements of the RawPacket[] array
-        seg, ln, st = twin.run(ts_s, False, b.seg, b.off, b.length, b.cap, flags=flags)
+        seg, ln, st = twin.run(ts_s, False, b.seg, b.off, b.length, b.cap, flags=flags,
+                               abort_on_error=abort)
         pb = b.copy()
         pb.seg, pb.length = seg, ln
         fb, ts_f = fault(pb, rng, ts_r)
         fl = np.zeros(fb.n, np.uint32)
         fl[rng.random(fb.n) < 0.05] = N.PKT_FLAG_SILENCE
         fl[rng.random(fb.n) < 0.03] = N.PKT_FLAG_DISCARD
-        _, _, st_r = twin.run(ts_f, True, fb.seg, fb.off, fb.length, fb.cap, flags=fl)
+        _, _, st_r = twin.run(ts_f, True, fb.seg, fb.off, fb.length, fb.cap, flags=fl,
+                              abort_on_error=abort)
         seen |= set(int(v) for v in st) | set(int(v) for v in st_r)
-    # the mix really exercised the drop paths, not only clean round trips
+    O.set_check_replay(True)
+    # the mix really exercised the drop paths, not only clean round trips (SRTCP
+    # replay checks are not config-gated, so replays show up either way)
     assert {N.STATUS_OK, N.STATUS_DROP_AUTH, N.STATUS_DROP_REPLAY, N.STATUS_SKIPPED} <= seen, seen
