@@ -1276,6 +1276,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k];
         }
+
         inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
         sha1_compress(h, c);
     }
