@@ -1684,13 +1684,45 @@ __device__ __forceinline__ void f8_xor_block(const F8Job &j, int jb, const uint3
     }
 }
 
+// Running HMAC-SHA1 inner hash of one packet, fed 64-B blocks as soon as
+// they are final (protect: once the F8 pass has ciphered them).
+struct F8Mac {
+    uint32_t h[5];
+    int next;   // next inner block to hash
+};
+
+// Hash the packet's inner blocks that lie wholly below byte `upto` (all of
+// them for upto = INT_MAX): the data [0, L) || suffix || padding of
+// authenticatePacketHMAC :269-278.
+__device__ void f8_mac_advance(const F8Job &j, F8Mac &m, int upto) {
+    const int nb_data = (j.L + 63) >> 6;
+    const int nb_inner = ((j.L + 12) >> 6) + 1;
+    while (m.next < nb_inner && (upto == 0x7fffffff || 64 * m.next + 64 <= upto)) {
+        const int b = m.next;
+        uint32_t w[16];
+        const uint4 *qp = reinterpret_cast<const uint4 *>(j.pkt + 64 * b);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (b < nb_data && 64 * b + 16 * q < j.L) v = qp[q];
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
+        inner_words(w, b, j.L, j.suffix);
+        sha1_compress(m.h, w);
+        m.next++;
+    }
+}
+
 // SRTPCipherF8.process :97-128 + processBlock :145-183 for two packets of one
 // key set at once (the second may be absent: has1 false), so both blocks of
 // the two-block AES round code do useful work: IV' = E(k_e ^ (k_s || 0x55..),
 // IV), then S(j) = E(k_e, IV' ^ S(j-1) ^ j), S(-1) = 0, j big-endian in bytes
-// 12..15, XORed over each packet's region.
+// 12..15, XORed over each packet's region.  With `mac` (protect) each packet's
+// HMAC inner hash follows the ciphering block by block (the MAC is over the
+// ciphertext), so the packet is read once more only from L1/L2.
 __device__ void f8_pair(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
-                        const F8Keys *f8, const F8Job &j0, const F8Job &j1, bool has1) {
+                        const F8Keys *f8, const F8Job &j0, const F8Job &j1, bool has1, bool mac,
+                        F8Mac &m0, F8Mac &m1) {
     uint32_t p0[4], p1[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) { p0[k] = j0.iv[k]; p1[k] = has1 ? j1.iv[k] : 0u; }
@@ -1699,63 +1731,61 @@ __device__ void f8_pair(const char *__restrict__ lds, const TeBase &tb, const Ke
         load_rk_uniform(f8->rk, rkf);
         aes_encrypt2(lds, tb, rkf, p0, p1);
     }
+    if (mac) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) m0.h[k] = m1.h[k] = sgpr(ks->ipad[k]);
+        m0.next = m1.next = 0;
+        // the header before the ciphered region is final from the start
+        f8_mac_advance(j0, m0, j0.off);
+        if (has1) f8_mac_advance(j1, m1, j1.off);
+    }
     const int n0 = j0.len > 0 ? (j0.len + 15) >> 4 : 0;
     const int n1 = has1 && j1.len > 0 ? (j1.len + 15) >> 4 : 0;
     const int nb = max(n0, n1);
-    if (nb == 0) return;
-    RoundKeys rk;
-    load_round_keys_uniform(ks, rk);
-    uint32_t s0[4] = {0u, 0u, 0u, 0u}, s1[4] = {0u, 0u, 0u, 0u};
-    for (int jb = 0; jb < nb; jb++) {
-        uint32_t x[4], y[4];
+    if (nb > 0) {
+        RoundKeys rk;
+        load_round_keys_uniform(ks, rk);
+        uint32_t s0[4] = {0u, 0u, 0u, 0u}, s1[4] = {0u, 0u, 0u, 0u};
+        for (int jb = 0; jb < nb; jb++) {
+            uint32_t x[4], y[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) { x[k] = s0[k] ^ p0[k]; y[k] = s1[k] ^ p1[k]; }
-        x[3] ^= bswap((uint32_t)jb);
-        y[3] ^= bswap((uint32_t)jb);
-        aes_encrypt2(lds, tb, rk, x, y);
+            for (int k = 0; k < 4; k++) { x[k] = s0[k] ^ p0[k]; y[k] = s1[k] ^ p1[k]; }
+            x[3] ^= bswap((uint32_t)jb);
+            y[3] ^= bswap((uint32_t)jb);
+            aes_encrypt2(lds, tb, rk, x, y);
 #pragma unroll
-        for (int k = 0; k < 4; k++) { s0[k] = x[k]; s1[k] = y[k]; }
-        if (jb < n0) f8_xor_block(j0, jb, s0);
-        if (jb < n1) f8_xor_block(j1, jb, s1);
-    }
-}
-
-// HMAC-SHA1 tag of packet bytes [0, L) || suffix (authenticatePacketHMAC :269-278).
-__device__ void hmac_packet(const KeySet *ks, const uint8_t *pkt, int L, uint32_t suffix,
-                            uint32_t h[5]) {
-#pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
-    const int nb_data = (L + 63) >> 6;
-    const int nb_inner = ((L + 12) >> 6) + 1;
-    for (int b = 0; b <= nb_inner; b++) {
-        uint32_t w[16];
-        const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (b < nb_data && 64 * b + 16 * m < L) v = qp[m];
-            w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+            for (int k = 0; k < 4; k++) { s0[k] = x[k]; s1[k] = y[k]; }
+            if (jb < n0) {
+                f8_xor_block(j0, jb, s0);
+                if (mac && jb + 1 < n0) f8_mac_advance(j0, m0, j0.off + 16 * (jb + 1));
+            }
+            if (jb < n1) {
+                f8_xor_block(j1, jb, s1);
+                if (mac && jb + 1 < n1) f8_mac_advance(j1, m1, j1.off + 16 * (jb + 1));
+            }
         }
-        if (b < nb_inner) inner_words(w, b, L, suffix);
-        else outer_words(w, h, ks);
-        sha1_compress(h, w);
+    }
+    if (mac) { // everything after the region is final: the remaining inner blocks
+        f8_mac_advance(j0, m0, 0x7fffffff);
+        if (has1) f8_mac_advance(j1, m1, 0x7fffffff);
     }
 }
 
-// Protect's trailer after the F8 pass: tag (SRTP) or E|index + tag (SRTCP;
-// the policy check guarantees an HMAC trailer there).
-__device__ __forceinline__ void f8_trailer(const KeySet *ks, const F8Job &j) {
+// Protect's trailer after the F8 pass: outer HMAC block, then the tag (SRTP)
+// or E|index + tag (SRTCP; the policy check guarantees an HMAC trailer there).
+__device__ __forceinline__ void f8_trailer(const KeySet *ks, const F8Job &j, F8Mac &m) {
     if (sgpr(ks->auth_type) == SRTP_NULL_AUTHENTICATION) return;
     const int T = (int)sgpr(ks->tag_len);
-    uint32_t hh[5];
-    hmac_packet(ks, j.pkt, j.L, j.suffix, hh);
+    uint32_t w[16];
+    outer_words(w, m.h, ks);
+    sha1_compress(m.h, w);
     int o = j.L;
     if (j.rtcp) {
         j.pkt[o] = (uint8_t)(j.suffix >> 24); j.pkt[o + 1] = (uint8_t)(j.suffix >> 16);
         j.pkt[o + 2] = (uint8_t)(j.suffix >> 8); j.pkt[o + 3] = (uint8_t)j.suffix;
         o += 4;
     }
-    tag_write(hh, j.pkt + o, T);
+    tag_write(m.h, j.pkt + o, T);
 }
 
 // This packet needs k_f8: final status OK, AES-F8 key set, and for unprotect
@@ -1802,17 +1832,21 @@ __global__ __launch_bounds__(kF8Block) void k_f8(BundleArgs a) {
         const F8Job j0 = f8_job(a, ks, pair || one0 ? q0 : q1);
         F8Job j1 = j0;
         if (pair) j1 = f8_job(a, ks, q1);
-        f8_pair(lds, tb, ks, a.f8keys + ks_u, j0, j1, pair);
-        if (!a.reverse) {
-            f8_trailer(ks, j0);
-            if (pair) f8_trailer(ks, j1);
+        const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+        F8Mac m0, m1;
+        f8_pair(lds, tb, ks, a.f8keys + ks_u, j0, j1, pair, mac, m0, m1);
+        if (mac) {
+            f8_trailer(ks, j0, m0);
+            if (pair) f8_trailer(ks, j1, m1);
         }
     });
     for_each_keyset(one1, k1, [&](uint32_t ks_u) { // lone second packets
         const KeySet *ks = a.keysets + ks_u;
         const F8Job j = f8_job(a, ks, q1);
-        f8_pair(lds, tb, ks, a.f8keys + ks_u, j, j, false);
-        if (!a.reverse) f8_trailer(ks, j);
+        const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+        F8Mac m0, m1;
+        f8_pair(lds, tb, ks, a.f8keys + ks_u, j, j, false, mac, m0, m1);
+        if (mac) f8_trailer(ks, j, m0);
     });
 }
 
