@@ -144,7 +144,10 @@ int srtp_transformer_close(srtp_engine *e, int32_t transformer);
  * `stream` (a hipStream_t, NULL = the default stream).  tids == NULL means every
  * packet belongs to `tid`; otherwise tids[i] (device array) names packet i's
  * transformer.  flags may be NULL.  reverse = 0: transform (protect),
- * reverse = 1: reverseTransform (unprotect). */
+ * reverse = 1: reverseTransform (unprotect).  The caller guarantees what
+ * srtp_transform_host checks on the host: every packet region [off[i],
+ * off[i] + cap[i] rounded up to 16) lies inside the segment, off[i] is 16-byte
+ * aligned and cap[i] <= 65535 (the device arrays are not read back to check). */
 int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
                           uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
                           const uint32_t *flags, int32_t *status, uint32_t n, void *stream);
