@@ -498,7 +498,8 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     {
         StageTimer t(e, s, SRTP_STAGE_WALK);
         HIPCHK(e, launch_walk(a, 0, s));
-        HIPCHK(e, launch_walk(a, 1, s));
+        // the limit pass only runs with abort-on-throw (k_walk returns at once otherwise)
+        if (a.abort_on_error) HIPCHK(e, launch_walk(a, 1, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
