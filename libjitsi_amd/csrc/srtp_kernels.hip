@@ -752,11 +752,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
         }
     }
     uint32_t key[kSortItems], loc[kSortItems];
-    WalkRec val[kSortItems];
 #pragma unroll
     for (int r = 0; r < kSortItems; r++) {
         const uint32_t i = base + r * kSortThreads + t;
-        if (i < sp.n) { key[r] = sp.sk[i]; val[r] = sp.sv[i]; }
+        if (i < sp.n) key[r] = sp.sk[i];
     }
     __syncthreads();
     // stable local ranks: items in order r-major, t-minor (= index order)
@@ -789,10 +788,11 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
     }
 #pragma unroll
     for (int r = 0; r < kSortItems; r++) {
-        if (base + r * kSortThreads + t < sp.n) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < sp.n) {
             const uint32_t pos = s_base[(key[r] >> sp.shift) & 255u] + loc[r];
             sp.dk[pos] = key[r];
-            sp.dv[pos] = val[r];
+            sp.dv[pos] = sp.sv[i]; // read here, not held across the ranking (a held copy went to scratch)
             if (sp.next_counts)
                 atomicAdd(&sp.next_counts[(pos / kSortTile) * 256 + ((key[r] >> (sp.shift + 8)) & 255u)], 1u);
         }
