@@ -3,34 +3,43 @@
 
 Workload (BASELINE.json configs[1], one bundle per GPU per step): 10,000
 concurrent SSRCs, fixed 1200-byte video RTP packets, AES_CM_128_HMAC_SHA1_80,
-a bundle of 2^18 packets resident in HBM.  One step = protect the bundle with
-a sender SRTPTransformer, unprotect it with a separate receiver transformer
-(SURVEY Q1).  Each step has its own bundle, staged in HBM before the clock
+bundles of 2^18 packets resident in HBM.  A sender SRTPTransformer protects
+bundles and a separate receiver transformer unprotects them, each
+on its own engine and HIP stream, as a bridge's send and receive threads do.
+Step i protects bundle i and unprotects bundle i-1 (protected the step
+before); the two streams join at the end of every step, so a step is always
+one protect and one unprotect of 2^18 packets and the timed steps have no
+start or end transient.  Every bundle is staged in HBM before the clock
 starts: bundle i is the base bundle with every SSRC's sequence numbers
-advanced by i times the packets per SSRC per bundle (fresh packets for the
-replay check; ROC wraps happen naturally).
+advanced by i times its packets per bundle (fresh packets for the replay
+check; ROC wraps happen naturally).  ``--serial``: one engine, one stream,
+step i = protect(i) then unprotect(i).
 
 Multi-GPU: one process per GPU (torchrun), contexts sharded by SSRC (each rank
-owns its own 10k SSRCs), no collective on the data path ("scaling": "weak").
-value = packets protected AND unprotected by all ranks / max-over-ranks time.
+owns its own SSRCs), no collective on the data path ("scaling": "weak").
+Without torchrun, ``--gpus N`` drives N GPUs from this one process (the
+in-process dispatcher deployment: one engine pair per GPU, one host thread
+enqueueing on all of them).  value = packets protected AND unprotected by all
+GPUs / wall time (max over ranks).
 
-Also reported: the dominant kernel's roofline (k_protect, HIP events on the
-bundle stream, algorithmic bytes L + (L+T) per packet) and a CPU baseline (the
-oracle restatement of the reference's per-packet path, timed on host cores).
+Also reported: the dominant kernel's roofline (HIP events on the bundle
+stream, algorithmic bytes L + (L+T) per packet), and a CPU baseline: the
+oracle's pinned C timing loop (oracle/oracle_bench.c) in the reference's call
+structure and a tuned-OpenSSL variant, on one core and on the box's CPU share.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
-import threading
 import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-RING = 160  # most distinct bundles staged in HBM (x 319 MB at the default size)
+RING = 160  # most distinct bundles staged in HBM per GPU (x 319 MB at the default size)
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -44,69 +53,87 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=1 << 18, help="bundle size per GPU")
     ap.add_argument("--ssrcs", type=int, default=10000, help="concurrent SSRCs per GPU")
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="SSRC popularity Zipf exponent (0: round-robin, every SSRC equal)")
     ap.add_argument("--len", type=int, default=1200, help="RTP packet length")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0,
+                    help="CPU baseline: seconds per measurement (4 measurements)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the box's CPU share: min(16, CPUs in the affinity set)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned-host end-to-end leg")
     ap.add_argument("--e2e-bundles", type=int, default=24)
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for the barrier/timing reduction (nccl = RCCL)")
     ap.add_argument("--serial", action="store_true",
-                    help="run the receiver on the sender's stream (no overlap between "
-                         "step i's unprotect and step i+1's protect)")
+                    help="one engine and stream: step i = protect(i) then unprotect(i)")
+    ap.add_argument("--pipe", default="free", choices=["free", "join", "lag1", "lag2"],
+                    help="coupling of the sender and receiver streams (see Side.step)")
     ap.add_argument("--policy", default="AES_CM_128_HMAC_SHA1_80",
                     help="protection profile; 'AES_CM_128_NULL_AUTH' (cipher only) is a "
                          "diagnostic split of the fused kernel, not the headline metric")
     return ap.parse_args()
 
 
-def cpu_baseline(seconds: float, threads: int, pkt_len: int, ssrcs: int):
-    """The oracle (C restatement of SRTPCryptoContext + SRTPCipherCTR + HMAC,
-    reference call structure: one 16-B AES call per keystream block, HMAC
-    re-keyed per packet) protecting+unprotecting config-2 packets on host
-    cores, one sender/receiver transformer pair per thread, sharded by SSRC."""
+def cpu_info():
+    """Model name and physical core count of the host (lscpu)."""
+    info = {"cpu_model": None, "physical_cores": None, "logical_cpus": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        kv = {}
+        for line in out.splitlines():
+            if ":" in line:
+                k, v = line.split(":", 1)
+                kv[k.strip()] = v.strip()
+        info["cpu_model"] = kv.get("Model name")
+        if kv.get("Core(s) per socket") and kv.get("Socket(s)"):
+            info["physical_cores"] = int(kv["Core(s) per socket"]) * int(kv["Socket(s)"])
+        info["flags_aes_sha"] = {f: f in kv.get("Flags", "").split() for f in ("aes", "sha_ni", "vaes")}
+    except Exception:
+        pass
+    return info
+
+
+def cpu_baseline(seconds: float, threads: int, L: int, nssrc: int, T: int):
+    """The oracle's pinned C loop (oracle/oracle_bench.c): each thread owns a
+    sender/receiver transformer pair and its share of the SSRCs, and protects
+    then unprotects 4096-packet bundles of L-byte packets.  MODE_REF follows the
+    reference's call structure (SRTPCipherCTR.java:68-121: one 16-B AES-ECB call
+    per keystream block plus the tail block; BaseSRTPCryptoContext.java:269-278
+    with the HMAC re-keyed per packet), MODE_TUNED uses one EVP AES-CTR call per
+    packet and a pre-keyed HMAC context."""
     from oracle import oracle as O
-    from libjitsi_amd import synth
     O.build()
-    n = 4096
-    per_thread_ssrc = max(1, ssrcs // threads)
-    pol = O.Policy(1, 16, 1, 20, 10, 14)
-    counts = [0] * threads
-    stop = [False]
+    res = {}
+    for name, mode in (("ref", O.MODE_REF), ("tuned", O.MODE_TUNED)):
+        for tag, th in (("one_core", 1), ("share", threads)):
+            n, el = O.bench_round_trips(mode, th, seconds, L, nssrc)
+            res[(name, tag)] = (n / el, n, el)
+    alg = 2 * (L + (L + T))
+    info = cpu_info()
 
-    def worker(t):
-        b = synth.rtp_bundle(n, per_thread_ssrc, pkt_len, seed=synth.SEED_BASE + 2 + 1000 * t)
-        (k, s), = synth.keys(2 + t, 1)
-        fs = O.Factory(True, k, s, pol, pol, O.MODE_REF)
-        fr = O.Factory(False, k, s, pol, pol, O.MODE_REF)
-        ts, tr = O.Transformer(O.KIND_RTP, fs, fs), O.Transformer(O.KIND_RTP, fr, fr)
-        step = -(-n // per_thread_ssrc)
-        o = b.off.astype(np.int64)
-        seg = b.seg.copy()
-        while not stop[0]:
-            ln = b.length.copy()
-            st1 = O.process(ts, False, seg, b.off, ln, b.cap)
-            st2 = O.process(tr, True, seg, b.off, ln, b.cap)
-            assert (st1 == 0).all() and (st2 == 0).all()
-            counts[t] += n
-            q = ((seg[o + 2].astype(np.int64) << 8) | seg[o + 3]) + step
-            seg[o + 2] = ((q >> 8) & 0xFF).astype(np.uint8)
-            seg[o + 3] = (q & 0xFF).astype(np.uint8)
+    def obj(name):
+        v1, n1, e1 = res[(name, "one_core")]
+        vn, nn, en = res[(name, "share")]
+        o = {"value": round(vn, 1), "threads": threads, "one_core": round(v1, 1),
+             "gbps": round(vn * alg / 1e9, 3), "packets": nn, "seconds": round(en, 2)}
+        if info.get("physical_cores"):
+            o["per_core_x_physical_cores"] = round(v1 * info["physical_cores"], 1)
+        return o
 
-    ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
-    t0 = time.perf_counter()
-    for th in ths:
-        th.start()
-    time.sleep(seconds)
-    stop[0] = True
-    for th in ths:
-        th.join()
-    dt = time.perf_counter() - t0
-    return sum(counts) / dt, sum(counts), dt
+    ref, tuned = obj("ref"), obj("tuned")
+    return {"value": ref["value"], "unit": "packets/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/oracle_bench.c pinned C loop, {threads} threads (the box's CPU "
+                      f"share) and 1 thread, {seconds:.0f} s each: 4096-packet bundles of {L}-B "
+                      f"RTP over {nssrc} SSRCs split across threads, protect then unprotect "
+                      f"(reference call structure; 'tuned' = EVP AES-CTR per packet + pre-keyed "
+                      f"HMAC)",
+            "ref": ref, "tuned": tuned, **info,
+            "note": "per_core_x_physical_cores scales the 1-thread rate to every physical "
+                    "core of the host (an upper bound; this run may use only the box's share)"}
 
 
-def e2e_leg(b, pols, keys, n, L, local_rank, bundles, depth=3):
+def e2e_leg(b, pols, keys, n, L, device, bundles, depth=3):
     """End-to-end through PCIe (SURVEY.md 8d "end-to-end: pinned host buffers,
     H2D + kernels + D2H"): the same workload's bundles held in pinned host
     slots of an SRTPPipeline, each bundle copied to HBM, processed, copied
@@ -116,7 +143,7 @@ def e2e_leg(b, pols, keys, n, L, local_rank, bundles, depth=3):
     the repeated sequence numbers are processed in full, not dropped.
     Returns directional packets/s (one bundle = one direction) and PCIe GB/s."""
     from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPPipeline, SRTPTransformer
-    eng = SRTPEngine(device=local_rank, check_replay=False, max_contexts=1 << 15,
+    eng = SRTPEngine(device=device, check_replay=False, max_contexts=1 << 15,
                      max_factories=8, max_transformers=8, max_batch=n)
     k, s = keys
     snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
@@ -152,11 +179,146 @@ def e2e_leg(b, pols, keys, n, L, local_rank, bundles, depth=3):
     pps = bundles * n / dt
     pcie = bundles * 2 * nb / dt / 1e9
     pl.close()
+    eng.close()
     return {"directional_pps": round(pps, 1), "round_trip_pps": round(pps / 2, 1),
             "pcie_gbps_h2d_plus_d2h": round(pcie, 2), "bundles": bundles, "depth": depth,
             "all_accepted": ok,
             "note": "pinned host slots -> H2D -> protect or unprotect -> D2H, bundles of the "
                     "same workload; checkReplay off so repeated bundles are processed in full"}
+
+
+class Side:
+    """One GPU's share: a sender engine + stream, a receiver engine + stream,
+    and the ring of staged bundles."""
+
+    def __init__(self, torch, device: int, shard: int, args, pols, total: int):
+        from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPTransformer, synth
+        self.torch = torch
+        dev = self.dev = torch.device("cuda", device)
+        n, L, nssrc = args.packets, args.len, args.ssrcs
+        seed = synth.SEED_BASE + 2 + 7919 * shard  # shard r owns its own SSRCs
+        if args.zipf > 0:
+            b = synth.rtp_bundle_skewed(n, nssrc, L, seed=seed, zipf_s=args.zipf)
+            counts = b.meta["counts"]
+        else:
+            b = synth.rtp_bundle(n, nssrc, L, seed=seed)
+            idx = np.arange(n) % nssrc
+            counts = np.bincount(idx, minlength=nssrc)[idx]
+        self.b = b
+        # context table >= 1.6x the SSRCs (load <= 0.31 at 10k); its size sets
+        # the sort's key width (2^15 slots + the invalid key: two radix passes)
+        max_ctx = 1 << max(12, (int(1.6 * nssrc) - 1).bit_length())
+        mk = dict(device=device, max_contexts=max_ctx, max_factories=64, max_transformers=64,
+                  max_batch=n)
+        self.eng = SRTPEngine(**mk)
+        self.eng_r = self.eng if args.serial else SRTPEngine(**mk)
+        (k, s), = synth.keys(2 + shard, 1)
+        self.keys = (k, s)
+        self.snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=self.eng))
+        self.rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=self.eng_r))
+        with torch.cuda.device(dev):
+            self.off = torch.from_numpy(b.off.view(np.int32)).to(dev)
+            self.cap = torch.from_numpy(b.cap.view(np.int32)).to(dev)
+            self.st = torch.empty(n, dtype=torch.int32, device=dev)
+            self.st_r = torch.empty(n, dtype=torch.int32, device=dev)
+            self.off64 = self.off.to(torch.int64)
+            self.step_seq = torch.from_numpy(counts.astype(np.int32)).to(dev)
+            # each engine's own stream: created with the engine, each gets a
+            # hardware queue of its own (two streams made later may share one,
+            # which serialises the two directions)
+            self.s_a = torch.cuda.ExternalStream(self.eng.stream_ptr, device=dev)
+            self.s_b = (self.s_a if args.serial else
+                        torch.cuda.ExternalStream(self.eng_r.stream_ptr, device=dev))
+            self.end_a, self.end_b = torch.cuda.Event(), torch.cuda.Event()
+            self.ev_b = [torch.cuda.Event() for _ in range(3)]  # receiver step ends (lag modes)
+            self.ring = min(total + 1, RING)
+            self.pending = None  # join mode: protected bundle whose unprotect is due
+            base = torch.from_numpy(b.seg).to(dev)
+            len0 = torch.from_numpy(b.length.view(np.int32)).to(dev)
+            self.segs, self.lens = [], []
+            for i in range(self.ring):
+                sg = base.clone()
+                if i:
+                    self.advance_seq(sg, i)
+                self.segs.append(sg)
+                self.lens.append(len0.clone())
+            del base
+        torch.cuda.synchronize(dev)
+        self.serial = args.serial
+        self.pipe = args.pipe
+        self.n, self.L = n, L
+
+    def advance_seq(self, seg, k):
+        """Advance every packet's RTP sequence number by k bundles' worth."""
+        o = self.off64
+        hi, lo = seg[o + 2].to(self.torch.int32), seg[o + 3].to(self.torch.int32)
+        q = ((hi << 8) | lo) + k * self.step_seq
+        seg[o + 2] = ((q >> 8) & 0xFF).to(self.torch.uint8)
+        seg[o + 3] = (q & 0xFF).to(self.torch.uint8)
+
+    def protect(self, i, stream):
+        j = i % self.ring
+        if i >= self.ring:  # reuse a staged bundle: its unprotect finished steps ago
+            with self.torch.cuda.stream(stream):
+                self.advance_seq(self.segs[j], self.ring)
+        self.eng.transform_device(False, self.snd.tid, self.segs[j], self.off, self.lens[j],
+                                  self.cap, self.st, stream=stream)
+
+    def unprotect(self, i, stream):
+        j = i % self.ring
+        self.eng_r.transform_device(True, self.rcv.tid, self.segs[j], self.off, self.lens[j],
+                                    self.cap, self.st_r, stream=stream)
+
+    def step(self, i):
+        """free: protect(i) on stream A, unprotect(i) on stream B after it; the
+        sender never waits for the receiver (the ring is deep enough).
+        lagK: as free, but protect(i) waits until unprotect(i - K) is done.
+        join: protect(i) on A beside unprotect(i - 1) on B, both after the
+        previous step's join.  Serial: protect(i) then unprotect(i) on one
+        stream."""
+        if self.serial:
+            self.protect(i, self.s_a)
+            self.unprotect(i, self.s_a)
+            return
+        if self.pipe != "join":
+            lag = {"free": 0, "lag1": 1, "lag2": 2}[self.pipe]
+            if lag and i >= lag:
+                self.s_a.wait_event(self.ev_b[(i - lag) % 3])
+            self.protect(i, self.s_a)
+            self.end_a.record(self.s_a)
+            self.s_b.wait_event(self.end_a)
+            self.unprotect(i, self.s_b)
+            self.ev_b[i % 3].record(self.s_b)
+            return
+        self.s_a.wait_event(self.end_b)
+        self.s_b.wait_event(self.end_a)
+        self.protect(i, self.s_a)
+        if self.pending is not None:
+            self.unprotect(self.pending, self.s_b)
+        self.pending = i
+        self.end_a.record(self.s_a)
+        self.end_b.record(self.s_b)
+
+    def serial_step(self, i):
+        """protect(i) then unprotect(i) on stream A (the stage-timing pass)."""
+        self.s_a.wait_event(self.end_b)
+        if self.pending is not None:
+            self.unprotect(self.pending, self.s_a)
+            self.pending = None
+        self.protect(i, self.s_a)
+        self.unprotect(i, self.s_a)
+        self.end_a.record(self.s_a)
+
+    def finish(self):
+        """Unprotect the last protected bundle (join mode), untimed."""
+        if self.pending is not None:
+            self.s_b.wait_event(self.end_a)
+            self.unprotect(self.pending, self.s_b)
+            self.pending = None
+        self.torch.cuda.synchronize(self.dev)
+
+    def bad(self):
+        return int((self.st != 0).sum()) + int((self.st_r != 0).sum())
 
 
 def main():
@@ -177,204 +339,169 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(args.backend)
-    dev = torch.device("cuda", local_rank)
+        devices = [local_rank]
+        mode = "process"
+    elif args.gpus > 1:
+        devices = list(range(args.gpus))  # in-process: this process drives every GPU
+        mode = "inproc"
+    else:
+        devices = [local_rank]
+        mode = "process"
+    n_gpus = world if mode == "process" else len(devices)
 
-    from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPTransformer, profile_policies, synth
-
-    n, L, nssrc = args.packets, args.len, args.ssrcs
-    # rank r owns its own SSRC shard: disjoint SSRC sets, per-GPU contexts only
-    b = synth.rtp_bundle(n, nssrc, L, seed=synth.SEED_BASE + 2 + 7919 * rank)
-    # context table: >= 1.6x the SSRCs (load <= 0.31 at 10k); its size sets the
-    # sort's key width (2^15 slots + the invalid key: 16 bits = two radix passes)
-    max_ctx = 1 << max(12, (int(1.6 * nssrc) - 1).bit_length())
-    # The sender and the receiver side each get an engine of their own (its own
-    # scratch, context table and bundle stream), as a send thread and a receive
-    # thread would: step i's unprotect (receiver stream, after step i's protect)
-    # overlaps step i+1's protect (sender stream).  --serial: one engine, one
-    # stream, every kernel in order.
-    eng = SRTPEngine(device=local_rank, max_contexts=max_ctx, max_factories=64,
-                     max_transformers=64, max_batch=n)
-    eng_r = eng if args.serial else SRTPEngine(device=local_rank, max_contexts=max_ctx,
-                                               max_factories=64, max_transformers=64,
-                                               max_batch=n)
-    (k, s), = synth.keys(2 + rank, 1)
+    from libjitsi_amd import SRTPPolicy, profile_policies
     if args.policy == "AES_CM_128_NULL_AUTH":
-        from libjitsi_amd import SRTPPolicy as P
-        pols = (P(1, 16, 0, 0, 0, 14),) * 2
+        pols = (SRTPPolicy(1, 16, 0, 0, 0, 14),) * 2
     else:
         pols = profile_policies(args.policy)
-    snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
-    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng_r))
+    n, L = args.packets, args.len
+    T = pols[0].authTagLength
+    n_timing = 40  # serial stage-timing steps (also the GPU's run-in before the warmup)
+    total = n_timing + args.warmup + args.steps
+    sides = [Side(torch, d, rank if mode == "process" else i, args, pols, total)
+             for i, d in enumerate(devices)]
+    sd0 = sides[0]
+    g = 0  # global step counter: each step has bundles of its own (fresh sequence numbers)
+    for sd in sides:  # loads the status-check kernels now, not between passes
+        sd.bad()
 
-    off = torch.from_numpy(b.off.view(np.int32)).to(dev)
-    cap = torch.from_numpy(b.cap.view(np.int32)).to(dev)
-    st = torch.empty(n, dtype=torch.int32, device=dev)      # sender statuses
-    st_r = torch.empty(n, dtype=torch.int32, device=dev)    # receiver statuses
-    off64 = off.to(torch.int64)
-    seq_step = -(-n // nssrc)  # packets per SSRC per bundle
-    stream = torch.cuda.current_stream(dev)
-    stream_r = stream if args.serial else torch.cuda.Stream(dev)
+    # achievable HBM bandwidth on this device (plain device-to-device copy of
+    # 512 MiB, read + write bytes), reported beside the 8 TB/s spec peak
+    copy_gbs = None
+    try:
+        with torch.cuda.device(sd0.dev):
+            src = torch.empty(1 << 29, dtype=torch.uint8, device=sd0.dev)
+            dst = torch.empty_like(src)
+            dst.copy_(src)
+            torch.cuda.synchronize(sd0.dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                dst.copy_(src)
+            e1.record()
+            torch.cuda.synchronize(sd0.dev)
+            copy_gbs = round(5 * 2 * src.numel() / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+            del src, dst
+    except Exception:
+        copy_gbs = None
 
-    def advance_seq(seg, k):
-        """Advance every packet's RTP sequence number by k bundles' worth."""
-        hi, lo = seg[off64 + 2].to(torch.int32), seg[off64 + 3].to(torch.int32)
-        q = ((hi << 8) | lo) + k * seq_step
-        seg[off64 + 2] = ((q >> 8) & 0xFF).to(torch.uint8)
-        seg[off64 + 3] = (q & 0xFF).to(torch.uint8)
-
-    # Every step gets its own bundle, staged in HBM before the clock starts
-    # (bundle i = the base bundle with each SSRC's sequence numbers advanced i
-    # bundles): the timed region is protect + unprotect only.  A ring of at
-    # most RING bundles (RING x 319 MB); a step count beyond it re-sequences a
-    # used bundle inside the loop.
-    total = args.warmup + args.steps
-    ring = min(total, RING)
-    base = torch.from_numpy(b.seg).to(dev)
-    len0 = torch.from_numpy(b.length.view(np.int32)).to(dev)
-    segs, lens = [], []
-    for i in range(ring):
-        sg = base.clone()
-        if i:
-            advance_seq(sg, i)
-        segs.append(sg)
-        lens.append(len0.clone())
-    del base
-    torch.cuda.synchronize(dev)
-
-    protected = [torch.cuda.Event() for _ in range(ring)]
-    received = [None] * ring
-
-    def step(i, serial=args.serial):
-        j = i % ring
-        if i >= ring:
-            if received[j] is not None:
-                stream.wait_event(received[j])  # unprotect of step i - ring is done
-            advance_seq(segs[j], ring)
-        eng.transform_device(False, snd.tid, segs[j], off, lens[j], cap, st, stream=stream)
-        rs = stream if serial else stream_r
-        if rs is not stream:
-            protected[j].record(stream)
-            rs.wait_event(protected[j])
-        eng_r.transform_device(True, rcv.tid, segs[j], off, lens[j], cap, st_r, stream=rs)
-        if rs is not stream:
-            received[j] = torch.cuda.Event()
-            received[j].record(rs)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize(dev)
-    bad = int((st != 0).sum()) + int((st_r != 0).sum())
-    if bad:
-        hist = torch.bincount(torch.cat([st, st_r]).to(torch.int64), minlength=10).tolist()
-        raise SystemExit(f"rank {rank}: {bad} packets not accepted after warmup; status "
-                         f"histogram {hist}")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for i in range(args.warmup, total):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    ok = (int((st != 0).sum()) == 0 and int((st_r != 0).sum()) == 0
-          and all(int((x != L).sum()) == 0 for x in lens))
-    # Per-stage HIP-event timing (k_protect's launch duration for the roofline)
-    # in a separate, untimed pass, serial (one stream, so no stage shares the
-    # GPU with the other direction): the event records would otherwise sit
-    # between the kernels of the timed steps.
-    engines = [eng] if eng_r is eng else [eng, eng_r]
+    # 1. Per-stage HIP-event timing (the roofline kernels' launch durations),
+    # untimed, serial on the first GPU (one stream: no stage shares the GPU
+    # with the other direction).  It runs right before the warmup, so that the
+    # GPU is busy, every kernel is loaded and the clocks are up when it starts.
+    engines = [sd0.eng] if sd0.eng_r is sd0.eng else [sd0.eng, sd0.eng_r]
     for e in engines:
         e.set_timing(True)
         e.read_timing()
-    for i in range(total, total + min(args.steps, 10)):
-        step(i, serial=True)
-    torch.cuda.synchronize(dev)
+    for _ in range(n_timing):
+        sd0.serial_step(g)
+        g += 1
+    for sd in sides[1:]:  # the other GPUs warm up the same way (untimed)
+        for k in range(n_timing):
+            sd.serial_step(k)
+    torch.cuda.synchronize(sd0.dev)
     timing = {}
     for e in engines:
         for key, (ms, cnt) in e.read_timing().items():
             m0, c0 = timing.get(key, (0.0, 0))
             timing[key] = (m0 + ms, c0 + cnt)
         e.set_timing(False)
-    ok = ok and int((st != 0).sum()) == 0 and int((st_r != 0).sum()) == 0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    ok = sd0.bad() == 0
+
+    # 2. Warmup, straight into the timed steps: no host work between them but
+    # the synchronisation the timing needs (an idle GPU lowers its clocks, and
+    # the first steps after a gap run slow).
+    for _ in range(args.warmup):
+        for sd in sides:
+            sd.step(g)
+        g += 1
+    if world > 1:
+        dist.barrier()
+    for sd in sides:
+        torch.cuda.synchronize(sd.dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for sd in sides:
+            sd.step(g)
+        g += 1
+    for sd in sides:
+        torch.cuda.synchronize(sd.dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ok = ok and all(sd.bad() == 0 for sd in sides)
+    for sd in sides:
+        sd.finish()
+    ok = ok and all(sd.bad() == 0 and all(int((x != L).sum()) == 0 for x in sd.lens[:min(g, sd.ring)])
+                    for sd in sides)
+    t = torch.tensor([dt], dtype=torch.float64, device=sd0.dev)
     if world > 1:
         if args.backend != "nccl":
             t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = float(t.item())
 
-    total_pkts = n * args.steps * world
+    total_pkts = n * args.steps * n_gpus
     pps = total_pkts / dt_max
-    T = pols[0].authTagLength
     alg_bytes_rt = 2 * (L + (L + T))  # protect L + (L+T), unprotect (L+T) + L
     gbs = pps * alg_bytes_rt / 1e9
-    prot_ms, prot_cnt = timing["protect"]
-    avg_prot_s = prot_ms / 1e3 / max(prot_cnt, 1)
-    achieved = n * (L + (L + T)) / avg_prot_s / 1e9
     stages = {k: (v[0] / max(v[1], 1)) for k, v in timing.items() if v[1]}
-    achieved_u = None
-    if "verify" in stages and stages["verify"] > 0:
-        achieved_u = n * (L + (L + T)) / (stages["verify"] / 1e3) / 1e9
+    alg_launch = n * (L + (L + T))
 
-    traffic = traffic_u = util = None
+    pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("packets") == n and pmc.get("len") == L:
-                traffic = pmc.get("k_protect_bytes_per_launch")
-                traffic_u = pmc.get("k_unprotect_bytes_per_launch")
-                util = pmc.get("k_protect_utilisation")
+            if pmc.get("packets") != n or pmc.get("len") != L:
+                pmc = {}
         except Exception:
-            traffic = None
+            pmc = {}
 
-    # achievable HBM bandwidth on this device (plain device-to-device copy of
-    # 512 MiB, read + write bytes), reported beside the 8 TB/s spec peak
-    copy_gbs = None
-    try:
-        src = torch.empty(1 << 29, dtype=torch.uint8, device=dev)
-        dst = torch.empty_like(src)
-        dst.copy_(src)
-        torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            dst.copy_(src)
-        e1.record()
-        torch.cuda.synchronize(dev)
-        copy_gbs = round(5 * 2 * src.numel() / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
-        del src, dst
-    except Exception:
-        copy_gbs = None
+    def roofline(stage, kernel, traffic_key, util_key=None):
+        if stage not in stages or stages[stage] <= 0:
+            return None
+        achieved = alg_launch / (stages[stage] / 1e3) / 1e9
+        r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+             "traffic": pmc.get(traffic_key), "avg_launch_ms": round(stages[stage], 4),
+             "algorithmic_bytes_per_launch": alg_launch,
+             "copy_measured_gbps": copy_gbs}
+        if r["traffic"]:
+            r["traffic_source"] = f"rocprofv3 FETCH_SIZE/WRITE_SIZE per {kernel} launch, profiles/pmc_traffic.json"
+            r["traffic_over_algorithmic"] = round(r["traffic"] / alg_launch, 3)
+        if util_key and pmc.get(util_key):
+            r["utilisation"] = pmc.get(util_key)
+        return r
+
+    r_prot = roofline("protect", "k_protect", "k_protect_bytes_per_launch", "k_protect_utilisation")
+    r_unp = roofline("verify", "k_unprotect", "k_unprotect_bytes_per_launch", "k_unprotect_utilisation")
+    cands = [r for r in (r_prot, r_unp) if r]
+    dominant = max(cands, key=lambda r: r["avg_launch_ms"]) if cands else None
+    other = [r for r in cands if r is not dominant]
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        v, cnt, cdt = cpu_baseline(args.cpu_seconds, threads, L, nssrc)
-        cpu = {"value": round(v, 1), "unit": "packets/s", "cores": threads, "kind": "port",
-               "sample": f"oracle/srtp_oracle.c (reference call structure, OpenSSL 3 AES-ECB per "
-                         f"16-B block + HMAC re-keyed per packet): {cnt} packets of {L} B "
-                         f"protected+unprotected in {cdt:.1f} s on {threads} threads, "
-                         f"4096-packet bundles, {nssrc} SSRCs split across threads",
-               "gbps": round(v * alg_bytes_rt / 1e9, 3)}
+    if rank == 0 and n_gpus == 1 and not args.no_cpu:
+        share = args.cpu_threads or max(1, min(16, len(os.sched_getaffinity(0))))
+        cpu = cpu_baseline(args.cpu_seconds, share, L, args.ssrcs, T)
 
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
-        del segs, lens
+    if rank == 0 and n_gpus == 1 and not args.no_e2e:
+        b = sd0.b
+        keys = sd0.keys
+        del sides, sd0
         torch.cuda.empty_cache()
-        e2e = e2e_leg(b, pols, (k, s), n, L, local_rank, args.e2e_bundles)
+        e2e = e2e_leg(b, pols, keys, n, L, devices[0], args.e2e_bundles)
 
     if rank == 0:
         line = {
             "metric": METRIC,
             "value": round(pps, 1),
             "unit": "packets/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 4),
@@ -384,29 +511,22 @@ def main():
             "dtype": "u8",
             "data": "synthetic (deterministic RTP packets, random payload, seeded keys)",
             "config": {"workload": "configs[1]: 10k concurrent SSRCs x 1200-B RTP, "
-                                   "AES_CM_128_HMAC_SHA1_80, protect then unprotect",
-                       "packets_per_gpu_per_step": n, "ssrcs_per_gpu": nssrc, "pkt_len": L,
-                       "parallelism": f"ssrc-sharded x{world}",
-                       "streams": "serial" if args.serial else
-                                  "sender + receiver engine, one stream each"},
+                                   "AES_CM_128_HMAC_SHA1_80, protect + unprotect per step",
+                       "packets_per_gpu_per_step": n, "ssrcs_per_gpu": args.ssrcs, "pkt_len": L,
+                       "ssrc_mix": f"zipf({args.zipf})" if args.zipf > 0 else "round-robin",
+                       "parallelism": f"ssrc-sharded x{n_gpus} ({'one process per GPU' if mode == 'process' else 'one process, all GPUs'})",
+                       "streams": "serial: protect(i), unprotect(i) on one stream" if args.serial else
+                                  {"free": "sender + receiver engine, one stream each: unprotect(i) "
+                                           "after protect(i), the sender runs ahead",
+                                   "join": "sender + receiver engine, one stream each: protect(i) "
+                                           "beside unprotect(i-1), joined every step"}.get(
+                                      args.pipe, f"sender + receiver engine, {args.pipe}")},
             "gbps": round(gbs, 2),
             "goodput_gbps": round(pps * L * 2 / 1e9, 2),
             "all_accepted": ok,
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
-            "roofline": {"bound": "hbm", "kernel": "k_protect", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "traffic_source": "rocprofv3 FETCH_SIZE/WRITE_SIZE per k_protect launch, "
-                                           "profiles/pmc_traffic.json" if traffic else None,
-                         "copy_measured_gbps": copy_gbs,
-                         "utilisation": util,
-                         "algorithmic_bytes_per_launch": n * (L + L + T)},
-            "roofline_k_unprotect": None if achieved_u is None else {
-                "bound": "hbm", "achieved": round(achieved_u, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved_u / HBM_PEAK_GBS, 4), "traffic": traffic_u,
-                "note": "the other dominant kernel (unprotect: tag check + speculative decryption), "
-                        "same algorithmic bytes per packet, HIP events of the same serial pass"},
+            "roofline": dominant,
+            "roofline_other": other[0] if other else None,
             "cpu_baseline": cpu,
             "e2e": e2e,
         }

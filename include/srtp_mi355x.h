@@ -42,14 +42,17 @@
  *
  * Ownership: the caller owns every buffer; the engine owns contexts, session
  * keys and device scratch, and zeroes keys when factories are closed.
- * Threading: calls on one engine are serialised internally; work is enqueued
- * on the given HIP stream (NULL = the default stream), so bundles that
- * touch the same transformer must be submitted on one stream (submission order
- * == processing order, as the reference's `synchronized` contexts give).
- * Bundles of one engine share its device scratch: a bundle submitted on a
- * different stream than the engine's previous one first waits (host-side) for
- * that stream.  Independent directions that should overlap on the device use
- * one engine each (e.g. a send-side and a receive-side engine).
+ * Threading: calls on one engine are serialised internally and are safe from
+ * any host thread: each call makes the engine's device current for its
+ * duration and restores the caller's device (one process may drive engines on
+ * several GPUs).  Bundles of one engine are processed in submission order
+ * (== the order the reference's `synchronized` contexts give): a bundle
+ * submitted on another stream than the engine's previous bundle waits for
+ * that bundle on the device, with no host stall.  Control-plane calls
+ * (factory/transformer close and rekey, context state, stats) first wait for
+ * every bundle the engine has enqueued.  Independent directions that should
+ * overlap on the device use one engine each (e.g. a send-side and a
+ * receive-side engine).
  */
 #ifndef SRTP_MI355X_H
 #define SRTP_MI355X_H
@@ -85,6 +88,7 @@ extern "C" {
 #define SRTP_STATUS_DROP_INVALID 7    /* len < 12 or len > cap (RawPacket.isInvalid) */
 #define SRTP_STATUS_NOT_PROCESSED 8   /* after an ERR_MALFORMED with abort_on_error */
 #define SRTP_STATUS_SKIPPED 9         /* SRTP_PKT_FLAG_SKIP (null element / predicate) */
+#define SRTP_NUM_STATUS 10
 
 /* per-packet flags (javax.media.Buffer values read at SRTPCryptoContext.java:609) */
 #define SRTP_PKT_FLAG_DISCARD 0x2u
@@ -111,7 +115,8 @@ typedef struct {
     int32_t device;            /* HIP device ordinal */
     int32_t check_replay;      /* SRTPCryptoContext.checkReplay, default 1 */
     int32_t abort_on_error;    /* SinglePacketTransformer rethrow semantics, default 1 */
-    uint32_t max_contexts;     /* (transformer, SSRC) contexts, default 1<<21 */
+    uint32_t max_contexts;     /* (transformer, SSRC) contexts, default 1<<20 (table of
+                                  next_pow2(2 * max_contexts) slots, 40 B each) */
     uint32_t max_factories;    /* default 1<<16 */
     uint32_t max_transformers; /* default 1<<16 */
     uint32_t max_batch;        /* initial scratch size in packets (grows), default 1<<16 */
@@ -140,8 +145,9 @@ int srtp_transformer_set_factory(srtp_engine *e, int32_t transformer, int32_t fa
                                  int32_t forward);
 int srtp_transformer_close(srtp_engine *e, int32_t transformer);
 
-/* Process one bundle whose buffers are device (HBM) pointers; asynchronous on
- * `stream` (a hipStream_t, NULL = the default stream).  tids == NULL means every
+/* Process one bundle whose buffers are device (HBM) pointers on the engine's
+ * device; asynchronous on `stream` (a hipStream_t of that device; NULL = the
+ * engine's own stream, srtp_engine_stream).  tids == NULL means every
  * packet belongs to `tid`; otherwise tids[i] (device array) names packet i's
  * transformer.  flags may be NULL.  reverse = 0: transform (protect),
  * reverse = 1: reverseTransform (unprotect).  The caller guarantees what
@@ -158,12 +164,37 @@ int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, in
                         uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
                         const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n);
 
+/* The engine's own non-blocking stream (created with the engine, so each
+ * engine has a hardware queue of its own): the stream NULL selects in
+ * srtp_transform_device, and the one srtp_transform_host and the pipeline
+ * run their kernels on. */
+void *srtp_engine_stream(srtp_engine *e);
+/* stream == NULL: wait for every bundle this engine has enqueued (any stream) */
 int srtp_engine_sync(srtp_engine *e, void *stream);
 /* returns 1 and fills *out if the transformer has a context for ssrc, else 0 */
 int srtp_get_context_state(srtp_engine *e, int32_t transformer, uint32_t ssrc,
                            srtp_ctx_state *out);
 /* number of live contexts in the engine's table */
 int64_t srtp_engine_num_contexts(srtp_engine *e);
+
+/* Per-engine counters (SURVEY.md 5 metrics).  The reference keeps none for
+ * auth / replay failures (SRTPCryptoContext.java:635-638 logs at debug level)
+ * and counts only exceptions (SinglePacketTransformer.java:42,54-59,140-148);
+ * here every final per-packet status is counted, cumulatively since engine
+ * creation.  ctx_overflow counts packets that found no free context slot (they
+ * get SRTP_STATUS_DROP_NO_CONTEXT); ctx_live / ctx_tombstones / ctx_slots
+ * describe the context table at the time of the call. */
+typedef struct {
+    uint64_t bundles, packets;           /* bundles / packets submitted */
+    uint64_t status[SRTP_NUM_STATUS];    /* final statuses, indexed by SRTP_STATUS_* */
+    uint64_t roc_rechecks;               /* unprotect tags re-checked under a ROC the walk
+                                            guessed differently from the speculation */
+    uint64_t repaired;                   /* packets whose speculative decryption was redone */
+    uint64_t ctx_overflow;               /* packets refused a new context: table full */
+    uint64_t ctx_live, ctx_tombstones, ctx_slots;
+    uint64_t rehashes;                   /* context-table rebuilds (tombstone cleanup) */
+} srtp_stats;
+int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
 
 /* Context-state export / import: lets a stream's ROC, s_l,
  * replay window and SRTCP indices follow it to another engine or GPU (SSRC
@@ -230,6 +261,56 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
 int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                          int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes);
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
+
+/* In-process multi-GPU dispatcher (SURVEY.md 8b engine_create(devices, opts),
+ * 8e): one engine per shard, shard i on device devices[i] (a device may host
+ * several shards).  A host bundle is split by shard = srtp_shard_of(SSRC)
+ * (RTP: RawPacket.getSSRC, RTCP: getRTCPSSRC) -- SRTP contexts are per
+ * (transformer, SSRC), SRTPTransformer.java:62,152-175, so each GPU owns its
+ * SSRCs' state and nothing crosses GPUs.  Every shard's sub-bundle keeps
+ * bundle order; statuses, lengths and packet bytes are scattered back in
+ * place.  Results are identical to one engine processing the whole bundle,
+ * including SinglePacketTransformer's abort-on-throw
+ * (SinglePacketTransformer.java:134-155,190-210), which the dispatcher
+ * reproduces across shards by running packets that could throw in phases of
+ * their own (see dispatch.cpp).  Factories and transformers are created on
+ * every shard with the same ids as one engine would assign.
+ * srtp_dispatch_plan is the host-only split (no GPU needed): per packet its
+ * shard (-1: handled without an engine) and phase; it returns the number of
+ * phases.  kinds[t] = transformer t's kind, tag_mask bit T = some policy has
+ * tag length T. */
+typedef struct srtp_dispatch srtp_dispatch;
+int32_t srtp_shard_of(uint32_t ssrc, int32_t n_shards);
+int32_t srtp_dispatch_plan(int32_t n_shards, int32_t abort_on_error, int32_t reverse,
+                           const int32_t *kinds, int32_t n_transformers, uint32_t tag_mask,
+                           const int32_t *tids, int32_t tid, const uint8_t *seg, size_t seg_bytes,
+                           const uint32_t *off, const uint32_t *len, const uint32_t *cap,
+                           const uint32_t *flags, uint32_t n, int32_t *shard, int32_t *phase);
+int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_engine_opts *opts,
+                         srtp_dispatch **out);
+void srtp_dispatch_destroy(srtp_dispatch *d);
+const char *srtp_dispatch_last_error(srtp_dispatch *d);
+int32_t srtp_dispatch_num_shards(srtp_dispatch *d);
+srtp_engine *srtp_dispatch_engine(srtp_dispatch *d, int32_t shard);
+int srtp_dispatch_factory_create(srtp_dispatch *d, int32_t sender, const uint8_t *master_key,
+                                 int32_t key_len, const uint8_t *master_salt, int32_t salt_len,
+                                 const srtp_policy *srtp, const srtp_policy *srtcp, int32_t *out);
+int srtp_dispatch_factory_close(srtp_dispatch *d, int32_t factory);
+int srtp_dispatch_transformer_create(srtp_dispatch *d, int32_t kind, int32_t fwd, int32_t rev,
+                                     int32_t *out);
+int srtp_dispatch_transformer_set_factory(srtp_dispatch *d, int32_t transformer, int32_t factory,
+                                          int32_t forward);
+int srtp_dispatch_transformer_close(srtp_dispatch *d, int32_t transformer);
+int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid,
+                                 uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                                 const uint32_t *cap, const uint32_t *flags, int32_t *status,
+                                 uint32_t n);
+int srtp_dispatch_get_context_state(srtp_dispatch *d, int32_t transformer, uint32_t ssrc,
+                                    srtp_ctx_state *out);
+int srtp_dispatch_set_context_state(srtp_dispatch *d, int32_t transformer, uint32_t ssrc,
+                                    int32_t forward, const srtp_ctx_state *st);
+/* srtp_stats summed over the shards */
+int srtp_dispatch_stats(srtp_dispatch *d, srtp_stats *out);
 
 /* Control-plane crypto without a GPU (used by CPU-side tests): RFC 3711 4.3
  * session keys exactly as SRTPCryptoContext.deriveSrtpKeys (rtcp = 0) /

@@ -36,6 +36,12 @@ EXPORTED = [
     "srtp_engine_read_timing", "srtp_derive_session_keys", "srtp_export_contexts",
     "srtp_set_context_state", "srtp_pipeline_create", "srtp_pipeline_destroy",
     "srtp_pipeline_slot_get", "srtp_pipeline_submit", "srtp_pipeline_wait",
+    "srtp_engine_stats", "srtp_engine_stream", "srtp_shard_of", "srtp_dispatch_plan", "srtp_dispatch_create",
+    "srtp_dispatch_destroy", "srtp_dispatch_last_error", "srtp_dispatch_num_shards",
+    "srtp_dispatch_engine", "srtp_dispatch_factory_create", "srtp_dispatch_factory_close",
+    "srtp_dispatch_transformer_create", "srtp_dispatch_transformer_set_factory",
+    "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host",
+    "srtp_dispatch_get_context_state", "srtp_dispatch_set_context_state", "srtp_dispatch_stats",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -61,6 +67,19 @@ class CtxState(C.Structure):
                 ("guessed_roc", C.c_int32), ("sent_index", C.c_int32),
                 ("received_index", C.c_int32), ("replay_window", C.c_uint64),
                 ("key_set", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    """srtp_stats (include/srtp_mi355x.h)"""
+    _fields_ = ([("bundles", C.c_uint64), ("packets", C.c_uint64),
+                 ("status", C.c_uint64 * 10)] +
+                [(n, C.c_uint64) for n in ("roc_rechecks", "repaired", "ctx_overflow", "ctx_live",
+                                           "ctx_tombstones", "ctx_slots", "rehashes")])
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "status"}
+        d["status"] = {STATUS_NAMES[i]: int(self.status[i]) for i in range(10)}
+        return d
 
 
 class PipelineSlot(C.Structure):
@@ -112,15 +131,44 @@ def lib() -> C.CDLL:
     L.srtp_pipeline_slot_get.argtypes = [vp, i32, C.POINTER(PipelineSlot)]
     L.srtp_pipeline_submit.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t]
     L.srtp_pipeline_wait.argtypes = [vp, i32]
+    L.srtp_engine_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.srtp_engine_stream.argtypes = [vp]
+    L.srtp_engine_stream.restype = vp
+    L.srtp_shard_of.argtypes = [u32, i32]
+    L.srtp_shard_of.restype = i32
+    L.srtp_dispatch_plan.argtypes = [i32, i32, i32, vp, i32, u32, vp, i32, vp, C.c_size_t, vp, vp, vp,
+                                     vp, u32, vp, vp]
+    L.srtp_dispatch_plan.restype = i32
+    L.srtp_dispatch_create.argtypes = [vp, i32, C.POINTER(EngineOpts), C.POINTER(vp)]
+    L.srtp_dispatch_destroy.argtypes = [vp]
+    L.srtp_dispatch_destroy.restype = None
+    L.srtp_dispatch_last_error.argtypes = [vp]
+    L.srtp_dispatch_last_error.restype = C.c_char_p
+    L.srtp_dispatch_num_shards.argtypes = [vp]
+    L.srtp_dispatch_num_shards.restype = i32
+    L.srtp_dispatch_engine.argtypes = [vp, i32]
+    L.srtp_dispatch_engine.restype = vp
+    L.srtp_dispatch_factory_create.argtypes = [vp, i32, pu8, i32, pu8, i32, C.POINTER(Policy),
+                                               C.POINTER(Policy), pi32]
+    L.srtp_dispatch_factory_close.argtypes = [vp, i32]
+    L.srtp_dispatch_transformer_create.argtypes = [vp, i32, i32, i32, pi32]
+    L.srtp_dispatch_transformer_set_factory.argtypes = [vp, i32, i32, i32]
+    L.srtp_dispatch_transformer_close.argtypes = [vp, i32]
+    L.srtp_dispatch_transform_host.argtypes = [vp, i32, vp, i32, vp, C.c_size_t, vp, vp, vp, vp, vp,
+                                               u32]
+    L.srtp_dispatch_get_context_state.argtypes = [vp, i32, u32, C.POINTER(CtxState)]
+    L.srtp_dispatch_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
+    L.srtp_dispatch_stats.argtypes = [vp, C.POINTER(Stats)]
     _lib = L
     return L
 
 
-def check(rc: int, engine=None, what: str = "") -> int:
+def check(rc: int, engine=None, what: str = "", dispatch=None) -> int:
     if rc < 0:
         msg = RC.get(rc, str(rc))
-        if engine:
-            detail = lib().srtp_engine_last_error(engine)
+        if engine or dispatch:
+            detail = (lib().srtp_dispatch_last_error(dispatch) if dispatch
+                      else lib().srtp_engine_last_error(engine))
             if detail:
                 msg += ": " + detail.decode(errors="replace")
         raise SrtpError(f"{what}: {msg}")

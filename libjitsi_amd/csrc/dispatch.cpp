@@ -1,0 +1,528 @@
+// dispatch.cpp -- in-process multi-GPU front end of the SRTP engine
+// (SURVEY.md 8b engine_create(devices, opts), 8e SSRC sharding).
+//
+// A libjitsi JVM is one process; it hands RawPacket[] bundles to the engine
+// through one JNI shim.  srtp_dispatch owns one engine per shard (one shard per
+// GPU, or several on one GPU for testing) and splits each host bundle by
+// shard = mix32(SSRC) % shards.  SRTP state is per (transformer, SSRC) context
+// (SRTPTransformer.java:62,152-175 keeps one context per SSRC, nothing else is
+// shared but the read-only factory keys), so a shard owns its SSRCs' contexts
+// and no data moves between GPUs.  Factories and transformers are replicated
+// to every shard with identical ids.
+//
+// Order and abort semantics.  Each shard receives its packets in bundle
+// order, which is all the per-context state machine needs.  The one
+// cross-shard dependency is SinglePacketTransformer's rethrow
+// (SinglePacketTransformer.java:134-155,190-210): a packet that throws aborts
+// the later packets of the same transformer's array, on every shard.  The
+// host plan therefore marks every packet that could throw (a superset of the
+// engine's throws: RawPacket.getHeaderLength / SRTPCipherCTR.process /
+// RawPacket.getSRTCPIndex bounds, see may_throw) and cuts the bundle into
+// phases: phase 2k holds each transformer's packets after its k-th such
+// packet and before its (k+1)-th, phase 2k+1 the (k+1)-th itself.  Phases run
+// one after the other (transformers are independent, so packets of different
+// transformers may share a phase); a packet of phase 2k+1 that comes back
+// ERR_MALFORMED aborts its transformer: its later packets are never submitted
+// and get NOT_PROCESSED, exactly as one engine bundle would report them.
+// Without abort_on_error, or without any packet that could throw (the normal
+// case), the whole bundle is one phase.
+//
+// Data path per shard: a worker thread packs its packets into pinned slots of
+// an srtp_pipeline on its engine (H2D, kernels and D2H of consecutive chunks
+// overlap), then scatters statuses, lengths and packet bytes back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <string.h>
+
+#include "../../include/srtp_mi355x.h"
+
+namespace {
+
+constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
+constexpr uint32_t kChunkPackets = 1u << 16;       // packets per pipeline slot
+constexpr size_t kChunkBytes = (size_t)64 << 20;   // segment bytes per pipeline slot
+constexpr int kDepth = 2;                          // pipeline slots per shard
+
+uint32_t mix32(uint32_t x) { // murmur3 fmix32 (libjitsi_amd/dispatch.py mix32)
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+
+uint32_t be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// RawPacket.getHeaderLength (RawPacket.java:602-614) with the signed extension
+// length (:544-556); kHdrThrow when the extension length lies outside cap.
+int32_t rtp_header_len(const uint8_t *pkt, uint32_t cap) {
+    const uint32_t b0 = pkt[0];
+    const int cc = (int)(b0 & 0x0fu);
+    int32_t h = 12 + 4 * cc;
+    if (b0 & 0x10u) {
+        const int idx = 12 + cc * 4 + 2;
+        if (idx + 1 >= (int)cap) return kHdrThrow;
+        const int ext = ((int)(int8_t)pkt[idx] * 256) | (int)pkt[idx + 1];
+        h += 4 + ext * 4;
+    }
+    return h;
+}
+
+// SRTPCipherCTR.process would throw on region [h, h + plen) (:99-120); the
+// AES-F8 (SRTPCipherF8.process :97-128) and NULL ciphers throw on a subset.
+bool cipher_may_throw(int32_t h, int32_t plen) {
+    if (h == kHdrThrow) return true;
+    if (plen < 0) return (plen % 16) != 0;
+    return plen > 0 && h < 0;
+}
+
+} // namespace
+
+// Plan of one bundle: the shard and phase of each packet (see the file
+// comment).  kinds[t] is transformer t's kind; tag_mask bit T is set when some
+// policy of the dispatcher has tag length T (0 for NULL authentication).
+// Packets that need no engine (SKIP flag, bad transformer id) get shard -1.
+// Returns the number of phases.
+static int32_t plan_bundle(int32_t n_shards, int32_t abort_on_error, int32_t reverse,
+                           const int32_t *kinds, int32_t n_transformers, uint32_t tag_mask,
+                           const int32_t *tids, int32_t tid, const uint8_t *seg, const uint32_t *off,
+                           const uint32_t *len, const uint32_t *cap, const uint32_t *flags, uint32_t n,
+                           int32_t *shard, int32_t *phase) {
+    int t_max = 0;
+    for (int T = 0; T < 32; T++)
+        if (tag_mask & (1u << T)) t_max = T;
+    std::vector<int32_t> rank((size_t)std::max(n_transformers, 1), 0);
+    int32_t n_phases = 1;
+    for (uint32_t i = 0; i < n; i++) {
+        const int32_t t = tids ? tids[i] : tid;
+        const uint32_t fl = flags ? flags[i] : 0u;
+        if ((fl & SRTP_PKT_FLAG_SKIP) || t < 0 || t >= n_transformers) {
+            shard[i] = -1;
+            phase[i] = 0;
+            continue;
+        }
+        const uint32_t L = len[i], C = cap[i];
+        const bool invalid = L < 12 || L > C || C > 65535u; // RawPacket.isInvalid :903-909
+        const uint8_t *pkt = seg + off[i];
+        const bool rtp = kinds[t] == SRTP_KIND_RTP;
+        shard[i] = invalid ? 0
+                           : (int32_t)(mix32(be32(pkt + (rtp ? 8 : 4))) % (uint32_t)n_shards);
+        bool mt = false;
+        if (abort_on_error && !invalid) {
+            if (rtp) {
+                const int32_t h = rtp_header_len(pkt, C);
+                if (!reverse) {
+                    mt = cipher_may_throw(h, (int32_t)L - (h == kHdrThrow ? 0 : h));
+                } else if (!(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ||
+                           h == kHdrThrow) {
+                    for (int T = 0; T < 32 && !mt; T++) {
+                        if (!(tag_mask & (1u << T))) continue;
+                        const int32_t newL = (int32_t)L - T > 0 ? (int32_t)L - T : 0;
+                        mt = cipher_may_throw(h, newL - (h == kHdrThrow ? 0 : h));
+                    }
+                }
+            } else if (reverse) {
+                // getSRTCPIndex at length - 4 - tag, decryption from byte 8
+                // (SRTCPCryptoContext.reverseTransformPacket :315-374)
+                mt = (int32_t)L < 12 + t_max;
+            }
+        }
+        phase[i] = 2 * rank[t] + (mt ? 1 : 0);
+        if (mt) rank[t]++;
+        n_phases = std::max(n_phases, phase[i] + 1);
+    }
+    return n_phases;
+}
+
+struct srtp_dispatch {
+    std::vector<srtp_engine *> engines;
+    std::vector<srtp_pipeline *> pipes;
+    std::vector<int32_t> kinds;  // transformer kinds (replicated ids)
+    uint32_t tag_mask = 0;
+    int32_t abort_on_error = 1;
+    std::mutex mu;
+    std::string last_error;
+
+    // worker threads, one per shard
+    struct Job {
+        const std::vector<uint32_t> *idx = nullptr;
+        int32_t reverse = 0;
+        int32_t rc = SRTP_OK;
+    };
+    std::vector<std::thread> workers;
+    std::vector<Job> jobs;
+    std::mutex wmu;
+    std::condition_variable cv_go, cv_done;
+    uint64_t generation = 0;
+    int pending = 0;
+    bool stop = false;
+    // the bundle being processed (valid while a generation runs)
+    const int32_t *b_tids = nullptr;
+    int32_t b_tid = -1;
+    uint8_t *b_seg = nullptr;
+    const uint32_t *b_off = nullptr, *b_cap = nullptr, *b_flags = nullptr;
+    uint32_t *b_len = nullptr;
+    int32_t *b_status = nullptr;
+};
+
+namespace {
+
+int dfail(srtp_dispatch *d, int code, const std::string &msg) {
+    d->last_error = msg;
+    return code;
+}
+
+size_t region(uint32_t cap) { return ((size_t)cap + 15) & ~(size_t)15; }
+
+// Shard s's share of one phase: chunks through the shard's pipeline slots.
+int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t reverse) {
+    srtp_pipeline *pl = d->pipes[(size_t)s];
+    srtp_pipeline_slot sl[kDepth];
+    for (int k = 0; k < kDepth; k++) {
+        int rc = srtp_pipeline_slot_get(pl, k, &sl[k]);
+        if (rc != SRTP_OK) return rc;
+    }
+    std::vector<uint32_t> chunk_of[kDepth]; // global packet indices in each slot
+    int busy[kDepth] = {0};
+    int rc_all = SRTP_OK;
+    auto drain = [&](int k) {
+        if (!busy[k]) return;
+        busy[k] = 0;
+        const int rc = srtp_pipeline_wait(pl, k);
+        if (rc != SRTP_OK) {
+            rc_all = rc;
+            return;
+        }
+        const std::vector<uint32_t> &ch = chunk_of[k];
+        for (size_t j = 0; j < ch.size(); j++) {
+            const uint32_t i = ch[j];
+            d->b_status[i] = sl[k].status[j];
+            d->b_len[i] = sl[k].len[j];
+            memcpy(d->b_seg + d->b_off[i], sl[k].seg + sl[k].off[j], region(d->b_cap[i]));
+        }
+    };
+    size_t pos = 0;
+    int k = 0;
+    while (pos < idx.size() && rc_all == SRTP_OK) {
+        drain(k);
+        if (rc_all != SRTP_OK) break;
+        std::vector<uint32_t> &ch = chunk_of[k];
+        ch.clear();
+        size_t bytes = 0;
+        while (pos < idx.size() && ch.size() < sl[k].max_packets) {
+            const uint32_t i = idx[pos];
+            const size_t r = region(d->b_cap[i]);
+            if (bytes + r > sl[k].seg_cap) break;
+            const uint32_t j = (uint32_t)ch.size();
+            sl[k].off[j] = (uint32_t)bytes;
+            sl[k].len[j] = d->b_len[i];
+            sl[k].cap[j] = d->b_cap[i];
+            sl[k].flags[j] = d->b_flags ? d->b_flags[i] : 0u;
+            sl[k].tids[j] = d->b_tids ? d->b_tids[i] : d->b_tid;
+            memcpy(sl[k].seg + bytes, d->b_seg + d->b_off[i], r);
+            bytes += r;
+            ch.push_back(i);
+            pos++;
+        }
+        if (ch.empty()) return SRTP_EINVAL; // a packet larger than a slot (cannot happen: cap <= 65535)
+        const int rc = srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes);
+        if (rc != SRTP_OK) return rc;
+        busy[k] = 1;
+        k = (k + 1) % kDepth;
+    }
+    for (int q = 0; q < kDepth; q++) drain((k + q) % kDepth);
+    return rc_all;
+}
+
+void worker_main(srtp_dispatch *d, int s) {
+    uint64_t seen = 0;
+    for (;;) {
+        std::unique_lock<std::mutex> lk(d->wmu);
+        d->cv_go.wait(lk, [&] { return d->stop || d->generation != seen; });
+        if (d->stop) return;
+        seen = d->generation;
+        srtp_dispatch::Job job = d->jobs[(size_t)s];
+        lk.unlock();
+        int rc = SRTP_OK;
+        if (job.idx && !job.idx->empty()) rc = run_shard(d, s, *job.idx, job.reverse);
+        lk.lock();
+        d->jobs[(size_t)s].rc = rc;
+        if (--d->pending == 0) d->cv_done.notify_all();
+    }
+}
+
+// Runs one phase on every shard at once; returns the first error.
+int run_phase(srtp_dispatch *d, const std::vector<std::vector<uint32_t>> &per_shard, int32_t reverse) {
+    std::unique_lock<std::mutex> lk(d->wmu);
+    for (size_t s = 0; s < d->engines.size(); s++) {
+        d->jobs[s].idx = &per_shard[s];
+        d->jobs[s].reverse = reverse;
+        d->jobs[s].rc = SRTP_OK;
+    }
+    d->pending = (int)d->engines.size();
+    d->generation++;
+    d->cv_go.notify_all();
+    d->cv_done.wait(lk, [&] { return d->pending == 0; });
+    for (auto &j : d->jobs)
+        if (j.rc != SRTP_OK) return j.rc;
+    return SRTP_OK;
+}
+
+// Calls f(engine) on every shard; fails unless every shard returns the same id.
+int replicate(srtp_dispatch *d, const std::function<int(srtp_engine *, int32_t *)> &f, int32_t *out) {
+    int32_t id0 = -1;
+    for (size_t s = 0; s < d->engines.size(); s++) {
+        int32_t id = -1;
+        const int rc = f(d->engines[s], &id);
+        if (rc != SRTP_OK)
+            return dfail(d, rc, std::string("shard ") + std::to_string(s) + ": " +
+                                    srtp_engine_last_error(d->engines[s]));
+        if (s == 0) id0 = id;
+        else if (id != id0) return dfail(d, SRTP_EINVAL, "shard ids diverged");
+    }
+    if (out) *out = id0;
+    return SRTP_OK;
+}
+
+int each(srtp_dispatch *d, const std::function<int(srtp_engine *)> &f) {
+    for (size_t s = 0; s < d->engines.size(); s++) {
+        const int rc = f(d->engines[s]);
+        if (rc != SRTP_OK)
+            return dfail(d, rc, std::string("shard ") + std::to_string(s) + ": " +
+                                    srtp_engine_last_error(d->engines[s]));
+    }
+    return SRTP_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int32_t srtp_shard_of(uint32_t ssrc, int32_t n_shards) {
+    return n_shards > 0 ? (int32_t)(mix32(ssrc) % (uint32_t)n_shards) : -1;
+}
+
+int32_t srtp_dispatch_plan(int32_t n_shards, int32_t abort_on_error, int32_t reverse,
+                           const int32_t *kinds, int32_t n_transformers, uint32_t tag_mask,
+                           const int32_t *tids, int32_t tid, const uint8_t *seg, size_t seg_bytes,
+                           const uint32_t *off, const uint32_t *len, const uint32_t *cap,
+                           const uint32_t *flags, uint32_t n, int32_t *shard, int32_t *phase) {
+    if (n_shards < 1 || !kinds || n_transformers < 0 || (n && (!seg || !off || !len || !cap ||
+                                                               !shard || !phase)))
+        return SRTP_EINVAL;
+    for (uint32_t i = 0; i < n; i++)
+        if (off[i] % 16 != 0 || cap[i] > 65535u || (uint64_t)off[i] + region(cap[i]) > seg_bytes)
+            return SRTP_EINVAL;
+    return plan_bundle(n_shards, abort_on_error, reverse, kinds, n_transformers, tag_mask, tids, tid,
+                       seg, off, len, cap, flags, n, shard, phase);
+}
+
+void srtp_dispatch_destroy(srtp_dispatch *d) {
+    if (!d) return;
+    {
+        std::lock_guard<std::mutex> lk(d->wmu);
+        d->stop = true;
+    }
+    d->cv_go.notify_all();
+    for (auto &w : d->workers)
+        if (w.joinable()) w.join();
+    for (auto *p : d->pipes) srtp_pipeline_destroy(p);
+    for (auto *e : d->engines) srtp_engine_destroy(e);
+    delete d;
+}
+
+int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_engine_opts *opts,
+                         srtp_dispatch **out) {
+    if (!devices || n_shards < 1 || n_shards > 256 || !out) return SRTP_EINVAL;
+    *out = nullptr;
+    srtp_dispatch *d = new (std::nothrow) srtp_dispatch();
+    if (!d) return SRTP_ENOMEM;
+    srtp_engine_opts o;
+    if (opts) o = *opts;
+    else srtp_engine_opts_default(&o);
+    d->abort_on_error = o.abort_on_error;
+    int rc = SRTP_OK;
+    for (int32_t s = 0; s < n_shards && rc == SRTP_OK; s++) {
+        srtp_engine_opts os = o;
+        os.device = devices[s];
+        srtp_engine *e = nullptr;
+        rc = srtp_engine_create(&os, &e);
+        if (rc != SRTP_OK) break;
+        d->engines.push_back(e);
+        srtp_pipeline *pl = nullptr;
+        rc = srtp_pipeline_create(e, kChunkPackets, kChunkBytes, kDepth, &pl);
+        if (rc != SRTP_OK) break;
+        d->pipes.push_back(pl);
+    }
+    if (rc == SRTP_OK) {
+        d->jobs.resize((size_t)n_shards);
+        try {
+            for (int32_t s = 0; s < n_shards; s++) d->workers.emplace_back(worker_main, d, (int)s);
+        } catch (...) {
+            rc = SRTP_ENOMEM;
+        }
+    }
+    if (rc != SRTP_OK) {
+        srtp_dispatch_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return SRTP_OK;
+}
+
+const char *srtp_dispatch_last_error(srtp_dispatch *d) { return d ? d->last_error.c_str() : ""; }
+
+int32_t srtp_dispatch_num_shards(srtp_dispatch *d) { return d ? (int32_t)d->engines.size() : 0; }
+
+srtp_engine *srtp_dispatch_engine(srtp_dispatch *d, int32_t shard) {
+    if (!d || shard < 0 || (size_t)shard >= d->engines.size()) return nullptr;
+    return d->engines[(size_t)shard];
+}
+
+int srtp_dispatch_factory_create(srtp_dispatch *d, int32_t sender, const uint8_t *master_key,
+                                 int32_t key_len, const uint8_t *master_salt, int32_t salt_len,
+                                 const srtp_policy *srtp, const srtp_policy *srtcp, int32_t *out) {
+    if (!d || !srtp || !srtcp) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    const int rc = replicate(d, [&](srtp_engine *e, int32_t *id) {
+        return srtp_factory_create(e, sender, master_key, key_len, master_salt, salt_len, srtp, srtcp, id);
+    }, out);
+    if (rc != SRTP_OK) return rc;
+    for (const srtp_policy *p : {srtp, srtcp}) {
+        const int T = p->auth_type == SRTP_NULL_AUTHENTICATION ? 0 : p->auth_tag_len;
+        if (T >= 0 && T < 32) d->tag_mask |= 1u << T;
+    }
+    return SRTP_OK;
+}
+
+int srtp_dispatch_factory_close(srtp_dispatch *d, int32_t factory) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    return each(d, [&](srtp_engine *e) { return srtp_factory_close(e, factory); });
+}
+
+int srtp_dispatch_transformer_create(srtp_dispatch *d, int32_t kind, int32_t fwd, int32_t rev,
+                                     int32_t *out) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    int32_t id = -1;
+    const int rc = replicate(d, [&](srtp_engine *e, int32_t *x) {
+        return srtp_transformer_create(e, kind, fwd, rev, x);
+    }, &id);
+    if (rc != SRTP_OK) return rc;
+    if ((size_t)id >= d->kinds.size()) d->kinds.resize((size_t)id + 1, SRTP_KIND_RTP);
+    d->kinds[(size_t)id] = kind;
+    if (out) *out = id;
+    return SRTP_OK;
+}
+
+int srtp_dispatch_transformer_set_factory(srtp_dispatch *d, int32_t t, int32_t f, int32_t forward) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    return each(d, [&](srtp_engine *e) { return srtp_transformer_set_factory(e, t, f, forward); });
+}
+
+int srtp_dispatch_transformer_close(srtp_dispatch *d, int32_t t) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    return each(d, [&](srtp_engine *e) { return srtp_transformer_close(e, t); });
+}
+
+int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid,
+                                 uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                                 const uint32_t *cap, const uint32_t *flags, int32_t *status,
+                                 uint32_t n) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    if (n == 0) return SRTP_OK;
+    if (!seg || !off || !len || !cap || !status) return dfail(d, SRTP_EINVAL, "null buffer");
+    const int32_t nt = (int32_t)d->kinds.size();
+    if (!tids && (tid < 0 || tid >= nt)) return dfail(d, SRTP_EINVAL, "bad transformer id");
+    std::vector<int32_t> shard(n), phase(n);
+    const int32_t n_phases = srtp_dispatch_plan((int32_t)d->engines.size(), d->abort_on_error, reverse,
+                                                d->kinds.data(), nt, d->tag_mask, tids, tid, seg,
+                                                seg_bytes, off, len, cap, flags, n, shard.data(),
+                                                phase.data());
+    if (n_phases < 0) return dfail(d, n_phases, "packet region outside the segment");
+    d->b_tids = tids; d->b_tid = tid; d->b_seg = seg; d->b_off = off; d->b_len = len;
+    d->b_cap = cap; d->b_flags = flags; d->b_status = status;
+    // packets grouped by phase (bundle order inside each)
+    std::vector<uint32_t> first((size_t)n_phases + 1, 0), by_phase(n);
+    for (uint32_t i = 0; i < n; i++) first[(size_t)phase[i] + 1]++;
+    for (int32_t ph = 0; ph < n_phases; ph++) first[(size_t)ph + 1] += first[(size_t)ph];
+    {
+        std::vector<uint32_t> fill(first.begin(), first.end() - 1);
+        for (uint32_t i = 0; i < n; i++) by_phase[fill[(size_t)phase[i]]++] = i;
+    }
+    std::vector<char> aborted((size_t)std::max(nt, 1), 0);
+    std::vector<std::vector<uint32_t>> per_shard(d->engines.size());
+    std::vector<uint32_t> probes; // packets of an odd phase, for the abort check
+    int rc = SRTP_OK;
+    for (int32_t ph = 0; ph < n_phases && rc == SRTP_OK; ph++) {
+        for (auto &v : per_shard) v.clear();
+        probes.clear();
+        for (uint32_t q = first[(size_t)ph]; q < first[(size_t)ph + 1]; q++) {
+            const uint32_t i = by_phase[q];
+            if (shard[i] < 0) { // SKIP flag or no such transformer
+                status[i] = SRTP_STATUS_SKIPPED;
+                continue;
+            }
+            const int32_t t = tids ? tids[i] : tid;
+            if (aborted[(size_t)t]) { // an earlier packet of t threw
+                status[i] = SRTP_STATUS_NOT_PROCESSED;
+                continue;
+            }
+            per_shard[(size_t)shard[i]].push_back(i);
+            if (ph & 1) probes.push_back(i);
+        }
+        rc = run_phase(d, per_shard, reverse);
+        for (uint32_t i : probes)
+            if (status[i] == SRTP_STATUS_ERR_MALFORMED) aborted[(size_t)(tids ? tids[i] : tid)] = 1;
+    }
+    if (rc != SRTP_OK) return dfail(d, rc, "shard bundle failed");
+    return SRTP_OK;
+}
+
+int srtp_dispatch_get_context_state(srtp_dispatch *d, int32_t t, uint32_t ssrc, srtp_ctx_state *out) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    return srtp_get_context_state(d->engines[(size_t)srtp_shard_of(ssrc, (int32_t)d->engines.size())], t,
+                                  ssrc, out);
+}
+
+int srtp_dispatch_set_context_state(srtp_dispatch *d, int32_t t, uint32_t ssrc, int32_t forward,
+                                    const srtp_ctx_state *st) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    return srtp_set_context_state(d->engines[(size_t)srtp_shard_of(ssrc, (int32_t)d->engines.size())], t,
+                                  ssrc, forward, st);
+}
+
+int srtp_dispatch_stats(srtp_dispatch *d, srtp_stats *out) {
+    if (!d || !out) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(d->mu);
+    memset(out, 0, sizeof *out);
+    return each(d, [&](srtp_engine *e) {
+        srtp_stats s;
+        const int rc = srtp_engine_stats(e, &s);
+        if (rc != SRTP_OK) return rc;
+        uint64_t *dst = reinterpret_cast<uint64_t *>(out);
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(&s);
+        for (size_t k = 0; k < sizeof s / sizeof(uint64_t); k++) dst[k] += src[k];
+        return SRTP_OK;
+    });
+}
+
+} // extern "C"

@@ -60,7 +60,12 @@ struct srtp_engine {
     // for it (bundles of one engine share its scratch)
     hipStream_t last_stream = nullptr;
     bool have_last = false;
-    unsigned long long *d_count = nullptr;
+    // recorded on the bundle's stream after each bundle: later bundles on other
+    // streams wait for it on the device, control-plane calls on the host
+    hipEvent_t ev_last = nullptr;
+    unsigned long long *d_count = nullptr; // [2] live / tombstone counts
+    unsigned long long *d_counters = nullptr; // [kCountReplicas][kCtrStride]
+    uint64_t n_bundles = 0, n_packets = 0, n_rehash = 0;
     uint32_t serial = 1;
 
     // staging for srtp_transform_host
@@ -166,8 +171,12 @@ void free_scratch(srtp_engine *e) {
     e->scratch_n = 0;
 }
 
+int quiesce(srtp_engine *e);
+
 int ensure_scratch(srtp_engine *e, uint32_t n) {
     if (n <= e->scratch_n) return SRTP_OK;
+    int qrc = quiesce(e); // the old scratch may still be in use by an enqueued bundle
+    if (qrc != SRTP_OK) return qrc;
     free_scratch(e);
     uint32_t m = std::max<uint32_t>(n, 1024);
     HIPCHK(e, dalloc(&e->p_slot, m));
@@ -241,6 +250,86 @@ struct StageTimer {
     }
 };
 
+// Makes the engine's device current for the duration of one C-ABI call and
+// restores the caller's device afterwards: every allocation, copy, launch and
+// synchronisation of an engine happens on its device whatever the calling
+// thread had current (a JVM thread may drive several engines).
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+#define GUARD(e)                                                                         \
+    DeviceGuard _guard((e)->opts.device);                                                \
+    if (!_guard.ok) return fail((e), SRTP_EDEVICE, "hipSetDevice failed")
+
+// Waits until every bundle this engine has enqueued (on any stream) and its
+// own stream's work have completed: the precondition of every control-plane
+// call that reads or rewrites device state the kernels use.
+int quiesce(srtp_engine *e) {
+    if (e->have_last) HIPCHK(e, hipEventSynchronize(e->ev_last));
+    if (e->stream) HIPCHK(e, hipStreamSynchronize(e->stream));
+    return SRTP_OK;
+}
+
+// Live and tombstone slots of the context table.
+int count_slots(srtp_engine *e, uint64_t *live, uint64_t *tomb) {
+    unsigned long long c[2] = {0, 0};
+    HIPCHK(e, hipMemsetAsync(e->d_count, 0, sizeof c, e->stream));
+    HIPCHK(e, launch_count_contexts(e->d_ctx_keys, e->ctx_cap, e->d_count, e->stream));
+    HIPCHK(e, hipMemcpyAsync(c, e->d_count, sizeof c, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    *live = c[0];
+    *tomb = c[1];
+    return SRTP_OK;
+}
+
+// Rebuilds the context table without tombstones (quiesced engine).  Transformer
+// closes (every DTLS rekey) and abort rollbacks leave tombstones; inserts reuse
+// them, and this keeps probe paths short once they pile up.
+int rehash(srtp_engine *e, uint64_t live) {
+    uint64_t *tk = nullptr;
+    CtxState *tc = nullptr;
+    int rc = SRTP_OK;
+    if (dalloc(&tk, live) != hipSuccess || dalloc(&tc, live) != hipSuccess) {
+        dfree(tk);
+        return fail(e, SRTP_ENOMEM, "rehash scratch");
+    }
+    unsigned long long n = 0;
+    hipStream_t s = e->stream;
+    do {
+        if (hipMemsetAsync(e->d_count, 0, 8, s) != hipSuccess ||
+            launch_rehash_collect(e->d_ctx_keys, e->d_ctx, e->ctx_cap, tk, tc, e->d_count, s) != hipSuccess ||
+            hipMemcpyAsync(&n, e->d_count, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            rc = fail(e, SRTP_EDEVICE, "rehash collect");
+            break;
+        }
+        if (n > live) { rc = fail(e, SRTP_EDEVICE, "rehash: live count changed"); break; }
+        if (hipMemsetAsync(e->d_ctx_keys, 0xff, (size_t)e->ctx_cap * sizeof(uint64_t), s) != hipSuccess ||
+            hipMemsetAsync(e->d_ctx, 0, (size_t)e->ctx_cap * sizeof(CtxState), s) != hipSuccess ||
+            launch_rehash_insert(e->d_ctx_keys, e->d_ctx, e->ctx_cap - 1, tk, tc, (uint32_t)n, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            rc = fail(e, SRTP_EDEVICE, "rehash insert");
+            break;
+        }
+        e->n_rehash++;
+    } while (0);
+    dfree(tk);
+    dfree(tc);
+    return rc;
+}
+
 uint64_t mix64_host(uint64_t x) {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
     x ^= x >> 27; x *= 0x94d049bb133111ebull;
@@ -257,7 +346,7 @@ int srtp_engine_opts_default(srtp_engine_opts *o) {
     o->device = 0;
     o->check_replay = 1;
     o->abort_on_error = 1;
-    o->max_contexts = 1u << 20;
+    o->max_contexts = 1u << 20; // table of next_pow2(2 x max_contexts) slots
     o->max_factories = 1u << 16;
     o->max_transformers = 1u << 16;
     o->max_batch = 1u << 16;
@@ -275,9 +364,11 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
     if (!e) return SRTP_ENOMEM;
     e->opts = o;
     int rc = SRTP_OK;
+    DeviceGuard guard(o.device);
     do {
-        if (hipSetDevice(o.device) != hipSuccess) { rc = SRTP_EDEVICE; break; }
+        if (!guard.ok) { rc = SRTP_EDEVICE; break; }
         if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { rc = SRTP_EDEVICE; break; }
+        if (hipEventCreateWithFlags(&e->ev_last, hipEventDisableTiming) != hipSuccess) { rc = SRTP_EDEVICE; break; }
         uint32_t te0[256];
         aes_te0_le(te0);
         if (upload_tables(te0) != hipSuccess) { rc = SRTP_EDEVICE; break; }
@@ -292,12 +383,14 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
             dalloc(&e->d_ctx_keys, e->ctx_cap) != hipSuccess ||
             dalloc(&e->d_ctx, e->ctx_cap) != hipSuccess ||
             dalloc(&e->e_min, 2 * (size_t)o.max_transformers) != hipSuccess ||
-            dalloc(&e->ctl, 2) != hipSuccess || dalloc(&e->d_count, 1) != hipSuccess) {
+            dalloc(&e->ctl, 2) != hipSuccess || dalloc(&e->d_count, 2) != hipSuccess ||
+            dalloc(&e->d_counters, (size_t)kCountReplicas * kCtrStride) != hipSuccess) {
             rc = SRTP_ENOMEM;
             break;
         }
         if (hipMemset(e->d_ctx_keys, 0xff, (size_t)e->ctx_cap * sizeof(uint64_t)) != hipSuccess ||
-            hipMemset(e->d_ctx, 0, (size_t)e->ctx_cap * sizeof(CtxState)) != hipSuccess) {
+            hipMemset(e->d_ctx, 0, (size_t)e->ctx_cap * sizeof(CtxState)) != hipSuccess ||
+            hipMemset(e->d_counters, 0, sizeof(unsigned long long) * kCountReplicas * kCtrStride) != hipSuccess) {
             rc = SRTP_EDEVICE;
             break;
         }
@@ -313,7 +406,8 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
 
 void srtp_engine_destroy(srtp_engine *e) {
     if (!e) return;
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    DeviceGuard guard(e->opts.device);
+    (void)quiesce(e);
     if (e->d_keysets) // zero session keys before release
         (void)hipMemset(e->d_keysets, 0, (size_t)e->max_keysets * sizeof(KeySet));
     if (e->d_f8keys)
@@ -325,9 +419,10 @@ void srtp_engine_destroy(srtp_engine *e) {
     }
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
     void *ptrs[] = {e->d_keysets, e->d_f8keys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
-                    e->e_min, e->ctl, e->d_count, e->h_seg, e->h_off, e->h_len, e->h_cap,
-                    e->h_flags, e->h_status, e->h_tids};
+                    e->e_min, e->ctl, e->d_count, e->d_counters, e->h_seg, e->h_off, e->h_len,
+                    e->h_cap, e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
+    if (e->ev_last) (void)hipEventDestroy(e->ev_last);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -339,6 +434,7 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
                         const srtp_policy *srtcp_pol, int32_t *out) {
     if (!e || !out || !mk || !ms) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    GUARD(e);
     // NULL-cipher profiles keep a 16-B master key + 14-B salt for the RFC 3711
     // 4.3 PRF (the reference throws there: SURVEY Q15) -- parity unpinned.
     if (key_len < 16 || salt_len < 14 || !policy_ok(srtp_pol, false) || !policy_ok(srtcp_pol, true))
@@ -372,13 +468,16 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
 int srtp_factory_close(srtp_engine *e, int32_t factory) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    GUARD(e);
+    int rc = quiesce(e); // enqueued bundles may still read the factory record
+    if (rc != SRTP_OK) return rc;
     return close_factory_locked(e, factory);
 }
 
 int srtp_transformer_create(srtp_engine *e, int32_t kind, int32_t fwd, int32_t rev, int32_t *out) {
     if (!e || !out) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    GUARD(e);
     if (kind != SRTP_KIND_RTP && kind != SRTP_KIND_RTCP) return fail(e, SRTP_EINVAL, "bad kind");
     if (fwd < 0 || (size_t)fwd >= e->factories.size() || rev < 0 ||
         (size_t)rev >= e->factories.size())
@@ -400,7 +499,9 @@ int srtp_transformer_set_factory(srtp_engine *e, int32_t t, int32_t f, int32_t f
     std::lock_guard<std::mutex> g(e->mu);
     if (t < 0 || (size_t)t >= e->transformers.size() || f < 0 || (size_t)f >= e->factories.size())
         return fail(e, SRTP_EINVAL, "bad id");
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    GUARD(e);
+    int qrc = quiesce(e); // enqueued bundles read the transformer and factory records
+    if (qrc != SRTP_OK) return qrc;
     int32_t &slot = forward ? e->transformers[t].fwd : e->transformers[t].rev;
     if (slot >= 0 && slot != f) {
         int rc = close_factory_locked(e, slot);
@@ -414,9 +515,11 @@ int srtp_transformer_close(srtp_engine *e, int32_t t) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
     if (t < 0 || (size_t)t >= e->transformers.size()) return fail(e, SRTP_EINVAL, "bad id");
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    GUARD(e);
+    int rc = quiesce(e); // enqueued bundles may still walk this transformer's contexts
+    if (rc != SRTP_OK) return rc;
     TransformerRec &tr = e->transformers[t];
-    int rc = close_factory_locked(e, tr.fwd);
+    rc = close_factory_locked(e, tr.fwd);
     if (rc != SRTP_OK) return rc;
     if (tr.rev != tr.fwd) {
         rc = close_factory_locked(e, tr.rev);
@@ -424,6 +527,12 @@ int srtp_transformer_close(srtp_engine *e, int32_t t) {
     }
     HIPCHK(e, launch_remove_transformer(e->d_ctx_keys, e->d_ctx, e->ctx_cap, (uint32_t)t, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    // Tombstones from repeated closes (a DTLS rekey closes the old transformer)
+    // are reused by inserts; rebuild once they hold a quarter of the table.
+    uint64_t live = 0, tomb = 0;
+    rc = count_slots(e, &live, &tomb);
+    if (rc != SRTP_OK) return rc;
+    if (tomb > e->ctx_cap / 4) return rehash(e, live);
     return SRTP_OK;
 }
 
@@ -437,10 +546,9 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         return fail(e, SRTP_EINVAL, "bad transformer id");
     int rc = ensure_scratch(e, n);
     if (rc != SRTP_OK) return rc;
-    if (e->have_last && e->last_stream != s) // scratch still in use on the other stream
-        HIPCHK(e, hipStreamSynchronize(e->last_stream));
-    e->last_stream = s;
-    e->have_last = true;
+    // bundles of one engine share its scratch and run in submission order: a
+    // bundle on another stream than the previous one waits for it on the device
+    if (e->have_last && e->last_stream != s) HIPCHK(e, hipStreamWaitEvent(s, e->ev_last, 0));
     BundleArgs a{};
     a.keysets = e->d_keysets;
     a.f8keys = e->d_f8keys;
@@ -458,6 +566,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.serial = e->serial++;
     static const int debug_mode = getenv("SRTP_DEBUG") ? atoi(getenv("SRTP_DEBUG")) : 0;
     a.debug = debug_mode;
+    a.counters = e->d_counters;
     a.p_slot = e->p_slot; a.sk_in = e->sk_in; a.sk_out = e->sk_out;
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
@@ -510,6 +619,13 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         HIPCHK(e, launch_protect(a, s));
         if (e->n_f8) HIPCHK(e, launch_f8(a, s));
     }
+#ifndef SRTP_DIAG_NO_EVLAST
+    HIPCHK(e, hipEventRecord(e->ev_last, s));
+#endif
+    e->last_stream = s;
+    e->have_last = true;
+    e->n_bundles++;
+    e->n_packets += n;
     return SRTP_OK;
 }
 
@@ -518,7 +634,10 @@ int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, 
                           const uint32_t *flags, int32_t *status, uint32_t n, void *stream) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    hipStream_t s = (hipStream_t)stream; // NULL = the default (null) stream
+    GUARD(e);
+    // NULL = the engine's own stream: every engine gets a hardware queue of its
+    // own, so a send-side and a receive-side engine overlap on the device
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s);
 }
 
@@ -544,8 +663,14 @@ int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, in
     if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
     int vr = validate_regions(e, off, cap, n, seg_bytes);
     if (vr != SRTP_OK) return vr;
+    GUARD(e);
     hipStream_t s = e->stream;
     size_t need = (seg_bytes + 15) & ~(size_t)15;
+    if ((need > e->h_seg_bytes || n > e->h_n) && e->have_last) {
+        // the staging buffers may still be in use by an enqueued bundle
+        int qrc = quiesce(e);
+        if (qrc != SRTP_OK) return qrc;
+    }
     if (need > e->h_seg_bytes) {
         dfree(e->h_seg);
         e->h_seg = nullptr;
@@ -579,8 +704,13 @@ int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, in
     return SRTP_OK;
 }
 
+void *srtp_engine_stream(srtp_engine *e) { return e ? (void *)e->stream : nullptr; }
+
 int srtp_engine_sync(srtp_engine *e, void *stream) {
     if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    GUARD(e);
+    if (!stream) return quiesce(e); // every bundle of this engine, whatever its stream
     HIPCHK(e, hipStreamSynchronize((hipStream_t)stream));
     return SRTP_OK;
 }
@@ -588,7 +718,9 @@ int srtp_engine_sync(srtp_engine *e, void *stream) {
 int srtp_get_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, srtp_ctx_state *out) {
     if (!e || !out) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    HIPCHK(e, hipDeviceSynchronize());
+    GUARD(e);
+    int qrc = quiesce(e);
+    if (qrc != SRTP_OK) return qrc;
     uint64_t key = ((uint64_t)(uint32_t)t << 32) | ssrc;
     uint32_t mask = e->ctx_cap - 1;
     uint32_t h = (uint32_t)mix64_host(key) & mask;
@@ -633,7 +765,9 @@ int srtp_export_contexts(srtp_engine *e, int32_t t, uint32_t *ssrcs, srtp_ctx_st
     if (!e || !count || (max && (!ssrcs || !states))) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
     if (t < 0 || (size_t)t >= e->transformers.size()) return fail(e, SRTP_EINVAL, "bad transformer id");
-    HIPCHK(e, hipDeviceSynchronize());
+    GUARD(e);
+    int qrc = quiesce(e);
+    if (qrc != SRTP_OK) return qrc;
     std::vector<uint64_t> keys(e->ctx_cap);
     std::vector<CtxState> ctx(e->ctx_cap);
     HIPCHK(e, hipMemcpy(keys.data(), e->d_ctx_keys, keys.size() * 8, hipMemcpyDeviceToHost));
@@ -674,7 +808,9 @@ int srtp_set_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, int32_t for
         s.a = st->sent_index; s.b = st->received_index;
     }
     s.birth = 0;
-    HIPCHK(e, hipDeviceSynchronize());
+    GUARD(e);
+    int qrc = quiesce(e);
+    if (qrc != SRTP_OK) return qrc;
     const uint64_t key = ((uint64_t)(uint32_t)t << 32) | ssrc;
     const uint32_t mask = e->ctx_cap - 1;
     uint32_t h = (uint32_t)mix64_host(key) & mask, free_slot = kNoSlot;
@@ -694,14 +830,38 @@ int srtp_set_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, int32_t for
 int64_t srtp_engine_num_contexts(srtp_engine *e) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
-    unsigned long long c = 0;
-    if (hipMemsetAsync(e->d_count, 0, 8, e->stream) != hipSuccess) return SRTP_EDEVICE;
-    if (launch_count_contexts(e->d_ctx_keys, e->ctx_cap, e->d_count, e->stream) != hipSuccess)
-        return SRTP_EDEVICE;
-    if (hipMemcpyAsync(&c, e->d_count, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
-        return SRTP_EDEVICE;
-    if (hipStreamSynchronize(e->stream) != hipSuccess) return SRTP_EDEVICE;
-    return (int64_t)c;
+    GUARD(e);
+    int rc = quiesce(e);
+    if (rc != SRTP_OK) return rc;
+    uint64_t live = 0, tomb = 0;
+    rc = count_slots(e, &live, &tomb);
+    if (rc != SRTP_OK) return rc;
+    return (int64_t)live;
+}
+
+int srtp_engine_stats(srtp_engine *e, srtp_stats *out) {
+    if (!e || !out) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    GUARD(e);
+    int rc = quiesce(e);
+    if (rc != SRTP_OK) return rc;
+    std::vector<unsigned long long> c((size_t)kCountReplicas * kCtrStride);
+    HIPCHK(e, hipMemcpy(c.data(), e->d_counters, c.size() * sizeof(c[0]), hipMemcpyDeviceToHost));
+    uint64_t sum[kCtrStride] = {0};
+    for (int r = 0; r < kCountReplicas; r++)
+        for (int k = 0; k < kCtrStride; k++) sum[k] += c[(size_t)r * kCtrStride + k];
+    memset(out, 0, sizeof *out);
+    out->bundles = e->n_bundles;
+    out->packets = e->n_packets;
+    for (int k = 0; k < SRTP_NUM_STATUS; k++) out->status[k] = sum[kCtrStatus + k];
+    out->roc_rechecks = sum[kCtrRocRecheck];
+    out->repaired = sum[kCtrRepaired];
+    out->ctx_overflow = sum[kCtrOverflow];
+    rc = count_slots(e, &out->ctx_live, &out->ctx_tombstones);
+    if (rc != SRTP_OK) return rc;
+    out->ctx_slots = e->ctx_cap;
+    out->rehashes = e->n_rehash;
+    return SRTP_OK;
 }
 
 int srtp_engine_set_timing(srtp_engine *e, int32_t enable) {
@@ -714,6 +874,7 @@ int srtp_engine_set_timing(srtp_engine *e, int32_t enable) {
 int srtp_engine_read_timing(srtp_engine *e, double *ms, uint64_t *count) {
     if (!e || !ms || !count) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
+    GUARD(e);
     for (int i = 0; i < SRTP_NUM_STAGES; i++) { ms[i] = 0.0; count[i] = 0; }
     for (auto &m : e->marks) {
         HIPCHK(e, hipEventSynchronize(m.b));
@@ -757,6 +918,7 @@ struct srtp_pipeline {
 };
 
 static void pipeline_free(srtp_pipeline *pl) {
+    DeviceGuard guard(pl->e->opts.device);
     for (auto &sl : pl->slots) {
         if (sl.busy && sl.ev_out) (void)hipEventSynchronize(sl.ev_out);
         void *hp[] = {sl.h.seg, sl.h.off, sl.h.len, sl.h.cap, sl.h.flags, sl.h.tids, sl.h.status};
@@ -788,8 +950,8 @@ int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_by
     pl->max_n = max_packets;
     pl->max_seg = (max_seg_bytes + 15) & ~(size_t)15;
     pl->slots.resize((size_t)depth);
-    bool ok = hipSetDevice(e->opts.device) == hipSuccess &&
-              hipStreamCreateWithFlags(&pl->s_in, hipStreamNonBlocking) == hipSuccess &&
+    DeviceGuard guard(e->opts.device);
+    bool ok = guard.ok && hipStreamCreateWithFlags(&pl->s_in, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&pl->s_out, hipStreamNonBlocking) == hipSuccess;
     for (auto &sl : pl->slots) {
         if (!ok) break;
@@ -839,6 +1001,7 @@ int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32
     std::lock_guard<std::mutex> gp(pl->mu);
     srtp_pipeline::Slot &sl = pl->slots[(size_t)slot];
     srtp_engine *e = pl->e;
+    GUARD(e);
     (void)pipeline_wait_locked(pl, sl); // the slot's previous bundle (its status is the caller's)
     if (n > pl->max_n || seg_bytes > pl->max_seg) return fail(e, SRTP_EINVAL, "bundle exceeds the slot");
     if (n == 0) return SRTP_OK;

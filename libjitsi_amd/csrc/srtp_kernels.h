@@ -36,6 +36,7 @@ struct BundleArgs {
     int32_t abort_on_error;
     uint32_t serial;       // bundle serial (context birth stamp)
     int32_t debug;         // diagnostics only (SRTP_DEBUG env): 0 in production
+    unsigned long long *counters; // [kCountReplicas][kCtrStride] cumulative event counters
     // per-bundle scratch
     uint32_t *p_slot;      // [n] context slot of packet p
     uint32_t *sk_in, *sk_out; // [n] sort keys (slot)
@@ -84,8 +85,18 @@ hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 hipError_t launch_f8(const BundleArgs &a, hipStream_t s);
 hipError_t launch_remove_transformer(uint64_t *ctx_keys, CtxState *ctx, uint32_t cap,
                                      uint32_t tid, hipStream_t s);
+// out[0] += live contexts, out[1] += tombstones
 hipError_t launch_count_contexts(const uint64_t *ctx_keys, uint32_t cap, unsigned long long *out,
                                  hipStream_t s);
+// Table rebuild without tombstones: collect the live (key, state) pairs into
+// tmp_keys / tmp_ctx (count in *n_live, which starts at 0), then the caller
+// resets the key array and re-inserts them.
+hipError_t launch_rehash_collect(const uint64_t *ctx_keys, const CtxState *ctx, uint32_t cap,
+                                 uint64_t *tmp_keys, CtxState *tmp_ctx, unsigned long long *n_live,
+                                 hipStream_t s);
+hipError_t launch_rehash_insert(uint64_t *ctx_keys, CtxState *ctx, uint32_t mask,
+                                const uint64_t *tmp_keys, const CtxState *tmp_ctx, uint32_t n,
+                                hipStream_t s);
 // Upload the LE T-table used by the AES rounds (once per device).
 hipError_t upload_tables(const uint32_t te0[256]);
 

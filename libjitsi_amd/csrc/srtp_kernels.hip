@@ -530,31 +530,68 @@ __device__ __forceinline__ int32_t packet_tid(const BundleArgs &a, uint32_t p) {
 }
 
 // ------------------------------------------------------- context hash table
+// Linear probing over (transformer << 32 | SSRC) keys.  A key absent from the
+// table is inserted into the first tombstone of its probe path (slots freed by
+// transformer close or abort rollback), else into the empty slot that ended
+// the path; a lost race for that slot re-probes.  Two lanes inserting the same
+// key see the same path, so the loser finds the winner's key.
 __device__ uint32_t ctx_lookup_insert(const BundleArgs &a, uint64_t key, bool may_create,
                                       uint32_t ks_new, bool *created) {
     *created = false;
-    uint32_t mask = a.ctx_mask;
-    uint32_t h = (uint32_t)mix64(key) & mask;
-    for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
-        uint64_t cur = __hip_atomic_load(&a.ctx_keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == key) return h;
-        if (cur == kEmptyKey) {
-            if (!may_create) return kNoSlot;
-            unsigned long long prev =
-                atomicCAS((unsigned long long *)&a.ctx_keys[h], (unsigned long long)kEmptyKey,
-                          (unsigned long long)key);
-            if (prev == kEmptyKey) {
-                CtxState s;
-                s.ks = ks_new; s.a = 0; s.b = 0; s.g = 0; s.window = 0; s.flags = 0;
-                s.birth = a.serial;
-                a.ctx[h] = s;
-                *created = true;
-                return h;
+    const uint32_t mask = a.ctx_mask;
+    const uint32_t h0 = (uint32_t)mix64(key) & mask;
+    for (int attempt = 0; attempt < 64; attempt++) {
+        uint32_t h = h0, tomb = kNoSlot, target = kNoSlot;
+        for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+            const uint64_t cur =
+                __hip_atomic_load(&a.ctx_keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == key) return h;
+            if (cur == kTombKey) {
+                if (tomb == kNoSlot) tomb = h;
+                continue;
             }
-            if (prev == key) return h;
+            if (cur == kEmptyKey) {
+                target = tomb != kNoSlot ? tomb : h;
+                break;
+            }
         }
+        if (target == kNoSlot) target = tomb; // whole table probed: only tombstones free
+        if (!may_create || target == kNoSlot) return kNoSlot;
+        const uint64_t expect = target == tomb ? kTombKey : kEmptyKey;
+        const unsigned long long prev = atomicCAS((unsigned long long *)&a.ctx_keys[target],
+                                                  (unsigned long long)expect,
+                                                  (unsigned long long)key);
+        if (prev == expect) {
+            CtxState s;
+            s.ks = ks_new; s.a = 0; s.b = 0; s.g = 0; s.window = 0; s.flags = 0;
+            s.birth = a.serial;
+            a.ctx[target] = s;
+            *created = true;
+            return target;
+        }
+        if (prev == key) return target;
+        // another key took the slot: probe again
     }
     return kNoSlot;
+}
+
+// Cumulative event counters: one 64-bit atomic per distinct value among the
+// wave's active lanes (normally one), on the wave's replica of the counters.
+__device__ __forceinline__ void count_event(const BundleArgs &a, bool valid, int idx) {
+#ifdef SRTP_DIAG_NO_COUNT
+    return;
+#endif
+    unsigned long long todo = __ballot(valid);
+    const uint32_t rep =
+        (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (uint32_t)(kCountReplicas - 1);
+    while (todo) {
+        const int lane = __ffsll((long long)todo) - 1;
+        const int v = __builtin_amdgcn_readlane(idx, lane);
+        const unsigned long long m = __ballot(valid && idx == v);
+        if ((int)(threadIdx.x & 63u) == lane)
+            atomicAdd(&a.counters[rep * kCtrStride + v], (unsigned long long)__popcll(m));
+        todo &= ~m;
+    }
 }
 
 // ============================================================== k_parse
@@ -610,7 +647,7 @@ __device__ __forceinline__ uint32_t parse_one(const BundleArgs &a, uint32_t p) {
     bool created;
     uint32_t slot = ctx_lookup_insert(a, key, may_create, ks_new, &created);
     if (slot == kNoSlot) {
-        if (may_create) atomicOr(&a.ctl->overflow, 1u);
+        if (may_create) atomicAdd(&a.counters[kCtrOverflow], 1ull); // table full
         a.w_status[p] = SRTP_STATUS_DROP_NO_CONTEXT;
         return invalid_key;
     }
@@ -951,7 +988,7 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                     rv.mid = a.mid + 5 * (size_t)p;
                     rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
                     ok = reverify_rtp(rv, ks, L, g);
-                    atomicAdd(&a.ctl->n_mismatch, 1u);
+                    atomicAdd(&a.counters[kCtrRocRecheck], 1ull);
                 }
                 if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
             }
@@ -1065,9 +1102,12 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         const uint32_t j = threadIdx.x + k * kWalkBlock;
         if (j < win) {
             const WalkRec r = a.sv_out[base + j];
+            const uint32_t key = a.sk_out[base + j];
             s_rec[j] = r;
-            s_key[j] = a.sk_out[base + j];
-            if (REV) {
+            s_key[j] = key;
+            // only walked records carry a packet index: k_parse leaves the
+            // record of a skipped / invalid packet unwritten (stale scratch)
+            if (REV && key <= a.ctx_mask) {
                 const uint32_t p = r.p & kRecIdxMask;
                 s_g0[j] = a.g0[p];
                 s_ok[j] = a.auth_ok[p];
@@ -1326,7 +1366,9 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     fill_te4(s_te);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
-    const bool todo = finish_status(a, p) == SRTP_STATUS_OK;
+    const int32_t fs = finish_status(a, p);
+    count_event(a, true, kCtrStatus + (fs & 15));
+    const bool todo = fs == SRTP_STATUS_OK;
     const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
@@ -1546,6 +1588,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     if (p < a.n) {
         L0 = (int)a.len[p];
         const int32_t st = finish_status(a, p);
+        count_event(a, true, kCtrStatus + (st & 15));
         const uint32_t slot = a.p_slot[p];
         if (slot != kNoSlot) {
             did = a.spec[p] != 0u;
@@ -1607,7 +1650,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
             store_chunk(pkt, c, span, d);
         }
     });
-    atomicAdd(&a.ctl->n_walk, 1u); // repaired packets (diagnostic)
+    atomicAdd(&a.counters[kCtrRepaired], 1ull);
 }
 
 // ============================================================== k_f8
@@ -1864,9 +1907,42 @@ __global__ void k_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap
 
 __global__ void k_count_contexts(const uint64_t *keys, uint32_t cap, unsigned long long *out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool live = i < cap && keys[i] != kEmptyKey && keys[i] != kTombKey;
-    unsigned long long m = __ballot(live);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(out, (unsigned long long)__popcll(m));
+    const uint64_t k = i < cap ? keys[i] : kEmptyKey;
+    const unsigned long long live = __ballot(k != kEmptyKey && k != kTombKey);
+    const unsigned long long tomb = __ballot(k == kTombKey);
+    if ((threadIdx.x & 63) == 0) {
+        if (live) atomicAdd(&out[0], (unsigned long long)__popcll(live));
+        if (tomb) atomicAdd(&out[1], (unsigned long long)__popcll(tomb));
+    }
+}
+
+__global__ void k_rehash_collect(const uint64_t *keys, const CtxState *ctx, uint32_t cap,
+                                 uint64_t *tmp_keys, CtxState *tmp_ctx, unsigned long long *n_live) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    const uint64_t k = keys[i];
+    if (k == kEmptyKey || k == kTombKey) return;
+    const unsigned long long j = atomicAdd(n_live, 1ull);
+    tmp_keys[j] = k;
+    tmp_ctx[j] = ctx[i];
+}
+
+__global__ void k_rehash_insert(uint64_t *keys, CtxState *ctx, uint32_t mask,
+                                const uint64_t *tmp_keys, const CtxState *tmp_ctx, uint32_t n) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t key = tmp_keys[j];
+    uint32_t h = (uint32_t)mix64(key) & mask;
+    // the table holds fewer live keys than slots: an empty slot exists
+    for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        const unsigned long long prev = atomicCAS((unsigned long long *)&keys[h],
+                                                  (unsigned long long)kEmptyKey,
+                                                  (unsigned long long)key);
+        if (prev == kEmptyKey) {
+            ctx[h] = tmp_ctx[j];
+            return;
+        }
+    }
 }
 
 // ============================================================== launchers
@@ -1910,6 +1986,20 @@ hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap
 hipError_t launch_count_contexts(const uint64_t *keys, uint32_t cap, unsigned long long *out,
                                  hipStream_t s) {
     hipLaunchKernelGGL(k_count_contexts, grid_for(cap), dim3(kBlock), 0, s, keys, cap, out);
+    return hipGetLastError();
+}
+hipError_t launch_rehash_collect(const uint64_t *keys, const CtxState *ctx, uint32_t cap,
+                                 uint64_t *tmp_keys, CtxState *tmp_ctx, unsigned long long *n_live,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_rehash_collect, grid_for(cap), dim3(kBlock), 0, s, keys, ctx, cap, tmp_keys,
+                       tmp_ctx, n_live);
+    return hipGetLastError();
+}
+hipError_t launch_rehash_insert(uint64_t *keys, CtxState *ctx, uint32_t mask, const uint64_t *tmp_keys,
+                                const CtxState *tmp_ctx, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rehash_insert, grid_for(n), dim3(kBlock), 0, s, keys, ctx, mask, tmp_keys,
+                       tmp_ctx, n);
     return hipGetLastError();
 }
 hipError_t upload_tables(const uint32_t te0[256]) {

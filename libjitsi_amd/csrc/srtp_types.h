@@ -78,10 +78,18 @@ constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would thro
 // bundle control block (zeroed per bundle)
 struct BundleCtl {
     uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk
-    uint32_t n_walk;
-    uint32_t n_mismatch;  // unprotect: guessed ROC differed from the verify pass
-    uint32_t overflow;    // context table full
+    uint32_t pad[3];
 };
+
+// Cumulative per-engine event counters (srtp_engine_stats), 64-bit, kept in
+// kCountReplicas copies so that one bundle's wave-aggregated atomics spread
+// over many addresses; the host sums the copies.
+constexpr int kCountReplicas = 64;
+constexpr int kCtrStatus = 0;        // [0, 16): final status counts (SRTP_STATUS_*)
+constexpr int kCtrRocRecheck = 16;   // unprotect tags re-checked under a walk ROC != the speculation
+constexpr int kCtrRepaired = 17;     // packets k_unprotect_fix re-ciphered
+constexpr int kCtrOverflow = 18;     // packets refused a new context (table full)
+constexpr int kCtrStride = 32;       // u64 words per replica (one 256-B line)
 
 // internal walk statuses (beyond SRTP_STATUS_*)
 constexpr int32_t kStPending = 100;

@@ -1,4 +1,5 @@
-"""Host-side SSRC sharding across GPUs.
+"""Host-side SSRC sharding across GPUs, Python view of the
+dispatcher's plan in ``libjitsi_amd/csrc/dispatch.cpp``.
 
 SRTP contexts are independent per (transformer, SSRC) -- SRTPTransformer keeps
 one context per SSRC and nothing else is shared except the read-only factory
@@ -7,41 +8,62 @@ into per-GPU sub-bundles by hashing the SSRC; each GPU owns its shard's
 context state and no collective is needed on the data path.  Packets keep
 their relative order inside a shard, which is all the per-context state
 machine depends on.
+
+``plan`` calls the product's own split (``srtp_dispatch_plan``, C ABI, runs
+without a GPU): the shard of every packet and the phase that reproduces
+SinglePacketTransformer's abort-on-throw across shards.  ``split`` /
+``merge`` are the per-shard index lists and their inverse.
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Sequence
 
 import numpy as np
 
-
-def mix32(x: np.ndarray) -> np.ndarray:
-    """murmur3 fmix32 finaliser (uint32 -> uint32)."""
-    x = np.asarray(x, dtype=np.uint64) & 0xFFFFFFFF
-    x ^= x >> 16
-    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
-    x ^= x >> 13
-    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
-    x ^= x >> 16
-    return x.astype(np.uint32)
+from . import _native as N
 
 
-def packet_ssrc(seg: np.ndarray, off: np.ndarray, rtcp: np.ndarray = None) -> np.ndarray:
-    """RawPacket.getSSRC (bytes 8..11) or getRTCPSSRC (bytes 4..7) per packet."""
-    o = off.astype(np.int64)
-    base = o + 8 if rtcp is None else o + np.where(rtcp, 4, 8)
-    b = [seg[base + k].astype(np.uint32) for k in range(4)]
-    return (b[0] << 24) | (b[1] << 16) | (b[2] << 8) | b[3]
+def shard_of_ssrc(ssrc: int, world: int) -> int:
+    """srtp_shard_of: murmur3 fmix32(SSRC) mod world."""
+    return int(N.lib().srtp_shard_of(int(ssrc) & 0xFFFFFFFF, int(world)))
 
 
-def shard_of(ssrc: np.ndarray, world: int) -> np.ndarray:
-    return (mix32(ssrc) % np.uint32(world)).astype(np.int32)
+def plan(world: int, seg: np.ndarray, off: np.ndarray, length: np.ndarray, cap: np.ndarray,
+         kinds: Sequence[int], tids=0, flags=None, reverse: bool = False,
+         abort_on_error: bool = True, tag_lens: Sequence[int] = (10,)):
+    """(shard[n], phase[n], n_phases) of a bundle, as srtp_dispatch_transform_host
+    splits it.  ``tids`` is one transformer id or one per packet; ``kinds[t]``
+    is transformer t's kind; ``tag_lens`` the tag lengths of the policies in use."""
+    n = len(off)
+    seg = np.ascontiguousarray(seg, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    length = np.ascontiguousarray(length, np.uint32)
+    cap = np.ascontiguousarray(cap, np.uint32)
+    kinds_a = np.ascontiguousarray(kinds, np.int32)
+    fl = None if flags is None else np.ascontiguousarray(flags, np.uint32)
+    if np.isscalar(tids):
+        tids_p, tid0 = None, int(tids)
+    else:
+        tids_a = np.ascontiguousarray(tids, np.int32)
+        tids_p, tid0 = tids_a.ctypes.data, -1
+    mask = 0
+    for t in tag_lens:
+        mask |= 1 << int(t)
+    shard = np.zeros(n, np.int32)
+    phase = np.zeros(n, np.int32)
+    rc = N.lib().srtp_dispatch_plan(int(world), int(abort_on_error), int(reverse),
+                                    kinds_a.ctypes.data, len(kinds_a), mask, tids_p, tid0,
+                                    seg.ctypes.data, seg.nbytes, off.ctypes.data,
+                                    length.ctypes.data, cap.ctypes.data,
+                                    None if fl is None else fl.ctypes.data, n,
+                                    shard.ctypes.data, phase.ctypes.data)
+    N.check(rc, None, "srtp_dispatch_plan")
+    return shard, phase, int(rc)
 
 
-def split(ssrc: np.ndarray, world: int) -> List[np.ndarray]:
+def split(shard: np.ndarray, world: int) -> List[np.ndarray]:
     """Packet indices per shard, each in original (array) order."""
-    sh = shard_of(ssrc, world)
-    return [np.nonzero(sh == r)[0] for r in range(world)]
+    return [np.nonzero(shard == r)[0] for r in range(world)]
 
 
 def merge(parts: List[np.ndarray], idx: List[np.ndarray], n: int) -> np.ndarray:

@@ -189,6 +189,11 @@ class SRTPEngine:
     def sync(self, stream=None):
         N.check(N.lib().srtp_engine_sync(self.h, stream), self.h, "srtp_engine_sync")
 
+    @property
+    def stream_ptr(self) -> int:
+        """hipStream_t of the engine's own stream (transform_device's default)."""
+        return N.lib().srtp_engine_stream(self.h) or 0
+
     def set_timing(self, enable: bool) -> None:
         N.check(N.lib().srtp_engine_set_timing(self.h, int(enable)), self.h, "set_timing")
 
@@ -201,6 +206,37 @@ class SRTPEngine:
 
     def num_contexts(self) -> int:
         return N.check(N.lib().srtp_engine_num_contexts(self.h), self.h, "num_contexts")
+
+    def stats(self) -> dict:
+        """srtp_engine_stats: cumulative per-status counts, ROC re-checks,
+        repairs, context-table occupancy / overflow / rehashes."""
+        st = N.Stats()
+        N.check(N.lib().srtp_engine_stats(self.h, C.byref(st)), self.h, "stats")
+        return st.as_dict()
+
+    # -- control plane used by SRTPContextFactory / SRTPTransformer ----------
+    def _factory_create(self, sender, key, salt, klen, slen, srtp, srtcp) -> int:
+        fid = C.c_int32()
+        rc = N.lib().srtp_factory_create(self.h, int(sender), key, klen, salt, slen, C.byref(srtp),
+                                         C.byref(srtcp), C.byref(fid))
+        N.check(rc, self.h, "SRTPContextFactory")
+        return fid.value
+
+    def _factory_close(self, fid: int) -> None:
+        N.check(N.lib().srtp_factory_close(self.h, fid), self.h, "close")
+
+    def _transformer_create(self, kind: int, fwd: int, rev: int) -> int:
+        tid = C.c_int32()
+        N.check(N.lib().srtp_transformer_create(self.h, kind, fwd, rev, C.byref(tid)), self.h,
+                "transformer_create")
+        return tid.value
+
+    def _transformer_set_factory(self, tid: int, fid: int, forward: bool) -> None:
+        N.check(N.lib().srtp_transformer_set_factory(self.h, tid, fid, int(forward)), self.h,
+                "setFactory")
+
+    def _transformer_close(self, tid: int) -> None:
+        N.check(N.lib().srtp_transformer_close(self.h, tid), self.h, "close")
 
     def context_state(self, transformer: "_SRTPBase", ssrc: int) -> Optional[dict]:
         st = N.CtxState()
@@ -262,7 +298,8 @@ class SRTPEngine:
                          n: Optional[int] = None, stream=None) -> None:
         """Enqueue a bundle whose buffers are device tensors (torch, on this
         engine's GPU).  ``tid`` is an int or an int32 device tensor.  Async on
-        ``stream`` (a torch.cuda.Stream or raw hipStream_t pointer)."""
+        ``stream`` (a torch.cuda.Stream or raw hipStream_t pointer; None = the
+        engine's own stream)."""
         if n is None:
             n = off.numel()
         if np.isscalar(tid):
@@ -276,26 +313,137 @@ class SRTPEngine:
         N.check(rc, self.h, "srtp_transform_device")
 
 
+class SRTPDispatcher:
+    """In-process multi-GPU engine (srtp_dispatch_*, C ABI): one engine per
+    shard on ``devices[i]`` (several shards may share a GPU), each bundle split
+    by SSRC (shard = srtp_shard_of(SSRC)), results identical to one engine.
+    Usable wherever an SRTPEngine is (``engine=`` of SRTPContextFactory)."""
+
+    def __init__(self, devices: Sequence[int], check_replay: bool = True,
+                 abort_on_error: bool = True, max_contexts: int = 1 << 20,
+                 max_factories: int = 1 << 14, max_transformers: int = 1 << 16,
+                 max_batch: int = 1 << 16):
+        L = N.lib()
+        o = N.EngineOpts()
+        L.srtp_engine_opts_default(C.byref(o))
+        o.check_replay, o.abort_on_error = int(check_replay), int(abort_on_error)
+        o.max_contexts, o.max_factories = max_contexts, max_factories
+        o.max_transformers, o.max_batch = max_transformers, max_batch
+        devs = (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        N.check(L.srtp_dispatch_create(devs, len(devices), C.byref(o), C.byref(h)), None,
+                "srtp_dispatch_create")
+        self.h = h
+        self.devices = list(devices)
+
+    @property
+    def shards(self) -> int:
+        return N.lib().srtp_dispatch_num_shards(self.h)
+
+    def shard_of(self, ssrc: int) -> int:
+        return N.lib().srtp_shard_of(ssrc & 0xFFFFFFFF, self.shards)
+
+    def close(self):
+        if self.h:
+            N.lib().srtp_dispatch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        return N.check(rc, None, what, dispatch=self.h)
+
+    def stats(self) -> dict:
+        st = N.Stats()
+        self._chk(N.lib().srtp_dispatch_stats(self.h, C.byref(st)), "stats")
+        return st.as_dict()
+
+    def context_state(self, transformer: "_SRTPBase", ssrc: int) -> Optional[dict]:
+        st = N.CtxState()
+        rc = self._chk(N.lib().srtp_dispatch_get_context_state(self.h, transformer.tid,
+                                                               ssrc & 0xFFFFFFFF, C.byref(st)),
+                       "get_context_state")
+        if rc == 0:
+            return None
+        return {k: getattr(st, k) for k, _ in N.CtxState._fields_}
+
+    def import_context(self, transformer: "_SRTPBase", ssrc: int, state: dict,
+                       forward: bool) -> None:
+        st = N.CtxState(**{k: state.get(k, 0) for k, _ in N.CtxState._fields_})
+        self._chk(N.lib().srtp_dispatch_set_context_state(self.h, transformer.tid, ssrc & 0xFFFFFFFF,
+                                                          int(forward), C.byref(st)),
+                  "import_context")
+
+    def _factory_create(self, sender, key, salt, klen, slen, srtp, srtcp) -> int:
+        fid = C.c_int32()
+        self._chk(N.lib().srtp_dispatch_factory_create(self.h, int(sender), key, klen, salt, slen,
+                                                       C.byref(srtp), C.byref(srtcp), C.byref(fid)),
+                  "SRTPContextFactory")
+        return fid.value
+
+    def _factory_close(self, fid: int) -> None:
+        self._chk(N.lib().srtp_dispatch_factory_close(self.h, fid), "close")
+
+    def _transformer_create(self, kind: int, fwd: int, rev: int) -> int:
+        tid = C.c_int32()
+        self._chk(N.lib().srtp_dispatch_transformer_create(self.h, kind, fwd, rev, C.byref(tid)),
+                  "transformer_create")
+        return tid.value
+
+    def _transformer_set_factory(self, tid: int, fid: int, forward: bool) -> None:
+        self._chk(N.lib().srtp_dispatch_transformer_set_factory(self.h, tid, fid, int(forward)),
+                  "setFactory")
+
+    def _transformer_close(self, tid: int) -> None:
+        self._chk(N.lib().srtp_dispatch_transformer_close(self.h, tid), "close")
+
+    def transform_host(self, reverse: bool, tid, seg: np.ndarray, off: np.ndarray,
+                       length: np.ndarray, cap: np.ndarray, flags=None) -> np.ndarray:
+        """As SRTPEngine.transform_host, split across the shards."""
+        n = len(off)
+        assert seg.dtype == np.uint8 and seg.flags.c_contiguous
+        off = np.ascontiguousarray(off, np.uint32)
+        cap = np.ascontiguousarray(cap, np.uint32)
+        assert length.dtype == np.uint32 and length.flags.c_contiguous and len(length) == n
+        status = np.zeros(n, np.int32)
+        fl = None if flags is None else np.ascontiguousarray(flags, np.uint32)
+        if np.isscalar(tid):
+            tids_p, tid0 = None, int(tid)
+        else:
+            tids = np.ascontiguousarray(tid, np.int32)
+            tids_p, tid0 = tids.ctypes.data, -1
+        rc = N.lib().srtp_dispatch_transform_host(
+            self.h, int(reverse), tids_p, tid0, seg.ctypes.data, seg.nbytes, off.ctypes.data,
+            length.ctypes.data, cap.ctypes.data, None if fl is None else fl.ctypes.data,
+            status.ctypes.data, n)
+        self._chk(rc, "srtp_dispatch_transform_host")
+        return status
+
+
 class SRTPContextFactory:
     """SRTPContextFactory(sender, masterKey, masterSalt, srtpPolicy, srtcpPolicy)."""
 
     def __init__(self, sender: bool, masterKey: bytes, masterSalt: bytes, srtpPolicy: SRTPPolicy,
-                 srtcpPolicy: SRTPPolicy, engine: Optional[SRTPEngine] = None):
+                 srtcpPolicy: SRTPPolicy, engine=None):
         self.engine = engine or SRTPEngine.default()
         key = (C.c_uint8 * len(masterKey)).from_buffer_copy(bytes(masterKey))
         salt = (C.c_uint8 * len(masterSalt)).from_buffer_copy(bytes(masterSalt))
-        fid = C.c_int32()
-        rc = N.lib().srtp_factory_create(self.engine.h, int(sender), key, len(masterKey), salt,
-                                         len(masterSalt), C.byref(srtpPolicy._c()),
-                                         C.byref(srtcpPolicy._c()), C.byref(fid))
-        C.memset(key, 0, len(masterKey))
-        C.memset(salt, 0, len(masterSalt))
-        N.check(rc, self.engine.h, "SRTPContextFactory")
-        self.fid = fid.value
+        try:
+            self.fid = self.engine._factory_create(sender, key, salt, len(masterKey),
+                                                   len(masterSalt), srtpPolicy._c(),
+                                                   srtcpPolicy._c())
+        finally:
+            C.memset(key, 0, len(masterKey))
+            C.memset(salt, 0, len(masterSalt))
         self.sender = sender
+        self.srtpPolicy, self.srtcpPolicy = srtpPolicy, srtcpPolicy
 
     def close(self):
-        N.check(N.lib().srtp_factory_close(self.engine.h, self.fid), self.engine.h, "close")
+        self.engine._factory_close(self.fid)
 
 
 class RawPacket:
@@ -357,10 +505,19 @@ def derive_session_keys(masterKey: bytes, masterSalt: bytes, rtcp: bool = False)
     return bytes(enc), bytes(auth), bytes(salt)
 
 
-def pack(pkts: Sequence[Optional[RawPacket]]):
-    """RawPacket[] -> (seg, off, len, cap, flags).  Each packet region is
-    16-byte aligned, holds the packet's buffer bytes from its offset, and has
-    room for the protect trailer (the in-place form of RawPacket.append/grow)."""
+def pack(pkts: Sequence[Optional[RawPacket]], predicate=None, reverse: bool = False):
+    """RawPacket[] -> (seg, off, len, cap, flags): the marshalling a JNI shim
+    does.  Each packet region is 16-byte aligned and holds the
+    packet's buffer bytes from its offset; ``cap`` is the Java buffer's length
+    after the offset, so RawPacket.isInvalid and the bounds the reference
+    reads against (getHeaderLength's extension field, readRegionToBuff) are the
+    same.  For protect, ``cap`` also leaves room for the trailer (the in-place
+    form of RawPacket.append / grow), so a packet whose header-extension
+    length field lies past its buffer reads the zero padding there instead of
+    throwing (the one protect-side difference from the reference's
+    AIOOBE).  ``None`` elements and packets the predicate rejects are flagged
+    SKIP (SinglePacketTransformer.java:121-216 never hands them to the
+    transformer)."""
     n = len(pkts)
     off = np.zeros(n, np.uint32)
     length = np.zeros(n, np.uint32)
@@ -368,19 +525,20 @@ def pack(pkts: Sequence[Optional[RawPacket]]):
     flags = np.zeros(n, np.uint32)
     pos = 0
     for i, p in enumerate(pkts):
-        if p is None:
+        if p is None or (predicate is not None and not predicate(p)):
             flags[i] = N.PKT_FLAG_SKIP
             cap[i] = 16
         else:
             avail = len(p.buffer) - p.offset
-            cap[i] = max(avail, p.length + TRAILER_ROOM)
+            fits = p.length <= avail
+            cap[i] = max(avail, p.length + TRAILER_ROOM) if fits and not reverse else max(avail, 0)
             length[i] = p.length
             flags[i] = p.flags & (N.PKT_FLAG_DISCARD | N.PKT_FLAG_SILENCE)
         off[i] = pos
         pos += (int(cap[i]) + 15) & ~15
     seg = np.zeros(max(pos, 16), np.uint8)
     for i, p in enumerate(pkts):
-        if p is not None:
+        if p is not None and not (flags[i] & N.PKT_FLAG_SKIP):
             src = np.frombuffer(bytes(p.buffer[p.offset:]), np.uint8)
             seg[off[i]:off[i] + len(src)] = src
     return seg, off, length, cap, flags
@@ -399,24 +557,51 @@ class PacketTransformer:
         raise NotImplementedError
 
 
-def _apply(pkts, seg, off, length, status) -> List[Optional[RawPacket]]:
-    """Write a processed bundle back into the RawPacket[] (in place)."""
+def _apply(pkts, transformers, reverse: bool, seg, off, length, status, flags):
+    """Write a processed bundle back into the RawPacket[] in place, as the
+    reference's per-packet calls leave it:
+
+    * protect, SRTP: RawPacket.append(tag) (RawPacket.java:203-220) -- in place
+      when the buffer has room after the payload, else a new buffer of exactly
+      length + tag at offset 0;
+    * protect, SRTCP: RawPacket.grow(4 + tag) (:885-893) always allocates a new
+      buffer of length + 4 + tag at offset 0 (SRTCPCryptoContext.java:413);
+    * unprotect: decrypted in place and shrunk (RawPacket.shrink :1284-1292),
+      including a packet whose tag check fails before it is dropped;
+    * a drop replaces the element with None (the RawPacket object itself keeps
+      what the reference did to it before returning null);
+    * a packet the reference throws on keeps the mutations made before the
+      throw (e.g. the shrink of authenticatePacket) and stays in the array, the
+      later packets of its transformer are left untouched, and the exception
+      is raised after the whole array was written back
+      (SinglePacketTransformer.java:134-155,190-210)."""
     err = None
     for i, p in enumerate(pkts):
-        if p is None:
+        if p is None or (flags[i] & N.PKT_FLAG_SKIP):
             continue
         st = int(status[i])
         if st in (N.STATUS_SKIPPED, N.STATUS_NOT_PROCESSED):
             continue
-        nl = int(length[i])
+        o, old, nl = int(off[i]), p.length, int(length[i])
+        t = transformers[i]
+        if not reverse and st == N.STATUS_OK and nl != old or (
+                not reverse and st == N.STATUS_OK and t.KIND == N.KIND_RTCP):
+            if t.KIND == N.KIND_RTCP:  # grow(4 + tag): always a fresh buffer
+                pol = t.forwardFactory.srtcpPolicy
+                buf = bytearray(old + 4 + pol.getAuthTagLength())
+                buf[:nl] = seg[o:o + nl].tobytes()
+                p.buffer, p.offset = buf, 0
+            elif nl > len(p.buffer) - p.offset:  # append reallocates
+                p.buffer, p.offset = bytearray(seg[o:o + nl].tobytes()), 0
+            else:
+                p.buffer[p.offset:p.offset + nl] = seg[o:o + nl].tobytes()
+        else:
+            upto = min(old, len(p.buffer) - p.offset)
+            p.buffer[p.offset:p.offset + upto] = seg[o:o + upto].tobytes()
+        p.length = nl
         if st == N.STATUS_ERR_MALFORMED:
             err = err if err is not None else i
-            continue
-        # RawPacket.append may reallocate: the packet gets a fresh buffer
-        p.buffer = bytearray(seg[off[i]:off[i] + nl].tobytes())
-        p.offset = 0
-        p.length = nl
-        if st != N.STATUS_OK:
+        elif st != N.STATUS_OK:
             pkts[i] = None
     if err is not None:
         raise SRTPTransformException(
@@ -428,35 +613,41 @@ class _SRTPBase(PacketTransformer):
     KIND = N.KIND_RTP
 
     def __init__(self, forwardFactory: SRTPContextFactory,
-                 reverseFactory: Optional[SRTPContextFactory] = None):
+                 reverseFactory: Optional[SRTPContextFactory] = None, packetPredicate=None):
         reverseFactory = reverseFactory or forwardFactory
         self.engine = forwardFactory.engine
         self.forwardFactory, self.reverseFactory = forwardFactory, reverseFactory
-        tid = C.c_int32()
-        N.check(N.lib().srtp_transformer_create(self.engine.h, self.KIND, forwardFactory.fid,
-                                                reverseFactory.fid, C.byref(tid)),
-                self.engine.h, type(self).__name__)
-        self.tid = tid.value
+        self.packetPredicate = packetPredicate
+        self.exceptionsInTransform = 0
+        self.exceptionsInReverseTransform = 0
+        self.tid = self.engine._transformer_create(self.KIND, forwardFactory.fid,
+                                                   reverseFactory.fid)
 
     def _set_factory(self, factory: SRTPContextFactory, forward: bool):
-        N.check(N.lib().srtp_transformer_set_factory(self.engine.h, self.tid, factory.fid,
-                                                     int(forward)), self.engine.h, "setFactory")
+        self.engine._transformer_set_factory(self.tid, factory.fid, forward)
         if forward:
             self.forwardFactory = factory
         else:
             self.reverseFactory = factory
 
     def close(self):
-        N.check(N.lib().srtp_transformer_close(self.engine.h, self.tid), self.engine.h, "close")
+        self.engine._transformer_close(self.tid)
 
     def _run(self, pkts, reverse):
         if pkts is None:
             return None
         if len(pkts) == 0:
             return pkts
-        seg, off, length, cap, flags = pack(pkts)
+        seg, off, length, cap, flags = pack(pkts, self.packetPredicate, reverse)
         status = self.engine.transform_host(reverse, self.tid, seg, off, length, cap, flags)
-        return _apply(pkts, seg, off, length, status)
+        try:
+            return _apply(pkts, [self] * len(pkts), reverse, seg, off, length, status, flags)
+        except SRTPTransformException:
+            if reverse:
+                self.exceptionsInReverseTransform += 1
+            else:
+                self.exceptionsInTransform += 1
+            raise
 
     def transform(self, pkts):
         return self._run(pkts, False)
@@ -492,9 +683,13 @@ class SRTCPTransformer(_SRTPBase):
 def transform_bundle(transformers: Sequence[Optional[_SRTPBase]], pkts, reverse: bool):
     """Process packets of many transformers in one GPU bundle (the batching the
     reference's 1-element arrays cannot express).  Equivalent to calling each
-    transformer's transform()/reverseTransform() on its packets in order."""
+    transformer's transform()/reverseTransform() on its packets in order; a
+    throw aborts the later packets of that transformer only, and is raised
+    once every packet was written back."""
     eng = next(t for t in transformers if t is not None).engine
-    seg, off, length, cap, flags = pack(pkts)
+    pkts = list(pkts)
+    masked = [p if t is not None else None for p, t in zip(pkts, transformers)]
+    seg, off, length, cap, flags = pack(masked, reverse=reverse)
     tids = np.array([t.tid if t is not None else -1 for t in transformers], np.int32)
     status = eng.transform_host(reverse, tids, seg, off, length, cap, flags)
-    return _apply(list(pkts), seg, off, length, status), status
+    return _apply(pkts, list(transformers), reverse, seg, off, length, status, flags), status

@@ -102,6 +102,42 @@ def rtp_bundle(n_packets: int, n_ssrc: int, pkt_len, seed: int, pt: int = 96,
                   {"ssrcs": ssrcs, "seq0": seq0, "seed": seed})
 
 
+def rtp_bundle_skewed(n_packets: int, n_ssrc: int, pkt_len, seed: int, zipf_s: float = 1.1,
+                      pt: int = 96, ts_step: int = 3000) -> Bundle:
+    """RTP packets whose SSRCs follow a Zipf(zipf_s) popularity over n_ssrc
+    streams (rank r has weight 1 / r^s), in random interleaving; each SSRC's
+    packets carry consecutive sequence numbers in bundle order.  meta["counts"]
+    holds each packet's SSRC's packet count in the bundle (the per-bundle
+    sequence advance)."""
+    rng = np.random.default_rng(seed)
+    ssrcs = distinct_u32(rng, n_ssrc)
+    w = 1.0 / np.arange(1, n_ssrc + 1, dtype=np.float64) ** zipf_s
+    s = rng.choice(n_ssrc, size=n_packets, p=w / w.sum())
+    seq0 = rng.integers(0, 65536, n_ssrc, dtype=np.uint32)
+    order = np.argsort(s, kind="stable")
+    rank = np.empty(n_packets, np.int64)
+    counts = np.bincount(s, minlength=n_ssrc)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    rank[order] = np.arange(n_packets) - np.repeat(starts, counts)
+    seq = ((seq0[s].astype(np.int64) + rank) & 0xFFFF).astype(np.uint32)
+    length = (np.full(n_packets, pkt_len, np.uint32) if not isinstance(pkt_len, tuple) else
+              rng.integers(pkt_len[0], pkt_len[1] + 1, n_packets, dtype=np.int64).astype(np.uint32))
+    off, cap, total = layout(length)
+    seg = rng.integers(0, 256, total, dtype=np.uint8)
+    o = off.astype(np.int64)
+    seg[o] = 0x80
+    seg[o + 1] = pt & 0x7F
+    seg[o + 2] = (seq >> 8).astype(np.uint8)
+    seg[o + 3] = (seq & 0xFF).astype(np.uint8)
+    ts = (seq.astype(np.uint64) * ts_step) & 0xFFFFFFFF
+    for k in range(4):
+        seg[o + 4 + k] = ((ts >> (24 - 8 * k)) & 0xFF).astype(np.uint8)
+        seg[o + 8 + k] = ((ssrcs[s] >> (24 - 8 * k)) & 0xFF).astype(np.uint8)
+    return Bundle(seg, off, length, cap, np.zeros(n_packets, np.uint32), ssrcs[s].copy(), seq,
+                  {"ssrcs": ssrcs, "seq0": seq0, "seed": seed, "counts": counts[s].astype(np.int64),
+                   "zipf_s": zipf_s})
+
+
 def rtcp_bundle(n_packets: int, n_ssrc: int, len_range=(28, 200), seed: int = 0,
                 ssrcs=None) -> Bundle:
     """RTCP SR/RR-shaped packets (V=2, PT 200/201, length field), random body."""

@@ -75,6 +75,9 @@ def lib():
         L.orc_hmac_sha1.argtypes = [u8p, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_derive_keys.argtypes = [u8p, u8p, C.c_int, u8p, u8p, u8p]
         L.orc_aes_f8.argtypes = [u8p, u8p, C.c_int, u8p, u8p, C.c_int]
+        L.orc_bench_round_trips.restype = C.c_int64
+        L.orc_bench_round_trips.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
+                                            C.c_uint32, C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -118,6 +121,17 @@ def aes_f8(key: bytes, salt: bytes, iv: bytes, data: bytes) -> bytes:
     d, dp = _u8(data if data else b"\0")
     lib().orc_aes_f8(kp, sp, len(salt), ip, dp, len(data))
     return d.tobytes()[:len(data)]
+
+
+def bench_round_trips(mode: int, threads: int, seconds: float, pkt_len: int, ssrcs: int,
+                      seed: int = 0x5EED0002):
+    """(packets protected+unprotected, wall seconds) of the pinned C timing
+    loop (oracle_bench.c)."""
+    el = C.c_double()
+    n = lib().orc_bench_round_trips(mode, threads, seconds, pkt_len, ssrcs, seed, C.byref(el))
+    if n < 0:
+        raise RuntimeError("oracle benchmark rejected a packet")
+    return int(n), el.value
 
 
 def set_check_replay(enabled: bool) -> None:

@@ -1,0 +1,165 @@
+"""GPU: the in-process multi-GPU dispatcher (srtp_dispatch_*).
+
+One process drives G engines -- one per GPU in production, G engines on
+device 0 here when the box has one GPU -- and every bundle is split by SSRC
+across them.  Each scenario runs through the dispatcher and through the oracle
+on identical bytes and must agree on every status, length, segment byte and
+context state (tests/harness.py), exactly as a single engine does: the
+dispatcher must be invisible.  Also: calls from a non-main host thread, the
+cross-shard abort-on-throw phases, stats summed over shards, and (with >= 2
+GPUs) engines on devices 0 and 1 driven from a thread whose current device is
+another one.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from libjitsi_amd import SRTPDispatcher, profile_policies, synth
+from libjitsi_amd import _native as N
+from oracle import oracle as O
+
+import test_gpu_parity as G
+from harness import Twin
+
+pytestmark = pytest.mark.gpu
+P80 = profile_policies("AES_CM_128_HMAC_SHA1_80")
+
+
+def _gpus():
+    import torch
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+@pytest.fixture(params=[2, 4], ids=["G2", "G4"])
+def dtwin(request, oracle):
+    if _gpus() < 1:
+        pytest.skip("no GPU visible")
+    d = SRTPDispatcher([0] * request.param, max_contexts=1 << 15, max_factories=256,
+                       max_transformers=1024)
+    yield Twin(d)
+    d.close()
+
+
+def test_dispatch_round_trips_and_configs(dtwin):
+    """C1 (one SSRC, seq wrap), C2 (1200 B), C3 (faults), C4 (SRTP+SRTCP,
+    three profiles, SDES and DTLS rekeys) through the dispatcher."""
+    G.test_config1_single_ssrc_160B_with_wrap(dtwin)
+    G.test_config2_video_1200B(dtwin)
+    G.test_config3_mixed_sizes_unprotect_with_faults(dtwin)
+    G.test_config4_srtp_srtcp_mixed_rekey(dtwin)
+    G.test_discard_silence_flags_skip_decrypt(dtwin)
+    G.test_roc_guess_overturned_by_walk(dtwin)
+    G.test_many_transformers_one_bundle(dtwin)
+    G.test_factory_close_no_new_contexts(dtwin)
+    G.test_capacity_and_skip(dtwin)
+
+
+def test_dispatch_every_ssrc_lands_on_its_shard(dtwin):
+    d = dtwin.engine
+    (k, s), = synth.keys(71, 1)
+    f = dtwin.factory(True, k, s, *P80)
+    t = dtwin.transformer(O.KIND_RTP, f)
+    b = synth.rtp_bundle(4000, 300, (60, 800), seed=72)
+    dtwin.run(t, False, b.seg, b.off, b.length, b.cap)
+    counts = [N.lib().srtp_engine_num_contexts(N.lib().srtp_dispatch_engine(d.h, i))
+              for i in range(d.shards)]
+    want = np.bincount([d.shard_of(int(x)) for x in b.meta["ssrcs"]], minlength=d.shards)
+    assert counts == want.tolist() and min(counts) > 0
+    st = d.stats()
+    assert st["status"]["OK"] == b.n and st["ctx_live"] == 300
+
+
+@pytest.mark.parametrize("abort", [True, False])
+def test_dispatch_malformed_abort_across_shards(oracle, abort):
+    """A throw on one shard aborts the same transformer's later packets on the
+    other shards (SinglePacketTransformer.java:134-155); other transformers
+    carry on.  Two transformers interleaved, malformed packets in both."""
+    if _gpus() < 1:
+        pytest.skip("no GPU visible")
+    d = SRTPDispatcher([0, 0, 0], abort_on_error=abort, max_contexts=4096, max_factories=64,
+                       max_transformers=64)
+    try:
+        twin = Twin(d)
+        (k, s), = synth.keys(12, 1)
+        f, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+        ts = [twin.transformer(O.KIND_RTP, f), twin.transformer(O.KIND_RTP, f)]
+        rs = [twin.transformer(O.KIND_RTP, fr), twin.transformer(O.KIND_RTP, fr)]
+        b = synth.rtp_bundle(600, 31, (40, 700), seed=73)
+        who = (np.arange(b.n) % 3 == 1).astype(int)
+        o = b.off.astype(np.int64)
+        for i in (100, 250, 430):  # CC=15 with X: the header length runs past the packet
+            b.seg[o[i]] = 0x9F
+        b.seg[o[31]] = 0x8F  # CC=15 without X on a 40-B packet: negative payload length
+        b.length[31] = 40
+        seg, ln, st = twin.run([ts[w] for w in who], False, b.seg, b.off, b.length, b.cap,
+                               abort_on_error=abort)
+        assert (st == N.STATUS_ERR_MALFORMED).any()
+        if abort:
+            assert (st == N.STATUS_NOT_PROCESSED).any()
+        twin.run([rs[w] for w in who], True, seg, b.off, ln, b.cap, abort_on_error=abort)
+        # SRTCP: index offset < 0 throws before auth
+        tc = twin.transformer(O.KIND_RTCP, fr)
+        cb = synth.rtcp_bundle(40, 6, len_range=(12, 40), seed=74)
+        twin.run(tc, True, cb.seg, cb.off, cb.length, cb.cap, abort_on_error=abort)
+    finally:
+        d.close()
+
+
+def test_dispatch_from_a_worker_thread(dtwin):
+    """The engines are driven from a host thread that is not the one that
+    created them (a JVM send or receive thread)."""
+    (k, s), = synth.keys(75, 1)
+    fs, fr = dtwin.factory(True, k, s, *P80), dtwin.factory(False, k, s, *P80)
+    snd, rcv = dtwin.transformer(O.KIND_RTP, fs), dtwin.transformer(O.KIND_RTP, fr)
+    b = synth.rtp_bundle(5000, 200, (60, 1400), seed=76)
+    err = []
+
+    def body():
+        try:
+            seg, ln, st = dtwin.run(snd, False, b.seg, b.off, b.length, b.cap)
+            dtwin.run(rcv, True, seg, b.off, ln, b.cap)
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the main thread
+            err.append(e)
+
+    th = threading.Thread(target=body)
+    th.start()
+    th.join(120)
+    assert not th.is_alive()
+    if err:
+        raise err[0]
+
+
+def test_dispatch_two_gpus_other_current_device(oracle):
+    """Engines on devices 0 and 1, driven from a thread whose current device
+    is the last GPU: every allocation and launch must still land on the
+    engine's own device (the C ABI's device guard)."""
+    n = _gpus()
+    if n < 2:
+        pytest.skip("needs two GPUs")
+    import torch
+    d = SRTPDispatcher([0, 1], max_contexts=4096, max_factories=64, max_transformers=64)
+    try:
+        twin = Twin(d)
+        (k, s), = synth.keys(77, 1)
+        fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+        snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+        b = synth.rtp_bundle(3000, 100, (60, 1400), seed=78)
+        err = []
+
+        def body():
+            try:
+                torch.cuda.set_device(n - 1)
+                seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+                twin.run(rcv, True, seg, b.off, ln, b.cap)
+                assert torch.cuda.current_device() == n - 1
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+
+        th = threading.Thread(target=body)
+        th.start()
+        th.join(120)
+        if err:
+            raise err[0]
+    finally:
+        d.close()
