@@ -44,7 +44,7 @@ struct srtp_engine {
     WalkRec *sv_in = nullptr, *sv_out = nullptr;
     int32_t *w_status = nullptr;
     uint32_t *w_cw = nullptr, *w_len = nullptr, *g0 = nullptr, *auth_ok = nullptr, *mid = nullptr;
-    uint32_t *tailc = nullptr, *spec = nullptr;
+    uint32_t *tailc = nullptr, *spec = nullptr, *long_list = nullptr;
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     // Two control blocks (BundleCtl + e_min row), alternating per bundle: each
@@ -161,12 +161,14 @@ uint32_t next_pow2(uint64_t x) {
 
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
-                    e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp};
+                    e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp,
+                    e->long_list};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
     e->w_status = nullptr;
     e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
+    e->long_list = nullptr;
     e->sort_temp = nullptr;
     e->scratch_n = 0;
 }
@@ -192,6 +194,7 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->mid, (size_t)5 * m));
     HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
     HIPCHK(e, dalloc(&e->spec, m));
+    HIPCHK(e, dalloc(&e->long_list, m / 256 + 2)); // at most one long chain per walk span
     e->sort_temp_bytes = sort_temp_bytes(m);
     HIPCHK(e, hipMalloc(&e->sort_temp, std::max<size_t>(e->sort_temp_bytes, 16)));
     // per-tile digit counts start at zero (each scan re-zeroes what it read)
@@ -571,7 +574,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
     a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
-    a.tailc = e->tailc; a.spec = e->spec;
+    a.tailc = e->tailc; a.spec = e->spec; a.long_list = e->long_list;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     a.sort_counts = ss.counts[0];
@@ -607,8 +610,10 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     {
         StageTimer t(e, s, SRTP_STAGE_WALK);
         HIPCHK(e, launch_walk(a, 0, s));
-        // the limit pass only runs with abort-on-throw (k_walk returns at once otherwise)
-        if (a.abort_on_error) HIPCHK(e, launch_walk(a, 1, s));
+        // second pass: abort-on-throw's limit pass when a packet may throw,
+        // else the wave-parallel walk of context chains longer than the
+        // first pass's window (returns at once when there are none)
+        HIPCHK(e, launch_walk(a, 1, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
@@ -619,9 +624,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         HIPCHK(e, launch_protect(a, s));
         if (e->n_f8) HIPCHK(e, launch_f8(a, s));
     }
-#ifndef SRTP_DIAG_NO_EVLAST
     HIPCHK(e, hipEventRecord(e->ev_last, s));
-#endif
     e->last_stream = s;
     e->have_last = true;
     e->n_bundles++;

@@ -45,10 +45,12 @@ struct BundleArgs {
     uint32_t *w_cw;        // [n] guessed ROC / SRTCP index word
     uint32_t *w_len;       // [n] length after processing
     uint32_t *g0;          // [n] unprotect: ROC the verify pass assumed
-    uint32_t *auth_ok;     // [n] unprotect: tag matched under g0
+    uint32_t *auth_ok;     // [n] unprotect: bit 0 tag matched under g0; bit 2: also checked
+                           // under g0 - 1, bit 1 its result
     uint32_t *mid;         // [5n] unprotect: inner SHA-1 state before the ROC block
     uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
     uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
+    uint32_t *long_list;   // [n / 256 + 2] sorted start index of each long context chain
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse
     int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse

@@ -71,6 +71,7 @@ __device__ __forceinline__ int64_t java_lshl(int64_t v, int64_t n) {
 // address is one v_perm_b32 of the state word and a per-lane base
 // (byte 1 <- state byte k, bytes 0 and 2 <- base).
 constexpr int kTeWords = 32768;  // 128 KB
+constexpr int kTeCounters = 16;  // per-workgroup status counts, after the image (which stays at LDS 0)
 constexpr int kAesBlock = 1024;  // threads per workgroup of the AES kernels (1 WG per CU)
 #ifndef SRTP_UNPROTECT_BLOCK
 #define SRTP_UNPROTECT_BLOCK 1024
@@ -575,25 +576,6 @@ __device__ uint32_t ctx_lookup_insert(const BundleArgs &a, uint64_t key, bool ma
     return kNoSlot;
 }
 
-// Cumulative event counters: one 64-bit atomic per distinct value among the
-// wave's active lanes (normally one), on the wave's replica of the counters.
-__device__ __forceinline__ void count_event(const BundleArgs &a, bool valid, int idx) {
-#ifdef SRTP_DIAG_NO_COUNT
-    return;
-#endif
-    unsigned long long todo = __ballot(valid);
-    const uint32_t rep =
-        (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (uint32_t)(kCountReplicas - 1);
-    while (todo) {
-        const int lane = __ffsll((long long)todo) - 1;
-        const int v = __builtin_amdgcn_readlane(idx, lane);
-        const unsigned long long m = __ballot(valid && idx == v);
-        if ((int)(threadIdx.x & 63u) == lane)
-            atomicAdd(&a.counters[rep * kCtrStride + v], (unsigned long long)__popcll(m));
-        todo &= ~m;
-    }
-}
-
 // ============================================================== k_parse
 // Returns the packet's sort key: its context slot, or ctx_mask + 1 when the
 // packet is not walked (skipped, invalid, dropped before the state machine).
@@ -981,7 +963,9 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                 a.w_len[p] = (uint32_t)newL;
                 bool ok;
                 if ((uint32_t)g == g0) {
-                    ok = auth_ok != 0;
+                    ok = (auth_ok & 1u) != 0;
+                } else if ((auth_ok & 4u) && (uint32_t)g == g0 - 1u) {
+                    ok = (auth_ok & 2u) != 0; // checked by the verify pass too
                 } else {
                     ReverifyArgs rv;
                     rv.pkt = a.seg + a.off[p];
@@ -1037,7 +1021,7 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
             if (c.auth != SRTP_NULL_AUTHENTICATION) {
                 newL = L - T - 4 > 0 ? L - T - 4 : 0;
                 a.w_len[p] = (uint32_t)newL;
-                if (!auth_ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
+                if (!(auth_ok & 1u)) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
             }
             if (decrypt && c.enc == SRTP_AESCM_ENCRYPTION && newL - 8 < 0) threw = true;
             if (!threw) {
@@ -1060,6 +1044,230 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
     }
     a.w_status[p] = SRTP_STATUS_OK;
     return true;
+}
+
+// ----------------------------------------------------- wave-parallel walk
+// A context chain longer than k_walk's LDS window (a skewed bundle: a few
+// SSRCs carry most packets) is walked by a whole wave, 256 records per step,
+// by speculating that every packet is the context's new highest index -- the
+// steady state of an in-order stream.  Under that assumption each packet's
+// guessed ROC (guessIndex, SRTPCryptoContext.java:457-475) depends only on
+// the previous packet's sequence number: roc_k = roc + sum of the wrap steps
+// d_j in {-1, 0, +1} of the packets before it, a prefix sum.  A packet keeps
+// the speculation when it is that new maximum (delta > 0: checkReplay
+// accepts, update :719-744 makes it s_l, and with d = +1 the new ROC), it
+// authenticates under its ROC (unprotect: the verify pass's result when its
+// guess was the same, else the midstate re-check), fits its capacity and does
+// not throw.  Every packet before the first one that breaks it is committed
+// in parallel; the replay window after them is the old window shifted by the
+// Java-masked distances (delta & 63, :730) of all of them, OR one bit per
+// packet at the masked distance of the packets after it (suffix sums).  The
+// breaking packet goes through walk_one, exactly as the serial walk, and the
+// speculation resumes after it.  SRTCP chains are walked serially.
+constexpr int kLongPer = 4;                      // records per lane per step
+constexpr int kLongStep = 64 * kLongPer;         // records per wave step
+
+__device__ __forceinline__ int32_t wave_excl_scan(int32_t x) {
+    const int lane = (int)(threadIdx.x & 63u);
+    int32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    return inc - x;
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        lo |= (uint32_t)__shfl_xor((int)lo, o, 64);
+        hi |= (uint32_t)__shfl_xor((int)hi, o, 64);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void bcast_state(CtxState &st) {
+    st.a = __builtin_amdgcn_readfirstlane(st.a);
+    st.b = __builtin_amdgcn_readfirstlane(st.b);
+    st.g = __builtin_amdgcn_readfirstlane(st.g);
+    st.flags = (uint32_t)__builtin_amdgcn_readfirstlane((int)st.flags);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)st.window);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(st.window >> 32));
+    st.window = ((uint64_t)hi << 32) | lo;
+}
+
+// LDS of the second k_walk pass when it walks long chains (the first pass's
+// staging arrays, unused then): one step's records and per-record results.
+struct LongLds {
+    WalkRec *rec;     // [kLongStep] the step's records, block order
+    uint32_t *roc;    // [kLongStep] guessed ROC under the speculation
+    uint32_t *g0;     // [kLongStep] unprotect: the verify pass's ROC
+    uint32_t *ok;     // [kLongStep] unprotect: the verify pass's auth bits
+    uint32_t *info;   // [kLongStep] bit 0: keeps the speculation; bits 1..: delta & 63
+};
+
+template <bool REV>
+__device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t key = a.sk_out[i0];
+    const uint32_t slot = key;
+    CtxState st = a.ctx[slot];
+    const KeySet *ks = a.keysets + st.ks;
+    WalkCtx c;
+    c.enc = ks->enc_type; c.auth = ks->auth_type; c.T = ks->tag_len; c.kind = ks->kind;
+    c.check_replay = a.check_replay != 0;
+    c.reverse = REV;
+    const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
+    const bool mac = c.auth != SRTP_NULL_AUTHENTICATION;
+    uint32_t i = i0;
+    for (;;) {
+        // stage the step's records (coalesced), count the chain's
+        int nv = 0;
+#pragma unroll
+        for (int k = 0; k < kLongPer; k++) {
+            const int j = lane + 64 * k;
+            const uint32_t idx = i + (uint32_t)j;
+            const bool v = idx < a.n && a.sk_out[idx] == key;
+            WalkRec r = WalkRec{0u, 0u, 0u, 0};
+            if (v) r = a.sv_out[idx];
+            sm.rec[j] = r;
+            if (REV) {
+                const uint32_t p = r.p & kRecIdxMask;
+                sm.g0[j] = v ? a.g0[p] : 0u;
+                sm.ok[j] = v ? a.auth_ok[p] : 0u;
+            }
+            nv += v ? 1 : 0;
+        }
+        const int nvalid = (int)__reduce_add_sync(~0ull, (unsigned)nv); // a prefix of the step
+        __syncthreads();
+        if (nvalid == 0) break;
+        int f = 0; // block position of the first packet that breaks the speculation
+        if (c.kind == SRTP_KIND_RTP && (st.flags & 1u)) {
+            // lane l owns block positions [4l, 4l + 4): wrap steps, their sum
+            const int p0 = lane * kLongPer;
+            int32_t lsum = 0;
+#pragma unroll 1
+            for (int r = 0; r < kLongPer; r++) {
+                const int pos = p0 + r;
+                if (pos >= nvalid) break;
+                const int32_t seq = (int32_t)(sm.rec[pos].word & 0xffffu);
+                const int32_t sl = pos ? (int32_t)(sm.rec[pos - 1].word & 0xffffu) : st.b;
+                int32_t d;
+                if (sl < 32768) d = (seq - sl > 32768) ? -1 : 0;
+                else d = (sl - 32768 > seq) ? 1 : 0;
+                lsum += d;
+            }
+            uint32_t roc = (uint32_t)st.a + (uint32_t)wave_excl_scan(lsum); // ROC before the lane
+            int first_bad = kLongPer;
+#pragma unroll 1
+            for (int r = 0; r < kLongPer; r++) {
+                const int pos = p0 + r;
+                if (pos >= nvalid) { first_bad = min(first_bad, r); break; }
+                const WalkRec rec = sm.rec[pos];
+                const int32_t seq = (int32_t)(rec.word & 0xffffu);
+                const int32_t sl = pos ? (int32_t)(sm.rec[pos - 1].word & 0xffffu) : st.b;
+                const uint32_t roc_prev = roc;
+                int32_t d;
+                if (sl < 32768) d = (seq - sl > 32768) ? -1 : 0;
+                else d = (sl - 32768 > seq) ? 1 : 0;
+                roc += (uint32_t)d;
+                const int64_t delta = (java_lshl((int64_t)(int32_t)roc, 16) | (int64_t)seq) -
+                                      (java_lshl((int64_t)(int32_t)roc_prev, 16) | (int64_t)sl);
+                const int L = (int)(rec.lc & 0xffffu), C = (int)(rec.lc >> 16);
+                bool g = delta > 0;
+                if (REV) {
+                    const int newL = mac ? (L - c.T > 0 ? L - c.T : 0) : L;
+                    if (!(rec.p & kRecSkipDec)) g = g && !enc_would_throw(c.enc, rec.h, newL - rec.h);
+                    if (g && mac) { // the tag under this ROC
+                        const uint32_t g0 = sm.g0[pos], okb = sm.ok[pos];
+                        if (roc == g0) {
+                            g = (okb & 1u) != 0u;
+                        } else if ((okb & 4u) && roc == g0 - 1u) {
+                            g = (okb & 2u) != 0u;
+                        } else {
+                            const uint32_t p = rec.p & kRecIdxMask;
+                            ReverifyArgs rv;
+                            rv.pkt = a.seg + a.off[p];
+                            rv.mid = a.mid + 5 * (size_t)p;
+                            rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
+                            g = reverify_rtp(rv, ks, L, (int32_t)roc);
+                        }
+                    }
+                } else {
+                    g = g && L + (mac ? c.T : 0) <= C && !enc_would_throw(c.enc, rec.h, L - rec.h);
+                }
+                sm.roc[pos] = roc;
+                sm.info[pos] = (g ? 1u : 0u) | ((uint32_t)((uint64_t)delta & 63u) << 1);
+                if (!g) { first_bad = r; break; }
+            }
+            const unsigned long long bad_lanes = __ballot(first_bad < kLongPer);
+            f = nvalid;
+            if (bad_lanes) {
+                const int bl = __ffsll((long long)bad_lanes) - 1;
+                f = min(f, bl * kLongPer + __builtin_amdgcn_readlane(first_bad, bl));
+            }
+            // commit block positions [0, f)
+            int32_t dsum = 0;
+            uint32_t recheck = 0u;
+#pragma unroll 1
+            for (int r = 0; r < kLongPer; r++) {
+                const int pos = p0 + r;
+                if (pos >= f) break;
+                const WalkRec rec = sm.rec[pos];
+                const uint32_t p = rec.p & kRecIdxMask;
+                const int L = (int)(rec.lc & 0xffffu);
+                const uint32_t rr = sm.roc[pos];
+                a.w_cw[p] = rr;
+                a.w_len[p] = (uint32_t)(REV ? (mac ? (L - c.T > 0 ? L - c.T : 0) : L) : L + (mac ? c.T : 0));
+                a.w_status[p] = SRTP_STATUS_OK;
+                if (REV && mac) {
+                    const uint32_t g0 = sm.g0[pos], okb = sm.ok[pos];
+                    if (rr != g0 && !((okb & 4u) && rr == g0 - 1u)) recheck++;
+                }
+                dsum += (int32_t)(sm.info[pos] >> 1);
+            }
+            if (f > 0) {
+                // masked shift distances after each committed packet (suffix sums)
+                const int32_t total = (int32_t)__reduce_add_sync(~0ull, (unsigned)dsum);
+                int32_t after = total - wave_excl_scan(dsum);
+                uint64_t bits = 0ull;
+#pragma unroll 1
+                for (int r = 0; r < kLongPer; r++) {
+                    const int pos = p0 + r;
+                    if (pos >= f) break;
+                    after -= (int32_t)(sm.info[pos] >> 1);
+                    if (after < 64) bits |= 1ull << after;
+                }
+                bits = wave_or64(bits);
+                st.window = (total < 64 ? st.window << total : 0ull) | bits;
+                st.a = (int32_t)sm.roc[f - 1];
+                st.b = (int32_t)(sm.rec[f - 1].word & 0xffffu);
+                st.g = st.a;
+                const uint32_t rc = (uint32_t)__reduce_add_sync(~0ull, recheck);
+                if (lane == 0 && rc) atomicAdd(&a.counters[kCtrRocRecheck], (unsigned long long)rc);
+            }
+        }
+        if (f < nvalid) { // the breaking packet (or every SRTCP packet): exactly as the serial walk
+            const int stop = c.kind == SRTP_KIND_RTP ? f + 1 : nvalid;
+            if (lane == 0) {
+                for (int k = f; k < stop; k++) {
+                    const WalkRec r = sm.rec[k];
+                    uint32_t g0 = 0u, ok = 0u;
+                    if (REV) { g0 = sm.g0[k]; ok = sm.ok[k]; }
+                    (void)walk_one(a, ks, c, st, r, g0, ok, false, tid);
+                }
+            }
+            bcast_state(st);
+            i += (uint32_t)stop;
+        } else {
+            i += (uint32_t)nvalid;
+        }
+        __syncthreads(); // the step's LDS is reused by the next
+        if (nvalid < kLongStep && f >= nvalid) break;
+    }
+    if (lane == 0) a.ctx[slot] = st;
 }
 
 // One wave per workgroup owns the context segments that START among kWalkSpan
@@ -1087,7 +1295,25 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
     __shared__ uint32_t s_start[kWalkSpan];
     __shared__ uint32_t s_nstart;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
-    if (limit_pass && !two_pass) return;
+    if (limit_pass && !two_pass) {
+        // second pass without abort-on-throw work: the long chains the first
+        // pass handed over, one per wave until none is left
+        const uint32_t n_long = a.ctl->n_long;
+        if (n_long == 0u || blockIdx.x >= n_long * 4u) return; // nothing (more) to do: no atomics
+        for (;;) {
+            uint32_t q = 0u;
+            if (threadIdx.x == 0) q = atomicAdd(&a.ctl->long_cursor, 1u);
+            q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
+            if (q >= n_long) return;
+            LongLds sm;
+            sm.rec = s_rec;
+            sm.roc = s_key;
+            sm.g0 = REV ? s_g0 : s_start;
+            sm.ok = REV ? s_ok : s_start;
+            sm.info = s_start;
+            walk_long<REV>(a, a.long_list[q], sm);
+        }
+    }
     if (!limit_pass) // the sort's last digit counts, zero again for the next bundle
         for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words;
              i += gridDim.x * kWalkBlock)
@@ -1143,6 +1369,12 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
         const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
         const uint32_t first_p = s_rec[j].p & kRecIdxMask;
+        // a chain running past the staged window goes to the wave-parallel
+        // walk of the second pass (unless abort-on-throw needs this one)
+        if (!two_pass && s_key[win - 1] == key && base + win < a.n && a.sk_out[base + win] == key) {
+            a.long_list[atomicAdd(&a.ctl->n_long, 1u)] = base + j;
+            continue;
+        }
         // One record of the chain; false ends it.
         auto step = [&](const WalkRec &r, uint32_t g0, uint32_t ok) -> bool {
             if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) return false;
@@ -1361,13 +1593,30 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     tag_write(h, pkt + o, T);
 }
 
+// Adds this workgroup's status counts (s_cnt, LDS) to the engine counters:
+// one 64-bit atomic per status present, on the workgroup's replica.
+__device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const uint32_t *s_cnt) {
+    if (threadIdx.x < kTeCounters && s_cnt[threadIdx.x]) {
+        const uint32_t rep = blockIdx.x & (uint32_t)(kCountReplicas - 1);
+        atomicAdd(&a.counters[rep * kCtrStride + kCtrStatus + threadIdx.x],
+                  (unsigned long long)s_cnt[threadIdx.x]);
+    }
+}
+
 __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
-    __shared__ uint32_t s_te[kTeWords];
-    fill_te4(s_te);
+    __shared__ uint32_t s_te[kTeWords + kTeCounters];
+    uint32_t *s_cnt = s_te + kTeWords;
+    if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+    fill_te4(s_te); // ends with a barrier
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t fs = -1;
+    if (p < a.n) {
+        fs = finish_status(a, p);
+        atomicAdd(&s_cnt[fs & 15], 1u);
+    }
+    __syncthreads();
+    flush_status_counts(a, s_cnt);
     if (p >= a.n) return;
-    const int32_t fs = finish_status(a, p);
-    count_event(a, true, kCtrStatus + (fs & 15));
     const bool todo = fs == SRTP_STATUS_OK;
     const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
     const TeBase tb = te_base();
@@ -1405,7 +1654,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     cs.iv[0] = cs.iv[1] = cs.iv[2] = cs.iv[3] = 0u;
     int end;       // bytes covered by the MAC and the decryption: [0, end) / [off, end)
     uint32_t suffix;
-    bool spec = false;
+    bool spec = false, far = false;
     if (rtp) {
         const int32_t seq = (int32_t)(bswap(hdr.x) & 0xffffu);
         int32_t g = st.a;
@@ -1413,6 +1662,15 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             const int32_t s_l = st.b;
             if (s_l < 32768) g = (seq - s_l > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
             else g = (s_l - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
+            // More than half a wrap ahead of s_l (and not just behind it): a
+            // context whose packets advance that far within one bundle -- a
+            // skewed bundle, one SSRC carrying many thousand packets -- wraps
+            // on the way, so the walk will guess one ROC higher than the
+            // bundle-start state does.  Speculate that forward ROC and check
+            // the tag under the start-state guess too (auth_ok bit 1).
+            const int32_t dist = (seq - s_l) & 0xffff;
+            far = dist > 32768 && dist < 65536 - 1024;
+            if (far) g = (int32_t)((uint32_t)g + 1u);
         }
         a.g0[p] = (uint32_t)g;
         end = do_mac ? (L - T > 0 ? L - T : 0) : L;
@@ -1523,7 +1781,15 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             else outer_words(d, h, ks);
             sha1_compress(h, d);
         }
-        a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+        uint32_t ok = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+        if (far) { // the tag under the start-state guess g0 - 1 (bit 1; bit 2: checked)
+            ReverifyArgs rv; // chunk nb_full still holds ciphertext: decryption comes below
+            rv.pkt = pkt;
+            rv.mid = a.mid + 5 * (size_t)p;
+            rv.tailc = nullptr;
+            ok |= (reverify_rtp(rv, ks, L, (int32_t)(suffix - 1u)) ? 2u : 0u) | 4u;
+        }
+        a.auth_ok[p] = ok;
     }
     if (spec) {
         // reload the round keys through an opaque copy of the key-set pointer:
@@ -1580,7 +1846,10 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
 // them must not cost more than a decryption), the workgroup builds the LDS
 // T-tables and repairs at full AES speed.
 __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
-    __shared__ uint32_t s_te[kTeWords];
+    __shared__ uint32_t s_te[kTeWords + kTeCounters];
+    uint32_t *s_cnt = s_te + kTeWords;
+    if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+    __syncthreads();
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     bool repair = false, did = false, need = false;
     uint32_t ks_id = 0;
@@ -1588,7 +1857,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     if (p < a.n) {
         L0 = (int)a.len[p];
         const int32_t st = finish_status(a, p);
-        count_event(a, true, kCtrStatus + (st & 15));
+        atomicAdd(&s_cnt[st & 15], 1u);
         const uint32_t slot = a.p_slot[p];
         if (slot != kNoSlot) {
             did = a.spec[p] != 0u;
@@ -1606,7 +1875,9 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
             repair = (did || need) && !(did && need && (!rtp || a.g0[p] == a.w_cw[p]));
         }
     }
-    if (!__syncthreads_or(repair)) return; // the common case: speculation was right
+    const bool any_repair = __syncthreads_or(repair);
+    flush_status_counts(a, s_cnt);
+    if (!any_repair) return; // the common case: speculation was right
     fill_te4(s_te);
     if (!repair) return;
     const TeBase tb = te_base();

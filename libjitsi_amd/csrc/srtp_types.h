@@ -78,7 +78,9 @@ constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would thro
 // bundle control block (zeroed per bundle)
 struct BundleCtl {
     uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk
-    uint32_t pad[3];
+    uint32_t n_long;      // context chains longer than the walk's LDS window (long_list)
+    uint32_t long_cursor; // next long chain to hand to a wave
+    uint32_t pad;
 };
 
 // Cumulative per-engine event counters (srtp_engine_stats), 64-bit, kept in

@@ -28,7 +28,7 @@ if [ "$MODE" = test ] || [ "$MODE" = both ]; then
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = bench ] || [ "$MODE" = both ]; then
-  run bench20 300 python bench.py --steps 20 --warmup 5 --no-e2e --cpu-seconds 5
+  run bench20 300 python bench.py --steps 20 --warmup 5
   run bench100 300 python bench.py --steps 100 --no-cpu --no-e2e
 fi
 exit 0
