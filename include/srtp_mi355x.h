@@ -146,8 +146,10 @@ int srtp_transformer_set_factory(srtp_engine *e, int32_t transformer, int32_t fa
 int srtp_transformer_close(srtp_engine *e, int32_t transformer);
 
 /* Process one bundle whose buffers are device (HBM) pointers on the engine's
- * device; asynchronous on `stream` (a hipStream_t of that device; NULL = the
- * engine's own stream, srtp_engine_stream).  tids == NULL means every
+ * device; asynchronous on `stream` (a hipStream_t of that device; NULL = its
+ * default stream, ordered with the caller's default-stream work).  For a
+ * send-side and a receive-side engine to overlap on the device, pass each its
+ * own stream (srtp_engine_stream).  tids == NULL means every
  * packet belongs to `tid`; otherwise tids[i] (device array) names packet i's
  * transformer.  flags may be NULL.  reverse = 0: transform (protect),
  * reverse = 1: reverseTransform (unprotect).  The caller guarantees what
@@ -164,10 +166,10 @@ int srtp_transform_host(srtp_engine *e, int32_t reverse, const int32_t *tids, in
                         uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
                         const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n);
 
-/* The engine's own non-blocking stream (created with the engine, so each
- * engine has a hardware queue of its own): the stream NULL selects in
- * srtp_transform_device, and the one srtp_transform_host and the pipeline
- * run their kernels on. */
+/* The engine's own non-blocking stream, created with the engine so that each
+ * engine gets a hardware queue of its own (streams created later may share
+ * one, which serialises them): srtp_transform_host and the pipeline run their
+ * kernels on it, and srtp_transform_device callers can. */
 void *srtp_engine_stream(srtp_engine *e);
 /* stream == NULL: wait for every bundle this engine has enqueued (any stream) */
 int srtp_engine_sync(srtp_engine *e, void *stream);

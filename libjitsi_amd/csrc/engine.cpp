@@ -65,6 +65,9 @@ struct srtp_engine {
     hipEvent_t ev_last = nullptr;
     unsigned long long *d_count = nullptr; // [2] live / tombstone counts
     unsigned long long *d_counters = nullptr; // [kCountReplicas][kCtrStride]
+#ifdef SRTP_STAMPS
+    unsigned long long *d_stamps[2] = {nullptr, nullptr}; // diagnostic build: protect / unprotect
+#endif
     uint64_t n_bundles = 0, n_packets = 0, n_rehash = 0;
     uint32_t serial = 1;
 
@@ -570,6 +573,11 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     static const int debug_mode = getenv("SRTP_DEBUG") ? atoi(getenv("SRTP_DEBUG")) : 0;
     a.debug = debug_mode;
     a.counters = e->d_counters;
+#ifdef SRTP_STAMPS
+    if (!e->d_stamps[reverse ? 1 : 0])
+        HIPCHK(e, hipMalloc(&e->d_stamps[reverse ? 1 : 0], (size_t)(1u << 20) * 4 * 8));
+    a.stamps = e->d_stamps[reverse ? 1 : 0];
+#endif
     a.p_slot = e->p_slot; a.sk_in = e->sk_in; a.sk_out = e->sk_out;
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
@@ -638,9 +646,11 @@ int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, 
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
     GUARD(e);
-    // NULL = the engine's own stream: every engine gets a hardware queue of its
-    // own, so a send-side and a receive-side engine overlap on the device
-    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    // NULL = the device's default (null) stream, ordered with the caller's
+    // other default-stream work (torch's default stream is NULL too); callers
+    // that want the two directions to overlap pass each engine's own stream
+    // (srtp_engine_stream: one hardware queue per engine)
+    hipStream_t s = (hipStream_t)stream;
     return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s);
 }
 
@@ -891,6 +901,20 @@ int srtp_engine_read_timing(srtp_engine *e, double *ms, uint64_t *count) {
     e->marks.clear();
     return SRTP_OK;
 }
+
+#ifdef SRTP_STAMPS
+// Diagnostic build only (tools/stamps.sh): per-wave stamps of the last
+// k_protect (reverse = 0) / k_unprotect (reverse = 1) launch.
+int srtp_debug_stamps(srtp_engine *e, int32_t reverse, unsigned long long *out, uint32_t waves) {
+    if (!e || !out || !e->d_stamps[reverse ? 1 : 0]) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    GUARD(e);
+    int rc = quiesce(e);
+    if (rc != SRTP_OK) return rc;
+    HIPCHK(e, hipMemcpy(out, e->d_stamps[reverse ? 1 : 0], (size_t)waves * 4 * 8, hipMemcpyDeviceToHost));
+    return SRTP_OK;
+}
+#endif
 
 int srtp_derive_session_keys(const uint8_t mk[16], const uint8_t ms[14], int32_t rtcp,
                              uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]) {

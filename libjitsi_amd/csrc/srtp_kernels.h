@@ -37,6 +37,9 @@ struct BundleArgs {
     uint32_t serial;       // bundle serial (context birth stamp)
     int32_t debug;         // diagnostics only (SRTP_DEBUG env): 0 in production
     unsigned long long *counters; // [kCountReplicas][kCtrStride] cumulative event counters
+#ifdef SRTP_STAMPS
+    unsigned long long *stamps;   // diagnostic build only: per-wave start / filled / end times
+#endif
     // per-bundle scratch
     uint32_t *p_slot;      // [n] context slot of packet p
     uint32_t *sk_in, *sk_out; // [n] sort keys (slot)

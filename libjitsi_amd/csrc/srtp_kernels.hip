@@ -1593,6 +1593,26 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     tag_write(h, pkt + o, T);
 }
 
+#ifdef SRTP_STAMPS
+// Diagnostic build (tools/stamps.sh): per wave, the realtime clock (100 MHz) at
+// kernel entry, after the T-table fill and at the end, plus the XCC id.
+#define STAMP(slot)                                                                        \
+    do {                                                                                   \
+        const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                     \
+        if ((threadIdx.x & 63u) == 0u)                                                     \
+            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 4 + (slot)] = _t; \
+    } while (0)
+#define STAMP_XCC()                                                                        \
+    do {                                                                                   \
+        if ((threadIdx.x & 63u) == 0u)                                                     \
+            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 4 + 3] = \
+                (unsigned long long)__smid();                                             \
+    } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#define STAMP_XCC() do {} while (0)
+#endif
+
 // Adds this workgroup's status counts (s_cnt, LDS) to the engine counters:
 // one 64-bit atomic per status present, on the workgroup's replica.
 __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const uint32_t *s_cnt) {
@@ -1606,8 +1626,11 @@ __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const u
 __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords + kTeCounters];
     uint32_t *s_cnt = s_te + kTeWords;
+    STAMP(0);
+    STAMP_XCC();
     if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
     fill_te4(s_te); // ends with a barrier
+    STAMP(1);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     int32_t fs = -1;
     if (p < a.n) {
@@ -1628,6 +1651,7 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
                     sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
                         sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
     });
+    STAMP(2);
 }
 
 // ============================================================== k_unprotect
@@ -1818,9 +1842,13 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     }
 }
 
+
 __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords];
+    STAMP(0);
+    STAMP_XCC();
     fill_te4(s_te);
+    STAMP(1);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
     const uint32_t slot = a.p_slot[p];
@@ -1835,6 +1863,7 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
                       sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
                           sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
     });
+    STAMP(2);
 }
 
 // ============================================================== k_unprotect_fix
@@ -1903,6 +1932,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
             make_iv_rtcp(ks, hdr, sidx, spec.iv);
             make_iv_rtcp(ks, hdr, a.w_cw[p] & 0x7FFFFFFFu, real.iv);
         }
+        if (real.off < 0 || real.off > real.end) real.off = real.end; // nothing to cipher
         spec.off = real.off;
         spec.end = did ? real.end : 0;
         const int end = real.end;

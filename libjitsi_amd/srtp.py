@@ -298,8 +298,10 @@ class SRTPEngine:
                          n: Optional[int] = None, stream=None) -> None:
         """Enqueue a bundle whose buffers are device tensors (torch, on this
         engine's GPU).  ``tid`` is an int or an int32 device tensor.  Async on
-        ``stream`` (a torch.cuda.Stream or raw hipStream_t pointer; None = the
-        engine's own stream)."""
+        ``stream`` (a torch.cuda.Stream or raw hipStream_t pointer); None =
+        the device's default stream (torch's default stream too), ordered after
+        the torch work that produced the tensors there.  ``stream_ptr`` is the
+        engine's own stream (one hardware queue per engine)."""
         if n is None:
             n = off.numel()
         if np.isscalar(tid):
