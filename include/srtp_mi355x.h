@@ -321,6 +321,55 @@ int srtp_derive_session_keys(const uint8_t master_key[16], const uint8_t master_
                              int32_t rtcp, uint8_t enc_key[16], uint8_t auth_key[20],
                              uint8_t salt_key[14]);
 
+/* DTLS-SRTP keying (control plane, host only): what
+ * DtlsPacketTransformer.initializeSRTPTransformer does after the handshake
+ * (transform/dtls/DtlsPacketTransformer.java:549-690).
+ *
+ * srtp_tls_export_keying_material is the RFC 5705 exporter the reference calls
+ * through BouncyCastle's TlsContext.exportKeyingMaterial(ExporterLabel.dtls_srtp,
+ * null, n) (:614-617): PRF(master_secret, label, client_random ||
+ * server_random)[0..out_len) with no context value.  prf selects the TLS PRF
+ * of the negotiated version: SRTP_TLS_PRF_TLS10 (DTLS 1.0, RFC 2246 5: P_MD5 xor
+ * P_SHA1 over the secret's halves -- the version the reference offers,
+ * TlsClientImpl.java:148-155) or SRTP_TLS_PRF_SHA256 (DTLS 1.2, RFC 5246 5).
+ * The label for DTLS-SRTP is SRTP_DTLS_EXPORTER_LABEL.
+ *
+ * srtp_dtls_profile_keys fills the policies of a negotiated protection profile
+ * (:574-612; the _32 profiles keep a 10-byte SRTCP tag) and splits
+ * keying_material_len = 2 * (key + salt) bytes of exported material as client
+ * key | server key | client salt | server salt (:618-638).  km == NULL fills
+ * only the lengths and policies.  Unknown profile: SRTP_EPOLICY (the
+ * reference's IllegalArgumentException).
+ *
+ * srtp_dtls_transformer_create builds both factories (the client's is a sender
+ * iff is_client, the server's iff !is_client: :639-652) and a transformer of
+ * `kind` whose forward factory is this side's own and reverse the peer's
+ * (:653-690).  NULL-cipher profiles, which export no master key (the
+ * reference then fails deriving session keys), return
+ * SRTP_EPOLICY.  out_factories (may be NULL) receives {client, server} factory ids
+ * -- the caller closes them with the transformer, as
+ * SRTPTransformer.close() closes both (SRTPTransformer.java:132-150). */
+#define SRTP_PROFILE_AES128_CM_HMAC_SHA1_80 0x0001
+#define SRTP_PROFILE_AES128_CM_HMAC_SHA1_32 0x0002
+#define SRTP_PROFILE_NULL_HMAC_SHA1_80 0x0005
+#define SRTP_PROFILE_NULL_HMAC_SHA1_32 0x0006
+#define SRTP_TLS_PRF_TLS10 0
+#define SRTP_TLS_PRF_SHA256 1
+#define SRTP_DTLS_EXPORTER_LABEL "EXTRACTOR-dtls_srtp"
+typedef struct {
+    srtp_policy srtp, srtcp;
+    int32_t key_len, salt_len, keying_material_len;
+    uint8_t client_key[16], server_key[16];
+    uint8_t client_salt[14], server_salt[14];
+} srtp_dtls_keys;
+int srtp_tls_export_keying_material(int32_t prf, const uint8_t *master_secret, int32_t secret_len,
+                                    const uint8_t client_random[32], const uint8_t server_random[32],
+                                    const char *label, uint8_t *out, int32_t out_len);
+int srtp_dtls_profile_keys(int32_t profile, const uint8_t *km, int32_t km_len, srtp_dtls_keys *out);
+int srtp_dtls_transformer_create(srtp_engine *e, int32_t profile, int32_t is_client, int32_t kind,
+                                 const uint8_t *km, int32_t km_len, int32_t *out_transformer,
+                                 int32_t out_factories[2]);
+
 #ifdef __cplusplus
 }
 #endif

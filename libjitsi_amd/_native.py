@@ -42,6 +42,7 @@ EXPORTED = [
     "srtp_dispatch_transformer_create", "srtp_dispatch_transformer_set_factory",
     "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host",
     "srtp_dispatch_get_context_state", "srtp_dispatch_set_context_state", "srtp_dispatch_stats",
+    "srtp_tls_export_keying_material", "srtp_dtls_profile_keys", "srtp_dtls_transformer_create",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -80,6 +81,14 @@ class Stats(C.Structure):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "status"}
         d["status"] = {STATUS_NAMES[i]: int(self.status[i]) for i in range(10)}
         return d
+
+
+class DtlsKeys(C.Structure):
+    """srtp_dtls_keys (include/srtp_mi355x.h)"""
+    _fields_ = [("srtp", Policy), ("srtcp", Policy), ("key_len", C.c_int32),
+                ("salt_len", C.c_int32), ("keying_material_len", C.c_int32),
+                ("client_key", C.c_uint8 * 16), ("server_key", C.c_uint8 * 16),
+                ("client_salt", C.c_uint8 * 14), ("server_salt", C.c_uint8 * 14)]
 
 
 class PipelineSlot(C.Structure):
@@ -132,6 +141,10 @@ def lib() -> C.CDLL:
     L.srtp_pipeline_submit.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t]
     L.srtp_pipeline_wait.argtypes = [vp, i32]
     L.srtp_engine_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.srtp_tls_export_keying_material.argtypes = [i32, C.c_char_p, i32, C.c_char_p, C.c_char_p,
+                                                  C.c_char_p, vp, i32]
+    L.srtp_dtls_profile_keys.argtypes = [i32, C.c_char_p, i32, C.POINTER(DtlsKeys)]
+    L.srtp_dtls_transformer_create.argtypes = [vp, i32, i32, i32, C.c_char_p, i32, pi32, pi32]
     L.srtp_engine_stream.argtypes = [vp]
     L.srtp_engine_stream.restype = vp
     L.srtp_shard_of.argtypes = [u32, i32]

@@ -71,6 +71,13 @@ def lib():
         L.orc_get_state.argtypes = [vp, C.c_uint32, C.POINTER(CtxState)]
         L.orc_num_contexts.restype = C.c_uint32
         L.orc_num_contexts.argtypes = [vp]
+        L.orc_tls_export.restype = C.c_int
+        L.orc_tls_export.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p, C.c_char_p,
+                                     C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_export_contexts.restype = C.c_uint32
+        L.orc_export_contexts.argtypes = [vp, u32p, C.POINTER(CtxState), C.c_uint32]
+        L.orc_set_context_state.restype = C.c_int
+        L.orc_set_context_state.argtypes = [vp, C.c_uint32, C.c_int, C.POINTER(CtxState)]
         L.orc_aes128_encrypt_block.argtypes = [u8p, u8p, u8p]
         L.orc_hmac_sha1.argtypes = [u8p, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_derive_keys.argtypes = [u8p, u8p, C.c_int, u8p, u8p, u8p]
@@ -171,6 +178,20 @@ class Transformer:
     def num_contexts(self) -> int:
         return lib().orc_num_contexts(self.h)
 
+    def export_contexts(self) -> dict:
+        """{ssrc: state} of every context (orc_export_contexts)."""
+        n = lib().orc_export_contexts(self.h, None, None, 0)
+        ssrcs = (C.c_uint32 * max(n, 1))()
+        states = (CtxState * max(n, 1))()
+        lib().orc_export_contexts(self.h, ssrcs, states, n)
+        return {int(ssrcs[i]): {k: getattr(states[i], k) for k, _ in CtxState._fields_}
+                for i in range(n)}
+
+    def import_context(self, ssrc: int, state: dict, forward: bool) -> None:
+        st = CtxState(**{k: state.get(k, 0) for k, _ in CtxState._fields_})
+        if lib().orc_set_context_state(self.h, ssrc & 0xFFFFFFFF, int(forward), C.byref(st)) != 0:
+            raise ValueError("factory closed")
+
     def __del__(self):
         try:
             lib().orc_transformer_free(self.h)
@@ -203,3 +224,13 @@ def process(transformers, reverse: bool, seg: np.ndarray, off: np.ndarray, lengt
                       fl.ctypes.data_as(u32), status.ctypes.data_as(C.POINTER(C.c_int32)),
                       n, int(abort_on_error))
     return status
+
+
+def tls_export(prf: int, secret: bytes, client_random: bytes, server_random: bytes,
+               label: bytes, n: int) -> bytes:
+    """RFC 5705 exporter over the TLS PRF (OpenSSL TLS1-PRF; prf 0 = TLS 1.0
+    MD5-SHA1, 1 = TLS 1.2 SHA256) -- orc_tls_export."""
+    out = C.create_string_buffer(max(n, 1))
+    if lib().orc_tls_export(prf, secret, len(secret), client_random, server_random, label, out, n):
+        raise RuntimeError("TLS1-PRF failed")
+    return out.raw[:n]

@@ -11,6 +11,9 @@
 
 #include <openssl/evp.h>
 #include <openssl/hmac.h>
+#include <openssl/kdf.h>
+#include <openssl/core_names.h>
+#include <openssl/params.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -393,11 +396,8 @@ void orc_transformer_free(orc_transformer *t) {
 /* SRTPTransformer.getContext :152-175 / SRTCPTransformer.getContext :144-167:
  * lazily derive a context from the factory's default context (roc 0, kdr 0 ->
  * the session keys depend only on the master key/salt and the label). */
-static orc_ctx *get_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) {
-    orc_ctx *x = map_get(&t->map, ssrc);
-    if (x) return x;
-    if (!f || f->closed) return NULL;
-    x = (orc_ctx *)calloc(1, sizeof *x);
+static orc_ctx *make_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) {
+    orc_ctx *x = (orc_ctx *)calloc(1, sizeof *x);
     x->ssrc = ssrc; x->kind = t->kind; x->mode = f->mode;
     x->policy = (t->kind == ORC_KIND_RTP) ? f->srtp : f->srtcp;
     orc_derive_keys(f->master_key, f->master_salt, t->kind == ORC_KIND_RTCP, x->enc_key,
@@ -412,6 +412,14 @@ static orc_ctx *get_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) {
     x->hmac = HMAC_CTX_new();
     x->hmac_work = HMAC_CTX_new();
     HMAC_Init_ex(x->hmac, x->auth_key, 20, EVP_sha1(), NULL);
+    return x;
+}
+
+static orc_ctx *get_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) {
+    orc_ctx *x = map_get(&t->map, ssrc);
+    if (x) return x;
+    if (!f || f->closed) return NULL;
+    x = make_context(t, ssrc, f);
     map_put(&t->map, ssrc, x);
     return x;
 }
@@ -721,3 +729,72 @@ int orc_get_state(orc_transformer *t, uint32_t ssrc, orc_ctx_state *out) {
 }
 
 uint32_t orc_num_contexts(orc_transformer *t) { return t->map.count; }
+
+/* Context-state export / import (the engine's srtp_export_contexts /
+ * srtp_set_context_state; the reference has no such API -- the state is the
+ * private fields of SRTPCryptoContext :96-135 / SRTCPCryptoContext :54-59).
+ * Export: up to max (ssrc, state) pairs in map order, returns the count held. */
+uint32_t orc_export_contexts(orc_transformer *t, uint32_t *ssrcs, orc_ctx_state *states, uint32_t max) {
+    uint32_t n = 0;
+    for (uint32_t i = 0; i < t->map.cap; i++) {
+        if (!t->map.vals[i]) continue;
+        if (n < max) {
+            ssrcs[n] = t->map.keys[i];
+            orc_get_state(t, t->map.keys[i], &states[n]);
+        }
+        n++;
+    }
+    return n;
+}
+
+/* Import: create or replace the context for ssrc, keyed by the transformer's
+ * forward or reverse factory (which must be open), with the given state.
+ * Returns 0, or -1 when that factory is closed. */
+int orc_set_context_state(orc_transformer *t, uint32_t ssrc, int forward, const orc_ctx_state *st) {
+    orc_factory *f = forward ? t->fwd : t->rev;
+    if (!f || f->closed) return -1;
+    orc_ctx *x = make_context(t, ssrc, f);
+    x->roc = st->roc; x->s_l = st->s_l; x->seq_num_set = st->seq_num_set;
+    x->guessed_roc = st->guessed_roc;
+    x->sent_index = st->sent_index; x->received_index = st->received_index;
+    x->replay_window = (int64_t)st->replay_window;
+    const uint32_t mask = t->map.cap - 1;
+    for (uint32_t i = mix32(ssrc) & mask;; i = (i + 1) & mask) {
+        if (!t->map.vals[i]) break;
+        if (t->map.keys[i] == ssrc) {
+            ctx_free(t->map.vals[i]);
+            t->map.vals[i] = x;
+            return 0;
+        }
+    }
+    map_put(&t->map, ssrc, x);
+    return 0;
+}
+
+/* RFC 5705 keying-material exporter (no context value) over the TLS PRF, via
+ * OpenSSL's TLS1-PRF KDF: the checker for the engine's
+ * srtp_tls_export_keying_material (what BouncyCastle's
+ * TlsContext.exportKeyingMaterial does for DtlsPacketTransformer.java:614-617).
+ * prf 0: TLS 1.0/1.1 (MD5-SHA1), 1: TLS 1.2 (SHA256).  Returns 0 on success. */
+int orc_tls_export(int prf, const uint8_t *secret, int secret_len, const uint8_t cr[32],
+                   const uint8_t sr[32], const char *label, uint8_t *out, int out_len) {
+    EVP_KDF *kdf = EVP_KDF_fetch(NULL, "TLS1-PRF", NULL);
+    if (!kdf) return -1;
+    EVP_KDF_CTX *kc = EVP_KDF_CTX_new(kdf);
+    EVP_KDF_free(kdf);
+    if (!kc) return -1;
+    size_t ll = strlen(label);
+    uint8_t *seed = (uint8_t *)malloc(ll + 64);
+    memcpy(seed, label, ll);
+    memcpy(seed + ll, cr, 32);
+    memcpy(seed + ll + 32, sr, 32);
+    OSSL_PARAM ps[4];
+    ps[0] = OSSL_PARAM_construct_utf8_string(OSSL_KDF_PARAM_DIGEST, prf ? (char *)"SHA256" : (char *)"MD5-SHA1", 0);
+    ps[1] = OSSL_PARAM_construct_octet_string(OSSL_KDF_PARAM_SECRET, (void *)secret, (size_t)secret_len);
+    ps[2] = OSSL_PARAM_construct_octet_string(OSSL_KDF_PARAM_SEED, seed, ll + 64);
+    ps[3] = OSSL_PARAM_construct_end();
+    int rc = EVP_KDF_derive(kc, out, (size_t)out_len, ps) == 1 ? 0 : -1;
+    EVP_KDF_CTX_free(kc);
+    free(seed);
+    return rc;
+}

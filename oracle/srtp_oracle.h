@@ -110,8 +110,17 @@ typedef struct {
 } orc_ctx_state;
 int orc_get_state(orc_transformer *t, uint32_t ssrc, orc_ctx_state *out);
 uint32_t orc_num_contexts(orc_transformer *t);
+/* Context-state export / import, as the engine's srtp_export_contexts /
+ * srtp_set_context_state (no reference API; the state is SRTPCryptoContext's
+ * private fields :96-135). */
+uint32_t orc_export_contexts(orc_transformer *t, uint32_t *ssrcs, orc_ctx_state *states, uint32_t max);
+int orc_set_context_state(orc_transformer *t, uint32_t ssrc, int forward, const orc_ctx_state *st);
 
 /* Primitive helpers exposed for the KAT tests. */
+/* RFC 5705 exporter over the TLS PRF (OpenSSL TLS1-PRF KDF); prf 0 = TLS 1.0
+ * MD5-SHA1, 1 = TLS 1.2 SHA256 (DtlsPacketTransformer.java:614-617). */
+int orc_tls_export(int prf, const uint8_t *secret, int secret_len, const uint8_t cr[32],
+                   const uint8_t sr[32], const char *label, uint8_t *out, int out_len);
 void orc_aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]);
 void orc_hmac_sha1(const uint8_t *key, int key_len, const uint8_t *msg, size_t n, uint8_t out[20]);
 /* RFC 3711 4.3 PRF exactly as SRTPCryptoContext.deriveSrtpKeys (labels 0/1/2)

@@ -1,98 +1,177 @@
-"""GPU: context-state export / import.
+"""Context-state export / import, pinned to the oracle.
 
 A receiver's SRTP and SRTCP contexts are exported from one engine and imported
-into a second engine (another GPU in a re-sharded deployment); the second
-engine then continues the streams exactly as the first one does -- same
-statuses, lengths, plaintext and final state -- including rejecting replays of
-packets only the first engine ever saw.
+into a second engine (another GPU in a re-sharded deployment).  The oracle does
+the same export / import (orc_export_contexts / orc_set_context_state) on its
+own pair of transformers, and every step is compared engine-vs-oracle:
+
+* the engine's export equals the oracle's export, field by field;
+* after the import, the second engine continues the streams exactly as the
+  second oracle does (statuses, lengths, bytes, state) -- including rejecting
+  replays of packets only the first engine ever saw;
+* states that no traffic produced (arbitrary ROC / s_l / window / SRTCP index,
+  seqNumSet false, an import over an existing context) behave identically.
+
+The state is SRTPCryptoContext's private fields (roc, s_l, seqNumSet,
+guessedROC, replayWindow: SRTPCryptoContext.java:96-135) and
+SRTCPCryptoContext's (sentIndex, receivedIndex, replayWindow: :54-59); the
+reference has no export API, so the oracle's import is the definition.
 """
 import numpy as np
 import pytest
 
-from libjitsi_amd import SRTCPTransformer, SRTPContextFactory, SRTPTransformer, profile_policies, synth
+from libjitsi_amd import profile_policies, synth
+from oracle import oracle as O
 
-pytestmark = pytest.mark.gpu
+from harness import STATE_KEYS_RTCP, STATE_KEYS_RTP, Twin
+
 P80 = profile_policies("AES_CM_128_HMAC_SHA1_80")
+P32 = profile_policies("AES_CM_128_HMAC_SHA1_32")
+ALL_KEYS = ("roc", "s_l", "seq_num_set", "guessed_roc", "sent_index", "received_index",
+            "replay_window")
 
 
-def run(eng, t, reverse, b, seg=None, ln=None):
-    seg = (b.seg if seg is None else seg).copy()
-    ln = (b.length if ln is None else ln).copy()
-    st = eng.transform_host(reverse, t.tid, seg, b.off, ln, b.cap)
-    return seg, ln, st
+def assert_same_export(eng, twin_t):
+    ex_e = eng.export_contexts(twin_t.e)
+    ex_o = twin_t.o.export_contexts()
+    assert sorted(ex_e) == sorted(ex_o)
+    keys = STATE_KEYS_RTP if twin_t.kind == O.KIND_RTP else STATE_KEYS_RTCP
+    for ssrc, so in ex_o.items():
+        for k in keys:
+            assert int(ex_e[ssrc][k]) == int(so[k]), (hex(ssrc), k, ex_e[ssrc], so)
+    return ex_e
 
 
-def test_export_import_continues_streams(engine_factory):
+def import_both(eng, twin_t, ex, forward=False):
+    for ssrc, st in ex.items():
+        eng.import_context(twin_t.e, ssrc, st, forward=forward)
+        twin_t.o.import_context(ssrc, st, forward=forward)
+
+
+def protected_copy(b, seg, ln):
+    pb = b.copy()
+    pb.seg, pb.length = seg, ln
+    return pb
+
+
+@pytest.mark.gpu
+def test_export_import_continues_streams(engine_factory, oracle):
     A = engine_factory(max_contexts=4096, max_factories=64, max_transformers=64)
     B = engine_factory(max_contexts=4096, max_factories=64, max_transformers=64)
+    ta, tb = Twin(A), Twin(B)
     (k, s), = synth.keys(61, 1)
-    snd = SRTPTransformer(SRTPContextFactory(True, k, s, *P80, engine=A))
-    rcv_a = SRTPTransformer(SRTPContextFactory(False, k, s, *P80, engine=A))
-    csnd = SRTCPTransformer(SRTPContextFactory(True, k, s, *P80, engine=A))
-    crcv_a = SRTCPTransformer(SRTPContextFactory(False, k, s, *P80, engine=A))
+    fs, fr = ta.factory(True, k, s, *P80), ta.factory(False, k, s, *P80)
+    snd, rcv_a = ta.transformer(O.KIND_RTP, fs), ta.transformer(O.KIND_RTP, fr)
+    csnd, crcv_a = ta.transformer(O.KIND_RTCP, fs), ta.transformer(O.KIND_RTCP, fr)
     seq0 = np.array([65500, 100, 40000, 7], np.uint32)
     full = synth.rtp_bundle(400, 4, (60, 1200), seed=62, seq0=seq0)
     rtcp = synth.rtcp_bundle(60, 4, seed=63, ssrcs=full.meta["ssrcs"])
     parts = [synth.select(full, np.arange(i, i + 100)) for i in range(0, 400, 100)]
     cparts = [synth.select(rtcp, np.arange(i, i + 20)) for i in range(0, 60, 20)]
-    prot = []
-    for part in parts[:2]:  # history only engine A sees
-        seg, ln, st = run(A, snd, False, part)
-        assert (st == 0).all()
-        prot.append((seg, ln))
-        _, _, st = run(A, rcv_a, True, part, seg, ln)
-        assert (st == 0).all()
-    cprot = []
-    for part in cparts[:2]:
-        seg, ln, st = run(A, csnd, False, part)
-        cprot.append((seg, ln))
-        _, _, st = run(A, crcv_a, True, part, seg, ln)
-        assert (st == 0).all()
+    prot, cprot = [], []
+    for part in parts[:3]:  # history only engine A sees; part 2 is protected for later
+        seg, ln, st = ta.run(snd, False, part.seg, part.off, part.length, part.cap)
+        prot.append(protected_copy(part, seg, ln))
+    for pb in prot[:2]:
+        ta.run(rcv_a, True, pb.seg, pb.off, pb.length, pb.cap)
+    for part in cparts:
+        seg, ln, st = ta.run(csnd, False, part.seg, part.off, part.length, part.cap)
+        cprot.append(protected_copy(part, seg, ln))
+    for pb in cprot[:2]:
+        ta.run(crcv_a, True, pb.seg, pb.off, pb.length, pb.cap)
 
-    ex = A.export_contexts(rcv_a)
-    cex = A.export_contexts(crcv_a)
-    assert sorted(ex) == sorted(int(x) for x in full.meta["ssrcs"])
-    assert len(cex) == 4
-    rcv_b = SRTPTransformer(SRTPContextFactory(False, k, s, *P80, engine=B))
-    crcv_b = SRTCPTransformer(SRTPContextFactory(False, k, s, *P80, engine=B))
-    for ssrc, stt in ex.items():
-        B.import_context(rcv_b, ssrc, stt, forward=False)
-    for ssrc, stt in cex.items():
-        B.import_context(crcv_b, ssrc, stt, forward=False)
-    for ssrc, stt in ex.items():
-        got = B.context_state(rcv_b, ssrc)
-        for key in ("roc", "s_l", "seq_num_set", "guessed_roc", "replay_window"):
-            assert got[key] == stt[key]
+    ex = assert_same_export(A, rcv_a)
+    cex = assert_same_export(A, crcv_a)
+    assert sorted(ex) == sorted(int(x) for x in full.meta["ssrcs"]) and len(cex) == 4
+    gs, gr = tb.factory(True, k, s, *P80), tb.factory(False, k, s, *P80)
+    rcv_b, crcv_b = tb.transformer(O.KIND_RTP, gr), tb.transformer(O.KIND_RTCP, gr)
+    import_both(B, rcv_b, ex)
+    import_both(B, crcv_b, cex)
+    assert_same_export(B, rcv_b)
+    assert_same_export(B, crcv_b)
 
-    # new traffic plus replays of what only A has seen: A and B must agree
-    new_seg, new_ln, st = run(A, snd, False, parts[2])
-    assert (st == 0).all()
-    replay = synth.select(parts[1], np.arange(0, 100, 7))
-    rseg = np.zeros_like(replay.seg)
-    for j, i in enumerate(range(0, 100, 7)):  # protected bytes of those packets
-        o, L = int(parts[1].off[i]), int(prot[1][1][i])
-        rseg[replay.off[j]:replay.off[j] + L] = prot[1][0][o:o + L]
-    rlen = prot[1][1][np.arange(0, 100, 7)].astype(np.uint32)
-    for part, seg, ln in ((parts[2], new_seg, new_ln), (replay, rseg, rlen)):
-        sa, la, sta = run(A, rcv_a, True, part, seg, ln)
-        sb, lb, stb = run(B, rcv_b, True, part, seg, ln)
-        assert (sta == stb).all() and (la == lb).all() and np.array_equal(sa, sb)
-    assert (stb == 1).all()  # the replays: DROP_REPLAY on the importing engine too
-    cseg, cln, st = run(A, csnd, False, cparts[2])
-    sa, la, sta = run(A, crcv_a, True, cparts[2], cseg, cln)
-    sb, lb, stb = run(B, crcv_b, True, cparts[2], cseg, cln)
-    assert (sta == 0).all() and (sta == stb).all() and np.array_equal(sa, sb)
-    for ssrc in ex:
-        a, b = A.context_state(rcv_a, ssrc), B.context_state(rcv_b, ssrc)
-        for key in ("roc", "s_l", "seq_num_set", "guessed_roc", "replay_window"):
-            assert a[key] == b[key]
-    for ssrc in cex:
-        a, b = A.context_state(crcv_a, ssrc), B.context_state(crcv_b, ssrc)
-        for key in ("received_index", "replay_window"):
-            assert a[key] == b[key]
+    # new traffic, then replays of what only A has seen: B against its oracle
+    idx = np.arange(0, 100, 7)
+    replay = synth.select(prot[1], idx)
+    for pb in (prot[2], replay):
+        seg_b, ln_b, st_b = tb.run(rcv_b, True, pb.seg, pb.off, pb.length, pb.cap)
+        seg_a, ln_a, st_a = ta.run(rcv_a, True, pb.seg, pb.off, pb.length, pb.cap)
+        assert (st_a == st_b).all() and (ln_a == ln_b).all() and np.array_equal(seg_a, seg_b)
+    assert (st_b == 1).all()  # the replays: DROP_REPLAY on the importing engine too
+    tb.run(crcv_b, True, cprot[2].seg, cprot[2].off, cprot[2].length, cprot[2].cap)
+    tb.run(crcv_b, True, cprot[1].seg, cprot[1].off, cprot[1].length, cprot[1].cap)  # replays
+    assert_same_export(B, rcv_b)
+    assert_same_export(B, crcv_b)
 
 
+@pytest.mark.gpu
+def test_import_arbitrary_states(engine_factory, oracle):
+    """States no traffic produced, imported into fresh and existing contexts,
+    then driven by packets around the imported s_l / ROC / window."""
+    E = engine_factory(max_contexts=4096, max_factories=64, max_transformers=64)
+    tw = Twin(E)
+    (k, s), = synth.keys(65, 1)
+    fs, fr = tw.factory(True, k, s, *P32), tw.factory(False, k, s, *P32)
+    snd, rcv = tw.transformer(O.KIND_RTP, fs), tw.transformer(O.KIND_RTP, fr)
+    csnd, crcv = tw.transformer(O.KIND_RTCP, fs), tw.transformer(O.KIND_RTCP, fr)
+    rng = np.random.default_rng(66)
+    n_ssrc = 24
+    seq0 = rng.integers(0, 65536, n_ssrc).astype(np.uint32)
+    b = synth.rtp_bundle(40 * n_ssrc, n_ssrc, (60, 500), seed=67, seq0=seq0)
+    ssrcs = [int(x) for x in b.meta["ssrcs"]]
+    # give half the receivers' SSRCs an existing context first (import overwrites it)
+    warm = synth.select(b, np.nonzero(np.isin(b.ssrc, ssrcs[::2]))[0][:48])
+    # sender states: ROC r so the packets carry index r * 2^16 + seq
+    rocs = rng.integers(0, 1 << 20, n_ssrc)
+    for i, ssrc in enumerate(ssrcs):
+        st = {"roc": int(rocs[i]), "s_l": int(seq0[i]), "seq_num_set": 1}
+        E.import_context(snd.e, ssrc, st, forward=True)
+        snd.o.import_context(ssrc, st, forward=True)
+    seg, ln, st = tw.run(snd, False, b.seg, b.off, b.length, b.cap)
+    pb = protected_copy(b, seg, ln)
+    pw = synth.select(pb, np.nonzero(np.isin(b.ssrc, ssrcs[::2]))[0][:48])
+    assert warm.n == pw.n
+    tw.run(rcv, True, pw.seg, pw.off, pw.length, pw.cap, check_state=False)
+    for i, ssrc in enumerate(ssrcs):
+        mode = i % 4
+        window = int(rng.integers(0, 1 << 62)) | 1
+        if mode == 0:    # exact: receiver already at s_l - 1 with the sender's ROC
+            st = {"roc": int(rocs[i]), "s_l": int((seq0[i] - 1) & 0xFFFF), "seq_num_set": 1,
+                  "replay_window": window}
+        elif mode == 1:  # seqNumSet false: first packet sets s_l
+            st = {"roc": int(rocs[i]), "s_l": 0, "seq_num_set": 0}
+        elif mode == 2:  # receiver behind by ~20 packets, sparse window
+            st = {"roc": int(rocs[i]), "s_l": int((seq0[i] - 20) & 0xFFFF), "seq_num_set": 1,
+                  "replay_window": window}
+        else:            # receiver ahead: the early packets are stale or replays
+            st = {"roc": int(rocs[i]), "s_l": int((seq0[i] + 10) & 0xFFFF), "seq_num_set": 1,
+                  "replay_window": window}
+        E.import_context(rcv.e, ssrc, st, forward=False)
+        rcv.o.import_context(ssrc, st, forward=False)
+    _, _, st2 = tw.run(rcv, True, pb.seg, pb.off, pb.length, pb.cap)
+    assert (st2 == 0).sum() > 0.5 * pb.n and (st2 != 0).any()
+    assert_same_export(E, rcv)
+
+    # SRTCP: imported sent_index continues the E-flag index; receiver windows
+    cb = synth.rtcp_bundle(6 * 8, 8, seed=68, ssrcs=np.array(ssrcs[:8], np.uint32))
+    for i, ssrc in enumerate(ssrcs[:8]):
+        base = int(rng.integers(100, (1 << 31) - 100))
+        st = {"sent_index": base}
+        E.import_context(csnd.e, ssrc, st, forward=True)
+        csnd.o.import_context(ssrc, st, forward=True)
+        rst = {"received_index": base - 3 + (i % 3) * 4, "replay_window": (1 << 40) - 1}
+        E.import_context(crcv.e, ssrc, rst, forward=False)
+        crcv.o.import_context(ssrc, rst, forward=False)
+    seg, ln, st = tw.run(csnd, False, cb.seg, cb.off, cb.length, cb.cap)
+    pc = protected_copy(cb, seg, ln)
+    tw.run(crcv, True, pc.seg, pc.off, pc.length, pc.cap)
+    assert_same_export(E, csnd)
+    assert_same_export(E, crcv)
+
+
+@pytest.mark.gpu
 def test_import_needs_open_factory(engine_factory):
+    from libjitsi_amd import SRTPContextFactory, SRTPTransformer
     E = engine_factory(max_contexts=1024, max_factories=16, max_transformers=16)
     (k, s), = synth.keys(64, 1)
     f = SRTPContextFactory(False, k, s, *P80, engine=E)
@@ -100,3 +179,36 @@ def test_import_needs_open_factory(engine_factory):
     f.close()
     with pytest.raises(Exception):
         E.import_context(t, 1234, {"roc": 1, "s_l": 5, "seq_num_set": 1}, forward=False)
+
+
+def test_oracle_export_import_round_trip(oracle):
+    """CPU: the oracle's own export -> import -> continue equals continuing
+    the original transformer (and a closed factory refuses the import)."""
+    (k, s), = synth.keys(69, 1)
+    pol = [O.Policy(p.encType, p.encKeyLength, p.authType, p.authKeyLength, p.authTagLength,
+                    p.saltKeyLength) for p in P80]
+    fs, fr = O.Factory(True, k, s, *pol), O.Factory(False, k, s, *pol)
+    fr2 = O.Factory(False, k, s, *pol)
+    snd, rcv = O.Transformer(O.KIND_RTP, fs, fs), O.Transformer(O.KIND_RTP, fr, fr)
+    rcv2 = O.Transformer(O.KIND_RTP, fr2, fr2)
+    b = synth.rtp_bundle(300, 3, (60, 400), seed=70, seq0=[65400, 1, 30000])
+    seg, ln = b.seg.copy(), b.length.copy()
+    assert (O.process(snd, False, seg, b.off, ln, b.cap) == 0).all()
+    half = synth.select(protected_copy(b, seg, ln), np.arange(150))
+    rest = synth.select(protected_copy(b, seg, ln), np.r_[140:300])
+    assert (O.process(rcv, True, half.seg.copy(), half.off, half.length.copy(), half.cap) == 0).all()
+    ex = rcv.export_contexts()
+    assert len(ex) == 3 and all(st["seq_num_set"] == 1 for st in ex.values())
+    for ssrc, st in ex.items():
+        rcv2.import_context(ssrc, st, forward=False)
+    assert rcv2.export_contexts() == ex
+    outs = []
+    for t in (rcv, rcv2):
+        sg, l2 = rest.seg.copy(), rest.length.copy()
+        outs.append((O.process(t, True, sg, rest.off, l2, rest.cap), sg, l2))
+    assert (outs[0][0] == outs[1][0]).all() and np.array_equal(outs[0][1], outs[1][1])
+    assert (outs[0][0][:10] == 1).all() and (outs[0][0][10:] == 0).all()
+    assert rcv.export_contexts() == rcv2.export_contexts()
+    fr2.close()
+    with pytest.raises(ValueError):
+        rcv2.import_context(1, {"roc": 0}, forward=False)
