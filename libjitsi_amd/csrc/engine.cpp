@@ -575,7 +575,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.counters = e->d_counters;
 #ifdef SRTP_STAMPS
     if (!e->d_stamps[reverse ? 1 : 0])
-        HIPCHK(e, hipMalloc(&e->d_stamps[reverse ? 1 : 0], (size_t)(1u << 20) * 4 * 8));
+        HIPCHK(e, hipMalloc(&e->d_stamps[reverse ? 1 : 0], (size_t)(1u << 20) * 8 * 8));
     a.stamps = e->d_stamps[reverse ? 1 : 0];
 #endif
     a.p_slot = e->p_slot; a.sk_in = e->sk_in; a.sk_out = e->sk_out;
@@ -911,7 +911,7 @@ int srtp_debug_stamps(srtp_engine *e, int32_t reverse, unsigned long long *out, 
     GUARD(e);
     int rc = quiesce(e);
     if (rc != SRTP_OK) return rc;
-    HIPCHK(e, hipMemcpy(out, e->d_stamps[reverse ? 1 : 0], (size_t)waves * 4 * 8, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(out, e->d_stamps[reverse ? 1 : 0], (size_t)waves * 8 * 8, hipMemcpyDeviceToHost));
     return SRTP_OK;
 }
 #endif

@@ -195,6 +195,32 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
 }
 
+// ------------------------------------------------------ progress priority
+// The AES kernels run one workgroup of 16 waves per CU (the LDS image), all
+// waves with the same work.  The SIMD arbiter favours older waves, so without
+// help the waves of a SIMD finish one after another and the last ones run
+// with nothing to hide their LDS latency.  SRTP_PRIO: each wave lowers its
+// issue priority as it advances through its packets, so they stay abreast.
+#ifndef SRTP_PRIO
+#define SRTP_PRIO 1
+#endif
+__device__ __forceinline__ int wave_max_i(int x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ void progress_prio(int b, int nbw) {
+#if SRTP_PRIO
+    const int q = __builtin_amdgcn_readfirstlane((4 * b) / (nbw + 1));
+    if (q <= 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)b; (void)nbw;
+#endif
+}
+
 // ------------------------------------------------- fused AES-CM + SHA-1 step
 // One SHA-1 round t (compile-time after unrolling) on working state v[0..4].
 template <int t>
@@ -341,8 +367,33 @@ __device__ __forceinline__ void ks_sha_half(const char *__restrict__ lds, const 
                                             const RoundKeys &rk, const CtrPre &cp, int j0,
                                             uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
     uint32_t x[4], y[4];
-    ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
     constexpr int t = 40 * P;
+#if defined(SRTP_EXP_NOSHA) && defined(SRTP_EXP_NOAES) // diagnostic: neither
+#pragma unroll
+    for (int k = 0; k < 4; k++) { K8[k] = cp.r[k] ^ (uint32_t)j0; K8[4 + k] = cp.r[k] + (uint32_t)j0; }
+    (void)x; (void)y; (void)v; (void)w;
+    return;
+#elif defined(SRTP_EXP_NOSHA) // diagnostic builds: AES only / SHA-1 only (results wrong)
+    ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
+#pragma unroll
+    for (int r = 3; r < 10; r++) aes_round2(lds, tb, rk.k + 4 * r, x, y);
+    aes_last2(lds, tb, rk.k + 40, x, y);
+#pragma unroll
+    for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
+    return;
+#elif defined(SRTP_EXP_NOAES)
+#pragma unroll
+    for (int k = 0; k < 4; k++) { x[k] = cp.r[k] ^ (uint32_t)j0; y[k] = cp.r[k] + (uint32_t)j0; }
+    sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
+    sha1_rounds4<t + 8>(v, w); sha1_rounds4<t + 12>(v, w);
+    sha1_rounds4<t + 16>(v, w); sha1_rounds4<t + 20>(v, w);
+    sha1_rounds4<t + 24>(v, w); sha1_rounds4<t + 28>(v, w);
+    sha1_rounds4<t + 32>(v, w); sha1_rounds4<t + 36>(v, w);
+#pragma unroll
+    for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
+    return;
+#endif
+    ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
     sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
     // rounds 3..10: SHA-1 rounds t+8 .. t+39 inside the round asm, at its LDS
     // wait points (aes_rounds_asm.inc)
@@ -1454,6 +1505,11 @@ __device__ __forceinline__ void load_chunk(const uint8_t *pkt, int b, int lim, u
 
 // Whole 64-B chunk b (inside the packet: no bounds checks, no branches).
 __device__ __forceinline__ void load_chunk_full(const uint8_t *pkt, int b, uint32_t d[16]) {
+#ifdef SRTP_EXP_NOMEM // diagnostic build: no packet loads in the fused loops (results wrong)
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = (uint32_t)(uintptr_t)pkt * (uint32_t)(k + 1) + (uint32_t)b;
+    return;
+#endif
     const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -1463,9 +1519,96 @@ __device__ __forceinline__ void load_chunk_full(const uint8_t *pkt, int b, uint3
 }
 
 __device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint32_t d[16]) {
+#ifdef SRTP_EXP_NOMEM
+    if (d[0] != 0x9e3779b9u) return;
+#endif
     uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
 #pragma unroll
     for (int m = 0; m < 4; m++) qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+}
+
+// ---------------------------------------------- quad-cooperative chunk access
+// One lane per packet reads its 64-B chunk as four 16-B pieces, each wave
+// instruction touching 64 lines.  With SRTP_COALESCE the four lanes of a quad
+// read each other's chunks instead -- lane m of the quad takes piece m of every
+// quad packet, so one instruction covers 16 whole 64-B chunks -- and a 4x4
+// transpose across the quad (DPP quad_perm, VALU only) hands every lane its
+// own packet's chunk.  Stores go the same way back.  Only lanes active in the
+// calling loop iteration (at the same chunk b) take part; a piece whose quad
+// lane is inactive is read / written by the packet's own lane.
+#ifndef SRTP_COALESCE
+#define SRTP_COALESCE 0
+#endif
+template <int CTRL>
+__device__ __forceinline__ uint32_t qdpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t qbcast(uint32_t x) { return qdpp<CTRL>(x); }
+
+// transpose of r[reg][lane-in-quad] over the quad, one stage per lane-index bit
+template <int S>
+__device__ __forceinline__ void quad_tstage(uint32_t r[4], bool hi) {
+    constexpr int CTRL = S == 1 ? 0xB1 : 0x4E; // quad_perm [1,0,3,2] / [2,3,0,1]
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        if (a & S) continue;
+        const int bb = a | S;
+        const uint32_t xa = qdpp<CTRL>(r[a]), xb = qdpp<CTRL>(r[bb]);
+        const uint32_t na = hi ? xb : r[a];
+        const uint32_t nb = hi ? r[bb] : xa;
+        r[a] = na;
+        r[bb] = nb;
+    }
+}
+__device__ __forceinline__ void quad_transpose(uint32_t d[16]) {
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        uint32_t r[4] = {d[e], d[4 + e], d[8 + e], d[12 + e]};
+        quad_tstage<1>(r, (lane & 1u) != 0u);
+        quad_tstage<2>(r, (lane & 2u) != 0u);
+        d[e] = r[0]; d[4 + e] = r[1]; d[8 + e] = r[2]; d[12 + e] = r[3];
+    }
+}
+__device__ __forceinline__ uint32_t quad_peer_off(uint32_t own, int i) {
+    return i == 0 ? qbcast<0x00>(own) : i == 1 ? qbcast<0x55>(own) : i == 2 ? qbcast<0xAA>(own)
+                                                                            : qbcast<0xFF>(own);
+}
+// True when all four lanes of this lane's quad are active in the calling loop
+// iteration: only then do they share their chunks (else each lane reads and
+// writes its own, as load_chunk_full / store_chunk_full).
+__device__ __forceinline__ bool quad_full() {
+    const uint32_t qb = __lane_id() & ~3u;
+    return ((__ballot(1) >> qb) & 0xFull) == 0xFull;
+}
+// Issue the loads of chunk b: in a full quad lane m reads piece m of every
+// quad packet (d[4i..4i+3] = piece m of packet i), else its own pieces.
+// load_chunk_quad_finish (after the loads have had time to land) transposes.
+__device__ __forceinline__ void load_chunk_quad_issue(const uint8_t *seg, uint32_t off, int b,
+                                                      bool full, uint32_t d[16]) {
+    const uint32_t m = __lane_id() & 3u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t po = full ? quad_peer_off(off, i) + 16u * m : off + 16u * (uint32_t)i;
+        const uint4 v = *reinterpret_cast<const uint4 *>(seg + po + 64u * (uint32_t)b);
+        d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void load_chunk_quad_finish(bool full, uint32_t d[16]) {
+    if (full) quad_transpose(d);
+}
+// Store chunk b (d is clobbered).
+__device__ __forceinline__ void store_chunk_quad(uint8_t *seg, uint32_t off, int b, bool full,
+                                                 uint32_t d[16]) {
+    if (full) quad_transpose(d);
+    const uint32_t m = __lane_id() & 3u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t po = full ? quad_peer_off(off, i) + 16u * m : off + 16u * (uint32_t)i;
+        *reinterpret_cast<uint4 *>(seg + po + 64u * (uint32_t)b) =
+            make_uint4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
+    }
 }
 
 // Store the 16-B pieces of chunk b that overlap the ciphered range [off, end).
@@ -1531,22 +1674,36 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         ctr_chunk_pre(lds, tb, rk, cp, cs, 0, c);
         store_chunk(pkt, 0, cs, c);
         const int hq = cs.off >> 4;
+        const int nbw = SRTP_PRIO ? wave_max_i(B) : 0;
         for (b = 1; b < B; b++) {
             // packets past ~4 KB: the generic loop below finishes them
             if (ctr_pre_exhausted(4 * b - hq)) break;
+            progress_prio(b, nbw);
             uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
             uint32_t K[16], d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
             ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+#if SRTP_COALESCE
+            const bool full = quad_full();
+            load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
+#else
             load_chunk_full(pkt, b, d);
+#endif
             ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
+#if SRTP_COALESCE
+            load_chunk_quad_finish(full, d);
+#endif
             ctr_apply_wave(cs, b, K, d);
-            store_chunk_full(pkt, b, d);
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k];
+#if SRTP_COALESCE
+            store_chunk_quad(a.seg, a.off[p], b, full, d);
+#else
+            store_chunk_full(pkt, b, d);
+#endif
         }
 
         inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
@@ -1595,17 +1752,23 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 
 #ifdef SRTP_STAMPS
 // Diagnostic build (tools/stamps.sh): per wave, the realtime clock (100 MHz) at
-// kernel entry, after the T-table fill and at the end, plus the XCC id.
+// kernel entry, after the T-table fill and at the end (slots 0-2), the XCC id
+// (slot 3) and the shader clock counter at the same points (slots 4-6).
 #define STAMP(slot)                                                                        \
     do {                                                                                   \
         const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                     \
-        if ((threadIdx.x & 63u) == 0u)                                                     \
-            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 4 + (slot)] = _t; \
+        const unsigned long long _c = __builtin_amdgcn_s_memtime();                         \
+        if ((threadIdx.x & 63u) == 0u) {                                                   \
+            unsigned long long *_s =                                                       \
+                a.stamps + (size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8; \
+            _s[(slot)] = _t;                                                               \
+            _s[4 + (slot)] = _c;                                                           \
+        }                                                                                  \
     } while (0)
 #define STAMP_XCC()                                                                        \
     do {                                                                                   \
         if ((threadIdx.x & 63u) == 0u)                                                     \
-            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 4 + 3] = \
+            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 3] = \
                 (unsigned long long)__smid();                                             \
     } while (0)
 #else
@@ -1755,21 +1918,35 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             ctr_chunk_pre(lds, tb, rk, cp, cs, 0, d);
             store_chunk(pkt, 0, cs, d); // cs.end = 0 without speculation: no store
         }
+        const int nbw = SRTP_PRIO ? wave_max_i(nb_full) : 0;
         for (b = 1; b < nb_full; b++) {
             if (ctr_pre_exhausted(4 * b - hq)) break; // generic loop finishes
+            progress_prio(b, nbw);
             uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
             uint32_t K[16], d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
             ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+#if SRTP_COALESCE
+            const bool full = quad_full();
+            load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
+#else
             load_chunk_full(pkt, b, d);
+#endif
             ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
+#if SRTP_COALESCE
+            load_chunk_quad_finish(full, d);
+#endif
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k]; // ciphertext of chunk b, hashed next
             ctr_apply_wave(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
+#if SRTP_COALESCE
+            store_chunk_quad(a.seg, a.off[p], b, full, d);
+#else
             store_chunk_full(pkt, b, d);
+#endif
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);

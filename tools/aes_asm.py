@@ -122,7 +122,7 @@ def emit(name, blocks, last, tables=4):
 SHA_K = [0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xCA62C1D6]
 
 
-def sha_rounds(t0, n=4):
+def sha_rounds(t0, n=4, multi_k=False):
     """gfx950 instructions of SHA-1 rounds t0 .. t0+n-1 on the role registers
     %[ha]..%[he] (a..e on entry) and the 16-word schedule %[w0..15]; the
     working variable that becomes the new `a` is written in place of `e`,
@@ -142,7 +142,8 @@ def sha_rounds(t0, n=4):
         L.append(f"v_bitop3_b32 %[sf], {b}, {c}, {d} bitop3:{op:#x}")
         L.append(f"v_alignbit_b32 %[sr], {a}, {a}, 27")
         L.append(f"v_add3_u32 {e}, {e}, %[sf], %[sr]")
-        L.append(f"v_add3_u32 {e}, {e}, %[sk], {w0}")
+        sk = f"%[sk{t // 20}]" if multi_k else "%[sk]"
+        L.append(f"v_add3_u32 {e}, {e}, {sk}, {w0}")
         L.append(f"v_alignbit_b32 {b}, {b}, {b}, 2")
         regs = [e, a, b, c, d]
     return L
@@ -196,5 +197,119 @@ def emit_sha(name, blocks, last, t0, tables=4):
     # roles after 4 rounds: a in v[1], b in v[2], c in v[3], d in v[4], e in v[0]
     s.append("    const uint32_t e_ = v[0];")
     s.append("    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4]; v[4] = e_;")
+    s.append("}")
+    return "\n".join(s)
+
+
+# ------------------------------------------- skewed multi-round pipeline + SHA
+def pipe_body(blocks, n_mid, sha, last=True):
+    """n_mid middle rounds (+ the last round if `last`) on the blocks, with no
+    drain between rounds: lookup groups are issued in the order
+    (round r, block 0), (round r, block 1), (round r+1, block 0), ... and a
+    group's 16 addresses are computed as soon as the same block's previous
+    group has landed and been folded -- while the other block's group is still
+    in flight -- so each wave keeps up to 15 LDS reads outstanding through all
+    rounds.  `sha` (a list of SHA-1 instructions) is spread over the wait
+    points.  Round keys: %[k<r>_<j>] for round index r = 0 .. n_rounds-1."""
+    nb = len(blocks)
+    n_rounds = n_mid + (1 if last else 0)
+    groups = [(r, i) for r in range(n_rounds) for i in range(nb)]
+    L = []
+    issued, landed = 0, -1        # reads issued; highest read index known landed
+    consumed = [0] * len(groups)  # columns folded per group
+    n_waits = 0
+    # reads per group index g: 16g .. 16g+15
+    def fold_available():
+        out = []
+        for g in range(len(groups)):
+            r, i = groups[g]
+            while consumed[g] < 4 and 16 * g + 4 * consumed[g] + 3 <= landed:
+                j = consumed[g]
+                z = blocks[i]
+                a, b, c, d = (f"%[t{16 * i + 4 * j + t}]" for t in range(4))
+                k = f"%[k{r}_{j}]"
+                if last and r == n_rounds - 1:
+                    out += [f"v_perm_b32 {a}, {b}, {a}, %[s4]",
+                            f"v_perm_b32 {c}, {d}, {c}, %[s5]",
+                            f"v_bitop3_b32 %[{z}{j}], {a}, {c}, {k} bitop3:0x96"]
+                else:
+                    out += [f"v_bitop3_b32 {a}, {a}, {b}, {c} bitop3:0x96",
+                            f"v_bitop3_b32 %[{z}{j}], {a}, {d}, {k} bitop3:0x96"]
+                consumed[g] += 1
+        return out
+    # wait points: count them first to spread the SHA stream evenly
+    total_reads = 16 * len(groups)
+    est_waits = total_reads - 15 + len(groups)
+    sha_pos = 0
+    def sha_take(w):
+        nonlocal sha_pos
+        want = min(len(sha), (len(sha) * (w + 1)) // est_waits)
+        out = sha[sha_pos:want]
+        sha_pos = max(sha_pos, want)
+        return out
+    def wait_for(idx):
+        """wait until read index idx has landed"""
+        nonlocal landed, n_waits
+        if idx <= landed:
+            return
+        cnt = issued - 1 - idx  # reads after idx that may stay in flight
+        L.extend(sha_take(n_waits))
+        n_waits += 1
+        L.append(f"s_waitcnt lgkmcnt({min(cnt, MAX_LGKM)})")
+        landed = idx
+        L.extend(fold_available())
+    for g, (r, i) in enumerate(groups):
+        if g >= nb:  # the same block's previous group must be folded
+            wait_for(16 * (g - nb) + 15)
+            assert consumed[g - nb] == 4
+        z = blocks[i]
+        for j in range(4):
+            for t in range(4):
+                L.append(f"v_perm_b32 %[t{16 * i + 4 * j + t}], %[{z}{(j + t) & 3}], %[b{t}], %[s{t}]")
+        for q in range(16):
+            if issued - (landed + 1) >= MAX_LGKM:
+                wait_for(issued - MAX_LGKM)
+            L.append(f"ds_read_b32 %[t{16 * i + q}], %[t{16 * i + q}]")
+            issued += 1
+    wait_for(issued - 1)
+    L.extend(sha[sha_pos:])
+    assert all(c == 4 for c in consumed)
+    return L
+
+
+def emit_pipe_sha(name, blocks, n_mid, t0, n_sha, last=True):
+    """Rounds (n_mid middle + last) of the block pair as one skewed pipeline
+    with SHA-1 rounds t0 .. t0+n_sha-1 spread over its waits.  Round keys come
+    from rkr[4 * r + j]."""
+    sha = sha_rounds(t0, n_sha, multi_k=True)
+    body = pipe_body(blocks, n_mid, sha, last)
+    nb = len(blocks)
+    n_rounds = n_mid + (1 if last else 0)
+    args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
+    s = [f"template <> __device__ __forceinline__ void {name}<{t0}>({args}, const uint32_t bs[4],",
+         "        const uint32_t *__restrict__ rkr, uint32_t v[5], uint32_t w[16]) {",
+         f"    uint32_t t[{16 * nb}], sf, sr, sx;"]
+    s.append("    asm volatile(")
+    for ln in body:
+        s.append(f'        "{ln}\\n"')
+    outs = [f'[{z}{i}] "+v"({z}[{i}])' for z in blocks for i in range(4)]
+    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(16 * nb)]
+    outs += [f'[h{r}] "+v"(v[{i}])' for i, r in enumerate("abcde")]
+    outs += [f'[w{i}] "+v"(w[{i}])' for i in range(16)]
+    outs += ['[sf] "=&v"(sf)', '[sr] "=&v"(sr)', '[sx] "=&v"(sx)']
+    ins = [f'[b{i}] "v"(bs[{i}])' for i in range(4)]
+    ins += [f'[s{i}] "s"({SEL4[i]})' for i in range(4)]
+    if last:
+        ins += ['[s4] "s"(0x0c0c0601u)', '[s5] "s"(0x04000c0cu)']
+    ins += [f'[k{r}_{j}] "s"(rkr[{4 * r + j}])' for r in range(n_rounds) for j in range(4)]
+    ks = sorted({(t0 + q) // 20 for q in range(n_sha)})
+    ins += [f'[sk{k}] "s"({SHA_K[k]:#010x}u)' for k in ks]
+    s.append("        : " + ",\n          ".join(outs))
+    s.append("        : " + ",\n          ".join(ins))
+    s.append('        : "memory");')
+    # after n_sha rounds register i holds role (i + n_sha) mod 5
+    s.append(f"    const uint32_t o_[5] = {{v[0], v[1], v[2], v[3], v[4]}};")
+    s.append(f"#pragma unroll")
+    s.append(f"    for (int i = 0; i < 5; i++) v[(i + {n_sha}) % 5] = o_[i];")
     s.append("}")
     return "\n".join(s)

@@ -3,7 +3,8 @@ SRTP_STAMPS: libsrtp_stamps.so, built by tools/stamps.sh).
 
 Runs the bench workload (2^18 x 1200-B packets, 10k SSRCs) serially for a few
 bundles, then reads each wave's realtime-clock stamps (100 MHz) of the last
-launch: entry, after the LDS T-table fill, end; and __smid (XCC / SE / CU).
+launch: entry, after the LDS T-table fill, end; __smid (XCC / SE / CU); and the
+shader clock counter (s_memtime) at the same points, for the clock the waves ran at.
 Prints the spread of wave start / end times over the launch, per XCC."""
 import ctypes as C
 import json
@@ -54,9 +55,9 @@ def main():
     waves = n // 64
     out = {}
     for name, rev in (("k_protect", 0), ("k_unprotect", 1)):
-        buf = np.zeros(waves * 4, np.uint64)
+        buf = np.zeros(waves * 8, np.uint64)
         N.check(L_.srtp_debug_stamps(eng.h, rev, buf.ctypes.data, waves), eng.h, "stamps")
-        t = buf.reshape(waves, 4)
+        t = buf.reshape(waves, 8)
         t0 = t[:, 0].min()
         start = (t[:, 0] - t0) / 100.0  # us
         filled = (t[:, 1] - t0) / 100.0
@@ -79,6 +80,10 @@ def main():
             per[int(x)] = {"waves": int(m.sum()), "end_median": float(np.median(end[m])),
                            "end_max": float(end[m].max()), "busy_median": float(np.median((end - filled)[m]))}
         r["per_xcc"] = per
+        # shader clock over the wave's life / realtime (100 MHz): the clock it ran at
+        dclk = (t[:, 6] - t[:, 4]).astype(np.float64)
+        dt = (t[:, 2] - t[:, 0]).astype(np.float64) / 100.0  # us
+        r["shader_clock_mhz"] = np.percentile(dclk / np.maximum(dt, 1e-3), [0, 50, 100]).round(0).tolist()
         r["smid_distinct"] = int(len(np.unique(smid)))
         out[name] = r
     print(json.dumps(out, indent=1))
