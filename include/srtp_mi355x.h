@@ -132,6 +132,8 @@ typedef struct {
 int srtp_engine_opts_default(srtp_engine_opts *opts);
 int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out);
 void srtp_engine_destroy(srtp_engine *e);
+/* the options the engine was created with */
+int srtp_engine_get_opts(srtp_engine *e, srtp_engine_opts *out);
 const char *srtp_engine_last_error(srtp_engine *e);
 
 int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *master_key,
@@ -263,6 +265,48 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
 int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                          int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes);
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
+
+/* Bundle aggregator over the pipeline: per-packet submits
+ * from any number of threads become bundles.  Replaces the reference's
+ * one-packet-at-a-time calls through the transform chain
+ * (RTPConnectorInputStream.java:425-452 receive, RTPConnectorOutputStream.java
+ * :268-300,652-830 send; each a 1-element array through
+ * SinglePacketTransformer.java:121-216).
+ *
+ * srtp_aggregator_submit copies one packet (len bytes; protect leaves 16
+ * bytes of trailer room) into the open bundle of its direction; a bundle is
+ * sealed when it holds max_packets packets or max_bytes bytes, when its oldest
+ * packet has waited deadline_us, or on srtp_aggregator_flush.  Sealed bundles
+ * run in sealing order; when one completes, `cb` is called (on the
+ * aggregator's dispatch thread) once per packet, in bundle order, with the
+ * packet's cookie, final status (SRTP_STATUS_*; -1 if the bundle could not be
+ * submitted) and processed bytes, valid only during the call.  So packets
+ * of one direction -- and thus of one transformer -- complete in the order
+ * they were accepted.  Every packet is its own 1-element array, as in the
+ * reference: one packet's exception (SRTP_STATUS_ERR_MALFORMED) does not stop
+ * the others, which requires an engine with abort_on_error = 0
+ * (srtp_aggregator_create returns SRTP_EINVAL otherwise).  When every slot is
+ * sealed or in flight, submit blocks (backpressure).  flush seals the open
+ * bundles and waits until every accepted packet has completed; destroy does
+ * the same, then stops the threads. */
+typedef struct srtp_aggregator srtp_aggregator;
+typedef struct {
+    uint32_t max_packets; /* per bundle, default 1<<14 */
+    size_t max_bytes;     /* per bundle (segment), default 24 MB */
+    uint32_t deadline_us; /* default 1000 */
+    int32_t depth;        /* pipeline slots (3..16), default 4 */
+} srtp_aggregator_opts;
+typedef void (*srtp_aggregator_cb)(void *user, uint64_t cookie, int32_t status, const uint8_t *data,
+                                   uint32_t len);
+int srtp_aggregator_opts_default(srtp_aggregator_opts *opts);
+int srtp_aggregator_create(srtp_engine *e, const srtp_aggregator_opts *opts, srtp_aggregator_cb cb,
+                           void *user, srtp_aggregator **out);
+int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt,
+                           uint32_t len, uint32_t flags, uint64_t cookie);
+int srtp_aggregator_flush(srtp_aggregator *a);
+int srtp_aggregator_stats(srtp_aggregator *a, uint64_t *accepted, uint64_t *completed,
+                          uint64_t *bundles);
+void srtp_aggregator_destroy(srtp_aggregator *a);
 
 /* In-process multi-GPU dispatcher (SURVEY.md 8b engine_create(devices, opts),
  * 8e): one engine per shard, shard i on device devices[i] (a device may host

@@ -6,12 +6,12 @@ profiles):
 bundles of packets from many SSRC contexts are protected/unprotected by
 hand-written gfx950 kernels behind the C ABI in include/srtp_mi355x.h.
 """
-from .srtp import (PacketTransformer, RawPacket, SRTCPTransformer, SRTPContextFactory,  # noqa: F401
-                   SRTPDispatcher,
+from .srtp import (PacketTransformer, RawPacket, SRTCPTransformer, SRTPAggregator,  # noqa: F401
+                   SRTPContextFactory, SRTPDispatcher,
                    SRTPEngine, SRTPPipeline, SRTPPolicy, SRTPTransformer, SRTPTransformException, pack,
                    profile_policies, transform_bundle)
 from . import _native  # noqa: F401
 
-__all__ = ["PacketTransformer", "RawPacket", "SRTCPTransformer", "SRTPContextFactory", "SRTPDispatcher", "SRTPEngine",
+__all__ = ["PacketTransformer", "RawPacket", "SRTCPTransformer", "SRTPAggregator", "SRTPContextFactory", "SRTPDispatcher", "SRTPEngine",
            "SRTPPipeline", "SRTPPolicy", "SRTPTransformer", "SRTPTransformException", "pack", "profile_policies",
            "transform_bundle"]

@@ -43,6 +43,9 @@ EXPORTED = [
     "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host",
     "srtp_dispatch_get_context_state", "srtp_dispatch_set_context_state", "srtp_dispatch_stats",
     "srtp_tls_export_keying_material", "srtp_dtls_profile_keys", "srtp_dtls_transformer_create",
+    "srtp_engine_get_opts", "srtp_aggregator_opts_default", "srtp_aggregator_create",
+    "srtp_aggregator_submit", "srtp_aggregator_flush", "srtp_aggregator_stats",
+    "srtp_aggregator_destroy",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -89,6 +92,14 @@ class DtlsKeys(C.Structure):
                 ("salt_len", C.c_int32), ("keying_material_len", C.c_int32),
                 ("client_key", C.c_uint8 * 16), ("server_key", C.c_uint8 * 16),
                 ("client_salt", C.c_uint8 * 14), ("server_salt", C.c_uint8 * 14)]
+
+
+class AggregatorOpts(C.Structure):
+    _fields_ = [("max_packets", C.c_uint32), ("max_bytes", C.c_size_t), ("deadline_us", C.c_uint32),
+                ("depth", C.c_int32)]
+
+
+AGG_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(C.c_uint8), C.c_uint32)
 
 
 class PipelineSlot(C.Structure):
@@ -141,6 +152,15 @@ def lib() -> C.CDLL:
     L.srtp_pipeline_submit.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t]
     L.srtp_pipeline_wait.argtypes = [vp, i32]
     L.srtp_engine_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.srtp_engine_get_opts.argtypes = [vp, C.POINTER(EngineOpts)]
+    L.srtp_aggregator_opts_default.argtypes = [C.POINTER(AggregatorOpts)]
+    L.srtp_aggregator_create.argtypes = [vp, C.POINTER(AggregatorOpts), AGG_CB, vp, C.POINTER(vp)]
+    L.srtp_aggregator_submit.argtypes = [vp, i32, i32, C.c_char_p, u32, u32, C.c_uint64]
+    L.srtp_aggregator_flush.argtypes = [vp]
+    L.srtp_aggregator_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64)]
+    L.srtp_aggregator_destroy.argtypes = [vp]
+    L.srtp_aggregator_destroy.restype = None
     L.srtp_tls_export_keying_material.argtypes = [i32, C.c_char_p, i32, C.c_char_p, C.c_char_p,
                                                   C.c_char_p, vp, i32]
     L.srtp_dtls_profile_keys.argtypes = [i32, C.c_char_p, i32, C.POINTER(DtlsKeys)]

@@ -1009,6 +1009,12 @@ void srtp_pipeline_destroy(srtp_pipeline *pl) {
     if (pl) pipeline_free(pl);
 }
 
+int srtp_engine_get_opts(srtp_engine *e, srtp_engine_opts *out) {
+    if (!e || !out) return SRTP_EINVAL;
+    *out = e->opts;
+    return SRTP_OK;
+}
+
 int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *out) {
     if (!pl || !out || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
     *out = pl->slots[(size_t)slot].h;

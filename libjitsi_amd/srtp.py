@@ -426,6 +426,55 @@ class SRTPDispatcher:
         return status
 
 
+class SRTPAggregator:
+    """Per-packet submits from many threads -> bundles (srtp_aggregator_*,
+    SURVEY.md 8f.2).  ``callback(cookie, status, data)`` runs on the
+    aggregator's dispatch thread once per packet, in bundle order; packets of
+    one direction complete in the order they were accepted.  The engine must
+    have abort_on_error=False: each packet is its own 1-element RawPacket[]
+    as in the reference's RTPConnector streams (RTPConnectorInputStream.java
+    :425-452, RTPConnectorOutputStream.java:268-300,652-830)."""
+
+    def __init__(self, engine: "SRTPEngine", callback, max_packets: int = 1 << 14,
+                 max_bytes: int = 24 << 20, deadline_us: int = 1000, depth: int = 4):
+        self.engine = engine
+        o = N.AggregatorOpts(max_packets, max_bytes, deadline_us, depth)
+
+        def _cb(user, cookie, status, data, length):
+            callback(int(cookie), int(status), C.string_at(data, length) if length else b"")
+
+        self._cb = N.AGG_CB(_cb)  # kept alive with the aggregator
+        h = C.c_void_p()
+        N.check(N.lib().srtp_aggregator_create(engine.h, C.byref(o), self._cb, None, C.byref(h)),
+                engine.h, "srtp_aggregator_create")
+        self.h = h
+
+    def submit(self, reverse: bool, transformer: "_SRTPBase", data: bytes, flags: int = 0,
+               cookie: int = 0) -> None:
+        data = bytes(data)
+        N.check(N.lib().srtp_aggregator_submit(self.h, int(reverse), transformer.tid, data,
+                                               len(data), flags, cookie), None, "submit")
+
+    def flush(self) -> None:
+        N.check(N.lib().srtp_aggregator_flush(self.h), self.engine.h, "flush")
+
+    def stats(self) -> dict:
+        a, c, b = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        N.lib().srtp_aggregator_stats(self.h, C.byref(a), C.byref(c), C.byref(b))
+        return {"accepted": a.value, "completed": c.value, "bundles": b.value}
+
+    def close(self) -> None:
+        if self.h:
+            N.lib().srtp_aggregator_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SRTPContextFactory:
     """SRTPContextFactory(sender, masterKey, masterSalt, srtpPolicy, srtcpPolicy)."""
 
