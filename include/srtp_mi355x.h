@@ -364,6 +364,11 @@ int srtp_dispatch_stats(srtp_dispatch *d, srtp_stats *out);
 int srtp_derive_session_keys(const uint8_t master_key[16], const uint8_t master_salt[14],
                              int32_t rtcp, uint8_t enc_key[16], uint8_t auth_key[20],
                              uint8_t salt_key[14]);
+/* The same for a 16- or 32-byte master key (AES-128 / AES-256 PRF, RFC 6188
+ * 4.1): enc_key receives key_len bytes. */
+int srtp_derive_session_keys_n(const uint8_t *master_key, int32_t key_len,
+                               const uint8_t master_salt[14], int32_t rtcp, uint8_t *enc_key,
+                               uint8_t auth_key[20], uint8_t salt_key[14]);
 
 /* DTLS-SRTP keying (control plane, host only): what
  * DtlsPacketTransformer.initializeSRTPTransformer does after the handshake

@@ -43,7 +43,7 @@ EXPORTED = [
     "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host",
     "srtp_dispatch_get_context_state", "srtp_dispatch_set_context_state", "srtp_dispatch_stats",
     "srtp_tls_export_keying_material", "srtp_dtls_profile_keys", "srtp_dtls_transformer_create",
-    "srtp_engine_get_opts", "srtp_aggregator_opts_default", "srtp_aggregator_create",
+    "srtp_engine_get_opts", "srtp_derive_session_keys_n", "srtp_aggregator_opts_default", "srtp_aggregator_create",
     "srtp_aggregator_submit", "srtp_aggregator_flush", "srtp_aggregator_stats",
     "srtp_aggregator_destroy",
 ]
@@ -143,6 +143,7 @@ def lib() -> C.CDLL:
     L.srtp_engine_set_timing.argtypes = [vp, i32]
     L.srtp_engine_read_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.srtp_derive_session_keys.argtypes = [pu8, pu8, i32, pu8, pu8, pu8]
+    L.srtp_derive_session_keys_n.argtypes = [C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, pu8]
     L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
     L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_pipeline_create.argtypes = [vp, u32, C.c_size_t, i32, C.POINTER(vp)]

@@ -26,8 +26,8 @@ struct srtp_engine {
     std::string last_error;
 
     KeySet *d_keysets = nullptr;
-    F8Keys *d_f8keys = nullptr; // IV' keys of AES-F8 key sets (same index)
-    uint32_t n_f8 = 0;          // AES-F8 key sets created: k_f8 runs only when > 0
+    ExtKeys *d_extkeys = nullptr; // round keys of the k_ext key sets (same index)
+    uint32_t n_ext = 0;           // AES-F8 / AES-256-CM key sets created: k_ext runs only when > 0
     uint32_t n_keysets = 0, max_keysets = 0;
     FactoryRec *d_factories = nullptr;
     std::vector<FactoryRec> factories;
@@ -107,16 +107,20 @@ void dfree(void *p) {
     if (p) (void)hipFree(p);
 }
 
-// Profiles the engine implements: AES_CM_128 or NULL cipher x HMAC_SHA1 or NULL
-// auth (SRTPPolicy.java; profile tables DtlsPacketTransformer.java:574-612,
-// SDesTransformEngine.java:129-147).  Tag length <= 12 keeps the reference's
-// readRegionToBuff in range for every packet of >= 12 bytes.
+// Profiles the engine implements: AES-CM with a 128- or 256-bit key, AES-F8
+// (128), or NULL cipher x HMAC_SHA1 or NULL auth (SRTPPolicy.java; profile
+// tables DtlsPacketTransformer.java:574-612, SDesTransformEngine.java:129-147;
+// AES-256-CM is what SRTPCryptoContext does with encKeyLength 32, e.g. from
+// ZRTP's AES3, ZRTPTransformEngine.java:873-900).  Tag length <= 12 keeps the
+// reference's readRegionToBuff in range for every packet of >= 12 bytes.
 bool policy_ok(const srtp_policy *p, bool rtcp) {
     if (!p) return false;
     if (p->enc_type != SRTP_NULL_ENCRYPTION && p->enc_type != SRTP_AESCM_ENCRYPTION &&
         p->enc_type != SRTP_AESF8_ENCRYPTION)
         return false;
-    if (p->enc_type != SRTP_NULL_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+    if (p->enc_type != SRTP_NULL_ENCRYPTION && p->salt_key_len != 14) return false;
+    if (p->enc_type == SRTP_AESF8_ENCRYPTION && p->enc_key_len != 16) return false;
+    if (p->enc_type == SRTP_AESCM_ENCRYPTION && p->enc_key_len != 16 && p->enc_key_len != 32)
         return false;
     // SRTCP F8 ciphers [8, 8 + length - 4 - tag) (SRTCPCryptoContext :285-291):
     // inside the packet only with an HMAC trailer of >= 4 tag bytes after it
@@ -130,17 +134,33 @@ bool policy_ok(const srtp_policy *p, bool rtcp) {
     return true;
 }
 
-void build_keyset(const uint8_t mk[16], const uint8_t ms[14], bool rtcp, const srtp_policy *pol,
-                  KeySet *ks, F8Keys *f8) {
+// Master key bytes a policy uses (BaseSRTPCryptoContext copies encKeyLength
+// of them, :187-190): 32 for AES-256-CM, else 16 (the NULL cipher keeps the
+// AES-128 PRF, see srtp_factory_create).
+int master_key_len(const srtp_policy *pol) {
+    return pol->enc_type == SRTP_AESCM_ENCRYPTION && pol->enc_key_len == 32 ? 32 : 16;
+}
+
+void build_keyset(const uint8_t *mk, const uint8_t ms[14], bool rtcp, const srtp_policy *pol,
+                  KeySet *ks, ExtKeys *ext) {
     memset(ks, 0, sizeof *ks);
-    memset(f8, 0, sizeof *f8);
-    uint8_t enc[16], auth[20], salt[16] = {0};
-    derive_session_keys(mk, ms, rtcp, enc, auth, salt);
-    aes128_expand_le(enc, ks->rk);
+    memset(ext, 0, sizeof *ext);
+    const int klen = master_key_len(pol);
+    uint8_t enc[32], auth[20], salt[16] = {0};
+    // RFC 3711 4.3 with the AES-128 or AES-256 PRF (RFC 6188 4.1), as
+    // deriveSrtpKeys :393-447 does with a key of encKeyLength bytes
+    derive_session_keys_n(mk, klen, ms, rtcp, enc, auth, salt);
+    if (klen == 32) { // AES-256-CM: k_ext
+        ext->nr = aes_expand_le(enc, 32, ext->rk);
+        ks->ext = 1;
+    } else {
+        aes128_expand_le(enc, ks->rk);
+    }
     if (pol->enc_type == SRTP_AESF8_ENCRYPTION) { // SRTPCipherF8.deriveForIV :66-95
         uint8_t m[16];
         for (int i = 0; i < 16; i++) m[i] = (uint8_t)(enc[i] ^ (i < 14 ? salt[i] : 0x55));
-        aes128_expand_le(m, f8->rk);
+        ext->nr = aes_expand_le(m, 16, ext->rk);
+        ks->ext = 1;
         memset(m, 0, sizeof m);
     }
     hmac_sha1_midstates(auth, ks->ipad, ks->opad);
@@ -383,7 +403,7 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
         e->ctx_bits = 0;
         while ((1u << e->ctx_bits) < e->ctx_cap) e->ctx_bits++;
         if (dalloc(&e->d_keysets, e->max_keysets) != hipSuccess ||
-            dalloc(&e->d_f8keys, e->max_keysets) != hipSuccess ||
+            dalloc(&e->d_extkeys, e->max_keysets) != hipSuccess ||
             dalloc(&e->d_factories, o.max_factories) != hipSuccess ||
             dalloc(&e->d_transformers, o.max_transformers) != hipSuccess ||
             dalloc(&e->d_ctx_keys, e->ctx_cap) != hipSuccess ||
@@ -416,15 +436,15 @@ void srtp_engine_destroy(srtp_engine *e) {
     (void)quiesce(e);
     if (e->d_keysets) // zero session keys before release
         (void)hipMemset(e->d_keysets, 0, (size_t)e->max_keysets * sizeof(KeySet));
-    if (e->d_f8keys)
-        (void)hipMemset(e->d_f8keys, 0, (size_t)e->max_keysets * sizeof(F8Keys));
+    if (e->d_extkeys)
+        (void)hipMemset(e->d_extkeys, 0, (size_t)e->max_keysets * sizeof(ExtKeys));
     free_scratch(e);
     for (auto &m : e->marks) {
         (void)hipEventDestroy(m.a);
         (void)hipEventDestroy(m.b);
     }
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
-    void *ptrs[] = {e->d_keysets, e->d_f8keys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
+    void *ptrs[] = {e->d_keysets, e->d_extkeys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
                     e->e_min, e->ctl, e->d_count, e->d_counters, e->h_seg, e->h_off, e->h_len,
                     e->h_cap, e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
@@ -443,20 +463,21 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
     GUARD(e);
     // NULL-cipher profiles keep a 16-B master key + 14-B salt for the RFC 3711
     // 4.3 PRF (the reference throws there: SURVEY Q15) -- parity unpinned.
-    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp_pol, false) || !policy_ok(srtcp_pol, true))
+    if (!policy_ok(srtp_pol, false) || !policy_ok(srtcp_pol, true))
         return fail(e, SRTP_EPOLICY, "unsupported SRTP policy");
+    if (key_len < std::max(master_key_len(srtp_pol), master_key_len(srtcp_pol)) || salt_len < 14)
+        return fail(e, SRTP_EPOLICY, "master key / salt shorter than the policy");
     if (e->factories.size() >= e->opts.max_factories || e->n_keysets + 2 > e->max_keysets)
         return fail(e, SRTP_EFULL, "factory table full");
     KeySet ks[2];
-    F8Keys f8[2];
+    ExtKeys f8[2];
     build_keyset(mk, ms, false, srtp_pol, &ks[0], &f8[0]);
     build_keyset(mk, ms, true, srtcp_pol, &ks[1], &f8[1]);
     HIPCHK(e, hipMemcpy(e->d_keysets + e->n_keysets, ks, sizeof ks, hipMemcpyHostToDevice));
-    HIPCHK(e, hipMemcpy(e->d_f8keys + e->n_keysets, f8, sizeof f8, hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_extkeys + e->n_keysets, f8, sizeof f8, hipMemcpyHostToDevice));
+    e->n_ext += (uint32_t)(ks[0].ext + ks[1].ext);
     memset(ks, 0, sizeof ks);
     memset(f8, 0, sizeof f8);
-    e->n_f8 += (srtp_pol->enc_type == SRTP_AESF8_ENCRYPTION) +
-               (srtcp_pol->enc_type == SRTP_AESF8_ENCRYPTION);
     FactoryRec f;
     f.open = 1;
     f.ks_rtp = (int32_t)e->n_keysets;
@@ -557,7 +578,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (e->have_last && e->last_stream != s) HIPCHK(e, hipStreamWaitEvent(s, e->ev_last, 0));
     BundleArgs a{};
     a.keysets = e->d_keysets;
-    a.f8keys = e->d_f8keys;
+    a.extkeys = e->d_extkeys;
     a.factories = e->d_factories;
     a.transformers = e->d_transformers;
     a.ctx_keys = e->d_ctx_keys;
@@ -626,11 +647,11 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
         HIPCHK(e, launch_unprotect_fix(a, s));
-        if (e->n_f8) HIPCHK(e, launch_f8(a, s));
+        if (e->n_ext) HIPCHK(e, launch_ext(a, s));
     } else {
         StageTimer t(e, s, SRTP_STAGE_PROTECT);
         HIPCHK(e, launch_protect(a, s));
-        if (e->n_f8) HIPCHK(e, launch_f8(a, s));
+        if (e->n_ext) HIPCHK(e, launch_ext(a, s));
     }
     HIPCHK(e, hipEventRecord(e->ev_last, s));
     e->last_stream = s;
@@ -920,6 +941,13 @@ int srtp_derive_session_keys(const uint8_t mk[16], const uint8_t ms[14], int32_t
                              uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]) {
     if (!mk || !ms || !enc || !auth || !salt) return SRTP_EINVAL;
     derive_session_keys(mk, ms, rtcp != 0, enc, auth, salt);
+    return SRTP_OK;
+}
+
+int srtp_derive_session_keys_n(const uint8_t *mk, int32_t key_len, const uint8_t ms[14], int32_t rtcp,
+                               uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+    if (!mk || !ms || !enc || !auth || !salt || (key_len != 16 && key_len != 32)) return SRTP_EINVAL;
+    derive_session_keys_n(mk, key_len, ms, rtcp != 0, enc, auth, salt);
     return SRTP_OK;
 }
 

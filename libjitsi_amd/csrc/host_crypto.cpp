@@ -1,4 +1,4 @@
-// host_crypto.cpp -- see host_crypto.h.  FIPS-197 AES-128 and FIPS 180-4
+// host_crypto.cpp -- see host_crypto.h.  FIPS-197 AES-128/256 and FIPS 180-4
 // SHA-1, written for clarity (control plane only).
 #include "host_crypto.h"
 
@@ -59,37 +59,50 @@ void aes_te0_le(uint32_t te0[256]) {
     }
 }
 
-void aes128_expand_le(const uint8_t key[16], uint32_t rk[44]) {
+// FIPS-197 5.2 key expansion for Nk = 4 (AES-128) or 8 (AES-256) words.
+int aes_expand_le(const uint8_t *key, int key_len, uint32_t rk[60]) {
     const uint8_t *S = sbox().s;
-    uint8_t w[176];
-    memcpy(w, key, 16);
+    const int nk = key_len / 4, nr = nk + 6, total = 4 * (nr + 1);
+    uint8_t w[240];
+    memcpy(w, key, (size_t)key_len);
     uint8_t rcon = 1;
-    for (int i = 16; i < 176; i += 4) {
-        uint8_t t[4] = {w[i - 4], w[i - 3], w[i - 2], w[i - 1]};
-        if (i % 16 == 0) {
+    for (int i = nk; i < total; i++) {
+        uint8_t t[4] = {w[4 * i - 4], w[4 * i - 3], w[4 * i - 2], w[4 * i - 1]};
+        if (i % nk == 0) {
             uint8_t t0 = t[0];
             t[0] = (uint8_t)(S[t[1]] ^ rcon);
             t[1] = S[t[2]];
             t[2] = S[t[3]];
             t[3] = S[t0];
             rcon = xtime(rcon);
+        } else if (nk > 6 && i % nk == 4) {
+            for (int k = 0; k < 4; k++) t[k] = S[t[k]];
         }
-        for (int k = 0; k < 4; k++) w[i + k] = (uint8_t)(w[i - 16 + k] ^ t[k]);
+        for (int k = 0; k < 4; k++) w[4 * i + k] = (uint8_t)(w[4 * (i - nk) + k] ^ t[k]);
     }
-    for (int i = 0; i < 44; i++)
+    for (int i = 0; i < total; i++)
         rk[i] = (uint32_t)w[4 * i] | ((uint32_t)w[4 * i + 1] << 8) | ((uint32_t)w[4 * i + 2] << 16) |
                 ((uint32_t)w[4 * i + 3] << 24);
+    memset(w, 0, sizeof w);
+    return nr;
 }
 
-void aes128_encrypt_block(const uint32_t rk[44], const uint8_t in[16], uint8_t out[16]) {
+void aes128_expand_le(const uint8_t key[16], uint32_t rk[44]) {
+    uint32_t t[60];
+    aes_expand_le(key, 16, t);
+    memcpy(rk, t, 44 * 4);
+    memset(t, 0, sizeof t);
+}
+
+void aes_encrypt_block_nr(const uint32_t *rk, int nr, const uint8_t in[16], uint8_t out[16]) {
     const uint8_t *S = sbox().s;
     uint8_t st[16];
     for (int i = 0; i < 16; i++) st[i] = (uint8_t)(in[i] ^ (rk[i / 4] >> (8 * (i % 4))));
-    for (int r = 1; r <= 10; r++) {
+    for (int r = 1; r <= nr; r++) {
         uint8_t t[16];
         for (int c = 0; c < 4; c++)
             for (int row = 0; row < 4; row++) t[4 * c + row] = S[st[4 * ((c + row) % 4) + row]];
-        if (r != 10) {
+        if (r != nr) {
             for (int c = 0; c < 4; c++) {
                 uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
                 t[4 * c + 0] = (uint8_t)(xtime(a0) ^ (xtime(a1) ^ a1) ^ a2 ^ a3);
@@ -101,6 +114,10 @@ void aes128_encrypt_block(const uint32_t rk[44], const uint8_t in[16], uint8_t o
         for (int i = 0; i < 16; i++) st[i] = (uint8_t)(t[i] ^ (rk[4 * r + i / 4] >> (8 * (i % 4))));
     }
     memcpy(out, st, 16);
+}
+
+void aes128_encrypt_block(const uint32_t rk[44], const uint8_t in[16], uint8_t out[16]) {
+    aes_encrypt_block_nr(rk, 10, in, out);
 }
 
 void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {
@@ -123,13 +140,13 @@ void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {
 }
 
 // SRTPCipherCTR.getCipherStream (:68-92) for the short key-derivation streams.
-static void cipher_stream(const uint32_t rk[44], uint8_t *out, int length, const uint8_t iv[16]) {
+static void cipher_stream(const uint32_t *rk, int nr, uint8_t *out, int length, const uint8_t iv[16]) {
     uint8_t in[16], blk[16];
     memcpy(in, iv, 14);
     for (int ctr = 0; ctr * 16 < length; ctr++) {
         in[14] = (uint8_t)(ctr >> 8);
         in[15] = (uint8_t)ctr;
-        aes128_encrypt_block(rk, in, blk);
+        aes_encrypt_block_nr(rk, nr, in, blk);
         int n = length - ctr * 16 < 16 ? length - ctr * 16 : 16;
         memcpy(out + ctr * 16, blk, (size_t)n);
     }
@@ -137,17 +154,22 @@ static void cipher_stream(const uint32_t rk[44], uint8_t *out, int length, const
 
 void derive_session_keys(const uint8_t mk[16], const uint8_t ms[14], bool rtcp, uint8_t enc[16],
                          uint8_t auth[20], uint8_t salt[14]) {
-    uint32_t rk[44];
-    aes128_expand_le(mk, rk);
+    derive_session_keys_n(mk, 16, ms, rtcp, enc, auth, salt);
+}
+
+void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], bool rtcp,
+                           uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+    uint32_t rk[60];
+    const int nr = aes_expand_le(mk, key_len, rk);
     uint8_t iv[16];
     const int base = rtcp ? 3 : 0;
     uint8_t *outs[3] = {enc, auth, salt};
-    const int lens[3] = {16, 20, 14};
+    const int lens[3] = {key_len, 20, 14};
     for (int lab = 0; lab < 3; lab++) {
         memcpy(iv, ms, 14);
         iv[7] ^= (uint8_t)(base + lab); // computeIv: key_id = label << 48 lands in byte 7
         iv[14] = iv[15] = 0;
-        cipher_stream(rk, outs[lab], lens[lab], iv);
+        cipher_stream(rk, nr, outs[lab], lens[lab], iv);
     }
     memset(rk, 0, sizeof rk);
 }

@@ -11,6 +11,10 @@ namespace srtp {
 // 4i..4i+3 in little-endian order (byte 4i in bits 0..7), the layout the
 // gfx950 T-table rounds use.
 void aes128_expand_le(const uint8_t key[16], uint32_t rk_le[44]);
+// AES-128 (key_len 16) or AES-256 (32) key expansion in the same layout;
+// returns the number of rounds (10 / 14), 4 * (nr + 1) words written.
+int aes_expand_le(const uint8_t *key, int key_len, uint32_t rk_le[60]);
+void aes_encrypt_block_nr(const uint32_t *rk_le, int nr, const uint8_t in[16], uint8_t out[16]);
 void aes128_encrypt_block(const uint32_t rk_le[44], const uint8_t in[16], uint8_t out[16]);
 // SHA-1 compression of one 64-byte block into state[5].
 void sha1_compress(uint32_t state[5], const uint8_t block[64]);
@@ -23,6 +27,10 @@ void aes_te0_le(uint32_t te0[256]);
 // :158-211) with kdr == 0.
 void derive_session_keys(const uint8_t master_key[16], const uint8_t master_salt[14], bool rtcp,
                          uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]);
+// The same with a 16- or 32-byte master key: the PRF is AES-128 / AES-256 and
+// the session encryption key is key_len bytes (RFC 6188 4.1 for AES-256).
+void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], bool rtcp,
+                           uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
 // HMAC-SHA1 ipad/opad midstates for a 20-byte key.
 void hmac_sha1_midstates(const uint8_t key[20], uint32_t ipad[5], uint32_t opad[5]);
 

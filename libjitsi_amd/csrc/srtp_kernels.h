@@ -14,7 +14,7 @@ constexpr int kSortMaxPass = 4; // 8-bit digits: context tables up to 2^31 slots
 struct BundleArgs {
     // engine tables (HBM resident)
     const KeySet *keysets;
-    const F8Keys *f8keys;  // [keysets] IV' keys of the AES-F8 key sets
+    const ExtKeys *extkeys;  // [keysets] round keys of the k_ext key sets (AES-F8 IV', AES-256)
     const FactoryRec *factories;
     const TransformerRec *transformers;
     uint64_t *ctx_keys;
@@ -87,7 +87,7 @@ hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 // AES-F8 packets after the final statuses: protect (F8 + HMAC + trailer) or
 // decryption of the accepted unprotected packets.
-hipError_t launch_f8(const BundleArgs &a, hipStream_t s);
+hipError_t launch_ext(const BundleArgs &a, hipStream_t s);
 hipError_t launch_remove_transformer(uint64_t *ctx_keys, CtxState *ctx, uint32_t cap,
                                      uint32_t tid, hipStream_t s);
 // out[0] += live contexts, out[1] += tombstones

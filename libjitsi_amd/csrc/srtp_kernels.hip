@@ -1809,7 +1809,7 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     const char *lds = reinterpret_cast<const char *>(s_te);
     for_each_keyset(todo, ks_id, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
-        if (sgpr(ks->enc_type) == SRTP_AESF8_ENCRYPTION) return; // k_f8
+        if (sgpr(ks->ext)) return; // AES-F8 / AES-256-CM: k_ext
         protect_one(a, ks, lds, tb, p,
                     sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
                         sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
@@ -1834,7 +1834,8 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     const int T = (int)sgpr(ks->tag_len);
     const bool rtp = sgpr(ks->kind) == SRTP_KIND_RTP;
     const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
-    const bool aes = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
+    // speculative decryption: AES-128-CM only (k_ext deciphers the rest)
+    const bool aes = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext);
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
     Ctr cs;
     cs.off = 0;
@@ -2037,7 +2038,7 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     for_each_keyset(todo, st.ks, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
         unprotect_one(a, ks, lds, tb, p, st,
-                      sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
+                      sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
                           sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
     });
     STAMP(2);
@@ -2070,7 +2071,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
             ks_id = a.ctx[slot].ks;
             const KeySet *ks = a.keysets + ks_id;
             const bool rtp = ks->kind == SRTP_KIND_RTP;
-            if (st == SRTP_STATUS_OK && ks->enc_type == SRTP_AESCM_ENCRYPTION) {
+            if (st == SRTP_STATUS_OK && ks->enc_type == SRTP_AESCM_ENCRYPTION && !ks->ext) {
                 if (rtp) {
                     const uint32_t fl = a.flags ? a.flags[p] : 0u;
                     need = !(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
@@ -2131,9 +2132,10 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     atomicAdd(&a.counters[kCtrRepaired], 1ull);
 }
 
-// ============================================================== k_f8
-// AES-F8 packets (SRTPCipherF8; SDES F8_128_HMAC_SHA1_80), after the final
-// statuses of k_protect / k_unprotect_fix.  Protect: F8 encryption, then the
+// ============================================================== k_ext
+// Packets of the key sets the fused kernels leave out -- AES-F8 (SRTPCipherF8;
+// SDES F8_128_HMAC_SHA1_80) and AES-256-CM -- after the final statuses of
+// k_protect / k_unprotect_fix.  Protect: encryption, then the
 // HMAC over the ciphertext and the trailer.  Unprotect: k_unprotect already
 // checked the tag (HMAC is over the ciphertext, independent of the cipher) and
 // did not speculate, so only the accepted packets are deciphered here.  The F8
@@ -2242,7 +2244,7 @@ __device__ void f8_mac_advance(const F8Job &j, F8Mac &m, int upto) {
 // HMAC inner hash follows the ciphering block by block (the MAC is over the
 // ciphertext), so the packet is read once more only from L1/L2.
 __device__ void f8_pair(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
-                        const F8Keys *f8, const F8Job &j0, const F8Job &j1, bool has1, bool mac,
+                        const ExtKeys *f8, const F8Job &j0, const F8Job &j1, bool has1, bool mac,
                         F8Mac &m0, F8Mac &m1) {
     uint32_t p0[4], p1[4];
 #pragma unroll
@@ -2309,22 +2311,105 @@ __device__ __forceinline__ void f8_trailer(const KeySet *ks, const F8Job &j, F8M
     tag_write(m.h, j.pkt + o, T);
 }
 
-// This packet needs k_f8: final status OK, AES-F8 key set, and for unprotect
+// ------------------------------------------------------------- AES-256-CM
+// SRTPCipherCTR with a 32-byte session key (RFC 6188; BouncyCastle's AES engine
+// runs 14 rounds for it): the same counter blocks as AES-128-CM, so a lane takes
+// one packet and ciphers two blocks at a time; protect feeds the HMAC inner hash
+// as the blocks become final, then writes the trailer, as for F8.
+struct RoundKeys256 {
+    uint32_t k[60];
+};
+
+__device__ __forceinline__ void load_rk256_uniform(const uint32_t *__restrict__ p, RoundKeys256 &rk) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+    for (int i = 0; i < 15; i++) {
+        const uint4 v = q[i];
+        rk.k[4 * i] = sgpr(v.x); rk.k[4 * i + 1] = sgpr(v.y);
+        rk.k[4 * i + 2] = sgpr(v.z); rk.k[4 * i + 3] = sgpr(v.w);
+    }
+}
+
+__device__ __forceinline__ void aes256_encrypt2(const char *__restrict__ lds, const TeBase &tb,
+                                                const RoundKeys256 &rk, uint32_t a[4], uint32_t b[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) { a[j] ^= rk.k[j]; b[j] ^= rk.k[j]; }
+#pragma unroll
+    for (int r = 1; r < 14; r++) aes_round2(lds, tb, rk.k + 4 * r, a, b);
+    aes_last2(lds, tb, rk.k + 56, a, b);
+}
+
+// One AES-256-CM packet's job: the CTR IV and the ciphered region [off, L) --
+// protect: the packet before its trailer; unprotect: after the final shrink
+// (SRTPCryptoContext.processPacketAESCM :491-530, SRTCPCryptoContext :236-265).
+__device__ __forceinline__ F8Job cm_job(const BundleArgs &a, const KeySet *ks, uint32_t p) {
+    F8Job j;
+    j.pkt = a.seg + a.off[p];
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(j.pkt);
+    const int T = (int)sgpr(ks->tag_len);
+    const bool mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    const uint32_t cw = a.w_cw[p];
+    j.rtcp = sgpr(ks->kind) == SRTP_KIND_RTCP;
+    if (!j.rtcp) {
+        make_iv_rtp(ks, hdr, cw, j.iv);
+        j.L = (int)a.len[p] - (!a.reverse && mac ? T : 0);
+        j.off = rtp_header_len(j.pkt, hdr.x & 0xffu, (int)a.cap[p]);
+        j.suffix = cw;
+    } else {
+        make_iv_rtcp(ks, hdr, cw & 0x7FFFFFFFu, j.iv);
+        j.L = (int)a.len[p] - (!a.reverse && mac ? 4 + T : 0);
+        j.off = 8;
+        j.suffix = (cw & 0x7FFFFFFFu) | 0x80000000u;
+    }
+    j.len = j.L - j.off;
+    return j;
+}
+
+__device__ void cm256_one(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
+                          const ExtKeys *ext, const F8Job &j, bool mac) {
+    F8Mac m;
+    if (mac) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) m.h[k] = sgpr(ks->ipad[k]);
+        m.next = 0;
+        f8_mac_advance(j, m, j.off);
+    }
+    const int nb = j.len > 0 ? (j.len + 15) >> 4 : 0;
+    if (nb > 0) {
+        RoundKeys256 rk;
+        load_rk256_uniform(ext->rk, rk);
+        for (int jb = 0; jb < nb; jb += 2) {
+            uint32_t x[4], y[4];
+            ctr_input(j.iv, jb, x);
+            ctr_input(j.iv, jb + 1, y);
+            aes256_encrypt2(lds, tb, rk, x, y);
+            f8_xor_block(j, jb, x);
+            if (jb + 1 < nb) f8_xor_block(j, jb + 1, y);
+            if (mac) f8_mac_advance(j, m, j.off + 16 * min(jb + 2, nb));
+        }
+    }
+    if (mac) {
+        f8_mac_advance(j, m, 0x7fffffff);
+        f8_trailer(ks, j, m);
+    }
+}
+
+// This packet needs k_ext: final status OK, an ext key set, and for unprotect
 // decryption is due (SRTP: no DISCARD/SILENCE flag; SRTCP: the E flag).
-__device__ __forceinline__ bool f8_todo(const BundleArgs &a, uint32_t p, uint32_t *ks_id) {
+__device__ __forceinline__ bool ext_todo(const BundleArgs &a, uint32_t p, uint32_t *ks_id) {
     if (p >= a.n || a.status[p] != SRTP_STATUS_OK) return false;
     const uint32_t slot = a.p_slot[p];
     if (slot == kNoSlot) return false;
     *ks_id = a.ctx[slot].ks;
     const KeySet *ks = a.keysets + *ks_id;
-    if (ks->enc_type != SRTP_AESF8_ENCRYPTION) return false;
+    if (!ks->ext) return false;
     if (!a.reverse) return true;
     if (ks->kind == SRTP_KIND_RTP)
         return !((a.flags ? a.flags[p] : 0u) & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
     return (a.w_cw[p] & 0x80000000u) != 0;
 }
 
-// ============================================================== k_f8
+// ============================================================== k_ext
 // AES-F8 packets (SRTPCipherF8; SDES F8_128_HMAC_SHA1_80), after the final
 // statuses of k_protect / k_unprotect_fix.  Protect: F8 encryption, then the
 // HMAC over the ciphertext and the trailer.  Unprotect: k_unprotect already
@@ -2333,14 +2418,14 @@ __device__ __forceinline__ bool f8_todo(const BundleArgs &a, uint32_t p, uint32_
 // keystream is a chain, so a lane walks packets block by block -- two packets
 // per lane (2g, 2g+1) through the two-block AES rounds when they share a key
 // set (packets of one transformer usually sit side by side), else one by one.
-constexpr int kF8Block = 512; // two packets per lane: 1024 packets per workgroup, one per CU
+constexpr int kExtBlock = 512; // two packets per lane: 1024 packets per workgroup, one per CU
 
-__global__ __launch_bounds__(kF8Block) void k_f8(BundleArgs a) {
+__global__ __launch_bounds__(kExtBlock) void k_ext(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t q0 = 2 * g, q1 = 2 * g + 1;
     uint32_t k0 = 0, k1 = 0;
-    const bool t0 = f8_todo(a, q0, &k0), t1 = f8_todo(a, q1, &k1);
+    const bool t0 = ext_todo(a, q0, &k0), t1 = ext_todo(a, q1, &k1);
     if (!__syncthreads_or(t0 || t1)) return;
     fill_te4(s_te);
     const TeBase tb = te_base();
@@ -2350,12 +2435,18 @@ __global__ __launch_bounds__(kF8Block) void k_f8(BundleArgs a) {
     for_each_keyset(pair || one0, t0 ? k0 : k1, [&](uint32_t ks_u) {
         // pairs, and lone first packets (which take their key set's pass)
         const KeySet *ks = a.keysets + ks_u;
+        if (sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION) { // AES-256-CM
+            const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+            cm256_one(lds, tb, ks, a.extkeys + ks_u, cm_job(a, ks, pair || one0 ? q0 : q1), mac);
+            if (pair) cm256_one(lds, tb, ks, a.extkeys + ks_u, cm_job(a, ks, q1), mac);
+            return;
+        }
         const F8Job j0 = f8_job(a, ks, pair || one0 ? q0 : q1);
         F8Job j1 = j0;
         if (pair) j1 = f8_job(a, ks, q1);
         const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
         F8Mac m0, m1;
-        f8_pair(lds, tb, ks, a.f8keys + ks_u, j0, j1, pair, mac, m0, m1);
+        f8_pair(lds, tb, ks, a.extkeys + ks_u, j0, j1, pair, mac, m0, m1);
         if (mac) {
             f8_trailer(ks, j0, m0);
             if (pair) f8_trailer(ks, j1, m1);
@@ -2363,10 +2454,14 @@ __global__ __launch_bounds__(kF8Block) void k_f8(BundleArgs a) {
     });
     for_each_keyset(one1, k1, [&](uint32_t ks_u) { // lone second packets
         const KeySet *ks = a.keysets + ks_u;
-        const F8Job j = f8_job(a, ks, q1);
         const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+        if (sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION) {
+            cm256_one(lds, tb, ks, a.extkeys + ks_u, cm_job(a, ks, q1), mac);
+            return;
+        }
+        const F8Job j = f8_job(a, ks, q1);
         F8Mac m0, m1;
-        f8_pair(lds, tb, ks, a.f8keys + ks_u, j, j, false, mac, m0, m1);
+        f8_pair(lds, tb, ks, a.extkeys + ks_u, j, j, false, mac, m0, m1);
         if (mac) f8_trailer(ks, j, m0);
     });
 }
@@ -2451,9 +2546,9 @@ hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_unprotect_fix, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_f8(const BundleArgs &a, hipStream_t s) {
+hipError_t launch_ext(const BundleArgs &a, hipStream_t s) {
     const uint32_t lanes = (a.n + 1) / 2; // two packets per lane
-    hipLaunchKernelGGL(k_f8, dim3((lanes + kF8Block - 1) / kF8Block), dim3(kF8Block), 0, s, a);
+    hipLaunchKernelGGL(k_ext, dim3((lanes + kExtBlock - 1) / kExtBlock), dim3(kExtBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,

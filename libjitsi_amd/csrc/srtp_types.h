@@ -17,7 +17,7 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 // :158-211.  The HMAC key is stored as its two SHA-1 midstates (ipad/opad),
 // so the per-packet MAC costs no key blocks.
 struct alignas(256) KeySet {
-    uint32_t rk[4 * (kAesRounds + 1)]; // AES-128 round keys, little-endian column words
+    uint32_t rk[4 * (kAesRounds + 1)]; // AES-128 round keys (AES-128-CM), little-endian column words
     uint32_t ipad[5];                  // SHA-1 state after (authKey ^ 0x36..) block
     uint32_t opad[5];                  // SHA-1 state after (authKey ^ 0x5c..) block
     uint32_t salt[4];                  // session salt bytes 0..13 as LE words (14,15 = 0)
@@ -25,17 +25,21 @@ struct alignas(256) KeySet {
     int32_t auth_type;                 // SRTP_NULL_AUTHENTICATION / SRTP_HMACSHA1_AUTHENTICATION
     int32_t tag_len;                   // policy.getAuthTagLength()
     int32_t kind;                      // SRTP_KIND_RTP / SRTP_KIND_RTCP
-    uint32_t pad[2];
+    int32_t ext;                       // 1: cipher run by k_ext (AES-F8, AES-256-CM), keys in ExtKeys
+    uint32_t pad;
 };
 static_assert(sizeof(KeySet) == 256, "KeySet is one 256-B record");
 
-// AES-F8 IV' key of a key set (SRTPCipherF8.deriveForIV :66-95: the session
-// key ^ (session salt || 0x55 0x55)), kept beside KeySet, indexed by key-set id.
-struct alignas(64) F8Keys {
-    uint32_t rk[4 * (kAesRounds + 1)]; // round keys, little-endian column words
-    uint32_t pad[4];
+// Round keys of the key sets whose cipher k_ext runs, beside KeySet, indexed by
+// key-set id: AES-F8's IV' key (SRTPCipherF8.deriveForIV :66-95: the session
+// key ^ (session salt || 0x55 0x55); 10 rounds), or the AES-256-CM session
+// key (14 rounds; RFC 6188).
+struct alignas(64) ExtKeys {
+    uint32_t rk[60]; // 4 * (nr + 1) round-key words, little-endian column words
+    int32_t nr;      // 10 or 14
+    uint32_t pad[3];
 };
-static_assert(sizeof(F8Keys) == 192, "F8Keys is 192 B");
+static_assert(sizeof(ExtKeys) == 256, "ExtKeys is 256 B");
 
 struct FactoryRec {      // SRTPContextFactory
     int32_t open;        // 0 after close(): getDefaultContext() == null

@@ -133,8 +133,10 @@ class SRTPPipeline:
 def profile_policies(profile: str):
     """(srtpPolicy, srtcpPolicy) of a DTLS-SRTP protection profile, as the table
     in transform/dtls/DtlsPacketTransformer.java:574-612 builds them (note the
-    10-byte SRTCP tag of the _32 profiles), or of the SDES F8 crypto suite
-    (transform/sdes/SDesTransformEngine.java:129-176: AES-F8, 10-byte tags)."""
+    10-byte SRTCP tag of the _32 profiles), of the SDES F8 crypto suite
+    (transform/sdes/SDesTransformEngine.java:129-176: AES-F8, 10-byte tags), or
+    of the AES-256-CM suites (RFC 6188; SDesControlImpl.java:71-72 lists them,
+    ZRTP's AES3 yields the same policy, ZRTPTransformEngine.java:873-900)."""
     P = SRTPPolicy
     table = {
         "AES_CM_128_HMAC_SHA1_80": (P.AESCM_ENCRYPTION, 16, 14, 10, 10),
@@ -142,6 +144,9 @@ def profile_policies(profile: str):
         "NULL_HMAC_SHA1_80": (P.NULL_ENCRYPTION, 0, 0, 10, 10),
         "NULL_HMAC_SHA1_32": (P.NULL_ENCRYPTION, 0, 0, 4, 10),
         "F8_128_HMAC_SHA1_80": (P.AESF8_ENCRYPTION, 16, 14, 10, 10),
+        # AES-256-CM (RFC 6188): SRTPCryptoContext with encKeyLength 32
+        "AES_256_CM_HMAC_SHA1_80": (P.AESCM_ENCRYPTION, 32, 14, 10, 10),
+        "AES_256_CM_HMAC_SHA1_32": (P.AESCM_ENCRYPTION, 32, 14, 4, 10),
     }
     enc, klen, slen, rtp_tag, rtcp_tag = table[profile]
     return (P(enc, klen, P.HMACSHA1_AUTHENTICATION, 20, rtp_tag, slen),
@@ -548,11 +553,14 @@ TRAILER_ROOM = 16  # largest trailer: SRTCP E|index (4) + 12-byte tag
 
 
 def derive_session_keys(masterKey: bytes, masterSalt: bytes, rtcp: bool = False):
-    """The engine's host-side RFC 3711 4.3 key derivation (no GPU needed)."""
-    mk = (C.c_uint8 * 16).from_buffer_copy(bytes(masterKey)[:16])
-    ms = (C.c_uint8 * 14).from_buffer_copy(bytes(masterSalt)[:14])
-    enc, auth, salt = (C.c_uint8 * 16)(), (C.c_uint8 * 20)(), (C.c_uint8 * 14)()
-    N.check(N.lib().srtp_derive_session_keys(mk, ms, int(rtcp), enc, auth, salt), None, "kdf")
+    """The engine's host-side RFC 3711 4.3 key derivation (no GPU needed); a
+    32-byte master key selects the AES-256 PRF and a 32-byte session key
+    (RFC 6188 4.1)."""
+    mk = bytes(masterKey)
+    klen = 32 if len(mk) >= 32 else 16
+    enc, auth, salt = (C.c_uint8 * klen)(), (C.c_uint8 * 20)(), (C.c_uint8 * 14)()
+    N.check(N.lib().srtp_derive_session_keys_n(mk[:klen], klen, bytes(masterSalt)[:14], int(rtcp),
+                                               enc, auth, salt), None, "kdf")
     return bytes(enc), bytes(auth), bytes(salt)
 
 

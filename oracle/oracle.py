@@ -81,6 +81,7 @@ def lib():
         L.orc_aes128_encrypt_block.argtypes = [u8p, u8p, u8p]
         L.orc_hmac_sha1.argtypes = [u8p, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_derive_keys.argtypes = [u8p, u8p, C.c_int, u8p, u8p, u8p]
+        L.orc_derive_keys_n.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, u8p, u8p]
         L.orc_aes_f8.argtypes = [u8p, u8p, C.c_int, u8p, u8p, C.c_int]
         L.orc_bench_round_trips.restype = C.c_int64
         L.orc_bench_round_trips.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
@@ -111,12 +112,15 @@ def hmac_sha1(key: bytes, msg: bytes) -> bytes:
 
 
 def derive_keys(master_key: bytes, master_salt: bytes, rtcp: bool = False):
-    k, kp = _u8(master_key)
+    """RFC 3711 4.3 session keys (a 32-byte master key: the AES-256 PRF and a
+    32-byte cipher key, RFC 6188 4.1)."""
+    klen = 32 if len(master_key) >= 32 else 16
+    k, kp = _u8(master_key[:klen])
     s, sp = _u8(master_salt)
-    enc, auth, salt = np.zeros(16, np.uint8), np.zeros(20, np.uint8), np.zeros(14, np.uint8)
+    enc, auth, salt = np.zeros(klen, np.uint8), np.zeros(20, np.uint8), np.zeros(14, np.uint8)
     P = C.POINTER(C.c_uint8)
-    lib().orc_derive_keys(kp, sp, int(rtcp), enc.ctypes.data_as(P), auth.ctypes.data_as(P),
-                          salt.ctypes.data_as(P))
+    lib().orc_derive_keys_n(kp, klen, sp, int(rtcp), enc.ctypes.data_as(P),
+                            auth.ctypes.data_as(P), salt.ctypes.data_as(P))
     return enc.tobytes(), auth.tobytes(), salt.tobytes()
 
 

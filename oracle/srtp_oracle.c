@@ -36,7 +36,7 @@ static inline int j_lbit(int64_t v, int64_t n) { return (int)(((uint64_t)v >> (n
 /* ---------- structures -------------------------------------------------- */
 struct orc_factory {
     int sender, mode, closed;
-    uint8_t master_key[16], master_salt[14];
+    uint8_t master_key[32], master_salt[14];
     orc_policy srtp, srtcp;
 };
 
@@ -45,8 +45,9 @@ typedef struct orc_ctx {
     int kind;
     orc_policy policy;
     int mode;
-    uint8_t enc_key[16], auth_key[20], salt_key[14];
-    EVP_CIPHER_CTX *ecb;  /* AES-128 keyed with the session key */
+    uint8_t enc_key[32], auth_key[20], salt_key[14];
+    int key_len; /* 16 or 32 (AES-256-CM) */
+    EVP_CIPHER_CTX *ecb;  /* AES-128 / AES-256 keyed with the session key */
     EVP_CIPHER_CTX *ctr;  /* tuned mode */
     EVP_CIPHER_CTX *f8;   /* AES-F8: IV' cipher keyed with encKey ^ (salt || 0x55..) */
     HMAC_CTX *hmac;       /* ref: re-keyed per packet; tuned: pre-keyed template */
@@ -77,6 +78,15 @@ struct orc_transformer {
 static EVP_CIPHER_CTX *aes_ecb_new(const uint8_t key[16]) {
     EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
     EVP_EncryptInit_ex(c, EVP_aes_128_ecb(), NULL, key, NULL);
+    EVP_CIPHER_CTX_set_padding(c, 0);
+    return c;
+}
+
+/* AES-128 or AES-256 (key_len 32) ECB, for AES-256-CM and its PRF */
+static EVP_CIPHER_CTX *aes_ecb_new_n(const uint8_t *key, int key_len) {
+    if (key_len != 32) return aes_ecb_new(key);
+    EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
+    EVP_EncryptInit_ex(c, EVP_aes_256_ecb(), NULL, key, NULL);
     EVP_CIPHER_CTX_set_padding(c, 0);
     return c;
 }
@@ -223,7 +233,15 @@ static void authenticate_packet_hmac(orc_ctx *x, const uint8_t *buf, int len, in
  * (:128-136, :158-211). */
 void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp, uint8_t enc[16],
                      uint8_t auth[20], uint8_t salt[14]) {
-    EVP_CIPHER_CTX *c = aes_ecb_new(mk);
+    orc_derive_keys_n(mk, 16, ms, rtcp, enc, auth, salt);
+}
+
+/* deriveSrtpKeys :393-447 / deriveSrtcpKeys with a master key of key_len
+ * bytes: the PRF is AES-128 or AES-256 (RFC 6188 4.1), the session key key_len
+ * bytes. */
+void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
+                       uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+    EVP_CIPHER_CTX *c = aes_ecb_new_n(mk, key_len);
     uint8_t iv[16];
     int base = rtcp ? 3 : 0;
     for (int lab = 0; lab < 3; lab++) {
@@ -231,7 +249,7 @@ void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp, uint8
         iv[7] ^= (uint8_t)(base + lab);
         iv[14] = iv[15] = 0;
         if (lab == 0)
-            get_cipher_stream(c, enc, 16, iv);
+            get_cipher_stream(c, enc, key_len, iv);
         else if (lab == 1)
             get_cipher_stream(c, auth, 20, iv);
         else
@@ -327,7 +345,9 @@ static int policy_ok(const orc_policy *p, int rtcp) {
     if (p->enc_type != ORC_NULL_ENCRYPTION && p->enc_type != ORC_AESCM_ENCRYPTION &&
         p->enc_type != ORC_AESF8_ENCRYPTION)
         return 0;
-    if (p->enc_type != ORC_NULL_ENCRYPTION && (p->enc_key_len != 16 || p->salt_key_len != 14))
+    if (p->enc_type != ORC_NULL_ENCRYPTION && p->salt_key_len != 14) return 0;
+    if (p->enc_type == ORC_AESF8_ENCRYPTION && p->enc_key_len != 16) return 0;
+    if (p->enc_type == ORC_AESCM_ENCRYPTION && p->enc_key_len != 16 && p->enc_key_len != 32)
         return 0;
     /* SRTCP F8 ciphers [8, 8 + length - 4 - tag) (SRTCPCryptoContext :285-291),
      * which leaves the packet unless an HMAC trailer of >= 4 tag bytes follows */
@@ -348,10 +368,14 @@ orc_factory *orc_factory_new(int sender, const uint8_t *mk, int key_len, const u
     /* NULL-cipher profiles: the reference throws in key derivation;
      * here they keep a 16-B master key + 14-B salt for the AES-CM PRF, as RFC 3711
      * 4.3 prescribes -- behaviour "parity unpinned". */
-    if (key_len < 16 || salt_len < 14 || !policy_ok(srtp, 0) || !policy_ok(srtcp, 1)) return NULL;
+    if (salt_len < 14 || !policy_ok(srtp, 0) || !policy_ok(srtcp, 1)) return NULL;
+    /* BaseSRTPCryptoContext copies encKeyLength bytes of the master key (:187-190) */
+    const int need = (srtp->enc_type == ORC_AESCM_ENCRYPTION && srtp->enc_key_len == 32) ||
+                     (srtcp->enc_type == ORC_AESCM_ENCRYPTION && srtcp->enc_key_len == 32) ? 32 : 16;
+    if (key_len < need) return NULL;
     orc_factory *f = (orc_factory *)calloc(1, sizeof *f);
     f->sender = sender; f->mode = mode;
-    memcpy(f->master_key, mk, 16);
+    memcpy(f->master_key, mk, (size_t)need);
     memcpy(f->master_salt, ms, 14);
     f->srtp = *srtp; f->srtcp = *srtcp;
     return f;
@@ -361,7 +385,7 @@ orc_factory *orc_factory_new(int sender, const uint8_t *mk, int key_len, const u
 void orc_factory_close(orc_factory *f) {
     if (!f || f->closed) return;
     f->closed = 1;
-    memset(f->master_key, 0, 16);
+    memset(f->master_key, 0, sizeof f->master_key);
     memset(f->master_salt, 0, 14);
 }
 
@@ -400,14 +424,16 @@ static orc_ctx *make_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) 
     orc_ctx *x = (orc_ctx *)calloc(1, sizeof *x);
     x->ssrc = ssrc; x->kind = t->kind; x->mode = f->mode;
     x->policy = (t->kind == ORC_KIND_RTP) ? f->srtp : f->srtcp;
-    orc_derive_keys(f->master_key, f->master_salt, t->kind == ORC_KIND_RTCP, x->enc_key,
-                    x->auth_key, x->salt_key);
-    x->ecb = aes_ecb_new(x->enc_key);
+    x->key_len = x->policy.enc_type == ORC_AESCM_ENCRYPTION && x->policy.enc_key_len == 32 ? 32 : 16;
+    orc_derive_keys_n(f->master_key, x->key_len, f->master_salt, t->kind == ORC_KIND_RTCP,
+                      x->enc_key, x->auth_key, x->salt_key);
+    x->ecb = aes_ecb_new_n(x->enc_key, x->key_len);
     if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) /* deriveSrtpKeys :443-444 */
         x->f8 = f8_iv_cipher_new(x->enc_key, x->salt_key, 14);
     if (x->mode == ORC_MODE_TUNED) {
         x->ctr = EVP_CIPHER_CTX_new();
-        EVP_EncryptInit_ex(x->ctr, EVP_aes_128_ctr(), NULL, x->enc_key, NULL);
+        EVP_EncryptInit_ex(x->ctr, x->key_len == 32 ? EVP_aes_256_ctr() : EVP_aes_128_ctr(), NULL,
+                           x->enc_key, NULL);
     }
     x->hmac = HMAC_CTX_new();
     x->hmac_work = HMAC_CTX_new();

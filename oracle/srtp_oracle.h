@@ -130,6 +130,8 @@ void orc_aes_f8(const uint8_t key[16], const uint8_t *salt, int salt_len, const 
                 uint8_t *data, int len);
 void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp,
                      uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]);
+void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
+                       uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
 
 /* CPU baseline timing (oracle_bench.c): packets protected AND unprotected by
  * `threads` pinned threads in about `seconds` (-1 on a rejected packet). */
