@@ -56,6 +56,8 @@ def parse_args():
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="SSRC popularity Zipf exponent (0: round-robin, every SSRC equal)")
     ap.add_argument("--len", type=int, default=1200, help="RTP packet length")
+    ap.add_argument("--align", type=int, default=16,
+                    help="packet region alignment in the bundle segment (bytes, >= 16)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="CPU baseline: seconds per measurement (4 measurements)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -204,6 +206,7 @@ class Side:
             b = synth.rtp_bundle(n, nssrc, L, seed=seed)
             idx = np.arange(n) % nssrc
             counts = np.bincount(idx, minlength=nssrc)[idx]
+        b = synth.realign(b, args.align)
         self.b = b
         # context table >= 1.6x the SSRCs (load <= 0.31 at 10k); its size sets
         # the sort's key width (2^15 slots + the invalid key: two radix passes)
@@ -513,6 +516,7 @@ def main():
             "config": {"workload": "configs[1]: 10k concurrent SSRCs x 1200-B RTP, "
                                    "AES_CM_128_HMAC_SHA1_80, protect + unprotect per step",
                        "packets_per_gpu_per_step": n, "ssrcs_per_gpu": args.ssrcs, "pkt_len": L,
+                       "region_align": args.align,
                        "ssrc_mix": f"zipf({args.zipf})" if args.zipf > 0 else "round-robin",
                        "parallelism": f"ssrc-sharded x{n_gpus} ({'one process per GPU' if mode == 'process' else 'one process, all GPUs'})",
                        "streams": "serial: protect(i), unprotect(i) on one stream" if args.serial else

@@ -178,6 +178,28 @@ def concat(bundles) -> Bundle:
                   np.concatenate([b.seq for b in bundles]), {})
 
 
+def realign(b: Bundle, align: int) -> Bundle:
+    """The same packets with every region starting on an `align`-byte boundary
+    (caps unchanged; the gap after each region is zero)."""
+    if align <= 16:
+        return b
+    stride = ((b.cap.astype(np.int64) + align - 1) // align) * align
+    off = np.zeros(b.n, np.int64)
+    if b.n > 1:
+        off[1:] = np.cumsum(stride[:-1])
+    seg = np.zeros(int(off[-1] + stride[-1]) if b.n else 16, np.uint8)
+    src = b.off.astype(np.int64)
+    if b.n and np.all(b.cap == b.cap[0]):  # vectorised for uniform caps
+        c = int(b.cap[0])
+        idx = src[:, None] + np.arange(c)[None, :]
+        seg[(off[:, None] + np.arange(c)[None, :]).ravel()] = b.seg[idx.ravel()]
+    else:
+        for i in range(b.n):
+            seg[off[i]:off[i] + b.cap[i]] = b.seg[src[i]:src[i] + b.cap[i]]
+    return Bundle(seg, off.astype(np.uint32), b.length.copy(), b.cap.copy(), b.flags.copy(),
+                  b.ssrc.copy(), b.seq.copy(), dict(b.meta))
+
+
 def select(b: Bundle, order: np.ndarray) -> Bundle:
     """Re-pack packets of b in the given order (indices may repeat: duplicates)."""
     order = np.asarray(order, np.int64)

@@ -28,8 +28,8 @@ import json
 import os
 import sys
 
-KERNELS = ("k_parse", "k_unprotect", "k_walk<true>", "k_walk<false>", "k_protect",
-           "k_unprotect_fix", "rocprim")
+KERNELS = ("k_parse", "k_sort_scatter", "k_unprotect", "k_walk<true>", "k_walk<false>", "k_protect",
+           "k_unprotect_fix", "k_ext")
 
 
 def short(name: str) -> str:
@@ -119,6 +119,9 @@ def main():
                 # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles; 1024 SIMDs
                 cyc = c["GRBM_GUI_ACTIVE"] / 8
                 d["valu_busy_frac"] = round(c["SQ_INSTS_VALU"] * 2 / (1024 * cyc), 3)
+                # at the issue rate tools/valu_bench.hip measures for the loop's
+                # instructions (1.28 cycles per wave64 instruction per SIMD, 4 waves/SIMD)
+                d["valu_busy_frac_measured_rate"] = round(c["SQ_INSTS_VALU"] * 1.28 / (1024 * cyc), 3)
         if "SQ_BUSY_CYCLES" in c:
             d["sq_busy_cycles"] = c["SQ_BUSY_CYCLES"]
         for name in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
@@ -147,6 +150,9 @@ def main():
                 k: kp.get(k) for k in ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac",
                                        "eff_clock_ghz")}
             ku = derived.get("k_unprotect", {})
+            js["k_unprotect_utilisation"] = {
+                k: ku.get(k) for k in ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac",
+                                       "eff_clock_ghz")}
             if "hbm_bytes" in ku:
                 js.update({"k_unprotect_bytes_per_launch": round(ku["hbm_bytes"]),
                            "k_unprotect_read_bytes": round(ku["hbm_read_bytes"]),
