@@ -70,6 +70,8 @@ extern "C" {
 #define SRTP_NULL_ENCRYPTION 0
 #define SRTP_AESCM_ENCRYPTION 1
 #define SRTP_AESF8_ENCRYPTION 2 /* SRTPCipherF8 (SDES F8_128_HMAC_SHA1_80) */
+#define SRTP_TWOFISH_ENCRYPTION 3   /* counter mode over Twofish (ZRTP "2FS") */
+#define SRTP_TWOFISHF8_ENCRYPTION 4 /* F8 over Twofish */
 #define SRTP_NULL_AUTHENTICATION 0
 #define SRTP_HMACSHA1_AUTHENTICATION 1
 
@@ -369,6 +371,16 @@ int srtp_derive_session_keys(const uint8_t master_key[16], const uint8_t master_
 int srtp_derive_session_keys_n(const uint8_t *master_key, int32_t key_len,
                                const uint8_t master_salt[14], int32_t rtcp, uint8_t *enc_key,
                                uint8_t auth_key[20], uint8_t salt_key[14]);
+/* The same with the policy's cipher as the PRF: AES for SRTP_AESCM / AESF8 /
+ * NULL, Twofish for SRTP_TWOFISH(F8)_ENCRYPTION (BaseSRTPCryptoContext.java
+ * :197-226 keys that cipher with the master key). */
+int srtp_derive_session_keys_for(int32_t enc_type, const uint8_t *master_key, int32_t key_len,
+                                 const uint8_t master_salt[14], int32_t rtcp, uint8_t *enc_key,
+                                 uint8_t auth_key[20], uint8_t salt_key[14]);
+/* One block of the policy's cipher: AES-128/256 (key_len 16 / 32) or Twofish
+ * (enc_type SRTP_TWOFISH*, key_len 16 / 24 / 32). */
+int srtp_block_encrypt(int32_t enc_type, const uint8_t *key, int32_t key_len, const uint8_t in[16],
+                       uint8_t out[16]);
 
 /* DTLS-SRTP keying (control plane, host only): what
  * DtlsPacketTransformer.initializeSRTPTransformer does after the handshake

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("SRTP_MI355X_LIB") or os.path.join(_HERE, "libsrtp_mi3
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "srtp_mi355x.h")
 
 # include/srtp_mi355x.h
-NULL_ENCRYPTION, AESCM_ENCRYPTION = 0, 1
+NULL_ENCRYPTION, AESCM_ENCRYPTION, AESF8_ENCRYPTION, TWOFISH_ENCRYPTION, TWOFISHF8_ENCRYPTION = range(5)
 NULL_AUTHENTICATION, HMACSHA1_AUTHENTICATION = 0, 1
 KIND_RTP, KIND_RTCP = 0, 1
 (STATUS_OK, STATUS_DROP_REPLAY, STATUS_DROP_AUTH, STATUS_DROP_VERSION, STATUS_DROP_NO_CONTEXT,
@@ -43,7 +43,8 @@ EXPORTED = [
     "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host",
     "srtp_dispatch_get_context_state", "srtp_dispatch_set_context_state", "srtp_dispatch_stats",
     "srtp_tls_export_keying_material", "srtp_dtls_profile_keys", "srtp_dtls_transformer_create",
-    "srtp_engine_get_opts", "srtp_derive_session_keys_n", "srtp_aggregator_opts_default", "srtp_aggregator_create",
+    "srtp_engine_get_opts", "srtp_derive_session_keys_n", "srtp_derive_session_keys_for",
+    "srtp_block_encrypt", "srtp_aggregator_opts_default", "srtp_aggregator_create",
     "srtp_aggregator_submit", "srtp_aggregator_flush", "srtp_aggregator_stats",
     "srtp_aggregator_destroy",
 ]
@@ -144,6 +145,8 @@ def lib() -> C.CDLL:
     L.srtp_engine_read_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.srtp_derive_session_keys.argtypes = [pu8, pu8, i32, pu8, pu8, pu8]
     L.srtp_derive_session_keys_n.argtypes = [C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, pu8]
+    L.srtp_derive_session_keys_for.argtypes = [i32, C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, pu8]
+    L.srtp_block_encrypt.argtypes = [i32, C.c_char_p, i32, C.c_char_p, pu8]
     L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
     L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_pipeline_create.argtypes = [vp, u32, C.c_size_t, i32, C.POINTER(vp)]

@@ -27,6 +27,7 @@ struct srtp_engine {
 
     KeySet *d_keysets = nullptr;
     ExtKeys *d_extkeys = nullptr; // round keys of the k_ext key sets (same index)
+    TwofishKeys *d_tfkeys = nullptr; // 2 per key set, allocated with the first Twofish factory
     uint32_t n_ext = 0;           // AES-F8 / AES-256-CM key sets created: k_ext runs only when > 0
     uint32_t n_keysets = 0, max_keysets = 0;
     FactoryRec *d_factories = nullptr;
@@ -113,18 +114,22 @@ void dfree(void *p) {
 // AES-256-CM is what SRTPCryptoContext does with encKeyLength 32, e.g. from
 // ZRTP's AES3, ZRTPTransformEngine.java:873-900).  Tag length <= 12 keeps the
 // reference's readRegionToBuff in range for every packet of >= 12 bytes.
+bool is_twofish(int enc) { return enc == SRTP_TWOFISH_ENCRYPTION || enc == SRTP_TWOFISHF8_ENCRYPTION; }
+bool is_f8(int enc) { return enc == SRTP_AESF8_ENCRYPTION || enc == SRTP_TWOFISHF8_ENCRYPTION; }
+
 bool policy_ok(const srtp_policy *p, bool rtcp) {
     if (!p) return false;
     if (p->enc_type != SRTP_NULL_ENCRYPTION && p->enc_type != SRTP_AESCM_ENCRYPTION &&
-        p->enc_type != SRTP_AESF8_ENCRYPTION)
+        p->enc_type != SRTP_AESF8_ENCRYPTION && !is_twofish(p->enc_type))
         return false;
     if (p->enc_type != SRTP_NULL_ENCRYPTION && p->salt_key_len != 14) return false;
     if (p->enc_type == SRTP_AESF8_ENCRYPTION && p->enc_key_len != 16) return false;
-    if (p->enc_type == SRTP_AESCM_ENCRYPTION && p->enc_key_len != 16 && p->enc_key_len != 32)
+    if ((p->enc_type == SRTP_AESCM_ENCRYPTION || is_twofish(p->enc_type)) && p->enc_key_len != 16 &&
+        p->enc_key_len != 32)
         return false;
     // SRTCP F8 ciphers [8, 8 + length - 4 - tag) (SRTCPCryptoContext :285-291):
     // inside the packet only with an HMAC trailer of >= 4 tag bytes after it
-    if (rtcp && p->enc_type == SRTP_AESF8_ENCRYPTION &&
+    if (rtcp && is_f8(p->enc_type) &&
         (p->auth_type == SRTP_NULL_AUTHENTICATION || p->auth_tag_len < 4))
         return false;
     if (p->auth_type != SRTP_NULL_AUTHENTICATION && p->auth_type != SRTP_HMACSHA1_AUTHENTICATION)
@@ -135,34 +140,42 @@ bool policy_ok(const srtp_policy *p, bool rtcp) {
 }
 
 // Master key bytes a policy uses (BaseSRTPCryptoContext copies encKeyLength
-// of them, :187-190): 32 for AES-256-CM, else 16 (the NULL cipher keeps the
-// AES-128 PRF, see srtp_factory_create).
+// of them, :187-190): 32 for the 256-bit AES-CM / Twofish policies, else 16
+// (the NULL cipher keeps the AES-128 PRF, see srtp_factory_create).
 int master_key_len(const srtp_policy *pol) {
-    return pol->enc_type == SRTP_AESCM_ENCRYPTION && pol->enc_key_len == 32 ? 32 : 16;
+    return pol->enc_type != SRTP_NULL_ENCRYPTION && pol->enc_key_len == 32 ? 32 : 16;
 }
 
 void build_keyset(const uint8_t *mk, const uint8_t ms[14], bool rtcp, const srtp_policy *pol,
-                  KeySet *ks, ExtKeys *ext) {
+                  KeySet *ks, ExtKeys *ext, TwofishKeys *tf) {
     memset(ks, 0, sizeof *ks);
     memset(ext, 0, sizeof *ext);
+    memset(tf, 0, 2 * sizeof *tf);
     const int klen = master_key_len(pol);
+    const bool twofish = is_twofish(pol->enc_type);
     uint8_t enc[32], auth[20], salt[16] = {0};
-    // RFC 3711 4.3 with the AES-128 or AES-256 PRF (RFC 6188 4.1), as
-    // deriveSrtpKeys :393-447 does with a key of encKeyLength bytes
-    derive_session_keys_n(mk, klen, ms, rtcp, enc, auth, salt);
-    if (klen == 32) { // AES-256-CM: k_ext
+    // RFC 3711 4.3 with the policy's cipher as the PRF -- AES-128, AES-256
+    // (RFC 6188 4.1) or Twofish -- as deriveSrtpKeys :393-447 does with a key
+    // of encKeyLength bytes
+    derive_session_keys_cipher(twofish, mk, klen, ms, rtcp, enc, auth, salt);
+    // SRTPCipherF8.deriveForIV :66-95: the IV' key is key ^ (salt || 0x55..)
+    uint8_t m[32];
+    for (int i = 0; i < klen; i++) m[i] = (uint8_t)(enc[i] ^ (i < 14 ? salt[i] : 0x55));
+    if (twofish) { // k_ext, Twofish tables
+        twofish_schedule(enc, klen, tf[0].K, tf[0].T);
+        if (is_f8(pol->enc_type)) twofish_schedule(m, klen, tf[1].K, tf[1].T);
+        ks->ext = 1;
+    } else if (klen == 32) { // AES-256-CM: k_ext
         ext->nr = aes_expand_le(enc, 32, ext->rk);
         ks->ext = 1;
     } else {
         aes128_expand_le(enc, ks->rk);
     }
-    if (pol->enc_type == SRTP_AESF8_ENCRYPTION) { // SRTPCipherF8.deriveForIV :66-95
-        uint8_t m[16];
-        for (int i = 0; i < 16; i++) m[i] = (uint8_t)(enc[i] ^ (i < 14 ? salt[i] : 0x55));
+    if (pol->enc_type == SRTP_AESF8_ENCRYPTION) {
         ext->nr = aes_expand_le(m, 16, ext->rk);
         ks->ext = 1;
-        memset(m, 0, sizeof m);
     }
+    memset(m, 0, sizeof m);
     hmac_sha1_midstates(auth, ks->ipad, ks->opad);
     for (int i = 0; i < 4; i++)
         ks->salt[i] = (uint32_t)salt[4 * i] | ((uint32_t)salt[4 * i + 1] << 8) |
@@ -438,13 +451,15 @@ void srtp_engine_destroy(srtp_engine *e) {
         (void)hipMemset(e->d_keysets, 0, (size_t)e->max_keysets * sizeof(KeySet));
     if (e->d_extkeys)
         (void)hipMemset(e->d_extkeys, 0, (size_t)e->max_keysets * sizeof(ExtKeys));
+    if (e->d_tfkeys)
+        (void)hipMemset(e->d_tfkeys, 0, 2 * (size_t)e->max_keysets * sizeof(TwofishKeys));
     free_scratch(e);
     for (auto &m : e->marks) {
         (void)hipEventDestroy(m.a);
         (void)hipEventDestroy(m.b);
     }
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
-    void *ptrs[] = {e->d_keysets, e->d_extkeys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
+    void *ptrs[] = {e->d_keysets, e->d_extkeys, e->d_tfkeys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
                     e->e_min, e->ctl, e->d_count, e->d_counters, e->h_seg, e->h_off, e->h_len,
                     e->h_cap, e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
@@ -471,8 +486,18 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
         return fail(e, SRTP_EFULL, "factory table full");
     KeySet ks[2];
     ExtKeys f8[2];
-    build_keyset(mk, ms, false, srtp_pol, &ks[0], &f8[0]);
-    build_keyset(mk, ms, true, srtcp_pol, &ks[1], &f8[1]);
+    std::vector<TwofishKeys> tf(4);
+    build_keyset(mk, ms, false, srtp_pol, &ks[0], &f8[0], &tf[0]);
+    build_keyset(mk, ms, true, srtcp_pol, &ks[1], &f8[1], &tf[2]);
+    if (is_twofish(srtp_pol->enc_type) || is_twofish(srtcp_pol->enc_type)) {
+        if (!e->d_tfkeys && dalloc(&e->d_tfkeys, 2 * (size_t)e->max_keysets) != hipSuccess) {
+            std::fill(tf.begin(), tf.end(), TwofishKeys{});
+            return fail(e, SRTP_ENOMEM, "Twofish key table");
+        }
+        HIPCHK(e, hipMemcpy(e->d_tfkeys + 2 * (size_t)e->n_keysets, tf.data(), 4 * sizeof(TwofishKeys),
+                            hipMemcpyHostToDevice));
+    }
+    std::fill(tf.begin(), tf.end(), TwofishKeys{});
     HIPCHK(e, hipMemcpy(e->d_keysets + e->n_keysets, ks, sizeof ks, hipMemcpyHostToDevice));
     HIPCHK(e, hipMemcpy(e->d_extkeys + e->n_keysets, f8, sizeof f8, hipMemcpyHostToDevice));
     e->n_ext += (uint32_t)(ks[0].ext + ks[1].ext);
@@ -579,6 +604,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     BundleArgs a{};
     a.keysets = e->d_keysets;
     a.extkeys = e->d_extkeys;
+    a.tfkeys = e->d_tfkeys;
     a.factories = e->d_factories;
     a.transformers = e->d_transformers;
     a.ctx_keys = e->d_ctx_keys;
@@ -948,6 +974,33 @@ int srtp_derive_session_keys_n(const uint8_t *mk, int32_t key_len, const uint8_t
                                uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
     if (!mk || !ms || !enc || !auth || !salt || (key_len != 16 && key_len != 32)) return SRTP_EINVAL;
     derive_session_keys_n(mk, key_len, ms, rtcp != 0, enc, auth, salt);
+    return SRTP_OK;
+}
+
+int srtp_derive_session_keys_for(int32_t enc_type, const uint8_t *mk, int32_t key_len,
+                                 const uint8_t ms[14], int32_t rtcp, uint8_t *enc, uint8_t auth[20],
+                                 uint8_t salt[14]) {
+    if (!mk || !ms || !enc || !auth || !salt || (key_len != 16 && key_len != 32)) return SRTP_EINVAL;
+    derive_session_keys_cipher(is_twofish(enc_type), mk, key_len, ms, rtcp != 0, enc, auth, salt);
+    return SRTP_OK;
+}
+
+int srtp_block_encrypt(int32_t enc_type, const uint8_t *key, int32_t key_len, const uint8_t in[16],
+                       uint8_t out[16]) {
+    if (!key || !in || !out) return SRTP_EINVAL;
+    if (is_twofish(enc_type)) {
+        if (key_len != 16 && key_len != 24 && key_len != 32) return SRTP_EINVAL;
+        std::vector<TwofishKeys> t(1);
+        twofish_schedule(key, key_len, t[0].K, t[0].T);
+        twofish_encrypt_block(t[0].K, t[0].T, in, out);
+        t[0] = TwofishKeys{};
+        return SRTP_OK;
+    }
+    if (key_len != 16 && key_len != 32) return SRTP_EINVAL;
+    uint32_t rk[60];
+    const int nr = aes_expand_le(key, key_len, rk);
+    aes_encrypt_block_nr(rk, nr, in, out);
+    memset(rk, 0, sizeof rk);
     return SRTP_OK;
 }
 

@@ -139,14 +139,161 @@ void sha1_compress(uint32_t h[5], const uint8_t blk[64]) {
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
 }
 
-// SRTPCipherCTR.getCipherStream (:68-92) for the short key-derivation streams.
-static void cipher_stream(const uint32_t *rk, int nr, uint8_t *out, int length, const uint8_t iv[16]) {
+// ------------------------------------------------------------------ Twofish
+// Schneier et al., "Twofish: A 128-Bit Block Cipher" (1998), 4.1-4.3, for the
+// ZRTP "2FS" policies (TWOFISH_ENCRYPTION / TWOFISHF8_ENCRYPTION, run by
+// BouncyCastle's TwofishEngine in the reference, BaseSRTPCryptoContext.java
+// :217-225).  The key schedule folds the key-dependent S-boxes and the MDS
+// matrix into four 256-word tables, which the GPU reads for g().
+namespace {
+
+struct TwofishQ {
+    uint8_t q[2][256];
+    TwofishQ() {
+        static const uint8_t t[2][4][16] = {
+            {{8, 1, 7, 13, 6, 15, 3, 2, 0, 11, 5, 9, 14, 12, 10, 4},
+             {14, 12, 11, 8, 1, 2, 3, 5, 15, 4, 10, 6, 7, 0, 9, 13},
+             {11, 10, 5, 14, 6, 13, 9, 0, 12, 8, 15, 3, 2, 4, 7, 1},
+             {13, 7, 15, 4, 1, 2, 6, 14, 9, 11, 3, 0, 8, 5, 12, 10}},
+            {{2, 8, 11, 13, 15, 7, 6, 14, 3, 1, 9, 4, 0, 10, 12, 5},
+             {1, 14, 2, 11, 4, 12, 3, 7, 6, 13, 10, 5, 15, 9, 0, 8},
+             {4, 12, 7, 5, 1, 6, 9, 10, 0, 14, 13, 8, 2, 11, 3, 15},
+             {11, 9, 5, 1, 12, 3, 13, 14, 6, 4, 7, 15, 2, 0, 8, 10}}};
+        auto r4 = [](unsigned v) { return ((v >> 1) | (v << 3)) & 15u; };
+        for (int w = 0; w < 2; w++)
+            for (unsigned x = 0; x < 256; x++) {
+                unsigned a = x >> 4, b = x & 15;
+                unsigned a1 = a ^ b, b1 = (a ^ r4(b) ^ (a << 3)) & 15;
+                unsigned a2 = t[w][0][a1], b2 = t[w][1][b1];
+                unsigned a3 = a2 ^ b2, b3 = (a2 ^ r4(b2) ^ (a2 << 3)) & 15;
+                q[w][x] = (uint8_t)((t[w][3][b3] << 4) | t[w][2][a3]);
+            }
+    }
+};
+
+const TwofishQ &tfq() {
+    static const TwofishQ t;
+    return t;
+}
+
+uint8_t gf_mul_poly(unsigned a, unsigned b, unsigned poly) {
+    unsigned r = 0;
+    for (; b; b >>= 1, a <<= 1) {
+        if (a & 0x100) a ^= poly;
+        if (b & 1) r ^= a;
+    }
+    return (uint8_t)r;
+}
+
+// which q each of the h stages applies to byte j: [k=4 stage, k>=3 stage,
+// before L1, before L0, last]
+const int kHq[4][5] = {{1, 1, 0, 0, 1}, {0, 1, 1, 0, 0}, {0, 0, 0, 1, 1}, {1, 0, 1, 1, 0}};
+const uint8_t kMds[4][4] = {
+    {0x01, 0xEF, 0x5B, 0x5B}, {0x5B, 0xEF, 0xEF, 0x01}, {0xEF, 0x5B, 0x01, 0xEF}, {0xEF, 0x01, 0xEF, 0x5B}};
+const uint8_t kRs[4][8] = {{0x01, 0xA4, 0x55, 0x87, 0x5A, 0x58, 0xDB, 0x9E},
+                           {0xA4, 0x56, 0x82, 0xF3, 0x1E, 0xC6, 0x68, 0xE5},
+                           {0x02, 0xA1, 0xFC, 0xC1, 0x47, 0xAE, 0x3D, 0x19},
+                           {0xA4, 0x55, 0x87, 0x5A, 0x58, 0xDB, 0x9E, 0x03}};
+
+uint8_t h_sbox(int j, uint8_t y, const uint32_t *L, int k) {
+    const uint8_t(*q)[256] = tfq().q;
+    auto lb = [&](int i) { return (uint8_t)(L[i] >> (8 * j)); };
+    if (k == 4) y = (uint8_t)(q[kHq[j][0]][y] ^ lb(3));
+    if (k >= 3) y = (uint8_t)(q[kHq[j][1]][y] ^ lb(2));
+    y = (uint8_t)(q[kHq[j][2]][y] ^ lb(1));
+    y = (uint8_t)(q[kHq[j][3]][y] ^ lb(0));
+    return q[kHq[j][4]][y];
+}
+
+uint32_t mds_col(int j, uint8_t y) {
+    return (uint32_t)gf_mul_poly(kMds[0][j], y, 0x169) | (uint32_t)gf_mul_poly(kMds[1][j], y, 0x169) << 8 |
+           (uint32_t)gf_mul_poly(kMds[2][j], y, 0x169) << 16 |
+           (uint32_t)gf_mul_poly(kMds[3][j], y, 0x169) << 24;
+}
+
+uint32_t h_word(uint32_t x, const uint32_t *L, int k) {
+    uint32_t z = 0;
+    for (int j = 0; j < 4; j++) z ^= mds_col(j, h_sbox(j, (uint8_t)(x >> (8 * j)), L, k));
+    return z;
+}
+
+} // namespace
+
+void twofish_schedule(const uint8_t *key, int key_len, uint32_t K[40], uint32_t T[4][256]) {
+    const int k = key_len / 8;
+    uint32_t even[4], odd[4], sv[4];
+    for (int i = 0; i < k; i++) {
+        const uint8_t *m = key + 8 * i;
+        even[i] = (uint32_t)m[0] | (uint32_t)m[1] << 8 | (uint32_t)m[2] << 16 | (uint32_t)m[3] << 24;
+        odd[i] = (uint32_t)m[4] | (uint32_t)m[5] << 8 | (uint32_t)m[6] << 16 | (uint32_t)m[7] << 24;
+        uint32_t w = 0;
+        for (int r = 0; r < 4; r++) {
+            uint8_t v = 0;
+            for (int c = 0; c < 8; c++) v ^= gf_mul_poly(kRs[r][c], m[c], 0x14D);
+            w |= (uint32_t)v << (8 * r);
+        }
+        sv[k - 1 - i] = w;
+    }
+    for (int i = 0; i < 20; i++) {
+        const uint32_t a = h_word(0x02020202u * (uint32_t)i, even, k);
+        const uint32_t b = rotl(h_word(0x02020202u * (uint32_t)i + 0x01010101u, odd, k), 8);
+        K[2 * i] = a + b;
+        K[2 * i + 1] = rotl(a + 2 * b, 9);
+    }
+    for (int j = 0; j < 4; j++)
+        for (int x = 0; x < 256; x++) T[j][x] = mds_col(j, h_sbox(j, (uint8_t)x, sv, k));
+    memset(even, 0, sizeof even);
+    memset(odd, 0, sizeof odd);
+    memset(sv, 0, sizeof sv);
+}
+
+void twofish_encrypt_block(const uint32_t K[40], const uint32_t T[4][256], const uint8_t in[16],
+                           uint8_t out[16]) {
+    auto g = [&](uint32_t x) {
+        return T[0][x & 255] ^ T[1][(x >> 8) & 255] ^ T[2][(x >> 16) & 255] ^ T[3][x >> 24];
+    };
+    uint32_t r[4];
+    for (int i = 0; i < 4; i++) {
+        uint32_t w;
+        memcpy(&w, in + 4 * i, 4); // little-endian host
+        r[i] = w ^ K[i];
+    }
+    for (int rd = 0; rd < 16; rd++) {
+        const uint32_t t0 = g(r[0]), t1 = g(rotl(r[1], 8));
+        const uint32_t f0 = t0 + t1 + K[2 * rd + 8], f1 = t0 + 2 * t1 + K[2 * rd + 9];
+        const uint32_t x = r[2] ^ f0;
+        const uint32_t n0 = (x >> 1) | (x << 31), n1 = rotl(r[3], 1) ^ f1;
+        r[2] = r[0];
+        r[3] = r[1];
+        r[0] = n0;
+        r[1] = n1;
+    }
+    for (int i = 0; i < 4; i++) {
+        const uint32_t c = r[(i + 2) & 3] ^ K[i + 4];
+        memcpy(out + 4 * i, &c, 4);
+    }
+}
+
+// SRTPCipherCTR.getCipherStream (:68-92) for the short key-derivation streams,
+// over AES (nr rounds of rk) or Twofish (tf_K / tf_T).
+struct PrfCipher {
+    const uint32_t *rk = nullptr;
+    int nr = 0;
+    const uint32_t *tf_K = nullptr;
+    const uint32_t (*tf_T)[256] = nullptr;
+    void encrypt(const uint8_t in[16], uint8_t out[16]) const {
+        if (tf_K) twofish_encrypt_block(tf_K, tf_T, in, out);
+        else aes_encrypt_block_nr(rk, nr, in, out);
+    }
+};
+
+static void cipher_stream(const PrfCipher &c, uint8_t *out, int length, const uint8_t iv[16]) {
     uint8_t in[16], blk[16];
     memcpy(in, iv, 14);
     for (int ctr = 0; ctr * 16 < length; ctr++) {
         in[14] = (uint8_t)(ctr >> 8);
         in[15] = (uint8_t)ctr;
-        aes_encrypt_block_nr(rk, nr, in, blk);
+        c.encrypt(in, blk);
         int n = length - ctr * 16 < 16 ? length - ctr * 16 : 16;
         memcpy(out + ctr * 16, blk, (size_t)n);
     }
@@ -159,8 +306,22 @@ void derive_session_keys(const uint8_t mk[16], const uint8_t ms[14], bool rtcp, 
 
 void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], bool rtcp,
                            uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+    derive_session_keys_cipher(false, mk, key_len, ms, rtcp, enc, auth, salt);
+}
+
+void derive_session_keys_cipher(bool twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
+                                bool rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
     uint32_t rk[60];
-    const int nr = aes_expand_le(mk, key_len, rk);
+    static thread_local uint32_t tK[40], tT[4][256];
+    PrfCipher prf;
+    if (twofish) {
+        twofish_schedule(mk, key_len, tK, tT);
+        prf.tf_K = tK;
+        prf.tf_T = tT;
+    } else {
+        prf.nr = aes_expand_le(mk, key_len, rk);
+        prf.rk = rk;
+    }
     uint8_t iv[16];
     const int base = rtcp ? 3 : 0;
     uint8_t *outs[3] = {enc, auth, salt};
@@ -169,9 +330,11 @@ void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14],
         memcpy(iv, ms, 14);
         iv[7] ^= (uint8_t)(base + lab); // computeIv: key_id = label << 48 lands in byte 7
         iv[14] = iv[15] = 0;
-        cipher_stream(rk, nr, outs[lab], lens[lab], iv);
+        cipher_stream(prf, outs[lab], lens[lab], iv);
     }
     memset(rk, 0, sizeof rk);
+    memset(tK, 0, sizeof tK);
+    memset(tT, 0, sizeof tT);
 }
 
 void hmac_sha1_midstates(const uint8_t key[20], uint32_t ipad[5], uint32_t opad[5]) {

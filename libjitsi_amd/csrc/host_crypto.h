@@ -31,6 +31,15 @@ void derive_session_keys(const uint8_t master_key[16], const uint8_t master_salt
 // the session encryption key is key_len bytes (RFC 6188 4.1 for AES-256).
 void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], bool rtcp,
                            uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+// With the Twofish PRF (twofish = true: the ZRTP Twofish policies key their
+// TwofishEngine with the master key).
+void derive_session_keys_cipher(bool twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
+                                bool rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+// Twofish key schedule (key_len 16, 24 or 32): subkeys K[40] and the four g()
+// tables (key-dependent S-boxes times the MDS columns); one block.
+void twofish_schedule(const uint8_t *key, int key_len, uint32_t K[40], uint32_t T[4][256]);
+void twofish_encrypt_block(const uint32_t K[40], const uint32_t T[4][256], const uint8_t in[16],
+                           uint8_t out[16]);
 // HMAC-SHA1 ipad/opad midstates for a 20-byte key.
 void hmac_sha1_midstates(const uint8_t key[20], uint32_t ipad[5], uint32_t opad[5]);
 

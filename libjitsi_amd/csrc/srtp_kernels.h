@@ -15,6 +15,7 @@ struct BundleArgs {
     // engine tables (HBM resident)
     const KeySet *keysets;
     const ExtKeys *extkeys;  // [keysets] round keys of the k_ext key sets (AES-F8 IV', AES-256)
+    const TwofishKeys *tfkeys; // [2 * keysets] Twofish session / F8 IV' keys (null: none yet)
     const FactoryRec *factories;
     const TransformerRec *transformers;
     uint64_t *ctx_keys;

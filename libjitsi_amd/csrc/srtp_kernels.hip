@@ -572,8 +572,9 @@ __device__ __forceinline__ bool ctr_would_throw(int32_t h, int plen) {
 // throws or a block is XORed at a negative offset (a negative length ciphers
 // nothing and a non-negative offset stays inside the packet).
 __device__ __forceinline__ bool enc_would_throw(int enc, int32_t h, int plen) {
-    if (enc == SRTP_AESCM_ENCRYPTION) return ctr_would_throw(h, plen);
-    if (enc == SRTP_AESF8_ENCRYPTION) return h == kHdrThrow || (plen > 0 && h < 0);
+    if (enc == SRTP_AESCM_ENCRYPTION || enc == SRTP_TWOFISH_ENCRYPTION) return ctr_would_throw(h, plen);
+    if (enc == SRTP_AESF8_ENCRYPTION || enc == SRTP_TWOFISHF8_ENCRYPTION)
+        return h == kHdrThrow || (plen > 0 && h < 0);
     return false;
 }
 
@@ -1074,7 +1075,9 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                 a.w_len[p] = (uint32_t)newL;
                 if (!(auth_ok & 1u)) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
             }
-            if (decrypt && c.enc == SRTP_AESCM_ENCRYPTION && newL - 8 < 0) threw = true;
+            if (decrypt && (c.enc == SRTP_AESCM_ENCRYPTION || c.enc == SRTP_TWOFISH_ENCRYPTION) &&
+                newL - 8 < 0)
+                threw = true;
             if (!threw) {
                 a.w_cw[p] = word;
                 // update :435-451 (reversed delta)
@@ -2243,17 +2246,13 @@ __device__ void f8_mac_advance(const F8Job &j, F8Mac &m, int upto) {
 // 12..15, XORed over each packet's region.  With `mac` (protect) each packet's
 // HMAC inner hash follows the ciphering block by block (the MAC is over the
 // ciphertext), so the packet is read once more only from L1/L2.
-__device__ void f8_pair(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
-                        const ExtKeys *f8, const F8Job &j0, const F8Job &j1, bool has1, bool mac,
+template <class Cipher>
+__device__ __forceinline__ void f8_pair(const Cipher &cipher, const KeySet *ks, const uint32_t ivp0[4],
+                        const uint32_t ivp1[4], const F8Job &j0, const F8Job &j1, bool has1, bool mac,
                         F8Mac &m0, F8Mac &m1) {
     uint32_t p0[4], p1[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) { p0[k] = j0.iv[k]; p1[k] = has1 ? j1.iv[k] : 0u; }
-    {
-        RoundKeys rkf;
-        load_rk_uniform(f8->rk, rkf);
-        aes_encrypt2(lds, tb, rkf, p0, p1);
-    }
+    for (int k = 0; k < 4; k++) { p0[k] = ivp0[k]; p1[k] = has1 ? ivp1[k] : 0u; }
     if (mac) {
 #pragma unroll
         for (int k = 0; k < 5; k++) m0.h[k] = m1.h[k] = sgpr(ks->ipad[k]);
@@ -2265,27 +2264,23 @@ __device__ void f8_pair(const char *__restrict__ lds, const TeBase &tb, const Ke
     const int n0 = j0.len > 0 ? (j0.len + 15) >> 4 : 0;
     const int n1 = has1 && j1.len > 0 ? (j1.len + 15) >> 4 : 0;
     const int nb = max(n0, n1);
-    if (nb > 0) {
-        RoundKeys rk;
-        load_round_keys_uniform(ks, rk);
-        uint32_t s0[4] = {0u, 0u, 0u, 0u}, s1[4] = {0u, 0u, 0u, 0u};
-        for (int jb = 0; jb < nb; jb++) {
-            uint32_t x[4], y[4];
+    uint32_t s0[4] = {0u, 0u, 0u, 0u}, s1[4] = {0u, 0u, 0u, 0u};
+    for (int jb = 0; jb < nb; jb++) {
+        uint32_t x[4], y[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) { x[k] = s0[k] ^ p0[k]; y[k] = s1[k] ^ p1[k]; }
-            x[3] ^= bswap((uint32_t)jb);
-            y[3] ^= bswap((uint32_t)jb);
-            aes_encrypt2(lds, tb, rk, x, y);
+        for (int k = 0; k < 4; k++) { x[k] = s0[k] ^ p0[k]; y[k] = s1[k] ^ p1[k]; }
+        x[3] ^= bswap((uint32_t)jb);
+        y[3] ^= bswap((uint32_t)jb);
+        cipher.encrypt2(x, y);
 #pragma unroll
-            for (int k = 0; k < 4; k++) { s0[k] = x[k]; s1[k] = y[k]; }
-            if (jb < n0) {
-                f8_xor_block(j0, jb, s0);
-                if (mac && jb + 1 < n0) f8_mac_advance(j0, m0, j0.off + 16 * (jb + 1));
-            }
-            if (jb < n1) {
-                f8_xor_block(j1, jb, s1);
-                if (mac && jb + 1 < n1) f8_mac_advance(j1, m1, j1.off + 16 * (jb + 1));
-            }
+        for (int k = 0; k < 4; k++) { s0[k] = x[k]; s1[k] = y[k]; }
+        if (jb < n0) {
+            f8_xor_block(j0, jb, s0);
+            if (mac && jb + 1 < n0) f8_mac_advance(j0, m0, j0.off + 16 * (jb + 1));
+        }
+        if (jb < n1) {
+            f8_xor_block(j1, jb, s1);
+            if (mac && jb + 1 < n1) f8_mac_advance(j1, m1, j1.off + 16 * (jb + 1));
         }
     }
     if (mac) { // everything after the region is final: the remaining inner blocks
@@ -2365,8 +2360,8 @@ __device__ __forceinline__ F8Job cm_job(const BundleArgs &a, const KeySet *ks, u
     return j;
 }
 
-__device__ void cm256_one(const char *__restrict__ lds, const TeBase &tb, const KeySet *ks,
-                          const ExtKeys *ext, const F8Job &j, bool mac) {
+template <class Cipher>
+__device__ __forceinline__ void cm_one(const Cipher &cipher, const KeySet *ks, const F8Job &j, bool mac) {
     F8Mac m;
     if (mac) {
 #pragma unroll
@@ -2375,24 +2370,80 @@ __device__ void cm256_one(const char *__restrict__ lds, const TeBase &tb, const 
         f8_mac_advance(j, m, j.off);
     }
     const int nb = j.len > 0 ? (j.len + 15) >> 4 : 0;
-    if (nb > 0) {
-        RoundKeys256 rk;
-        load_rk256_uniform(ext->rk, rk);
-        for (int jb = 0; jb < nb; jb += 2) {
-            uint32_t x[4], y[4];
-            ctr_input(j.iv, jb, x);
-            ctr_input(j.iv, jb + 1, y);
-            aes256_encrypt2(lds, tb, rk, x, y);
-            f8_xor_block(j, jb, x);
-            if (jb + 1 < nb) f8_xor_block(j, jb + 1, y);
-            if (mac) f8_mac_advance(j, m, j.off + 16 * min(jb + 2, nb));
-        }
+    for (int jb = 0; jb < nb; jb += 2) {
+        uint32_t x[4], y[4];
+        ctr_input(j.iv, jb, x);
+        ctr_input(j.iv, jb + 1, y);
+        cipher.encrypt2(x, y);
+        f8_xor_block(j, jb, x);
+        if (jb + 1 < nb) f8_xor_block(j, jb + 1, y);
+        if (mac) f8_mac_advance(j, m, j.off + 16 * min(jb + 2, nb));
     }
     if (mac) {
         f8_mac_advance(j, m, 0x7fffffff);
         f8_trailer(ks, j, m);
     }
 }
+
+// ------------------------------------------------------- block ciphers of k_ext
+// Two blocks per call (the two-block AES round code, or two interleaved
+// Twofish chains).
+// The AES round keys are (re)loaded into SGPRs by each call -- scalar loads
+// of one key set, cheap next to two blocks of rounds -- so no key array stays
+// live across a packet's chain.
+struct Aes128Cipher {
+    const char *lds;
+    TeBase tb;
+    const uint32_t *rk; // 44 words, wave-uniform
+    __device__ __forceinline__ void encrypt2(uint32_t a[4], uint32_t b[4]) const {
+        RoundKeys r;
+        load_rk_uniform(rk, r);
+        aes_encrypt2(lds, tb, r, a, b);
+    }
+};
+struct Aes256Cipher {
+    const char *lds;
+    TeBase tb;
+    const uint32_t *rk; // 60 words, wave-uniform
+    __device__ __forceinline__ void encrypt2(uint32_t a[4], uint32_t b[4]) const {
+        RoundKeys256 r;
+        load_rk256_uniform(rk, r);
+        aes256_encrypt2(lds, tb, r, a, b);
+    }
+};
+
+// Twofish (Schneier et al. 1998, 4.1-4.3) with the key schedule's g() tables
+// read from HBM through the caches (4 KB per key, the same for the whole key
+// set); the words are little-endian, like the AES state words.
+struct TwofishCipher {
+    const TwofishKeys *k;
+    __device__ __forceinline__ uint32_t g(uint32_t x) const {
+        const uint32_t *T = &k->T[0][0];
+        return T[x & 255u] ^ T[256u + ((x >> 8) & 255u)] ^ T[512u + ((x >> 16) & 255u)] ^
+               T[768u + (x >> 24)];
+    }
+    __device__ __forceinline__ void encrypt2(uint32_t a[4], uint32_t b[4]) const {
+        const uint32_t *K = k->K;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { a[i] ^= K[i]; b[i] ^= K[i]; }
+#pragma unroll 2
+        for (int r = 0; r < 16; r++) {
+            const uint32_t ka = K[2 * r + 8], kb = K[2 * r + 9];
+            const uint32_t ta0 = g(a[0]), ta1 = g(rotl(a[1], 8u));
+            const uint32_t tb0 = g(b[0]), tb1 = g(rotl(b[1], 8u));
+            const uint32_t na0 = rotl(a[2] ^ (ta0 + ta1 + ka), 31u);
+            const uint32_t na1 = rotl(a[3], 1u) ^ (ta0 + 2u * ta1 + kb);
+            const uint32_t nb0 = rotl(b[2] ^ (tb0 + tb1 + ka), 31u);
+            const uint32_t nb1 = rotl(b[3], 1u) ^ (tb0 + 2u * tb1 + kb);
+            a[2] = a[0]; a[3] = a[1]; a[0] = na0; a[1] = na1;
+            b[2] = b[0]; b[3] = b[1]; b[0] = nb0; b[1] = nb1;
+        }
+        const uint32_t oa[4] = {a[2] ^ K[4], a[3] ^ K[5], a[0] ^ K[6], a[1] ^ K[7]};
+        const uint32_t ob[4] = {b[2] ^ K[4], b[3] ^ K[5], b[0] ^ K[6], b[1] ^ K[7]};
+#pragma unroll
+        for (int i = 0; i < 4; i++) { a[i] = oa[i]; b[i] = ob[i]; }
+    }
+};
 
 // This packet needs k_ext: final status OK, an ext key set, and for unprotect
 // decryption is due (SRTP: no DISCARD/SILENCE flag; SRTCP: the E flag).
@@ -2420,6 +2471,50 @@ __device__ __forceinline__ bool ext_todo(const BundleArgs &a, uint32_t p, uint32
 // set (packets of one transformer usually sit side by side), else one by one.
 constexpr int kExtBlock = 512; // two packets per lane: 1024 packets per workgroup, one per CU
 
+// One key set's packets in k_ext: j0 (and j1 when has1, the lane's pair).
+__device__ __forceinline__ void ext_keyset(const BundleArgs &a, const char *__restrict__ lds, const TeBase &tb,
+                           uint32_t ks_u, uint32_t q0, uint32_t q1, bool has1) {
+    const KeySet *ks = a.keysets + ks_u;
+    const int enc = (int)sgpr(ks->enc_type);
+    const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    if (enc == SRTP_AESCM_ENCRYPTION || enc == SRTP_TWOFISH_ENCRYPTION) { // counter mode
+        const F8Job j0 = cm_job(a, ks, q0);
+        if (enc == SRTP_AESCM_ENCRYPTION) { // AES-256-CM
+            const Aes256Cipher c{lds, tb, a.extkeys[ks_u].rk};
+            cm_one(c, ks, j0, mac);
+            if (has1) cm_one(c, ks, cm_job(a, ks, q1), mac);
+        } else {
+            const TwofishCipher c{a.tfkeys + 2 * (size_t)ks_u};
+            cm_one(c, ks, j0, mac);
+            if (has1) cm_one(c, ks, cm_job(a, ks, q1), mac);
+        }
+        return;
+    }
+    // F8: IV' = E(k_e ^ (k_s || 0x55..), IV), then the chain under k_e
+    const F8Job j0 = f8_job(a, ks, q0);
+    F8Job j1 = j0;
+    if (has1) j1 = f8_job(a, ks, q1);
+    uint32_t p0[4], p1[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { p0[k] = j0.iv[k]; p1[k] = has1 ? j1.iv[k] : 0u; }
+    F8Mac m0, m1;
+    if (enc == SRTP_AESF8_ENCRYPTION) {
+        const Aes128Cipher ivc{lds, tb, a.extkeys[ks_u].rk};
+        ivc.encrypt2(p0, p1);
+        const Aes128Cipher c{lds, tb, ks->rk};
+        f8_pair(c, ks, p0, p1, j0, j1, has1, mac, m0, m1);
+    } else { // TWOFISHF8_ENCRYPTION
+        const TwofishCipher ivc{a.tfkeys + 2 * (size_t)ks_u + 1};
+        ivc.encrypt2(p0, p1);
+        const TwofishCipher c{a.tfkeys + 2 * (size_t)ks_u};
+        f8_pair(c, ks, p0, p1, j0, j1, has1, mac, m0, m1);
+    }
+    if (mac) {
+        f8_trailer(ks, j0, m0);
+        if (has1) f8_trailer(ks, j1, m1);
+    }
+}
+
 __global__ __launch_bounds__(kExtBlock) void k_ext(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2431,38 +2526,13 @@ __global__ __launch_bounds__(kExtBlock) void k_ext(BundleArgs a) {
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
     const bool pair = t0 && t1 && k0 == k1;
-    bool one0 = t0 && !pair, one1 = t1 && !pair;
+    const bool one0 = t0 && !pair, one1 = t1 && !pair;
+    // pairs, and lone first packets (which take their key set's pass)
     for_each_keyset(pair || one0, t0 ? k0 : k1, [&](uint32_t ks_u) {
-        // pairs, and lone first packets (which take their key set's pass)
-        const KeySet *ks = a.keysets + ks_u;
-        if (sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION) { // AES-256-CM
-            const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
-            cm256_one(lds, tb, ks, a.extkeys + ks_u, cm_job(a, ks, pair || one0 ? q0 : q1), mac);
-            if (pair) cm256_one(lds, tb, ks, a.extkeys + ks_u, cm_job(a, ks, q1), mac);
-            return;
-        }
-        const F8Job j0 = f8_job(a, ks, pair || one0 ? q0 : q1);
-        F8Job j1 = j0;
-        if (pair) j1 = f8_job(a, ks, q1);
-        const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
-        F8Mac m0, m1;
-        f8_pair(lds, tb, ks, a.extkeys + ks_u, j0, j1, pair, mac, m0, m1);
-        if (mac) {
-            f8_trailer(ks, j0, m0);
-            if (pair) f8_trailer(ks, j1, m1);
-        }
+        ext_keyset(a, lds, tb, ks_u, pair || one0 ? q0 : q1, q1, pair);
     });
     for_each_keyset(one1, k1, [&](uint32_t ks_u) { // lone second packets
-        const KeySet *ks = a.keysets + ks_u;
-        const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
-        if (sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION) {
-            cm256_one(lds, tb, ks, a.extkeys + ks_u, cm_job(a, ks, q1), mac);
-            return;
-        }
-        const F8Job j = f8_job(a, ks, q1);
-        F8Mac m0, m1;
-        f8_pair(lds, tb, ks, a.extkeys + ks_u, j, j, false, mac, m0, m1);
-        if (mac) f8_trailer(ks, j, m0);
+        ext_keyset(a, lds, tb, ks_u, q1, q1, false);
     });
 }
 

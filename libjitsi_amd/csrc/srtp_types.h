@@ -41,6 +41,18 @@ struct alignas(64) ExtKeys {
 };
 static_assert(sizeof(ExtKeys) == 256, "ExtKeys is 256 B");
 
+// Twofish key material of a key set (ZRTP "2FS": TWOFISH_ENCRYPTION /
+// TWOFISHF8_ENCRYPTION): subkeys and the four g() tables of the key schedule
+// (key-dependent S-boxes times the MDS columns).  Two per key set -- [0] the
+// session key, [1] the F8 IV' key -- in a table allocated with the first
+// Twofish factory.
+struct alignas(256) TwofishKeys {
+    uint32_t K[40];
+    uint32_t pad[24];
+    uint32_t T[4][256];
+};
+static_assert(sizeof(TwofishKeys) == 4352, "TwofishKeys is 4352 B");
+
 struct FactoryRec {      // SRTPContextFactory
     int32_t open;        // 0 after close(): getDefaultContext() == null
     int32_t ks_rtp;      // key set of its default SRTPCryptoContext

@@ -144,6 +144,13 @@ def profile_policies(profile: str):
         "NULL_HMAC_SHA1_80": (P.NULL_ENCRYPTION, 0, 0, 10, 10),
         "NULL_HMAC_SHA1_32": (P.NULL_ENCRYPTION, 0, 0, 4, 10),
         "F8_128_HMAC_SHA1_80": (P.AESF8_ENCRYPTION, 16, 14, 10, 10),
+        # ZRTP "2FS" Twofish policies (ZRTPTransformEngine.java:864-900: Twofish
+        # with HMAC-SHA1 "HS80"/"HS32"; key length 128 or 256 bits)
+        "TWOFISH_CM_128_HMAC_SHA1_80": (P.TWOFISH_ENCRYPTION, 16, 14, 10, 10),
+        "TWOFISH_CM_128_HMAC_SHA1_32": (P.TWOFISH_ENCRYPTION, 16, 14, 4, 10),
+        "TWOFISH_CM_256_HMAC_SHA1_80": (P.TWOFISH_ENCRYPTION, 32, 14, 10, 10),
+        "TWOFISH_F8_128_HMAC_SHA1_80": (P.TWOFISHF8_ENCRYPTION, 16, 14, 10, 10),
+        "TWOFISH_F8_256_HMAC_SHA1_80": (P.TWOFISHF8_ENCRYPTION, 32, 14, 10, 10),
         # AES-256-CM (RFC 6188): SRTPCryptoContext with encKeyLength 32
         "AES_256_CM_HMAC_SHA1_80": (P.AESCM_ENCRYPTION, 32, 14, 10, 10),
         "AES_256_CM_HMAC_SHA1_32": (P.AESCM_ENCRYPTION, 32, 14, 4, 10),
@@ -550,6 +557,25 @@ class RawPacket:
 
 
 TRAILER_ROOM = 16  # largest trailer: SRTCP E|index (4) + 12-byte tag
+
+
+def block_encrypt(enc_type: int, key: bytes, block: bytes) -> bytes:
+    """One block of the policy's cipher on the host (AES-128/256, Twofish)."""
+    out = (C.c_uint8 * 16)()
+    N.check(N.lib().srtp_block_encrypt(enc_type, bytes(key), len(key), bytes(block)[:16], out), None,
+            "block_encrypt")
+    return bytes(out)
+
+
+def derive_session_keys_for(enc_type: int, masterKey: bytes, masterSalt: bytes, rtcp: bool = False):
+    """Session keys with the policy's cipher as the PRF (Twofish for the ZRTP
+    Twofish policies, AES otherwise)."""
+    mk = bytes(masterKey)
+    klen = 32 if len(mk) >= 32 else 16
+    enc, auth, salt = (C.c_uint8 * klen)(), (C.c_uint8 * 20)(), (C.c_uint8 * 14)()
+    N.check(N.lib().srtp_derive_session_keys_for(enc_type, mk[:klen], klen, bytes(masterSalt)[:14],
+                                                 int(rtcp), enc, auth, salt), None, "kdf")
+    return bytes(enc), bytes(auth), bytes(salt)
 
 
 def derive_session_keys(masterKey: bytes, masterSalt: bytes, rtcp: bool = False):

@@ -82,6 +82,8 @@ def lib():
         L.orc_hmac_sha1.argtypes = [u8p, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_derive_keys.argtypes = [u8p, u8p, C.c_int, u8p, u8p, u8p]
         L.orc_derive_keys_n.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, u8p, u8p]
+        L.orc_derive_keys_twofish.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, u8p, u8p]
+        L.orc_twofish_encrypt_block.argtypes = [u8p, C.c_int, u8p, u8p]
         L.orc_aes_f8.argtypes = [u8p, u8p, C.c_int, u8p, u8p, C.c_int]
         L.orc_bench_round_trips.restype = C.c_int64
         L.orc_bench_round_trips.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
@@ -121,6 +123,26 @@ def derive_keys(master_key: bytes, master_salt: bytes, rtcp: bool = False):
     P = C.POINTER(C.c_uint8)
     lib().orc_derive_keys_n(kp, klen, sp, int(rtcp), enc.ctypes.data_as(P),
                             auth.ctypes.data_as(P), salt.ctypes.data_as(P))
+    return enc.tobytes(), auth.tobytes(), salt.tobytes()
+
+
+def twofish_block(key: bytes, block: bytes) -> bytes:
+    k, kp = _u8(key)
+    i, ip = _u8(block)
+    o = np.zeros(16, np.uint8)
+    lib().orc_twofish_encrypt_block(kp, len(key), ip, o.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return o.tobytes()
+
+
+def derive_keys_twofish(master_key: bytes, master_salt: bytes, rtcp: bool = False):
+    """Session keys of a Twofish policy (Twofish PRF, key length = master key's)."""
+    klen = 32 if len(master_key) >= 32 else 16
+    k, kp = _u8(master_key[:klen])
+    s, sp = _u8(master_salt)
+    enc, auth, salt = np.zeros(klen, np.uint8), np.zeros(20, np.uint8), np.zeros(14, np.uint8)
+    P = C.POINTER(C.c_uint8)
+    lib().orc_derive_keys_twofish(kp, klen, sp, int(rtcp), enc.ctypes.data_as(P),
+                                  auth.ctypes.data_as(P), salt.ctypes.data_as(P))
     return enc.tobytes(), auth.tobytes(), salt.tobytes()
 
 

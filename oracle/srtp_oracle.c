@@ -8,6 +8,7 @@
  */
 #define OPENSSL_SUPPRESS_DEPRECATED 1
 #include "srtp_oracle.h"
+#include "twofish.h"
 
 #include <openssl/evp.h>
 #include <openssl/hmac.h>
@@ -47,9 +48,9 @@ typedef struct orc_ctx {
     int mode;
     uint8_t enc_key[32], auth_key[20], salt_key[14];
     int key_len; /* 16 or 32 (AES-256-CM) */
-    EVP_CIPHER_CTX *ecb;  /* AES-128 / AES-256 keyed with the session key */
-    EVP_CIPHER_CTX *ctr;  /* tuned mode */
-    EVP_CIPHER_CTX *f8;   /* AES-F8: IV' cipher keyed with encKey ^ (salt || 0x55..) */
+    struct blk *ecb;      /* AES-128/256 or Twofish keyed with the session key */
+    EVP_CIPHER_CTX *ctr;  /* tuned mode (AES) */
+    struct blk *f8;       /* F8: IV' cipher keyed with encKey ^ (salt || 0x55..) */
     HMAC_CTX *hmac;       /* ref: re-keyed per packet; tuned: pre-keyed template */
     HMAC_CTX *hmac_work;
     /* SRTPCryptoContext state (:130-164) */
@@ -96,6 +97,54 @@ static inline void aes_block(EVP_CIPHER_CTX *c, const uint8_t in[16], uint8_t ou
     EVP_EncryptUpdate(c, out, &outl, in, 16);
 }
 
+/* A block cipher instance: AES through OpenSSL, or Twofish (twofish.c) --
+ * BaseSRTPCryptoContext picks AES.createBlockCipher() or TwofishEngine by the
+ * policy's cipher (:197-226). */
+typedef struct blk {
+    EVP_CIPHER_CTX *evp;
+    tf_key *tf;
+} blk_t;
+
+static int is_twofish(int enc) {
+    return enc == ORC_TWOFISH_ENCRYPTION || enc == ORC_TWOFISHF8_ENCRYPTION;
+}
+static int is_ctr(int enc) { return enc == ORC_AESCM_ENCRYPTION || enc == ORC_TWOFISH_ENCRYPTION; }
+static int is_f8(int enc) { return enc == ORC_AESF8_ENCRYPTION || enc == ORC_TWOFISHF8_ENCRYPTION; }
+
+static blk_t *blk_new(int twofish, const uint8_t *key, int key_len) {
+    blk_t *b = (blk_t *)calloc(1, sizeof *b);
+    if (twofish) {
+        b->tf = (tf_key *)calloc(1, sizeof *b->tf);
+        tf_set_key(b->tf, key, key_len);
+    } else {
+        b->evp = aes_ecb_new_n(key, key_len);
+    }
+    return b;
+}
+
+static void blk_free(blk_t *b) {
+    if (!b) return;
+    if (b->evp) EVP_CIPHER_CTX_free(b->evp);
+    if (b->tf) {
+        memset(b->tf, 0, sizeof *b->tf);
+        free(b->tf);
+    }
+    free(b);
+}
+
+static inline void blk_enc(blk_t *b, const uint8_t in[16], uint8_t out[16]) {
+    if (b->tf) tf_encrypt(b->tf, in, out);
+    else aes_block(b->evp, in, out);
+}
+
+void orc_twofish_encrypt_block(const uint8_t *key, int key_len, const uint8_t in[16],
+                               uint8_t out[16]) {
+    tf_key t;
+    tf_set_key(&t, key, key_len);
+    tf_encrypt(&t, in, out);
+    memset(&t, 0, sizeof t);
+}
+
 void orc_aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
     EVP_CIPHER_CTX *c = aes_ecb_new(key);
     aes_block(c, in, out);
@@ -111,18 +160,18 @@ void orc_hmac_sha1(const uint8_t *key, int key_len, const uint8_t *msg, size_t n
  * keystream is AES(iv[0..13] || u16_be(j)); one extra tail block is always
  * computed; a negative, non-multiple-of-16 length makes the tail arraycopy
  * throw (IndexOutOfBoundsException). */
-static int get_cipher_stream(EVP_CIPHER_CTX *c, uint8_t *out, int length, const uint8_t iv[16]) {
+static int get_cipher_stream(blk_t *c, uint8_t *out, int length, const uint8_t iv[16]) {
     uint8_t in[16], tmp[16];
     memcpy(in, iv, 14);
     int ctr, ctr_end = length / 16; /* Java int division truncates like C99 */
     for (ctr = 0; ctr < ctr_end; ctr++) {
         in[14] = (uint8_t)((ctr & 0xFF00) >> 8);
         in[15] = (uint8_t)(ctr & 0x00FF);
-        aes_block(c, in, out + ctr * 16);
+        blk_enc(c, in, out + ctr * 16);
     }
     in[14] = (uint8_t)((ctr & 0xFF00) >> 8);
     in[15] = (uint8_t)(ctr & 0x00FF);
-    aes_block(c, in, tmp);
+    blk_enc(c, in, tmp);
     int rem = length % 16; /* Java remainder has the dividend's sign, like C99 */
     if (rem < 0)
         return THROW;
@@ -144,7 +193,7 @@ static int cipher_ctr_process(orc_ctx *x, uint8_t *data, int buf_len, int off, i
         return THROW; /* data[i + off] AIOOBE on the first XOR (:119-120) */
     if (len == 0)
         return 0;
-    if (x->mode == ORC_MODE_TUNED) {
+    if (x->mode == ORC_MODE_TUNED && x->ctr) {
         int outl = 0;
         EVP_EncryptInit_ex(x->ctr, NULL, NULL, NULL, iv);
         EVP_EncryptUpdate(x->ctr, data + off, &outl, data + off, len);
@@ -162,11 +211,12 @@ static int cipher_ctr_process(orc_ctx *x, uint8_t *data, int buf_len, int off, i
 
 /* SRTPCipherF8.deriveForIV, SRTPCipherF8.java:66-95: the IV' cipher is keyed
  * with key ^ (salt || 0x55 0x55 ..) (the salt copied, the rest 0x55). */
-static EVP_CIPHER_CTX *f8_iv_cipher_new(const uint8_t key[16], const uint8_t *salt, int salt_len) {
-    uint8_t mk[16];
-    for (int i = 0; i < 16; i++)
+static blk_t *f8_iv_cipher_new(int twofish, const uint8_t *key, int key_len, const uint8_t *salt,
+                               int salt_len) {
+    uint8_t mk[32];
+    for (int i = 0; i < key_len; i++)
         mk[i] = (uint8_t)(key[i] ^ (i < salt_len ? salt[i] : 0x55));
-    EVP_CIPHER_CTX *c = aes_ecb_new(mk);
+    blk_t *c = blk_new(twofish, mk, key_len);
     memset(mk, 0, sizeof mk);
     return c;
 }
@@ -176,10 +226,10 @@ static EVP_CIPHER_CTX *f8_iv_cipher_new(const uint8_t key[16], const uint8_t *sa
  * bytes 12..15 big-endian; data[off + 16j + i] ^= S(j)[i].  The XOR loop
  * throws (AIOOBE) at a negative offset before touching the block; a negative
  * length processes nothing. */
-static int cipher_f8_process(EVP_CIPHER_CTX *c, EVP_CIPHER_CTX *f8c, uint8_t *data, int off,
-                             int len, const uint8_t iv[16]) {
+static int cipher_f8_process(blk_t *c, blk_t *f8c, uint8_t *data, int off, int len,
+                             const uint8_t iv[16]) {
     uint8_t ivp[16], S[16];
-    aes_block(f8c, iv, ivp);
+    blk_enc(f8c, iv, ivp);
     memset(S, 0, sizeof S);
     int64_t J = 0;
     int in_len = len;
@@ -189,7 +239,7 @@ static int cipher_f8_process(EVP_CIPHER_CTX *c, EVP_CIPHER_CTX *f8c, uint8_t *da
         S[12] ^= (uint8_t)(J >> 24); S[13] ^= (uint8_t)(J >> 16);
         S[14] ^= (uint8_t)(J >> 8);  S[15] ^= (uint8_t)J;
         J++;
-        aes_block(c, S, S);
+        blk_enc(c, S, S);
         if (off < 0) return THROW;
         for (int i = 0; i < n; i++) data[off + i] ^= S[i];
         in_len -= n;
@@ -200,10 +250,10 @@ static int cipher_f8_process(EVP_CIPHER_CTX *c, EVP_CIPHER_CTX *f8c, uint8_t *da
 
 void orc_aes_f8(const uint8_t key[16], const uint8_t *salt, int salt_len, const uint8_t iv[16],
                 uint8_t *data, int len) {
-    EVP_CIPHER_CTX *c = aes_ecb_new(key), *f = f8_iv_cipher_new(key, salt, salt_len);
+    blk_t *c = blk_new(0, key, 16), *f = f8_iv_cipher_new(0, key, 16, salt, salt_len);
     cipher_f8_process(c, f, data, 0, len, iv);
-    EVP_CIPHER_CTX_free(c);
-    EVP_CIPHER_CTX_free(f);
+    blk_free(c);
+    blk_free(f);
 }
 
 /* BaseSRTPCryptoContext.authenticatePacketHMAC, :269-278: tag_store =
@@ -239,9 +289,24 @@ void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp, uint8
 /* deriveSrtpKeys :393-447 / deriveSrtcpKeys with a master key of key_len
  * bytes: the PRF is AES-128 or AES-256 (RFC 6188 4.1), the session key key_len
  * bytes. */
+static void derive_keys_prf(int twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
+                            int rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+
 void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
                        uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
-    EVP_CIPHER_CTX *c = aes_ecb_new_n(mk, key_len);
+    derive_keys_prf(0, mk, key_len, ms, rtcp, enc, auth, salt);
+}
+
+/* Twofish policies: deriveSrtpKeys keys the TwofishEngine `cipher` with the
+ * master key, so the PRF is Twofish (BaseSRTPCryptoContext :217-225). */
+void orc_derive_keys_twofish(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
+                             uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+    derive_keys_prf(1, mk, key_len, ms, rtcp, enc, auth, salt);
+}
+
+static void derive_keys_prf(int twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
+                            int rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+    blk_t *c = blk_new(twofish, mk, key_len);
     uint8_t iv[16];
     int base = rtcp ? 3 : 0;
     for (int lab = 0; lab < 3; lab++) {
@@ -255,7 +320,7 @@ void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int
         else
             get_cipher_stream(c, salt, 14, iv);
     }
-    EVP_CIPHER_CTX_free(c);
+    blk_free(c);
 }
 
 /* ---------- RawPacket accessors (nm/RawPacket.java) --------------------- */
@@ -323,9 +388,9 @@ static void map_put(ctx_map *m, uint32_t k, orc_ctx *v) {
 
 static void ctx_free(orc_ctx *x) {
     if (!x) return;
-    if (x->ecb) EVP_CIPHER_CTX_free(x->ecb);
+    blk_free(x->ecb);
     if (x->ctr) EVP_CIPHER_CTX_free(x->ctr);
-    if (x->f8) EVP_CIPHER_CTX_free(x->f8);
+    blk_free(x->f8);
     if (x->hmac) HMAC_CTX_free(x->hmac);
     if (x->hmac_work) HMAC_CTX_free(x->hmac_work);
     memset(x, 0, sizeof *x);
@@ -342,16 +407,16 @@ static void map_clear(ctx_map *m) {
 
 /* ---------- factory / transformer -------------------------------------- */
 static int policy_ok(const orc_policy *p, int rtcp) {
-    if (p->enc_type != ORC_NULL_ENCRYPTION && p->enc_type != ORC_AESCM_ENCRYPTION &&
-        p->enc_type != ORC_AESF8_ENCRYPTION)
+    if (p->enc_type != ORC_NULL_ENCRYPTION && !is_ctr(p->enc_type) && !is_f8(p->enc_type))
         return 0;
     if (p->enc_type != ORC_NULL_ENCRYPTION && p->salt_key_len != 14) return 0;
     if (p->enc_type == ORC_AESF8_ENCRYPTION && p->enc_key_len != 16) return 0;
-    if (p->enc_type == ORC_AESCM_ENCRYPTION && p->enc_key_len != 16 && p->enc_key_len != 32)
+    if ((p->enc_type == ORC_AESCM_ENCRYPTION || is_twofish(p->enc_type)) && p->enc_key_len != 16 &&
+        p->enc_key_len != 32)
         return 0;
     /* SRTCP F8 ciphers [8, 8 + length - 4 - tag) (SRTCPCryptoContext :285-291),
      * which leaves the packet unless an HMAC trailer of >= 4 tag bytes follows */
-    if (rtcp && p->enc_type == ORC_AESF8_ENCRYPTION &&
+    if (rtcp && is_f8(p->enc_type) &&
         (p->auth_type == ORC_NULL_AUTHENTICATION || p->auth_tag_len < 4))
         return 0;
     if (p->auth_type != ORC_NULL_AUTHENTICATION && p->auth_type != ORC_HMACSHA1_AUTHENTICATION)
@@ -370,8 +435,8 @@ orc_factory *orc_factory_new(int sender, const uint8_t *mk, int key_len, const u
      * 4.3 prescribes -- behaviour "parity unpinned". */
     if (salt_len < 14 || !policy_ok(srtp, 0) || !policy_ok(srtcp, 1)) return NULL;
     /* BaseSRTPCryptoContext copies encKeyLength bytes of the master key (:187-190) */
-    const int need = (srtp->enc_type == ORC_AESCM_ENCRYPTION && srtp->enc_key_len == 32) ||
-                     (srtcp->enc_type == ORC_AESCM_ENCRYPTION && srtcp->enc_key_len == 32) ? 32 : 16;
+    const int need = (srtp->enc_type != ORC_NULL_ENCRYPTION && srtp->enc_key_len == 32) ||
+                     (srtcp->enc_type != ORC_NULL_ENCRYPTION && srtcp->enc_key_len == 32) ? 32 : 16;
     if (key_len < need) return NULL;
     orc_factory *f = (orc_factory *)calloc(1, sizeof *f);
     f->sender = sender; f->mode = mode;
@@ -424,13 +489,14 @@ static orc_ctx *make_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) 
     orc_ctx *x = (orc_ctx *)calloc(1, sizeof *x);
     x->ssrc = ssrc; x->kind = t->kind; x->mode = f->mode;
     x->policy = (t->kind == ORC_KIND_RTP) ? f->srtp : f->srtcp;
-    x->key_len = x->policy.enc_type == ORC_AESCM_ENCRYPTION && x->policy.enc_key_len == 32 ? 32 : 16;
-    orc_derive_keys_n(f->master_key, x->key_len, f->master_salt, t->kind == ORC_KIND_RTCP,
-                      x->enc_key, x->auth_key, x->salt_key);
-    x->ecb = aes_ecb_new_n(x->enc_key, x->key_len);
-    if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) /* deriveSrtpKeys :443-444 */
-        x->f8 = f8_iv_cipher_new(x->enc_key, x->salt_key, 14);
-    if (x->mode == ORC_MODE_TUNED) {
+    const int tf = is_twofish(x->policy.enc_type);
+    x->key_len = x->policy.enc_type != ORC_NULL_ENCRYPTION && x->policy.enc_key_len == 32 ? 32 : 16;
+    derive_keys_prf(tf, f->master_key, x->key_len, f->master_salt, t->kind == ORC_KIND_RTCP,
+                    x->enc_key, x->auth_key, x->salt_key);
+    x->ecb = blk_new(tf, x->enc_key, x->key_len);
+    if (is_f8(x->policy.enc_type)) /* deriveSrtpKeys :443-444 */
+        x->f8 = f8_iv_cipher_new(tf, x->enc_key, x->key_len, x->salt_key, 14);
+    if (x->mode == ORC_MODE_TUNED && !tf) {
         x->ctr = EVP_CIPHER_CTX_new();
         EVP_EncryptInit_ex(x->ctr, x->key_len == 32 ? EVP_aes_256_ctr() : EVP_aes_128_ctr(), NULL,
                            x->enc_key, NULL);
@@ -519,8 +585,8 @@ static int srtp_process_aesf8(orc_ctx *x, uint8_t *b, int len, int cap) {
 }
 
 static int srtp_encrypt(orc_ctx *x, uint8_t *b, int len, int cap) {
-    if (x->policy.enc_type == ORC_AESCM_ENCRYPTION) return srtp_process_aescm(x, b, len, cap);
-    if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) return srtp_process_aesf8(x, b, len, cap);
+    if (is_ctr(x->policy.enc_type)) return srtp_process_aescm(x, b, len, cap);
+    if (is_f8(x->policy.enc_type)) return srtp_process_aesf8(x, b, len, cap);
     return 0;
 }
 
@@ -629,10 +695,10 @@ static int srtcp_process_aesf8(orc_ctx *x, uint8_t *b, int L, int32_t index) {
 static int srtcp_transform(orc_ctx *x, uint8_t *b, uint32_t *len, int cap) {
     int L = (int)*len;
     int encrypt = 0;
-    if (x->policy.enc_type == ORC_AESCM_ENCRYPTION) {
+    if (is_ctr(x->policy.enc_type)) {
         if (srtcp_process_aescm(x, b, L, cap, x->sent_index) == THROW) return ORC_ERR_MALFORMED;
         encrypt = 1;
-    } else if (x->policy.enc_type == ORC_AESF8_ENCRYPTION) {
+    } else if (is_f8(x->policy.enc_type)) {
         if (srtcp_process_aesf8(x, b, L, x->sent_index) == THROW) return ORC_ERR_MALFORMED;
         encrypt = 1;
     }
@@ -672,9 +738,9 @@ static int srtcp_reverse(orc_ctx *x, uint8_t *b, uint32_t *len, int cap) {
         for (int i = 0; i < T; i++)
             if (x->temp_store[i] != x->tag_store[i]) return ORC_DROP_AUTH;
     }
-    if (decrypt && x->policy.enc_type == ORC_AESCM_ENCRYPTION)
+    if (decrypt && is_ctr(x->policy.enc_type))
         if (srtcp_process_aescm(x, b, L, cap, index) == THROW) return ORC_ERR_MALFORMED;
-    if (decrypt && x->policy.enc_type == ORC_AESF8_ENCRYPTION)
+    if (decrypt && is_f8(x->policy.enc_type))
         if (srtcp_process_aesf8(x, b, L, index) == THROW) return ORC_ERR_MALFORMED;
     srtcp_update(x, index);
     return ORC_OK;

@@ -132,6 +132,12 @@ void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp,
                      uint8_t enc[16], uint8_t auth[20], uint8_t salt[14]);
 void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
                        uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+/* Twofish policies: the PRF is Twofish keyed with the master key. */
+void orc_derive_keys_twofish(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
+                             uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+/* one Twofish block (twofish.c), key_len 16 / 24 / 32 */
+void orc_twofish_encrypt_block(const uint8_t *key, int key_len, const uint8_t in[16],
+                               uint8_t out[16]);
 
 /* CPU baseline timing (oracle_bench.c): packets protected AND unprotected by
  * `threads` pinned threads in about `seconds` (-1 on a rejected packet). */
