@@ -46,6 +46,7 @@ struct srtp_engine {
     int32_t *w_status = nullptr;
     uint32_t *w_cw = nullptr, *w_len = nullptr, *g0 = nullptr, *auth_ok = nullptr, *mid = nullptr;
     uint32_t *tailc = nullptr, *spec = nullptr, *long_list = nullptr;
+    uint32_t *spos = nullptr;
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     // Two control blocks (BundleCtl + e_min row), alternating per bundle: each
@@ -198,13 +199,13 @@ uint32_t next_pow2(uint64_t x) {
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
                     e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp,
-                    e->long_list};
+                    e->long_list, e->spos};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
     e->w_status = nullptr;
     e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
-    e->long_list = nullptr;
+    e->long_list = e->spos = nullptr;
     e->sort_temp = nullptr;
     e->scratch_n = 0;
 }
@@ -231,6 +232,7 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
     HIPCHK(e, dalloc(&e->spec, m));
     HIPCHK(e, dalloc(&e->long_list, m / 256 + 2)); // at most one long chain per walk span
+    HIPCHK(e, dalloc(&e->spos, m));
     e->sort_temp_bytes = sort_temp_bytes(m);
     HIPCHK(e, hipMalloc(&e->sort_temp, std::max<size_t>(e->sort_temp_bytes, 16)));
     // per-tile digit counts start at zero (each scan re-zeroes what it read)
@@ -630,6 +632,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
     a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
     a.tailc = e->tailc; a.spec = e->spec; a.long_list = e->long_list;
+    a.spos = e->spos;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     a.sort_counts = ss.counts[0];

@@ -55,6 +55,7 @@ struct BundleArgs {
     uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
     uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
     uint32_t *long_list;   // [n / 256 + 2] sorted start index of each long context chain
+    uint32_t *spos;        // [n] unprotect: each record's position in sort order (the last sort pass)
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse
     int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse

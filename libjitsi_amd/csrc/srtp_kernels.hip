@@ -774,6 +774,7 @@ struct SortPass {
     const uint32_t *counts;   // this pass's [tiles][256] digit counts
     uint32_t *next_counts;    // next pass's [tiles][256] counts, or null on the last pass
     uint32_t *zero;           // the previous pass's counts (this tile's row is re-zeroed), or null
+    uint32_t *spos;           // last unprotect pass: spos[packet] = its sorted position, or null
 };
 
 __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
@@ -863,7 +864,9 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
         if (i < sp.n) {
             const uint32_t pos = s_base[(key[r] >> sp.shift) & 255u] + loc[r];
             sp.dk[pos] = key[r];
-            sp.dv[pos] = sp.sv[i]; // read here, not held across the ranking (a held copy went to scratch)
+            const WalkRec rec = sp.sv[i]; // read here, not held across the ranking (a held copy went to scratch)
+            sp.dv[pos] = rec;
+            if (sp.spos) sp.spos[rec.p & kRecIdxMask] = pos;
             if (sp.next_counts)
                 atomicAdd(&sp.next_counts[(pos / kSortTile) * 256 + ((key[r] >> (sp.shift + 8)) & 255u)], 1u);
         }
@@ -889,6 +892,7 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
         // pass q re-zeroes pass q-1's counts (read by all of pass q-1); the last
         // pass's are re-zeroed by the walk (BundleArgs::sort_zero)
         sp.zero = q ? ss.counts[q - 1] : nullptr;
+        sp.spos = last && a.reverse ? a.spos : nullptr;
         hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
     }
     return hipGetLastError();
@@ -1820,6 +1824,28 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     STAMP(2);
 }
 
+// ============================================================== ROC guess
+// guessIndex (SRTPCryptoContext :457-475) against a context state: the ROC
+// the walk would guess for `seq` were it the context's next packet.
+__device__ __forceinline__ int32_t guess_roc(const CtxState &st, int32_t seq) {
+    if (!(st.flags & 1u)) return st.a; // seqNumSet false: the ROC as is
+    const int32_t s_l = st.b;
+    if (s_l < 32768) return (seq - s_l > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
+    return (s_l - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
+}
+
+// First sorted position of `key` (records are sorted by context), given
+// sk[hi] == key: a lower bound over [0, hi].
+__device__ __forceinline__ uint32_t chain_head(const uint32_t *__restrict__ sk, uint32_t hi, uint32_t key) {
+    uint32_t lo = 0u;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sk[mid] < key) lo = mid + 1u;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // ============================================================== k_unprotect
 // Unprotect, one lane per packet, before the walk: HMAC-SHA1 over the
 // ciphertext (SRTPCryptoContext.authenticatePacket :237-266 /
@@ -1845,24 +1871,12 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     cs.iv[0] = cs.iv[1] = cs.iv[2] = cs.iv[3] = 0u;
     int end;       // bytes covered by the MAC and the decryption: [0, end) / [off, end)
     uint32_t suffix;
-    bool spec = false, far = false;
+    bool spec = false;
     if (rtp) {
         const int32_t seq = (int32_t)(bswap(hdr.x) & 0xffffu);
-        int32_t g = st.a;
-        if (st.flags & 1u) { // guessIndex :457-475 on the bundle-start state
-            const int32_t s_l = st.b;
-            if (s_l < 32768) g = (seq - s_l > 32768) ? (int32_t)((uint32_t)st.a - 1u) : st.a;
-            else g = (s_l - 32768 > seq) ? (int32_t)((uint32_t)st.a + 1u) : st.a;
-            // More than half a wrap ahead of s_l (and not just behind it): a
-            // context whose packets advance that far within one bundle -- a
-            // skewed bundle, one SSRC carrying many thousand packets -- wraps
-            // on the way, so the walk will guess one ROC higher than the
-            // bundle-start state does.  Speculate that forward ROC and check
-            // the tag under the start-state guess too (auth_ok bit 1).
-            const int32_t dist = (seq - s_l) & 0xffff;
-            far = dist > 32768 && dist < 65536 - 1024;
-            if (far) g = (int32_t)((uint32_t)g + 1u);
-        }
+        // guessIndex on the bundle-start state (for a packet deep in a long
+        // chain, k_unprotect's state yields the chain's guess; see there)
+        const int32_t g = guess_roc(st, seq);
         a.g0[p] = (uint32_t)g;
         end = do_mac ? (L - T > 0 ? L - T : 0) : L;
         suffix = (uint32_t)g;
@@ -1986,15 +2000,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             else outer_words(d, h, ks);
             sha1_compress(h, d);
         }
-        uint32_t ok = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
-        if (far) { // the tag under the start-state guess g0 - 1 (bit 1; bit 2: checked)
-            ReverifyArgs rv; // chunk nb_full still holds ciphertext: decryption comes below
-            rv.pkt = pkt;
-            rv.mid = a.mid + 5 * (size_t)p;
-            rv.tailc = nullptr;
-            ok |= (reverify_rtp(rv, ks, L, (int32_t)(suffix - 1u)) ? 2u : 0u) | 4u;
-        }
-        a.auth_ok[p] = ok;
+        a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
     }
     if (spec) {
         // reload the round keys through an opaque copy of the key-set pointer:
@@ -2028,14 +2034,44 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords];
     STAMP(0);
     STAMP_XCC();
-    fill_te4(s_te);
-    STAMP(1);
+    // the packet's context state and whether it lies deep in a long chain
+    // (its kLongRank-th predecessor in sort order has its context), loaded
+    // while the T-tables fill
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.n) return;
-    const uint32_t slot = a.p_slot[p];
+    const bool live = p < a.n;
+    uint32_t slot = kNoSlot, pos = 0u;
+    if (live) {
+        slot = a.p_slot[p];
+        pos = a.spos[p];
+    }
     const bool todo = slot != kNoSlot;
     CtxState st = {};
-    if (todo) st = a.ctx[slot];
+    bool lng = false;
+    if (todo) {
+        st = a.ctx[slot];
+        lng = pos >= kLongRank && a.sk_out[pos - kLongRank] == slot;
+    }
+    fill_te4(s_te);
+    STAMP(1);
+    if (!live) return;
+    // The ROC speculated on is the walk's guess were the packet its context's
+    // next: guessIndex on the bundle-start state, exact while no earlier
+    // packet of the context in this bundle has wrapped.  Deep in a long chain
+    // (one SSRC carrying thousands of packets in one bundle) the chain may
+    // have wrapped on the way, maybe more than once: guess the ROC whose index
+    // lies nearest the chain head's index plus the packet's rank in the chain
+    // (exact for an in-order chain losing fewer than 32768 packets).  It is
+    // handed over as a state whose guessIndex returns it (seqNumSet clear), so
+    // nothing more stays live across the key-set loop.  A wrong guess only
+    // costs the walk a re-check of the tag.
+    if (lng) {
+        const uint32_t h = chain_head(a.sk_out, pos - kLongRank, slot);
+        const int32_t seq_h = (int32_t)(a.sv_out[h].word & 0xffffu);
+        const int32_t seq = (int32_t)(a.sv_out[pos].word & 0xffffu); // RTP: the packet's SEQ
+        const int64_t e = (int64_t)guess_roc(st, seq_h) * 65536 + seq_h + (int64_t)(pos - h);
+        st.a = (int32_t)((e - seq + 32768) >> 16);
+        st.flags &= ~1u;
+    }
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
     for_each_keyset(todo, st.ks, [&](uint32_t ks_u) {

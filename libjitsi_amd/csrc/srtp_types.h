@@ -91,6 +91,8 @@ constexpr uint32_t kRecSkipDec = 0x80000000u; // FLAG_DISCARD|FLAG_SILENCE: no d
 constexpr uint32_t kRecIdxMask = 0x0FFFFFFFu;
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
 
+constexpr uint32_t kLongRank = 1024; // k_unprotect: chain packets from this rank on get a rank-based ROC guess
+
 // bundle control block (zeroed per bundle)
 struct BundleCtl {
     uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk

@@ -136,3 +136,27 @@ def test_long_srtcp_chain(engine):
     pc.seg, pc.length = seg, ln
     rb = synth.select(pc, np.r_[0:3000, 100:130, 2990:3000])
     twin.run(cr, True, rb.seg, rb.off, rb.length, rb.cap)
+
+
+def test_multi_wrap_chain_with_loss(engine):
+    """One SSRC wrapping twice within one bundle, received with 45% loss and
+    light reordering.  k_unprotect guesses the ROC of a packet deep in a long
+    chain from its rank in the chain; with this much loss the guess drifts
+    more than half a wrap behind the true index for the later packets, so the
+    walk overturns those guesses and re-checks their tags -- slower, and
+    still bit-exact."""
+    twin = Twin(engine)
+    (k, s), = synth.keys(214, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    b = synth.rtp_bundle(1 << 17, 1, (60, 200), seed=215, seq0=[40000])  # wraps at 25536, 91072
+    seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+    assert (st == 0).all()
+    pb = b.copy()
+    pb.seg, pb.length = seg, ln
+    rng = np.random.default_rng(216)
+    keep = np.sort(rng.choice(b.n, int(0.55 * b.n), replace=False))
+    fb = faults(synth.select(pb, keep), rng, frac=0.001)
+    _, _, st2 = twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap)
+    assert (st2 == 0).sum() > 0.99 * keep.size
+    assert engine.context_state(rcv.e, int(b.ssrc[0]))["roc"] == 2
