@@ -74,6 +74,7 @@ extern "C" {
 #define SRTP_TWOFISHF8_ENCRYPTION 4 /* F8 over Twofish */
 #define SRTP_NULL_AUTHENTICATION 0
 #define SRTP_HMACSHA1_AUTHENTICATION 1
+#define SRTP_SKEIN_AUTHENTICATION 2 /* Skein-512 MAC, tag_len * 8 output bits (ZRTP "SK32"/"SK64") */
 
 /* transformer kinds */
 #define SRTP_KIND_RTP 0  /* SRTPTransformer */
@@ -103,7 +104,7 @@ extern "C" {
 #define SRTP_ENOMEM -2
 #define SRTP_EFULL -3   /* context / factory / transformer table full */
 #define SRTP_EDEVICE -4 /* HIP runtime error */
-#define SRTP_EPOLICY -5 /* policy outside AES_CM_128 / NULL x HMAC_SHA1 / NULL */
+#define SRTP_EPOLICY -5 /* policy outside the implemented ciphers x MACs (see srtp_factory_create) */
 
 typedef struct srtp_engine srtp_engine;
 
@@ -377,6 +378,16 @@ int srtp_derive_session_keys_n(const uint8_t *master_key, int32_t key_len,
 int srtp_derive_session_keys_for(int32_t enc_type, const uint8_t *master_key, int32_t key_len,
                                  const uint8_t master_salt[14], int32_t rtcp, uint8_t *enc_key,
                                  uint8_t auth_key[20], uint8_t salt_key[14]);
+/* The same with an auth key of auth_len bytes (1..64; 32 for ZRTP's Skein
+ * policies, whose authKeyLength is 32: ZRTPTransformEngine.java:867-872). */
+int srtp_derive_session_keys_auth(int32_t enc_type, const uint8_t *master_key, int32_t key_len,
+                                  const uint8_t master_salt[14], int32_t rtcp, uint8_t *enc_key,
+                                  uint8_t *auth_key, int32_t auth_len, uint8_t salt_key[14]);
+/* Skein-512 (version 1.3) keyed with key[0..key_len) (key_len 0: the plain
+ * hash), out_bits (1..512) output bits: the tag bccontrib's SkeinMac computes
+ * for SRTPPolicy.SKEIN_AUTHENTICATION (BaseSRTPCryptoContext.java:244-248). */
+int srtp_skein512_mac(const uint8_t *key, int32_t key_len, int32_t out_bits, const uint8_t *msg,
+                      size_t n, uint8_t *out);
 /* One block of the policy's cipher: AES-128/256 (key_len 16 / 32) or Twofish
  * (enc_type SRTP_TWOFISH*, key_len 16 / 24 / 32). */
 int srtp_block_encrypt(int32_t enc_type, const uint8_t *key, int32_t key_len, const uint8_t in[16],

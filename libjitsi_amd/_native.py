@@ -46,7 +46,7 @@ EXPORTED = [
     "srtp_engine_get_opts", "srtp_derive_session_keys_n", "srtp_derive_session_keys_for",
     "srtp_block_encrypt", "srtp_aggregator_opts_default", "srtp_aggregator_create",
     "srtp_aggregator_submit", "srtp_aggregator_flush", "srtp_aggregator_stats",
-    "srtp_aggregator_destroy",
+    "srtp_aggregator_destroy", "srtp_derive_session_keys_auth", "srtp_skein512_mac",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -147,6 +147,8 @@ def lib() -> C.CDLL:
     L.srtp_derive_session_keys_n.argtypes = [C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, pu8]
     L.srtp_derive_session_keys_for.argtypes = [i32, C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, pu8]
     L.srtp_block_encrypt.argtypes = [i32, C.c_char_p, i32, C.c_char_p, pu8]
+    L.srtp_derive_session_keys_auth.argtypes = [i32, C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, i32, pu8]
+    L.srtp_skein512_mac.argtypes = [C.c_char_p, i32, i32, C.c_char_p, C.c_size_t, pu8]
     L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
     L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_pipeline_create.argtypes = [vp, u32, C.c_size_t, i32, C.POINTER(vp)]

@@ -28,7 +28,9 @@ struct srtp_engine {
     KeySet *d_keysets = nullptr;
     ExtKeys *d_extkeys = nullptr; // round keys of the k_ext key sets (same index)
     TwofishKeys *d_tfkeys = nullptr; // 2 per key set, allocated with the first Twofish factory
-    uint32_t n_ext = 0;           // AES-F8 / AES-256-CM key sets created: k_ext runs only when > 0
+    SkeinKeys *d_skkeys = nullptr;   // 1 per key set, allocated with the first Skein factory
+    uint32_t n_ext = 0;           // k_ext key sets created (F8, AES-256, Twofish, Skein): k_ext runs only when > 0
+    uint32_t n_skein = 0;         // Skein-MAC key sets created: k_skein runs only when > 0
     uint32_t n_keysets = 0, max_keysets = 0;
     FactoryRec *d_factories = nullptr;
     std::vector<FactoryRec> factories;
@@ -133,9 +135,16 @@ bool policy_ok(const srtp_policy *p, bool rtcp) {
     if (rtcp && is_f8(p->enc_type) &&
         (p->auth_type == SRTP_NULL_AUTHENTICATION || p->auth_tag_len < 4))
         return false;
-    if (p->auth_type != SRTP_NULL_AUTHENTICATION && p->auth_type != SRTP_HMACSHA1_AUTHENTICATION)
+    if (p->auth_type != SRTP_NULL_AUTHENTICATION && p->auth_type != SRTP_HMACSHA1_AUTHENTICATION &&
+        p->auth_type != SRTP_SKEIN_AUTHENTICATION)
         return false;
     if (p->auth_type == SRTP_HMACSHA1_AUTHENTICATION && p->auth_key_len != 20) return false;
+    // Skein (ZRTP "SK32"/"SK64", authKeyLen 32, ZRTPTransformEngine.java:867-872):
+    // a key of one UBI block at most and a tag of >= 1 byte (the MAC's output
+    // is tag_len * 8 bits, SRTPCryptoContext.java:421-428)
+    if (p->auth_type == SRTP_SKEIN_AUTHENTICATION &&
+        (p->auth_key_len < 1 || p->auth_key_len > 64 || p->auth_tag_len < 1))
+        return false;
     if (p->auth_tag_len < 0 || p->auth_tag_len > 12) return false;
     return true;
 }
@@ -148,17 +157,20 @@ int master_key_len(const srtp_policy *pol) {
 }
 
 void build_keyset(const uint8_t *mk, const uint8_t ms[14], bool rtcp, const srtp_policy *pol,
-                  KeySet *ks, ExtKeys *ext, TwofishKeys *tf) {
+                  KeySet *ks, ExtKeys *ext, TwofishKeys *tf, SkeinKeys *sk) {
     memset(ks, 0, sizeof *ks);
     memset(ext, 0, sizeof *ext);
     memset(tf, 0, 2 * sizeof *tf);
+    memset(sk, 0, sizeof *sk);
     const int klen = master_key_len(pol);
     const bool twofish = is_twofish(pol->enc_type);
-    uint8_t enc[32], auth[20], salt[16] = {0};
+    const bool skein = pol->auth_type == SRTP_SKEIN_AUTHENTICATION;
+    const int auth_len = skein ? pol->auth_key_len : 20;
+    uint8_t enc[32], auth[64], salt[16] = {0};
     // RFC 3711 4.3 with the policy's cipher as the PRF -- AES-128, AES-256
     // (RFC 6188 4.1) or Twofish -- as deriveSrtpKeys :393-447 does with a key
-    // of encKeyLength bytes
-    derive_session_keys_cipher(twofish, mk, klen, ms, rtcp, enc, auth, salt);
+    // of encKeyLength bytes (and an auth key of authKeyLength bytes)
+    derive_session_keys_cipher(twofish, mk, klen, ms, rtcp, enc, auth, salt, auth_len);
     // SRTPCipherF8.deriveForIV :66-95: the IV' key is key ^ (salt || 0x55..)
     uint8_t m[32];
     for (int i = 0; i < klen; i++) m[i] = (uint8_t)(enc[i] ^ (i < 14 ? salt[i] : 0x55));
@@ -177,7 +189,12 @@ void build_keyset(const uint8_t *mk, const uint8_t ms[14], bool rtcp, const srtp
         ks->ext = 1;
     }
     memset(m, 0, sizeof m);
-    hmac_sha1_midstates(auth, ks->ipad, ks->opad);
+    if (skein) { // SkeinMac keyed once: the packets' MACs start from g0 (k_skein)
+        skein512_key_state(auth, auth_len, 8 * pol->auth_tag_len, sk->g0);
+        ks->ext = 1;
+    } else {
+        hmac_sha1_midstates(auth, ks->ipad, ks->opad);
+    }
     for (int i = 0; i < 4; i++)
         ks->salt[i] = (uint32_t)salt[4 * i] | ((uint32_t)salt[4 * i + 1] << 8) |
                       ((uint32_t)salt[4 * i + 2] << 16) | ((uint32_t)salt[4 * i + 3] << 24);
@@ -455,13 +472,15 @@ void srtp_engine_destroy(srtp_engine *e) {
         (void)hipMemset(e->d_extkeys, 0, (size_t)e->max_keysets * sizeof(ExtKeys));
     if (e->d_tfkeys)
         (void)hipMemset(e->d_tfkeys, 0, 2 * (size_t)e->max_keysets * sizeof(TwofishKeys));
+    if (e->d_skkeys)
+        (void)hipMemset(e->d_skkeys, 0, (size_t)e->max_keysets * sizeof(SkeinKeys));
     free_scratch(e);
     for (auto &m : e->marks) {
         (void)hipEventDestroy(m.a);
         (void)hipEventDestroy(m.b);
     }
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
-    void *ptrs[] = {e->d_keysets, e->d_extkeys, e->d_tfkeys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
+    void *ptrs[] = {e->d_keysets, e->d_extkeys, e->d_tfkeys, e->d_skkeys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
                     e->e_min, e->ctl, e->d_count, e->d_counters, e->h_seg, e->h_off, e->h_len,
                     e->h_cap, e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
@@ -489,8 +508,21 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
     KeySet ks[2];
     ExtKeys f8[2];
     std::vector<TwofishKeys> tf(4);
-    build_keyset(mk, ms, false, srtp_pol, &ks[0], &f8[0], &tf[0]);
-    build_keyset(mk, ms, true, srtcp_pol, &ks[1], &f8[1], &tf[2]);
+    SkeinKeys sk[2];
+    build_keyset(mk, ms, false, srtp_pol, &ks[0], &f8[0], &tf[0], &sk[0]);
+    build_keyset(mk, ms, true, srtcp_pol, &ks[1], &f8[1], &tf[2], &sk[1]);
+    const bool any_skein = srtp_pol->auth_type == SRTP_SKEIN_AUTHENTICATION ||
+                           srtcp_pol->auth_type == SRTP_SKEIN_AUTHENTICATION;
+    if (any_skein) {
+        if (!e->d_skkeys && dalloc(&e->d_skkeys, (size_t)e->max_keysets) != hipSuccess) {
+            memset(sk, 0, sizeof sk);
+            return fail(e, SRTP_ENOMEM, "Skein key table");
+        }
+        HIPCHK(e, hipMemcpy(e->d_skkeys + e->n_keysets, sk, sizeof sk, hipMemcpyHostToDevice));
+        memset(sk, 0, sizeof sk);
+        e->n_skein += (uint32_t)((srtp_pol->auth_type == SRTP_SKEIN_AUTHENTICATION) +
+                                 (srtcp_pol->auth_type == SRTP_SKEIN_AUTHENTICATION));
+    }
     if (is_twofish(srtp_pol->enc_type) || is_twofish(srtcp_pol->enc_type)) {
         if (!e->d_tfkeys && dalloc(&e->d_tfkeys, 2 * (size_t)e->max_keysets) != hipSuccess) {
             std::fill(tf.begin(), tf.end(), TwofishKeys{});
@@ -607,6 +639,8 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.keysets = e->d_keysets;
     a.extkeys = e->d_extkeys;
     a.tfkeys = e->d_tfkeys;
+    a.skkeys = e->d_skkeys;
+    a.has_skein = e->n_skein ? 1 : 0;
     a.factories = e->d_factories;
     a.transformers = e->d_transformers;
     a.ctx_keys = e->d_ctx_keys;
@@ -664,6 +698,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);
         HIPCHK(e, launch_unprotect(a, s));
+        if (e->n_skein) HIPCHK(e, launch_skein(a, s));
     }
     {
         StageTimer t(e, s, SRTP_STAGE_WALK);
@@ -681,6 +716,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         StageTimer t(e, s, SRTP_STAGE_PROTECT);
         HIPCHK(e, launch_protect(a, s));
         if (e->n_ext) HIPCHK(e, launch_ext(a, s));
+        if (e->n_skein) HIPCHK(e, launch_skein(a, s));
     }
     HIPCHK(e, hipEventRecord(e->ev_last, s));
     e->last_stream = s;
@@ -985,6 +1021,25 @@ int srtp_derive_session_keys_for(int32_t enc_type, const uint8_t *mk, int32_t ke
                                  uint8_t salt[14]) {
     if (!mk || !ms || !enc || !auth || !salt || (key_len != 16 && key_len != 32)) return SRTP_EINVAL;
     derive_session_keys_cipher(is_twofish(enc_type), mk, key_len, ms, rtcp != 0, enc, auth, salt);
+    return SRTP_OK;
+}
+
+int srtp_derive_session_keys_auth(int32_t enc_type, const uint8_t *mk, int32_t key_len,
+                                  const uint8_t ms[14], int32_t rtcp, uint8_t *enc, uint8_t *auth,
+                                  int32_t auth_len, uint8_t salt[14]) {
+    if (!mk || !ms || !enc || !auth || !salt || (key_len != 16 && key_len != 32) || auth_len < 1 ||
+        auth_len > 64)
+        return SRTP_EINVAL;
+    derive_session_keys_cipher(is_twofish(enc_type), mk, key_len, ms, rtcp != 0, enc, auth, salt,
+                               auth_len);
+    return SRTP_OK;
+}
+
+int srtp_skein512_mac(const uint8_t *key, int32_t key_len, int32_t out_bits, const uint8_t *msg,
+                      size_t n, uint8_t *out) {
+    if ((!key && key_len) || (!msg && n) || !out || key_len < 0 || out_bits < 1 || out_bits > 512)
+        return SRTP_EINVAL;
+    skein512_mac(key, key_len, out_bits, msg, n, out);
     return SRTP_OK;
 }
 

@@ -310,7 +310,7 @@ void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14],
 }
 
 void derive_session_keys_cipher(bool twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
-                                bool rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+                                bool rtcp, uint8_t *enc, uint8_t *auth, uint8_t salt[14], int auth_len) {
     uint32_t rk[60];
     static thread_local uint32_t tK[40], tT[4][256];
     PrfCipher prf;
@@ -325,7 +325,7 @@ void derive_session_keys_cipher(bool twofish, const uint8_t *mk, int key_len, co
     uint8_t iv[16];
     const int base = rtcp ? 3 : 0;
     uint8_t *outs[3] = {enc, auth, salt};
-    const int lens[3] = {key_len, 20, 14};
+    const int lens[3] = {key_len, auth_len, 14};
     for (int lab = 0; lab < 3; lab++) {
         memcpy(iv, ms, 14);
         iv[7] ^= (uint8_t)(base + lab); // computeIv: key_id = label << 48 lands in byte 7
@@ -351,6 +351,90 @@ void hmac_sha1_midstates(const uint8_t key[20], uint32_t ipad[5], uint32_t opad[
     sha1_compress(opad, bo);
     memset(bi, 0, 64);
     memset(bo, 0, 64);
+}
+
+// ------------------------------------------------------------ Skein-512
+// "The Skein Hash Function Family" 1.3: Threefish-512 (72 rounds, a subkey
+// every 4), UBI chaining, and the keyed form SkeinMac uses.  The host only
+// runs the key and config UBIs once per key set (plus whole MACs for the C
+// ABI's srtp_skein512_mac); the per-packet MAC is on the GPU.
+namespace {
+
+const int kSkR[8][4] = {{46, 36, 19, 37}, {33, 27, 14, 42}, {17, 49, 36, 39}, {44, 9, 54, 56},
+                        {39, 30, 34, 24}, {13, 50, 10, 17}, {25, 29, 39, 43}, {8, 35, 56, 22}};
+
+inline uint64_t rol64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
+
+// h = Threefish-512(key h, tweak {t0, t1}, m) ^ m
+void skein_block(uint64_t h[8], const uint64_t m[8], uint64_t t0, uint64_t t1) {
+    uint64_t k[9], t[3] = {t0, t1, t0 ^ t1}, v[8];
+    k[8] = kSkeinParity;
+    for (int i = 0; i < 8; i++) {
+        k[i] = h[i];
+        k[8] ^= h[i];
+        v[i] = m[i];
+    }
+    for (int s = 0; s <= 18; s++) {
+        for (int i = 0; i < 8; i++) v[i] += k[(s + i) % 9];
+        v[5] += t[s % 3];
+        v[6] += t[(s + 1) % 3];
+        v[7] += (uint64_t)s;
+        if (s == 18) break;
+        for (int r = 0; r < 4; r++) {
+            const int *R = kSkR[(4 * s + r) % 8];
+            // MIX on (0,1) (2,3) (4,5) (6,7), then the word permutation
+            // {2, 1, 4, 7, 6, 5, 0, 3}
+            for (int j = 0; j < 4; j++) {
+                v[2 * j] += v[2 * j + 1];
+                v[2 * j + 1] = rol64(v[2 * j + 1], R[j]) ^ v[2 * j];
+            }
+            const uint64_t w0 = v[0], w3 = v[3];
+            v[0] = v[2]; v[2] = v[4]; v[4] = v[6]; v[6] = w0;
+            v[3] = v[7]; v[7] = w3;
+        }
+    }
+    for (int i = 0; i < 8; i++) h[i] = v[i] ^ m[i];
+}
+
+// UBI(h, msg[0..n), type) over the whole message (zero-padded; one block of
+// zeros for an empty message)
+void skein_ubi(uint64_t h[8], const uint8_t *msg, size_t n, uint64_t type) {
+    size_t pos = 0;
+    bool first = true;
+    do {
+        uint8_t blk[64] = {0};
+        const size_t take = n - pos < 64 ? n - pos : 64;
+        if (take) memcpy(blk, msg + pos, take);
+        pos += take;
+        uint64_t m[8];
+        for (int i = 0; i < 8; i++) {
+            m[i] = 0;
+            for (int b = 7; b >= 0; b--) m[i] = (m[i] << 8) | blk[8 * i + b];
+        }
+        const uint64_t t1 = (type << 56) | (first ? 1ull << 62 : 0) | (pos == n ? 1ull << 63 : 0);
+        skein_block(h, m, pos, t1);
+        first = false;
+    } while (pos < n);
+}
+
+} // namespace
+
+void skein512_key_state(const uint8_t *key, int key_len, int out_bits, uint64_t g0[8]) {
+    memset(g0, 0, 64);
+    if (key_len > 0) skein_ubi(g0, key, (size_t)key_len, kSkeinTypeKey);
+    uint8_t cfg[32] = {'S', 'H', 'A', '3', 1, 0, 0, 0};
+    for (int i = 0; i < 8; i++) cfg[8 + i] = (uint8_t)((uint64_t)out_bits >> (8 * i));
+    skein_ubi(g0, cfg, sizeof cfg, kSkeinTypeCfg);
+}
+
+void skein512_mac(const uint8_t *key, int key_len, int out_bits, const uint8_t *msg, size_t n,
+                  uint8_t *out) {
+    uint64_t h[8];
+    skein512_key_state(key, key_len, out_bits, h);
+    skein_ubi(h, msg, n, kSkeinTypeMsg);
+    const uint8_t zero8[8] = {0};
+    skein_ubi(h, zero8, 8, kSkeinTypeOut);
+    for (int i = 0; i < (out_bits + 7) / 8; i++) out[i] = (uint8_t)(h[i / 8] >> (8 * (i % 8)));
 }
 
 } // namespace srtp

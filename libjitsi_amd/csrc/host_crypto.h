@@ -3,6 +3,7 @@
 // compression function (for the HMAC ipad/opad midstates).  Runs once per
 // factory; the per-packet path is on the GPU.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace srtp {
@@ -33,8 +34,10 @@ void derive_session_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14],
                            uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
 // With the Twofish PRF (twofish = true: the ZRTP Twofish policies key their
 // TwofishEngine with the master key).
+// auth_len: the policy's auth key length (20 for HMAC-SHA1, 32 for ZRTP's Skein).
 void derive_session_keys_cipher(bool twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
-                                bool rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+                                bool rtcp, uint8_t *enc, uint8_t *auth, uint8_t salt[14],
+                                int auth_len = 20);
 // Twofish key schedule (key_len 16, 24 or 32): subkeys K[40] and the four g()
 // tables (key-dependent S-boxes times the MDS columns); one block.
 void twofish_schedule(const uint8_t *key, int key_len, uint32_t K[40], uint32_t T[4][256]);
@@ -42,5 +45,17 @@ void twofish_encrypt_block(const uint32_t K[40], const uint32_t T[4][256], const
                            uint8_t out[16]);
 // HMAC-SHA1 ipad/opad midstates for a 20-byte key.
 void hmac_sha1_midstates(const uint8_t key[20], uint32_t ipad[5], uint32_t opad[5]);
+
+// Skein-512 (version 1.3): UBI block types, and the key-schedule parity
+// constant C240 of Threefish.
+constexpr uint64_t kSkeinParity = 0x1BD11BDAA9FC1A22ull;
+constexpr uint64_t kSkeinTypeKey = 0, kSkeinTypeCfg = 4, kSkeinTypeMsg = 48, kSkeinTypeOut = 63;
+// The chaining value of a keyed Skein-512 with out_bits output bits after the
+// key UBI (skipped for key_len 0) and the config UBI: SkeinMac's state before
+// the first message byte.
+void skein512_key_state(const uint8_t *key, int key_len, int out_bits, uint64_t g0[8]);
+// Whole Skein-512 MAC (key_len 0: the plain hash), ceil(out_bits / 8) bytes.
+void skein512_mac(const uint8_t *key, int key_len, int out_bits, const uint8_t *msg, size_t n,
+                  uint8_t *out);
 
 } // namespace srtp

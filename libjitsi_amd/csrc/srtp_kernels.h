@@ -16,6 +16,7 @@ struct BundleArgs {
     const KeySet *keysets;
     const ExtKeys *extkeys;  // [keysets] round keys of the k_ext key sets (AES-F8 IV', AES-256)
     const TwofishKeys *tfkeys; // [2 * keysets] Twofish session / F8 IV' keys (null: none yet)
+    const SkeinKeys *skkeys;   // [keysets] Skein-512 MAC keys (null: none yet)
     const FactoryRec *factories;
     const TransformerRec *transformers;
     uint64_t *ctx_keys;
@@ -37,6 +38,7 @@ struct BundleArgs {
     int32_t abort_on_error;
     uint32_t serial;       // bundle serial (context birth stamp)
     int32_t debug;         // diagnostics only (SRTP_DEBUG env): 0 in production
+    int32_t has_skein;     // the engine has Skein-MAC key sets (the walk's Skein re-check)
     unsigned long long *counters; // [kCountReplicas][kCtrStride] cumulative event counters
 #ifdef SRTP_STAMPS
     unsigned long long *stamps;   // diagnostic build only: per-wave start / filled / end times
@@ -83,6 +85,10 @@ SortScratch sort_scratch(void *temp, uint32_t n_max);
 hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s);
 // unprotect: fused tag check + speculative in-place decryption (before the walk)
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
+// Engines with Skein-MAC key sets.  Unprotect: those packets' tag check under
+// k_unprotect's ROC guess (after k_unprotect, before the walk).  Protect: their
+// trailers (after k_ext).
+hipError_t launch_skein(const BundleArgs &a, hipStream_t s);
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s);
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
 // unprotect: statuses/lengths out; undo/redo the rare speculation misses (after the walk)

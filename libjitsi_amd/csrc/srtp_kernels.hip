@@ -973,6 +973,168 @@ __device__ __forceinline__ bool reverify_rtp(ReverifyArgs r, const KeySet *ks, i
     return tag_matches(h, pkt + mac_len, T);
 }
 
+// ============================================================== Skein-512 MAC
+// SRTPPolicy.SKEIN_AUTHENTICATION (ZRTP "SK32"/"SK64"): bccontrib's SkeinMac,
+// keyed with the session auth key and an output of tag_len * 8 bits
+// (SRTPCryptoContext.java:421-428, SRTCPCryptoContext.java:185-192), fed the
+// same bytes as authenticatePacketHMAC (BaseSRTPCryptoContext.java:269-278):
+// the packet, then the ROC (SRTP) or the E|index word (SRTCP) big-endian.
+// Skein 1.3: each 64-B message block is one Threefish-512 encryption keyed
+// with the chaining value (UBI); the key and config blocks are folded into
+// SkeinKeys.g0 on the host.  Threefish is 64-bit add / rotate / xor, so it
+// runs on the VALU (two 32-bit ops each), one packet per lane.
+constexpr uint64_t kSkeinParity = 0x1BD11BDAA9FC1A22ull;
+constexpr uint64_t kSkeinMsg = 48ull << 56, kSkeinOut = 63ull << 56;
+constexpr uint64_t kSkeinFirst = 1ull << 62, kSkeinFinal = 1ull << 63;
+
+__device__ __forceinline__ constexpr int skein_rot(int d, int j) {
+    // Skein 1.3 Table 4: Threefish-512 rotation constants R(d mod 8, j)
+    constexpr int R[8][4] = {{46, 36, 19, 37}, {33, 27, 14, 42}, {17, 49, 36, 39}, {44, 9, 54, 56},
+                             {39, 30, 34, 24}, {13, 50, 10, 17}, {25, 29, 39, 43}, {8, 35, 56, 22}};
+    return R[d & 7][j];
+}
+
+template <int N>
+__device__ __forceinline__ uint64_t rotl64(uint64_t x) {
+    return (x << N) | (x >> (64 - N));
+}
+
+// Four rounds d0..d0+3 (MIX on word pairs, then the permutation {2,1,4,7,6,5,0,3}).
+template <int D0>
+__device__ __forceinline__ void threefish_rounds4(uint64_t v[8]) {
+#define SK_MIX(d)                                                                  \
+    v[0] += v[1]; v[1] = rotl64<skein_rot(d, 0)>(v[1]) ^ v[0];                     \
+    v[2] += v[3]; v[3] = rotl64<skein_rot(d, 1)>(v[3]) ^ v[2];                     \
+    v[4] += v[5]; v[5] = rotl64<skein_rot(d, 2)>(v[5]) ^ v[4];                     \
+    v[6] += v[7]; v[7] = rotl64<skein_rot(d, 3)>(v[7]) ^ v[6];                     \
+    { const uint64_t w0 = v[0], w3 = v[3];                                         \
+      v[0] = v[2]; v[2] = v[4]; v[4] = v[6]; v[6] = w0; v[3] = v[7]; v[7] = w3; }
+    SK_MIX(D0) SK_MIX(D0 + 1) SK_MIX(D0 + 2) SK_MIX(D0 + 3)
+#undef SK_MIX
+}
+
+template <int S>
+__device__ __forceinline__ void threefish_subkey(uint64_t v[8], const uint64_t k[9], const uint64_t t[3]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] += k[(S + i) % 9];
+    v[5] += t[S % 3];
+    v[6] += t[(S + 1) % 3];
+    v[7] += (uint64_t)S;
+}
+
+template <int S>
+__device__ __forceinline__ void threefish_from(uint64_t v[8], const uint64_t k[9], const uint64_t t[3]) {
+    if constexpr (S < 18) {
+        threefish_subkey<S>(v, k, t);
+        threefish_rounds4<4 * S>(v);
+        threefish_from<S + 1>(v, k, t);
+    } else {
+        threefish_subkey<18>(v, k, t);
+    }
+}
+
+// One UBI step: h = Threefish-512(key h, tweak {t0, t1}, m) ^ m (72 rounds).
+__device__ __forceinline__ void skein_ubi_block(uint64_t h[8], const uint64_t m[8], uint64_t t0, uint64_t t1) {
+    uint64_t k[9], v[8];
+    const uint64_t t[3] = {t0, t1, t0 ^ t1};
+    k[8] = kSkeinParity;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        k[i] = h[i];
+        k[8] ^= h[i];
+        v[i] = m[i];
+    }
+    threefish_from<0>(v, k, t);
+#pragma unroll
+    for (int i = 0; i < 8; i++) h[i] = v[i] ^ m[i];
+}
+
+// Message block b of pkt[0, L) || suffix (4 bytes big-endian), zero-padded,
+// as Skein's little-endian 64-bit words.  Reads 16-B units below L only (the
+// packet region is 16-B aligned and padded, so a unit may run past L).
+__device__ __forceinline__ void skein_msg_block(const uint8_t *pkt, int b, int L, uint32_t suffix_le,
+                                                uint64_t m[8]) {
+    const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (64 * b + 16 * q < L) v = qp[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int wp = 64 * b + 4 * k; // stream position of the word's byte 0
+        const int rem = L - wp;        // packet bytes in this word
+        uint32_t d = w[k] & (rem >= 4 ? ~0u : (rem <= 0 ? 0u : (1u << (8 * rem)) - 1u));
+        const int o = wp - L;          // suffix byte i sits at stream position L + i
+        if (o > -4 && o < 4) d |= o >= 0 ? (suffix_le >> (8 * o)) : (suffix_le << (8 * -o));
+        w[k] = d;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+}
+
+// Skein-MAC of pkt[0, L) || suffix under the key set's g0; returns the first
+// 12 output bytes as big-endian words (the layout tag_matches / tag_write use).
+// UNIFORM: g0 is the wave's key set (scalar registers); else per lane.
+template <bool UNIFORM>
+__device__ __forceinline__ void skein_mac(const SkeinKeys *sk, const uint8_t *pkt, int L, uint32_t suffix,
+                                          uint32_t tag[5]) {
+    uint64_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t g = sk->g0[i];
+        h[i] = UNIFORM ? ((uint64_t)sgpr((uint32_t)(g >> 32)) << 32) | sgpr((uint32_t)g) : g;
+    }
+    const int n = L + 4;
+    const int nb = (n + 63) >> 6;
+    const uint32_t sle = bswap(suffix);
+    // nb message blocks, then Output(G, No) = UBI(G, ToBytes(0, 8), Tout) --
+    // one block for No <= 512 -- through the same Threefish code
+    for (int b = 0; b <= nb; b++) {
+        uint64_t m[8];
+        uint64_t t0, t1;
+        if (b < nb) {
+            skein_msg_block(pkt, b, L, sle, m);
+            t0 = (uint64_t)min(64 * (b + 1), n);
+            t1 = kSkeinMsg | (b == 0 ? kSkeinFirst : 0ull) | (b == nb - 1 ? kSkeinFinal : 0ull);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) m[i] = 0ull;
+            t0 = 8;
+            t1 = kSkeinOut | kSkeinFirst | kSkeinFinal;
+        }
+        skein_ubi_block(h, m, t0, t1);
+    }
+    tag[0] = bswap((uint32_t)h[0]);
+    tag[1] = bswap((uint32_t)(h[0] >> 32));
+    tag[2] = bswap((uint32_t)h[1]);
+    tag[3] = tag[4] = 0u;
+}
+
+// The walk's re-check of a Skein-tagged SRTP packet under another ROC: the
+// whole MAC again (Skein packets are not deciphered before the walk, so the
+// packet still holds its ciphertext).  Only the walk instances launched for
+// engines with Skein key sets contain it.
+__device__ __forceinline__ bool skein_reverify(const SkeinKeys *sk, const uint8_t *pkt, int L, int T, uint32_t roc) {
+    int mac_len = L - T;
+    if (mac_len < 0) mac_len = 0;
+    uint32_t tag[5];
+    skein_mac<false>(sk, pkt, mac_len, roc, tag);
+    return tag_matches(tag, pkt + mac_len, T);
+}
+
+// The walk's tag re-check under ROC g, by the key set's MAC (SK: the engine
+// has Skein key sets).
+template <bool SK>
+__device__ __forceinline__ bool reverify_tag(const BundleArgs &a, ReverifyArgs rv, const KeySet *ks, int L,
+                                             int32_t g) {
+    if (SK && ks->auth_type == SRTP_SKEIN_AUTHENTICATION)
+        return skein_reverify(a.skkeys + (ks - a.keysets), rv.pkt, L, ks->tag_len, (uint32_t)g);
+    return reverify_rtp(rv, ks, L, g);
+}
+
 // ============================================================== k_walk
 // One lane per context: the serial state machine over the context's packets in
 // array order (records sorted by context slot, stable).
@@ -983,6 +1145,7 @@ struct WalkCtx {
 
 // Processes one packet; returns false when the rest of the context's packets
 // are aborted (a throw with abort_on_error).
+template <bool SK>
 __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, const WalkCtx &c,
                                          CtxState &st, const WalkRec &rec, uint32_t g0,
                                          uint32_t auth_ok, bool dry, int32_t tid) {
@@ -1027,7 +1190,7 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                     rv.pkt = a.seg + a.off[p];
                     rv.mid = a.mid + 5 * (size_t)p;
                     rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
-                    ok = reverify_rtp(rv, ks, L, g);
+                    ok = reverify_tag<SK>(a, rv, ks, L, g);
                     atomicAdd(&a.counters[kCtrRocRecheck], 1ull);
                 }
                 if (!ok) { a.w_status[p] = SRTP_STATUS_DROP_AUTH; return true; }
@@ -1166,7 +1329,7 @@ struct LongLds {
     uint32_t *info;   // [kLongStep] bit 0: keeps the speculation; bits 1..: delta & 63
 };
 
-template <bool REV>
+template <bool REV, bool SK>
 __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm) {
     const int lane = (int)(threadIdx.x & 63u);
     const uint32_t key = a.sk_out[i0];
@@ -1250,7 +1413,7 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm) {
                             rv.pkt = a.seg + a.off[p];
                             rv.mid = a.mid + 5 * (size_t)p;
                             rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
-                            g = reverify_rtp(rv, ks, L, (int32_t)roc);
+                            g = reverify_tag<SK>(a, rv, ks, L, (int32_t)roc);
                         }
                     }
                 } else {
@@ -1314,7 +1477,7 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm) {
                     const WalkRec r = sm.rec[k];
                     uint32_t g0 = 0u, ok = 0u;
                     if (REV) { g0 = sm.g0[k]; ok = sm.ok[k]; }
-                    (void)walk_one(a, ks, c, st, r, g0, ok, false, tid);
+                    (void)walk_one<SK>(a, ks, c, st, r, g0, ok, false, tid);
                 }
             }
             bcast_state(st);
@@ -1344,7 +1507,7 @@ constexpr int kWalkSpan = kWalkBlock * kWalkPer;
 constexpr int kWalkAhead = 256;
 constexpr int kWalkWin = kWalkSpan + kWalkAhead;
 
-template <bool REV>
+template <bool REV, bool SK>
 __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pass) {
     __shared__ WalkRec s_rec[kWalkWin];
     __shared__ uint32_t s_key[kWalkWin];
@@ -1369,7 +1532,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
             sm.g0 = REV ? s_g0 : s_start;
             sm.ok = REV ? s_ok : s_start;
             sm.info = s_start;
-            walk_long<REV>(a, a.long_list[q], sm);
+            walk_long<REV, SK>(a, a.long_list[q], sm);
         }
     }
     if (!limit_pass) // the sort's last digit counts, zero again for the next bundle
@@ -1437,7 +1600,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         auto step = [&](const WalkRec &r, uint32_t g0, uint32_t ok) -> bool {
             if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) return false;
             if (a.debug == 2) { st.window += r.p ^ g0 ^ ok; return true; }
-            return walk_one(a, ks, c, st, r, g0, ok, dry, tid);
+            return walk_one<SK>(a, ks, c, st, r, g0, ok, dry, tid);
         };
         // The staged window, from LDS only: no global load in this loop, so
         // nothing waits on vmcnt -- which would also wait for walk_one's
@@ -1862,7 +2025,9 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     const int L = (int)a.len[p];
     const int T = (int)sgpr(ks->tag_len);
     const bool rtp = sgpr(ks->kind) == SRTP_KIND_RTP;
-    const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    // HMAC-SHA1 here; a Skein-MAC key set's tags are checked by k_skein
+    // (its key sets are k_ext's: no speculation, so nothing is done here but g0)
+    const bool do_mac = sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
     // speculative decryption: AES-128-CM only (k_ext deciphers the rest)
     const bool aes = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext);
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
@@ -2448,6 +2613,26 @@ struct Aes256Cipher {
     }
 };
 
+// AES-256 (14 rounds), or AES-128 for a Skein key set's AES-128-CM (the
+// fused kernels' path is HMAC-only); wave-uniform choice.
+struct AesCmCipher {
+    const char *lds;
+    TeBase tb;
+    const uint32_t *rk;
+    bool a256;
+    __device__ __forceinline__ void encrypt2(uint32_t a[4], uint32_t b[4]) const {
+        if (a256) {
+            RoundKeys256 r;
+            load_rk256_uniform(rk, r);
+            aes256_encrypt2(lds, tb, r, a, b);
+        } else {
+            RoundKeys r;
+            load_rk_uniform(rk, r);
+            aes_encrypt2(lds, tb, r, a, b);
+        }
+    }
+};
+
 // Twofish (Schneier et al. 1998, 4.1-4.3) with the key schedule's g() tables
 // read from HBM through the caches (4 KB per key, the same for the whole key
 // set); the words are little-endian, like the AES state words.
@@ -2490,6 +2675,7 @@ __device__ __forceinline__ bool ext_todo(const BundleArgs &a, uint32_t p, uint32
     *ks_id = a.ctx[slot].ks;
     const KeySet *ks = a.keysets + *ks_id;
     if (!ks->ext) return false;
+    if (ks->enc_type == SRTP_NULL_ENCRYPTION) return false; // NULL cipher + Skein: k_skein only
     if (!a.reverse) return true;
     if (ks->kind == SRTP_KIND_RTP)
         return !((a.flags ? a.flags[p] : 0u) & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
@@ -2512,11 +2698,15 @@ __device__ __forceinline__ void ext_keyset(const BundleArgs &a, const char *__re
                            uint32_t ks_u, uint32_t q0, uint32_t q1, bool has1) {
     const KeySet *ks = a.keysets + ks_u;
     const int enc = (int)sgpr(ks->enc_type);
-    const bool mac = !a.reverse && sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    const int auth = (int)sgpr(ks->auth_type);
+    // HMAC fed as the blocks are ciphered; a Skein key set's trailer is
+    // k_skein's, after this pass
+    const bool mac = !a.reverse && auth == SRTP_HMACSHA1_AUTHENTICATION;
     if (enc == SRTP_AESCM_ENCRYPTION || enc == SRTP_TWOFISH_ENCRYPTION) { // counter mode
         const F8Job j0 = cm_job(a, ks, q0);
-        if (enc == SRTP_AESCM_ENCRYPTION) { // AES-256-CM
-            const Aes256Cipher c{lds, tb, a.extkeys[ks_u].rk};
+        if (enc == SRTP_AESCM_ENCRYPTION) { // AES-256-CM, or AES-128-CM of a Skein key set
+            const bool a256 = sgpr(a.extkeys[ks_u].nr) == 14;
+            const AesCmCipher c{lds, tb, a256 ? a.extkeys[ks_u].rk : ks->rk, a256};
             cm_one(c, ks, j0, mac);
             if (has1) cm_one(c, ks, cm_job(a, ks, q1), mac);
         } else {
@@ -2569,6 +2759,66 @@ __global__ __launch_bounds__(kExtBlock) void k_ext(BundleArgs a) {
     });
     for_each_keyset(one1, k1, [&](uint32_t ks_u) { // lone second packets
         ext_keyset(a, lds, tb, ks_u, q1, q1, false);
+    });
+}
+
+// ============================================================== k_skein
+// Skein-MAC key sets (engines that have them).  Unprotect, after k_unprotect
+// (which set each packet's ROC guess g0, and left these packets in place):
+// the tag check under g0 (SRTP) or of the packet and its E|index trailer
+// (SRTCP), as authenticatePacket :237-266 / SRTCPCryptoContext :333-353 do
+// with SkeinMac; the walk re-checks an SRTP tag whose ROC it guesses
+// differently.  Protect, after k_ext ciphered them (final statuses): the
+// trailer -- SRTCP's E|index word first (the MAC covers it; the NULL cipher
+// writes index 0, transformPacket :391-427), then the tag.
+constexpr int kSkeinBlock = 256;
+
+__global__ __launch_bounds__(kSkeinBlock) void k_skein(BundleArgs a) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    bool todo = false;
+    uint32_t ks_id = 0u;
+    if (p < a.n && (a.reverse || a.status[p] == SRTP_STATUS_OK)) {
+        const uint32_t slot = a.p_slot[p];
+        if (slot != kNoSlot) {
+            ks_id = a.ctx[slot].ks;
+            todo = a.keysets[ks_id].auth_type == SRTP_SKEIN_AUTHENTICATION;
+        }
+    }
+    for_each_keyset(todo, ks_id, [&](uint32_t ks_u) {
+        const KeySet *ks = a.keysets + ks_u;
+        const int T = (int)sgpr(ks->tag_len);
+        const bool rtp = sgpr(ks->kind) == SRTP_KIND_RTP;
+        uint8_t *pkt = a.seg + a.off[p];
+        const int L = (int)a.len[p]; // unprotect: as received; protect: final, with the trailer
+        int end, tag_at;
+        uint32_t suffix;
+        if (a.reverse) {
+            if (rtp) {
+                end = L - T > 0 ? L - T : 0;
+                suffix = a.g0[p];
+            } else {
+                end = L - 4 - T;
+                if (end < 0) return; // the reference throws here (k_walk)
+                suffix = ld_be32(pkt + end);
+            }
+            tag_at = L - T;
+        } else {
+            const uint32_t cw = a.w_cw[p];
+            if (rtp) {
+                end = L - T;
+                suffix = cw;
+            } else {
+                end = L - 4 - T;
+                suffix = sgpr(ks->enc_type) != SRTP_NULL_ENCRYPTION ? ((cw & 0x7FFFFFFFu) | 0x80000000u) : 0u;
+                pkt[end] = (uint8_t)(suffix >> 24); pkt[end + 1] = (uint8_t)(suffix >> 16);
+                pkt[end + 2] = (uint8_t)(suffix >> 8); pkt[end + 3] = (uint8_t)suffix;
+            }
+            tag_at = L - T;
+        }
+        uint32_t tag[5];
+        skein_mac<true>(a.skkeys + ks_u, pkt, end, suffix, tag);
+        if (a.reverse) a.auth_ok[p] = tag_matches(tag, pkt + tag_at, T) ? 1u : 0u;
+        else tag_write(tag, pkt + tag_at, T);
     });
 }
 
@@ -2636,12 +2886,20 @@ hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
                        dim3(kUnprotectBlock), 0, s, a);
     return hipGetLastError();
 }
+hipError_t launch_skein(const BundleArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_skein, dim3((a.n + kSkeinBlock - 1) / kSkeinBlock), dim3(kSkeinBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
     const dim3 grid((a.n + kWalkSpan - 1) / kWalkSpan);
-    if (a.reverse)
-        hipLaunchKernelGGL(k_walk<true>, grid, dim3(kWalkBlock), 0, s, a, limit_pass);
-    else
-        hipLaunchKernelGGL(k_walk<false>, grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+    if (a.reverse && a.has_skein) {
+        hipLaunchKernelGGL((k_walk<true, true>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+    } else if (a.reverse) {
+        hipLaunchKernelGGL((k_walk<true, false>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+    } else {
+        hipLaunchKernelGGL((k_walk<false, false>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+    }
     return hipGetLastError();
 }
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {

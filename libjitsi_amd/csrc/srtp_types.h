@@ -22,10 +22,10 @@ struct alignas(256) KeySet {
     uint32_t opad[5];                  // SHA-1 state after (authKey ^ 0x5c..) block
     uint32_t salt[4];                  // session salt bytes 0..13 as LE words (14,15 = 0)
     int32_t enc_type;                  // SRTP_NULL_ENCRYPTION / SRTP_AESCM_ENCRYPTION
-    int32_t auth_type;                 // SRTP_NULL_AUTHENTICATION / SRTP_HMACSHA1_AUTHENTICATION
+    int32_t auth_type;                 // SRTP_NULL_AUTHENTICATION / _HMACSHA1_ / _SKEIN_ (SkeinKeys)
     int32_t tag_len;                   // policy.getAuthTagLength()
     int32_t kind;                      // SRTP_KIND_RTP / SRTP_KIND_RTCP
-    int32_t ext;                       // 1: cipher run by k_ext (AES-F8, AES-256-CM), keys in ExtKeys
+    int32_t ext;                       // 1: packets run by k_ext (AES-F8, AES-256-CM, Twofish, Skein MAC)
     uint32_t pad;
 };
 static_assert(sizeof(KeySet) == 256, "KeySet is one 256-B record");
@@ -52,6 +52,16 @@ struct alignas(256) TwofishKeys {
     uint32_t T[4][256];
 };
 static_assert(sizeof(TwofishKeys) == 4352, "TwofishKeys is 4352 B");
+
+// Skein-512 MAC key of a key set (SKEIN_AUTHENTICATION, ZRTP "SK32"/"SK64":
+// bccontrib's SkeinMac keyed with the 32-byte session auth key and an output
+// of tag_len * 8 bits, SRTPCryptoContext.java:421-428): the chaining value
+// after the key and config UBIs, so a packet's MAC starts at its message
+// blocks.  Indexed by key-set id, allocated with the first Skein factory.
+struct alignas(64) SkeinKeys {
+    uint64_t g0[8];
+};
+static_assert(sizeof(SkeinKeys) == 64, "SkeinKeys is 64 B");
 
 struct FactoryRec {      // SRTPContextFactory
     int32_t open;        // 0 after close(): getDefaultContext() == null

@@ -155,6 +155,21 @@ def profile_policies(profile: str):
         "AES_256_CM_HMAC_SHA1_80": (P.AESCM_ENCRYPTION, 32, 14, 10, 10),
         "AES_256_CM_HMAC_SHA1_32": (P.AESCM_ENCRYPTION, 32, 14, 4, 10),
     }
+    # ZRTP "SK32" / "SK64" Skein-MAC policies (ZRTPTransformEngine.java:867-909:
+    # SKEIN_AUTHENTICATION with a 32-byte auth key, tag of srtpAuthTagLen / 8
+    # bytes, one policy for SRTP and SRTCP) over AES-CM ("AES1"/"AES3") or
+    # Twofish ("2FS1"/"2FS3")
+    skein = {
+        "AES_CM_128_SKEIN_32": (P.AESCM_ENCRYPTION, 16, 4),
+        "AES_CM_128_SKEIN_64": (P.AESCM_ENCRYPTION, 16, 8),
+        "AES_256_CM_SKEIN_64": (P.AESCM_ENCRYPTION, 32, 8),
+        "TWOFISH_CM_128_SKEIN_32": (P.TWOFISH_ENCRYPTION, 16, 4),
+        "TWOFISH_CM_256_SKEIN_64": (P.TWOFISH_ENCRYPTION, 32, 8),
+    }
+    if profile in skein:
+        enc, klen, tag = skein[profile]
+        pol = P(enc, klen, P.SKEIN_AUTHENTICATION, 32, tag, 14)
+        return pol, P(enc, klen, P.SKEIN_AUTHENTICATION, 32, tag, 14)
     enc, klen, slen, rtp_tag, rtcp_tag = table[profile]
     return (P(enc, klen, P.HMACSHA1_AUTHENTICATION, 20, rtp_tag, slen),
             P(enc, klen, P.HMACSHA1_AUTHENTICATION, 20, rtcp_tag, slen))
@@ -576,6 +591,27 @@ def derive_session_keys_for(enc_type: int, masterKey: bytes, masterSalt: bytes, 
     N.check(N.lib().srtp_derive_session_keys_for(enc_type, mk[:klen], klen, bytes(masterSalt)[:14],
                                                  int(rtcp), enc, auth, salt), None, "kdf")
     return bytes(enc), bytes(auth), bytes(salt)
+
+
+def derive_session_keys_auth(enc_type: int, masterKey: bytes, masterSalt: bytes, rtcp: bool = False,
+                             auth_len: int = 20):
+    """Session keys with an auth key of `auth_len` bytes (ZRTP's Skein
+    policies: 32, ZRTPTransformEngine.java:867-872)."""
+    mk = bytes(masterKey)
+    klen = 32 if len(mk) >= 32 else 16
+    enc, auth, salt = (C.c_uint8 * klen)(), (C.c_uint8 * auth_len)(), (C.c_uint8 * 14)()
+    N.check(N.lib().srtp_derive_session_keys_auth(enc_type, mk[:klen], klen, bytes(masterSalt)[:14],
+                                                  int(rtcp), enc, auth, auth_len, salt), None, "kdf")
+    return bytes(enc), bytes(auth), bytes(salt)
+
+
+def skein512_mac(key: bytes, msg: bytes, out_bits: int = 512) -> bytes:
+    """The engine's host Skein-512 (version 1.3): keyed like bccontrib's SkeinMac
+    (plain hash for an empty key), out_bits output bits."""
+    out = (C.c_uint8 * ((out_bits + 7) // 8))()
+    N.check(N.lib().srtp_skein512_mac(bytes(key), len(key), out_bits, bytes(msg), len(msg), out), None,
+            "skein512_mac")
+    return bytes(out)
 
 
 def derive_session_keys(masterKey: bytes, masterSalt: bytes, rtcp: bool = False):

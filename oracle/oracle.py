@@ -84,6 +84,8 @@ def lib():
         L.orc_derive_keys_n.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, u8p, u8p]
         L.orc_derive_keys_twofish.argtypes = [u8p, C.c_int, u8p, C.c_int, u8p, u8p, u8p]
         L.orc_twofish_encrypt_block.argtypes = [u8p, C.c_int, u8p, u8p]
+        L.orc_derive_keys_auth.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, u8p, u8p, C.c_int, u8p]
+        L.orc_skein512_mac.argtypes = [u8p, C.c_int, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_aes_f8.argtypes = [u8p, u8p, C.c_int, u8p, u8p, C.c_int]
         L.orc_bench_round_trips.restype = C.c_int64
         L.orc_bench_round_trips.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
@@ -143,6 +145,29 @@ def derive_keys_twofish(master_key: bytes, master_salt: bytes, rtcp: bool = Fals
     P = C.POINTER(C.c_uint8)
     lib().orc_derive_keys_twofish(kp, klen, sp, int(rtcp), enc.ctypes.data_as(P),
                                   auth.ctypes.data_as(P), salt.ctypes.data_as(P))
+    return enc.tobytes(), auth.tobytes(), salt.tobytes()
+
+
+def skein512(msg: bytes, out_bits: int = 512, key: bytes = b"") -> bytes:
+    """Skein-512 (version 1.3) of `msg`, keyed (Skein-MAC, as bccontrib's
+    SkeinMac) when `key` is non-empty."""
+    k, kp = _u8(key if key else b"\0")
+    m, mp = _u8(msg if msg else b"\0")
+    o = np.zeros((out_bits + 7) // 8, np.uint8)
+    lib().orc_skein512_mac(kp, len(key), out_bits, mp, len(msg), o.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return o.tobytes()
+
+
+def derive_keys_auth(master_key: bytes, master_salt: bytes, rtcp: bool = False, auth_len: int = 20,
+                     twofish: bool = False):
+    """Session keys with an auth key of `auth_len` bytes (Skein policies: 32)."""
+    klen = 32 if len(master_key) >= 32 else 16
+    k, kp = _u8(master_key[:klen])
+    s, sp = _u8(master_salt)
+    enc, auth, salt = np.zeros(klen, np.uint8), np.zeros(auth_len, np.uint8), np.zeros(14, np.uint8)
+    P = C.POINTER(C.c_uint8)
+    lib().orc_derive_keys_auth(int(twofish), kp, klen, sp, int(rtcp), enc.ctypes.data_as(P),
+                               auth.ctypes.data_as(P), auth_len, salt.ctypes.data_as(P))
     return enc.tobytes(), auth.tobytes(), salt.tobytes()
 
 

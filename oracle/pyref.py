@@ -3,6 +3,7 @@
 TEST INFRASTRUCTURE ONLY -- a second oracle used to cross-check the C oracle
 (oracle/srtp_oracle.c) on small bundles.  It shares no code with it: AES-128 is
 implemented here from FIPS-197, HMAC-SHA1 comes from Python's hashlib/hmac,
+Skein-512 is restated here from the Skein 1.3 paper,
 and the context state machine is restated directly from
 
   srtp/SRTPCryptoContext.java:237-744, srtp/SRTCPCryptoContext.java:106-451,
@@ -152,11 +153,69 @@ def f8_key_mask(key, salt):
     return bytes(k ^ (salt[i] if i < len(salt) else 0x55) for i, k in enumerate(key))
 
 
-def derive(mk, ms, rtcp):
+# ---------------------------------------------------------------- Skein-512
+# Skein 1.3 (Threefish-512 + UBI), restated here independently of oracle/skein.c
+# for SKEIN_AUTHENTICATION (BaseSRTPCryptoContext.java:244-248).
+_SK_R = ((46, 36, 19, 37), (33, 27, 14, 42), (17, 49, 36, 39), (44, 9, 54, 56),
+         (39, 30, 34, 24), (13, 50, 10, 17), (25, 29, 39, 43), (8, 35, 56, 22))
+_SK_PI = (2, 1, 4, 7, 6, 5, 0, 3)
+
+
+def threefish512(key, tweak, words):
+    k = list(key) + [0x1BD11BDAA9FC1A22]
+    for w in key:
+        k[8] ^= w
+    t = (tweak[0], tweak[1], tweak[0] ^ tweak[1])
+
+    def subkey(s):
+        sk = [k[(s + i) % 9] for i in range(8)]
+        sk[5] += t[s % 3]
+        sk[6] += t[(s + 1) % 3]
+        sk[7] += s
+        return [x & M64 for x in sk]
+
+    v = list(words)
+    for d in range(72):
+        if d % 4 == 0:
+            v = [(a + b) & M64 for a, b in zip(v, subkey(d // 4))]
+        e = []
+        for j in range(4):
+            x0 = (v[2 * j] + v[2 * j + 1]) & M64
+            r = _SK_R[d % 8][j]
+            x1 = (((v[2 * j + 1] << r) | (v[2 * j + 1] >> (64 - r))) & M64) ^ x0
+            e += [x0, x1]
+        v = [e[_SK_PI[i]] for i in range(8)]
+    return [(a + b) & M64 for a, b in zip(v, subkey(18))]
+
+
+def _ubi(g, msg: bytes, typ: int):
+    n = len(msg)
+    padded = msg + bytes(-n % 64 if n else 64)
+    for i in range(0, len(padded), 64):
+        blk = [int.from_bytes(padded[i + 8 * w:i + 8 * w + 8], "little") for w in range(8)]
+        pos = min(i + 64, n)
+        t1 = (typ << 56) | ((1 << 62) if i == 0 else 0) | ((1 << 63) if i + 64 >= len(padded) else 0)
+        c = threefish512(g, (pos, t1), blk)
+        g = [a ^ b for a, b in zip(c, blk)]
+    return g
+
+
+def skein512_mac(key: bytes, msg: bytes, out_bits: int) -> bytes:
+    g = [0] * 8
+    if key:
+        g = _ubi(g, key, 0)
+    cfg = b"SHA3" + (1).to_bytes(2, "little") + bytes(2) + out_bits.to_bytes(8, "little") + bytes(16)
+    g = _ubi(g, cfg, 4)
+    g = _ubi(g, msg, 48)
+    g = _ubi(g, bytes(8), 63)
+    return b"".join(w.to_bytes(8, "little") for w in g)[:(out_bits + 7) // 8]
+
+
+def derive(mk, ms, rtcp, auth_len=20):
     """RFC 3711 4.3 with kdr = 0 (computeIv label << 48 -> byte 7)."""
     rks = expand_key(mk)
     out = []
-    for lab, n in zip((3, 4, 5) if rtcp else (0, 1, 2), (16, 20, 14)):
+    for lab, n in zip((3, 4, 5) if rtcp else (0, 1, 2), (16, auth_len, 14)):
         iv = bytearray(ms[:14]) + b"\0\0"
         iv[7] ^= lab
         out.append(cipher_stream(rks, n, bytes(iv)))
@@ -167,7 +226,7 @@ def derive(mk, ms, rtcp):
 class Ctx:
     def __init__(self, policy, mk, ms, rtcp):
         self.policy = policy  # (enc, enc_len, auth, auth_len, tag, salt_len)
-        enc, auth, salt = derive(mk, ms, rtcp)
+        enc, auth, salt = derive(mk, ms, rtcp, policy[3] if policy[2] == 2 else 20)
         self.rks = expand_key(enc)
         self.f8rks = expand_key(f8_key_mask(enc, salt)) if policy[0] == 2 else None
         self.auth = auth
@@ -178,6 +237,8 @@ class Ctx:
         self.window = 0
 
     def mac(self, data: bytes, roc: int) -> bytes:
+        if self.policy[2] == 2:  # SkeinMac, tag_len * 8 output bits (SRTPCryptoContext.java:421-428)
+            return skein512_mac(self.auth, data + (roc & M32).to_bytes(4, "big"), 8 * self.policy[4])
         return hmac.new(self.auth, data + (roc & M32).to_bytes(4, "big"), hashlib.sha1).digest()
 
 

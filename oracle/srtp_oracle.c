@@ -8,6 +8,7 @@
  */
 #define OPENSSL_SUPPRESS_DEPRECATED 1
 #include "srtp_oracle.h"
+#include "skein.h"
 #include "twofish.h"
 
 #include <openssl/evp.h>
@@ -46,8 +47,9 @@ typedef struct orc_ctx {
     int kind;
     orc_policy policy;
     int mode;
-    uint8_t enc_key[32], auth_key[20], salt_key[14];
+    uint8_t enc_key[32], auth_key[64], salt_key[14];
     int key_len; /* 16 or 32 (AES-256-CM) */
+    sk_ctx skein;         /* SKEIN_AUTHENTICATION: keyed Skein-512, tag_len * 8 output bits */
     struct blk *ecb;      /* AES-128/256 or Twofish keyed with the session key */
     EVP_CIPHER_CTX *ctr;  /* tuned mode (AES) */
     struct blk *f8;       /* F8: IV' cipher keyed with encKey ^ (salt || 0x55..) */
@@ -59,7 +61,7 @@ typedef struct orc_ctx {
     /* SRTCPCryptoContext state (:54-59) */
     int32_t sent_index, received_index;
     int64_t replay_window; /* BaseSRTPCryptoContext.java:138 */
-    uint8_t tag_store[20];
+    uint8_t tag_store[64];
     uint8_t temp_store[100];
 } orc_ctx;
 
@@ -263,6 +265,14 @@ void orc_aes_f8(const uint8_t key[16], const uint8_t *salt, int salt_len, const 
 static void authenticate_packet_hmac(orc_ctx *x, const uint8_t *buf, int len, int32_t roc_in) {
     uint8_t rb[4] = {(uint8_t)(roc_in >> 24), (uint8_t)(roc_in >> 16), (uint8_t)(roc_in >> 8),
                      (uint8_t)roc_in};
+    if (x->policy.auth_type == ORC_SKEIN_AUTHENTICATION) {
+        /* the same update/update/doFinal sequence on bccontrib's SkeinMac; doFinal
+         * resets it to the keyed, configured state (skein.c) */
+        sk_update(&x->skein, buf, (size_t)len);
+        sk_update(&x->skein, rb, 4);
+        sk_final(&x->skein, x->tag_store);
+        return;
+    }
     unsigned int ol = 20;
     HMAC_CTX *h;
     if (x->mode == ORC_MODE_TUNED) {
@@ -290,22 +300,37 @@ void orc_derive_keys(const uint8_t mk[16], const uint8_t ms[14], int rtcp, uint8
  * bytes: the PRF is AES-128 or AES-256 (RFC 6188 4.1), the session key key_len
  * bytes. */
 static void derive_keys_prf(int twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
-                            int rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+                            int rtcp, uint8_t *enc, uint8_t *auth, int auth_len, uint8_t salt[14]);
 
 void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
                        uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
-    derive_keys_prf(0, mk, key_len, ms, rtcp, enc, auth, salt);
+    derive_keys_prf(0, mk, key_len, ms, rtcp, enc, auth, 20, salt);
+}
+
+/* with the policy's auth key length (32 for ZRTP's Skein, ZRTPTransformEngine.java:867-872) */
+void orc_derive_keys_auth(int twofish, const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
+                          uint8_t *enc, uint8_t *auth, int auth_len, uint8_t salt[14]) {
+    derive_keys_prf(twofish, mk, key_len, ms, rtcp, enc, auth, auth_len, salt);
+}
+
+void orc_skein512_mac(const uint8_t *key, int key_len, int out_bits, const uint8_t *msg, size_t n,
+                      uint8_t *out) {
+    sk_ctx c;
+    sk_init(&c, key, key_len, out_bits);
+    sk_update(&c, msg, n);
+    sk_final(&c, out);
+    memset(&c, 0, sizeof c);
 }
 
 /* Twofish policies: deriveSrtpKeys keys the TwofishEngine `cipher` with the
  * master key, so the PRF is Twofish (BaseSRTPCryptoContext :217-225). */
 void orc_derive_keys_twofish(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
                              uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
-    derive_keys_prf(1, mk, key_len, ms, rtcp, enc, auth, salt);
+    derive_keys_prf(1, mk, key_len, ms, rtcp, enc, auth, 20, salt);
 }
 
 static void derive_keys_prf(int twofish, const uint8_t *mk, int key_len, const uint8_t ms[14],
-                            int rtcp, uint8_t *enc, uint8_t auth[20], uint8_t salt[14]) {
+                            int rtcp, uint8_t *enc, uint8_t *auth, int auth_len, uint8_t salt[14]) {
     blk_t *c = blk_new(twofish, mk, key_len);
     uint8_t iv[16];
     int base = rtcp ? 3 : 0;
@@ -316,7 +341,7 @@ static void derive_keys_prf(int twofish, const uint8_t *mk, int key_len, const u
         if (lab == 0)
             get_cipher_stream(c, enc, key_len, iv);
         else if (lab == 1)
-            get_cipher_stream(c, auth, 20, iv);
+            get_cipher_stream(c, auth, auth_len, iv);
         else
             get_cipher_stream(c, salt, 14, iv);
     }
@@ -419,9 +444,15 @@ static int policy_ok(const orc_policy *p, int rtcp) {
     if (rtcp && is_f8(p->enc_type) &&
         (p->auth_type == ORC_NULL_AUTHENTICATION || p->auth_tag_len < 4))
         return 0;
-    if (p->auth_type != ORC_NULL_AUTHENTICATION && p->auth_type != ORC_HMACSHA1_AUTHENTICATION)
+    if (p->auth_type != ORC_NULL_AUTHENTICATION && p->auth_type != ORC_HMACSHA1_AUTHENTICATION &&
+        p->auth_type != ORC_SKEIN_AUTHENTICATION)
         return 0;
     if (p->auth_type == ORC_HMACSHA1_AUTHENTICATION && p->auth_key_len != 20) return 0;
+    /* Skein: a key of one UBI block at most, and a tag of >= 1 byte (the MAC's
+     * output length is tag_len * 8 bits, SRTPCryptoContext.java:421-428) */
+    if (p->auth_type == ORC_SKEIN_AUTHENTICATION &&
+        (p->auth_key_len < 1 || p->auth_key_len > 64 || p->auth_tag_len < 1))
+        return 0;
     /* <= 12 keeps readRegionToBuff in range for every packet of >= 12 bytes */
     if (p->auth_tag_len < 0 || p->auth_tag_len > 12) return 0;
     return 1;
@@ -491,8 +522,11 @@ static orc_ctx *make_context(orc_transformer *t, uint32_t ssrc, orc_factory *f) 
     x->policy = (t->kind == ORC_KIND_RTP) ? f->srtp : f->srtcp;
     const int tf = is_twofish(x->policy.enc_type);
     x->key_len = x->policy.enc_type != ORC_NULL_ENCRYPTION && x->policy.enc_key_len == 32 ? 32 : 16;
+    const int skein = x->policy.auth_type == ORC_SKEIN_AUTHENTICATION;
+    const int auth_len = skein ? x->policy.auth_key_len : 20;
     derive_keys_prf(tf, f->master_key, x->key_len, f->master_salt, t->kind == ORC_KIND_RTCP,
-                    x->enc_key, x->auth_key, x->salt_key);
+                    x->enc_key, x->auth_key, auth_len, x->salt_key);
+    if (skein) sk_init(&x->skein, x->auth_key, auth_len, 8 * x->policy.auth_tag_len);
     x->ecb = blk_new(tf, x->enc_key, x->key_len);
     if (is_f8(x->policy.enc_type)) /* deriveSrtpKeys :443-444 */
         x->f8 = f8_iv_cipher_new(tf, x->enc_key, x->key_len, x->salt_key, 14);

@@ -12,6 +12,8 @@
  *   srtp/BaseSRTPCryptoContext.java:178-278 (key storage, authenticatePacketHMAC)
  *   srtp/SRTPCipherCTR.java:68-121        (AES-CM keystream + XOR)
  *   srtp/SRTPCipherF8.java:66-183         (AES-F8 IV' key, keystream chain)
+ *   srtp/BaseSRTPCryptoContext.java:244-248, SRTPCryptoContext.java:421-428
+ *                                         (SKEIN_AUTHENTICATION: Skein-512 MAC, skein.c)
  *   srtp/SRTPTransformer.java:100-219, srtp/SRTCPTransformer.java:92-207,
  *   srtp/SRTPContextFactory.java:50-68    (per-transformer SSRC context map)
  *   nm/RawPacket.java:203-220,463-614,723-839,885-909,988-999,1284-1292
@@ -135,6 +137,13 @@ void orc_derive_keys_n(const uint8_t *mk, int key_len, const uint8_t ms[14], int
 /* Twofish policies: the PRF is Twofish keyed with the master key. */
 void orc_derive_keys_twofish(const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
                              uint8_t *enc, uint8_t auth[20], uint8_t salt[14]);
+/* key derivation with the policy's auth key length (Skein: 32), PRF AES or Twofish */
+void orc_derive_keys_auth(int twofish, const uint8_t *mk, int key_len, const uint8_t ms[14], int rtcp,
+                          uint8_t *enc, uint8_t *auth, int auth_len, uint8_t salt[14]);
+/* Skein-512 (skein.c, version 1.3) keyed with key[0..key_len) (key_len 0: plain
+ * hash), out_bits output bits: the tag SkeinMac computes */
+void orc_skein512_mac(const uint8_t *key, int key_len, int out_bits, const uint8_t *msg, size_t n,
+                      uint8_t *out);
 /* one Twofish block (twofish.c), key_len 16 / 24 / 32 */
 void orc_twofish_encrypt_block(const uint8_t *key, int key_len, const uint8_t in[16],
                                uint8_t out[16]);

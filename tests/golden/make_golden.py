@@ -50,6 +50,10 @@ PROFILES = {
     "NULL_HMAC_SHA1_80": ((0, 0, 1, 20, 10, 0), (0, 0, 1, 20, 10, 0)),
     "NULL_HMAC_SHA1_32": ((0, 0, 1, 20, 4, 0), (0, 0, 1, 20, 10, 0)),
     "F8_128_HMAC_SHA1_80": ((2, 16, 1, 20, 10, 14), (2, 16, 1, 20, 10, 14)),
+    # ZRTP Skein-MAC policies (ZRTPTransformEngine.java:867-909: SKEIN_AUTHENTICATION,
+    # 32-byte auth key, 4- or 8-byte tag, one policy for SRTP and SRTCP)
+    "AES_CM_128_SKEIN_32": ((1, 16, 2, 32, 4, 14), (1, 16, 2, 32, 4, 14)),
+    "AES_CM_128_SKEIN_64": ((1, 16, 2, 32, 8, 14), (1, 16, 2, 32, 8, 14)),
 }
 STATE_KEYS = ("roc", "s_l", "seq_num_set", "guessed_roc", "sent_index", "received_index",
               "replay_window")
@@ -586,10 +590,64 @@ def sdes_f8():
     r.save()
 
 
+def zrtp_skein():
+    r = Recorder("zrtp_skein", "ZRTP AES-CM with the Skein-512 MAC (SK32 / SK64: "
+                 "SKEIN_AUTHENTICATION, BaseSRTPCryptoContext.java:244-248, SkeinMac keyed with a "
+                 "32-byte auth key and tag_len * 8 output bits; Skein 1.3 pinned by its "
+                 "Skein-512-512 known answers, tests/test_skein.py): SRTP + SRTCP across a seq "
+                 "wrap, both tag lengths in one bundle, tamper/replay faults, ROC guesses "
+                 "overturned in-bundle (the tag re-checked under the walk's ROC), an SDES-style "
+                 "factory swap")
+    rng = np.random.default_rng(synth.SEED_BASE + 9)
+    keys = synth.keys(9, 3)
+    tx, rx, ctx, crx = [], [], [], []
+    for j, prof in enumerate(("AES_CM_128_SKEIN_32", "AES_CM_128_SKEIN_64")):
+        (k, s) = keys[j]
+        fs, fr = r.factory(True, k, s, prof), r.factory(False, k, s, prof)
+        tx.append(r.transformer(O.KIND_RTP, fs))
+        rx.append(r.transformer(O.KIND_RTP, fr))
+        ctx.append(r.transformer(O.KIND_RTCP, fs))
+        crx.append(r.transformer(O.KIND_RTCP, fr))
+    for step in range(2):
+        if step == 1:  # SDES-style swap on the SK32 pair: contexts keep their keys (Q16)
+            k2, s2 = keys[2]
+            r.set_factory(tx[0], r.factory(True, k2, s2, "AES_CM_128_SKEIN_32"), True)
+            r.set_factory(rx[0], r.factory(False, k2, s2, "AES_CM_128_SKEIN_32"), False)
+        bs = [synth.rtp_bundle(40, 3, (12, 1300), seed=900 + 10 * step + j, ext_frac=0.2,
+                               ssrcs=np.arange(3, dtype=np.uint32) + 700 + 10 * j,
+                               seq0=np.full(3, (65525 + 20 * step) & 0xFFFF, np.uint32))
+              for j in range(2)]
+        mb = synth.concat(bs)
+        tids = np.array([tx[0]] * 40 + [tx[1]] * 40)
+        which = rng.permutation(np.r_[np.zeros(40, int), np.ones(40, int)])  # interleave,
+        sel = np.empty(80, int)                                               # each stream in order
+        sel[which == 0] = np.arange(40)
+        sel[which == 1] = 40 + np.arange(40)
+        mb, tids = synth.select(mb, sel), tids[sel]
+        pb, st = r.bundle(tids, False, mb)
+        assert (st == 0).all()
+        fb = inject_faults(pb, rng, tag_len=4)
+        ssrc = np.array([int.from_bytes(fb.seg[o + 8:o + 12].tobytes(), "big") for o in fb.off])
+        r.bundle(np.where(ssrc < 710, rx[0], rx[1]), True, fb)
+        for j in range(2):
+            cb = synth.rtcp_bundle(10, 2, (12, 200), seed=920 + 10 * step + j,
+                                   ssrcs=np.arange(2, dtype=np.uint32) + 700 + 10 * j)
+            pc, st = r.bundle(ctx[j], False, cb)
+            assert (st == 0).all()
+            r.bundle(crx[j], True, synth.select(pc, np.array([0, 2, 1, 2, 3, 4, 5, 9, 6, 7, 8])))
+    for seqs in ([30000, 60000, 10, 20, 40000, 70, 33000], [20000, 52000, 52001, 100, 65535, 5]):
+        b = synth.rtp_bundle(len(seqs), 1, 333, seed=len(seqs) + 90,
+                             ssrcs=np.array([777], np.uint32))
+        set_seqs(b, seqs)
+        pb, _ = r.bundle(tx[1], False, b)
+        r.bundle(rx[1], True, pb)
+    r.save()
+
+
 SCENARIOS = [libsrtp_kat, c1_opus160_wrap, c2_video1200, c3_mixed_faults, c4_srtp_srtcp_rekey,
              edge_replay_quirks, edge_roc_overturn, lambda: edge_malformed(True),
              lambda: edge_malformed(False), edge_flags_lifecycle, edge_check_replay_off,
-             null_profiles, sdes_f8]
+             null_profiles, sdes_f8, zrtp_skein]
 
 if __name__ == "__main__":
     O.build()
