@@ -86,6 +86,7 @@ def lib():
         L.orc_twofish_encrypt_block.argtypes = [u8p, C.c_int, u8p, u8p]
         L.orc_derive_keys_auth.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, u8p, u8p, C.c_int, u8p]
         L.orc_skein512_mac.argtypes = [u8p, C.c_int, C.c_int, u8p, C.c_size_t, u8p]
+        L.orc_skein512_state0.argtypes = [u8p, C.c_int, C.c_int, C.POINTER(C.c_uint64)]
         L.orc_aes_f8.argtypes = [u8p, u8p, C.c_int, u8p, u8p, C.c_int]
         L.orc_bench_round_trips.restype = C.c_int64
         L.orc_bench_round_trips.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
@@ -156,6 +157,14 @@ def skein512(msg: bytes, out_bits: int = 512, key: bytes = b"") -> bytes:
     o = np.zeros((out_bits + 7) // 8, np.uint8)
     lib().orc_skein512_mac(kp, len(key), out_bits, mp, len(msg), o.ctypes.data_as(C.POINTER(C.c_uint8)))
     return o.tobytes()
+
+
+def skein512_iv(out_bits: int) -> list:
+    """Skein-512's chaining value after the config UBI (unkeyed): the IV."""
+    k, kp = _u8(b"\0")
+    o = np.zeros(8, np.uint64)
+    lib().orc_skein512_state0(kp, 0, out_bits, o.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return [int(x) for x in o]
 
 
 def derive_keys_auth(master_key: bytes, master_salt: bytes, rtcp: bool = False, auth_len: int = 20,

@@ -313,6 +313,15 @@ void orc_derive_keys_auth(int twofish, const uint8_t *mk, int key_len, const uin
     derive_keys_prf(twofish, mk, key_len, ms, rtcp, enc, auth, auth_len, salt);
 }
 
+/* the chaining value after the key (if any) and config UBIs: for key_len 0
+ * the paper's precomputed IV of Skein-512-out_bits */
+void orc_skein512_state0(const uint8_t *key, int key_len, int out_bits, uint64_t g0[8]) {
+    sk_ctx c;
+    sk_init(&c, key, key_len, out_bits);
+    memcpy(g0, c.g0, sizeof c.g0);
+    memset(&c, 0, sizeof c);
+}
+
 void orc_skein512_mac(const uint8_t *key, int key_len, int out_bits, const uint8_t *msg, size_t n,
                       uint8_t *out) {
     sk_ctx c;

@@ -144,6 +144,7 @@ void orc_derive_keys_auth(int twofish, const uint8_t *mk, int key_len, const uin
  * hash), out_bits output bits: the tag SkeinMac computes */
 void orc_skein512_mac(const uint8_t *key, int key_len, int out_bits, const uint8_t *msg, size_t n,
                       uint8_t *out);
+void orc_skein512_state0(const uint8_t *key, int key_len, int out_bits, uint64_t g0[8]);
 /* one Twofish block (twofish.c), key_len 16 / 24 / 32 */
 void orc_twofish_encrypt_block(const uint8_t *key, int key_len, const uint8_t in[16],
                                uint8_t out[16]);

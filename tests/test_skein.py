@@ -36,6 +36,14 @@ SKEIN_512_512_KAT = {
          "5188087AF4188773A332303E6667A7A210856F742139000071F48E8BA2A5ADB7",
 }
 
+# the paper's precomputed IVs (the chaining value after the config UBI)
+SKEIN_512_IV = {
+    512: [0x4903ADFF749C51CE, 0x0D95DE399746DF03, 0x8FD1934127C79BCE, 0x9A255629FF352CB1,
+          0x5DB62599DF6CA7B0, 0xEABE394CA9D5C3F4, 0x991112C71A75B523, 0xAE18A40B660FCC33],
+    256: [0xCCD044A12FDB3E13, 0xE83590301A79A9EB, 0x55AEA0614F816E6F, 0x2A2767A4AE9B94DB,
+          0xEC06025E74DD7683, 0xE7A436CDC4746251, 0xC36FBAF9393AD185, 0x3EEDBA1833EDFC13],
+}
+
 SKEIN_PROFILES = ["AES_CM_128_SKEIN_32", "AES_CM_128_SKEIN_64", "AES_256_CM_SKEIN_64",
                   "TWOFISH_CM_128_SKEIN_32", "TWOFISH_CM_256_SKEIN_64"]
 
@@ -47,6 +55,11 @@ def test_skein512_kat(n, oracle):
     assert O.skein512(msg).hex().upper() == want
     assert R.skein512_mac(b"", msg, 512).hex().upper() == want
     assert skein512_mac(b"", msg).hex().upper() == want
+
+
+@pytest.mark.parametrize("bits", sorted(SKEIN_512_IV))
+def test_skein512_iv(bits, oracle):
+    assert O.skein512_iv(bits) == SKEIN_512_IV[bits]
 
 
 def test_skein_mac_restatements_agree(oracle):
@@ -194,7 +207,9 @@ def test_skein_null_cipher_and_roc_overturn(engine):
     pc = cb.copy()
     pc.seg, pc.length = seg, ln
     _, _, st = tw.run(cr, True, pc.seg, pc.off, pc.length, pc.cap)
-    assert (st == 0).all()
+    # the NULL cipher's SRTCP trailer carries index 0 (transformPacket :391-427,
+    # SURVEY Q12): after each SSRC's first packet the receiver sees replays
+    assert (st[:2] == 0).all() and (st[2:] == N.STATUS_DROP_REPLAY).all()
     # ROC overturned in-bundle (AES-CM + Skein-32)
     pols = profile_policies("AES_CM_128_SKEIN_32")
     fs, fr = tw.factory(True, k, s, *pols), tw.factory(False, k, s, *pols)
