@@ -775,6 +775,7 @@ struct SortPass {
     uint32_t *next_counts;    // next pass's [tiles][256] counts, or null on the last pass
     uint32_t *zero;           // the previous pass's counts (this tile's row is re-zeroed), or null
     uint32_t *spos;           // last unprotect pass: spos[packet] = its sorted position, or null
+    uint32_t walk_max;        // largest key of a walked record (the context table's mask)
 };
 
 __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
@@ -866,7 +867,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
             sp.dk[pos] = key[r];
             const WalkRec rec = sp.sv[i]; // read here, not held across the ranking (a held copy went to scratch)
             sp.dv[pos] = rec;
-            if (sp.spos) sp.spos[rec.p & kRecIdxMask] = pos;
+            // only walked records carry a packet index: k_parse leaves the
+            // record of a skipped / invalid packet unwritten (stale scratch,
+            // whose index may lie anywhere)
+            if (sp.spos && key[r] <= sp.walk_max) sp.spos[rec.p & kRecIdxMask] = pos;
             if (sp.next_counts)
                 atomicAdd(&sp.next_counts[(pos / kSortTile) * 256 + ((key[r] >> (sp.shift + 8)) & 255u)], 1u);
         }
@@ -893,6 +897,7 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
         // pass's are re-zeroed by the walk (BundleArgs::sort_zero)
         sp.zero = q ? ss.counts[q - 1] : nullptr;
         sp.spos = last && a.reverse ? a.spos : nullptr;
+        sp.walk_max = a.ctx_mask;
         hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
     }
     return hipGetLastError();
