@@ -248,7 +248,7 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->mid, (size_t)5 * m));
     HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
     HIPCHK(e, dalloc(&e->spec, m));
-    HIPCHK(e, dalloc(&e->long_list, m / 256 + 2)); // at most one long chain per walk span
+    HIPCHK(e, dalloc(&e->long_list, m / kLongMin + 2)); // long chains are disjoint runs of >= kLongMin records
     HIPCHK(e, dalloc(&e->spos, m));
     e->sort_temp_bytes = sort_temp_bytes(m);
     HIPCHK(e, hipMalloc(&e->sort_temp, std::max<size_t>(e->sort_temp_bytes, 16)));

@@ -9,6 +9,12 @@
 namespace srtp {
 
 constexpr int kSortMaxPass = 4; // 8-bit digits: context tables up to 2^31 slots
+// Context chains of at least this many records in a bundle are walked by the
+// wave-parallel (speculative) walk, shorter ones lane-serially.
+#ifndef SRTP_LONG_MIN
+#define SRTP_LONG_MIN 256
+#endif
+constexpr uint32_t kLongMin = SRTP_LONG_MIN;
 
 // Everything one bundle needs; passed by value to every kernel.
 struct BundleArgs {
@@ -56,7 +62,7 @@ struct BundleArgs {
     uint32_t *mid;         // [5n] unprotect: inner SHA-1 state before the ROC block
     uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
     uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
-    uint32_t *long_list;   // [n / 256 + 2] sorted start index of each long context chain
+    uint32_t *long_list;   // [n / kLongMin + 2] sorted start index of each long context chain
     uint32_t *spos;        // [n] unprotect: each record's position in sort order (the last sort pass)
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse

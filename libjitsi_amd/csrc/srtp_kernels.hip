@@ -1525,7 +1525,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         // second pass without abort-on-throw work: the long chains the first
         // pass handed over, one per wave until none is left
         const uint32_t n_long = a.ctl->n_long;
-        if (n_long == 0u || blockIdx.x >= n_long * 4u) return; // nothing (more) to do: no atomics
+        if (n_long == 0u || blockIdx.x >= n_long) return; // nothing (more) to do: no atomics
         for (;;) {
             uint32_t q = 0u;
             if (threadIdx.x == 0) q = atomicAdd(&a.ctl->long_cursor, 1u);
@@ -1586,6 +1586,19 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         const uint32_t j = s_start[q];
         const uint32_t key = s_key[j];
         const uint32_t slot = key;
+        // A chain of kLongMin records or more goes to the wave-parallel walk of
+        // the second pass (unless abort-on-throw needs this one): walked here,
+        // its records would take one serial step each on this lane.  A key's
+        // records are contiguous, so the chain is that long iff the record
+        // kLongMin - 1 places on carries the key.
+        if (!two_pass) {
+            const uint32_t jl = j + kLongMin - 1u;
+            const uint32_t kl = jl < win ? s_key[jl] : (base + jl < a.n ? a.sk_out[base + jl] : ~0u);
+            if (kl == key) {
+                a.long_list[atomicAdd(&a.ctl->n_long, 1u)] = base + j;
+                continue;
+            }
+        }
         CtxState st = a.ctx[slot];
         const KeySet *ks = a.keysets + st.ks;
         WalkCtx c;
@@ -1595,12 +1608,6 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
         const int32_t E = limit_pass ? a.e_min[tid] : 0x7fffffff;
         const uint32_t first_p = s_rec[j].p & kRecIdxMask;
-        // a chain running past the staged window goes to the wave-parallel
-        // walk of the second pass (unless abort-on-throw needs this one)
-        if (!two_pass && s_key[win - 1] == key && base + win < a.n && a.sk_out[base + win] == key) {
-            a.long_list[atomicAdd(&a.ctl->n_long, 1u)] = base + j;
-            continue;
-        }
         // One record of the chain; false ends it.
         auto step = [&](const WalkRec &r, uint32_t g0, uint32_t ok) -> bool {
             if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) return false;
@@ -1611,6 +1618,55 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         // nothing waits on vmcnt -- which would also wait for walk_one's
         // status stores of earlier records.
         uint32_t jj = j;
+        // Fast prefix (SRTP with seqNumSet, outside the abort-on-throw passes):
+        // while each packet is the context's new highest index -- the steady
+        // state of an in-order stream -- the state machine reduces to guessIndex,
+        // a window shift and s_l/ROC advancing, with no replay drop; the packet
+        // keeps that path when its tag checked out under the verify pass's ROC
+        // and it neither throws nor (protect) overflows its capacity (the rules
+        // of walk_long's speculation).  Such records cost a few instructions
+        // here instead of walk_one's branches; the first record that leaves
+        // the path, and every record after it, goes through walk_one.
+        if (!two_pass && c.kind == SRTP_KIND_RTP && (st.flags & 1u) && a.debug == 0) {
+            const bool mac = c.auth != SRTP_NULL_AUTHENTICATION;
+            for (; jj < win; jj++) {
+                if (s_key[jj] != key) break;
+                const WalkRec rec = s_rec[jj];
+                const int32_t seq = (int32_t)(rec.word & 0xffffu);
+                const int32_t sl = st.b;
+                int32_t d; // guessIndex :457-475
+                if (sl < 32768) d = (seq - sl > 32768) ? -1 : 0;
+                else d = (sl - 32768 > seq) ? 1 : 0;
+                const uint32_t g = (uint32_t)st.a + (uint32_t)d;
+                const int64_t delta = (java_lshl((int64_t)(int32_t)g, 16) | (int64_t)seq) -
+                                      (java_lshl((int64_t)st.a, 16) | (int64_t)sl);
+                const int L = (int)(rec.lc & 0xffffu), C = (int)(rec.lc >> 16);
+                bool keep = delta > 0;
+                int newL;
+                if (REV) {
+                    newL = mac ? (L - c.T > 0 ? L - c.T : 0) : L;
+                    if (!(rec.p & kRecSkipDec)) keep = keep && !enc_would_throw(c.enc, rec.h, newL - rec.h);
+                    if (mac) {
+                        const uint32_t g0 = s_g0[jj], okb = s_ok[jj];
+                        keep = keep && (g == g0 ? (okb & 1u) != 0u
+                                                : (okb & 4u) != 0u && g == g0 - 1u && (okb & 2u) != 0u);
+                    }
+                } else {
+                    newL = L + (mac ? c.T : 0);
+                    keep = keep && newL <= C && !enc_would_throw(c.enc, rec.h, L - rec.h);
+                }
+                if (!keep) break;
+                const uint32_t p = rec.p & kRecIdxMask;
+                a.w_cw[p] = g;
+                a.w_len[p] = (uint32_t)newL;
+                a.w_status[p] = SRTP_STATUS_OK;
+                // update :719-744 for delta > 0: the window shifts by delta & 63
+                st.window = (uint64_t)java_lshl((int64_t)st.window, delta) | 1ull;
+                st.a = (int32_t)g;
+                st.b = seq;
+                st.g = (int32_t)g;
+            }
+        }
         bool more = true;
         for (; jj < win; jj++) {
             if (s_key[jj] != key) { more = false; break; }
@@ -2897,7 +2953,11 @@ hipError_t launch_skein(const BundleArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
-    const dim3 grid((a.n + kWalkSpan - 1) / kWalkSpan);
+    // the second launch also walks the handed-over chains, one wave each: a
+    // grid of up to n / kLongMin waves (those beyond the chain count, and
+    // beyond the spans in the abort-on-throw limit pass, exit at once)
+    const uint32_t spans = (a.n + kWalkSpan - 1) / kWalkSpan;
+    const dim3 grid(limit_pass ? max(spans, min((a.n + kLongMin - 1) / kLongMin, 8192u)) : spans);
     if (a.reverse && a.has_skein) {
         hipLaunchKernelGGL((k_walk<true, true>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
     } else if (a.reverse) {
