@@ -200,6 +200,8 @@ typedef struct {
     uint64_t ctx_overflow;               /* packets refused a new context: table full */
     uint64_t ctx_live, ctx_tombstones, ctx_slots;
     uint64_t rehashes;                   /* context-table rebuilds (tombstone cleanup) */
+    uint64_t chain_stalls;               /* walk tiles that gave up waiting for a long chain's
+                                            state from the tiles before (never expected) */
 } srtp_stats;
 int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
 

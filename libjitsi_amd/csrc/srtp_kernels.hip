@@ -1290,7 +1290,10 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
 // packet at the masked distance of the packets after it (suffix sums).  The
 // breaking packet goes through walk_one, exactly as the serial walk, and the
 // speculation resumes after it.  SRTCP chains are walked serially.
-constexpr int kLongPer = 4;                      // records per lane per step
+#ifndef SRTP_LONG_PER
+#define SRTP_LONG_PER 4
+#endif
+constexpr int kLongPer = SRTP_LONG_PER;          // records per lane per step
 constexpr int kLongStep = 64 * kLongPer;         // records per wave step
 
 __device__ __forceinline__ int32_t wave_excl_scan(int32_t x) {
@@ -1335,11 +1338,11 @@ struct LongLds {
 };
 
 template <bool REV, bool SK>
-__device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm) {
+__device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, const CtxState &st_in) {
     const int lane = (int)(threadIdx.x & 63u);
     const uint32_t key = a.sk_out[i0];
     const uint32_t slot = key;
-    CtxState st = a.ctx[slot];
+    CtxState st = st_in;
     const KeySet *ks = a.keysets + st.ks;
     WalkCtx c;
     c.enc = ks->enc_type; c.auth = ks->auth_type; c.T = ks->tag_len; c.kind = ks->kind;
@@ -1496,13 +1499,8 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm) {
     if (lane == 0) a.ctx[slot] = st;
 }
 
-// One wave per workgroup owns the context segments that START among kWalkSpan
-// consecutive sorted records, and stages those records plus a look-ahead of
-// kWalkAhead more in LDS with one coalesced pass (plus, for unprotect, the
-// verify pass's g0/auth_ok of each record, gathered in parallel); it compacts
-// the segment starts and lane l walks the l-th segment: the per-context chain
-// reads LDS (tens of cycles per record) instead of dependent HBM round trips.
-// Only a segment longer than the look-ahead reads its tail from global memory.
+// k_walk's geometry (see k_walk): one wave per workgroup, a span of kWalkSpan
+// sorted records ("tile") plus a look-ahead of kWalkAhead staged in LDS.
 constexpr int kWalkBlock = 64;
 #ifndef SRTP_WALK_PER
 #define SRTP_WALK_PER 4
@@ -1512,43 +1510,410 @@ constexpr int kWalkSpan = kWalkBlock * kWalkPer;
 constexpr int kWalkAhead = 256;
 constexpr int kWalkWin = kWalkSpan + kWalkAhead;
 
-template <bool REV, bool SK>
-__global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pass) {
+// ------------------------------------------------ chains across walk tiles
+// A context chain of kWalkSpan or more records (a heavy SSRC in a skewed
+// bundle, or one stream carrying the whole bundle) is walked by every first-
+// pass tile it crosses at once, under walk_long's speculation.  Each tile
+// evaluates its part of the chain locally: the wrap steps d from consecutive
+// sequence numbers (guessIndex :457-475 with s_l = the previous packet),
+// delta = d * 2^16 + seq - prev (no ROC in it), the window shifts delta & 63
+// (update :719-744), and the checks that keep the speculation (a new highest
+// index, no throw, the capacity, the verify pass's tag result under a ROC that
+// must equal g0 - (the d's so far), one ROC "x" the part must start from).
+// A part's effect on the state (ROC steps, window shift and bits, last s_l)
+// composes with its neighbours' like a scan operator.  Tiles take their
+// indices from a ticket counter, publish the effect of the part that runs on
+// into the next tile -- first as an aggregate, then as the exact state after
+// it -- and look back over the tiles before them for the state their part
+// starts from (decoupled look-back, 64 tiles per step, one per lane).  Then a
+// tile commits its records up to the first that breaks the speculation; the
+// chain's first break hands the rest of the chain, from that record on, to
+// the second pass's walk_long (exactly as the serial walk), and the tiles
+// after it commit nothing.  Published words are 8-byte {value, bundle epoch}
+// granules written and read with agent-scope atomics: each is valid on its
+// own, so neither side needs a fence.
+constexpr int kChainPer = kWalkSpan / kWalkBlock;  // records per lane of a part (4)
+static_assert(kLongMin == (uint32_t)kWalkSpan, "a long chain reaches the end of the tile it starts in");
+
+struct ChainAgg {
+    int32_t dsum;     // ROC steps
+    uint32_t x;       // ROC the part must start from (hasx)
+    uint32_t tshift;  // window shift, capped at 64
+    uint64_t bits;    // window bits set by the part's packets
+    int32_t s_l;      // sequence number of the last packet
+    bool hasx, broken;
+};
+struct ChainState {
+    uint32_t roc;
+    int32_t s_l;
+    uint64_t window;
+    bool broken;      // the speculation broke before (the rest is walk_long's)
+};
+
+__device__ __forceinline__ ChainState chain_apply(ChainState p, const ChainAgg &g) {
+    if (p.broken || g.broken || (g.hasx && p.roc != g.x) ||
+        (int64_t)(int32_t)p.roc + g.dsum > (int64_t)0x7fffffff) {
+        p.broken = true;
+        return p;
+    }
+    p.roc += (uint32_t)g.dsum;
+    p.s_l = g.s_l;
+    p.window = (g.tshift < 64u ? p.window << g.tshift : 0ull) | g.bits;
+    return p;
+}
+
+// g1, then g2
+__device__ __forceinline__ ChainAgg chain_compose(const ChainAgg &g1, const ChainAgg &g2) {
+    ChainAgg o;
+    o.broken = g1.broken || g2.broken ||
+               (g1.hasx && g2.hasx && g2.x - (uint32_t)g1.dsum != g1.x);
+    o.dsum = g1.dsum + g2.dsum;
+    o.hasx = g1.hasx || g2.hasx;
+    o.x = g1.hasx ? g1.x : g2.x - (uint32_t)g1.dsum;
+    o.tshift = min(g1.tshift + g2.tshift, 64u);
+    o.bits = (g2.tshift < 64u ? g1.bits << g2.tshift : 0ull) | g2.bits;
+    o.s_l = g2.s_l;
+    return o;
+}
+
+constexpr int kLinkWords = 10; // per tile: [0, 5) aggregate, [5, 9) state
+__device__ __forceinline__ void gran_put(uint64_t *p, uint32_t epoch, uint32_t v) {
+    __hip_atomic_store(p, ((uint64_t)v << 32) | epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool gran_get(const uint64_t *p, uint32_t epoch, uint32_t &v) {
+    const uint64_t g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = (uint32_t)(g >> 32);
+    return (uint32_t)g == epoch;
+}
+
+// Lanes 0..4 (aggregate) or 0..3 (state) store one granule each.
+__device__ __forceinline__ void chain_publish_agg(const BundleArgs &a, uint32_t tile, uint32_t epoch,
+                                                  const ChainAgg &g) {
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t v = (uint32_t)g.dsum;
+    if (lane == 1) v = g.x;
+    if (lane == 2) v = g.tshift | (g.hasx ? 0x80u : 0u) | (g.broken ? 0x100u : 0u) | ((uint32_t)g.s_l << 16);
+    if (lane == 3) v = (uint32_t)g.bits;
+    if (lane == 4) v = (uint32_t)(g.bits >> 32);
+    if (lane < 5) gran_put(a.tile_link + (size_t)tile * kLinkWords + lane, epoch, v);
+}
+__device__ __forceinline__ void chain_publish_state(const BundleArgs &a, uint32_t tile, uint32_t epoch,
+                                                    const ChainState &s) {
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t v = s.roc;
+    if (lane == 1) v = ((uint32_t)s.s_l & 0xffffu) | (s.broken ? 0x10000u : 0u);
+    if (lane == 2) v = (uint32_t)s.window;
+    if (lane == 3) v = (uint32_t)(s.window >> 32);
+    if (lane < 4) gran_put(a.tile_link + (size_t)tile * kLinkWords + 5 + lane, epoch, v);
+}
+
+// The exact state before tile `tile`'s first record, for a chain that runs
+// into it from the tiles before (each of them published its part).
+__device__ ChainState chain_lookback(const BundleArgs &a, uint32_t tile, uint32_t epoch) {
+    const int lane = (int)(threadIdx.x & 63u);
+    ChainAgg acc = {};     // the composed parts of the tiles after the current window
+    bool have_acc = false;
+    int32_t k0 = (int32_t)tile - 1;
+    for (;;) {
+        const int32_t k = k0 - lane;
+        const uint64_t *gl = a.tile_link + (size_t)(k < 0 ? 0 : k) * kLinkWords;
+        uint32_t v[9];
+        bool isP = false, done = k < 0;
+        for (uint32_t spin = 0;; spin++) {
+            if (!done) {
+                bool pr = true;
+#pragma unroll
+                for (int i = 5; i < 9; i++) pr &= gran_get(gl + i, epoch, v[i]);
+                if (pr) {
+                    isP = done = true;
+                } else {
+                    bool ar = true;
+#pragma unroll
+                    for (int i = 0; i < 5; i++) ar &= gran_get(gl + i, epoch, v[i]);
+                    done = ar;
+                }
+            }
+            const unsigned long long pm = __ballot(isP), dm = __ballot(done);
+            const int fp = pm ? __ffsll((long long)pm) - 1 : 64;
+            const unsigned long long need = fp >= 63 ? ~0ull : ((2ull << fp) - 1ull);
+            if ((dm & need) == need) break;
+            if (spin > (1u << 24)) { // never expected: report it and give up (results wrong, no hang)
+                if (lane == 0) atomicAdd(&a.counters[kCtrChainStall], 1ull);
+                ChainState bad = {};
+                bad.broken = true;
+                return bad;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        const unsigned long long pm = __ballot(isP);
+        const int fp = pm ? __ffsll((long long)pm) - 1 : 64;
+        // aggregates of lanes fp-1 (earliest tile) .. 0 (tile - 1 - 64 steps back)
+        ChainAgg win = {};
+        bool have_win = false;
+        for (int i = min(fp, 64) - 1; i >= 0; i--) {
+            ChainAgg g;
+            g.dsum = __builtin_amdgcn_readlane((int)v[0], i);
+            g.x = (uint32_t)__builtin_amdgcn_readlane((int)v[1], i);
+            const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)v[2], i);
+            g.tshift = w2 & 0x7fu;
+            g.hasx = (w2 & 0x80u) != 0u;
+            g.broken = (w2 & 0x100u) != 0u;
+            g.s_l = (int32_t)(w2 >> 16);
+            g.bits = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v[3], i) |
+                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v[4], i) << 32);
+            win = have_win ? chain_compose(win, g) : g;
+            have_win = true;
+        }
+        if (have_win) {
+            acc = have_acc ? chain_compose(win, acc) : win;
+            have_acc = true;
+        }
+        if (fp < 64) {
+            ChainState st;
+            st.roc = (uint32_t)__builtin_amdgcn_readlane((int)v[5], fp);
+            const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane((int)v[6], fp);
+            st.s_l = (int32_t)(w6 & 0xffffu);
+            st.broken = (w6 & 0x10000u) != 0u;
+            st.window = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v[7], fp) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v[8], fp) << 32);
+            return have_acc ? chain_apply(st, acc) : st;
+        }
+        k0 -= 64;
+    }
+}
+
+// Window shift and bits of the part's first f records (each lane's masked
+// distances m[]), as walk_long's commit computes them.
+__device__ __forceinline__ void chain_window(const uint32_t m[kChainPer], int f, uint32_t &tshift,
+                                             uint64_t &bits) {
+    const int lane = (int)(threadIdx.x & 63u);
+    int32_t msum = 0;
+#pragma unroll
+    for (int r = 0; r < kChainPer; r++)
+        if (lane * kChainPer + r < f) msum += (int32_t)m[r];
+    const int32_t total = (int32_t)__reduce_add_sync(~0ull, (unsigned)msum);
+    int32_t after = total - wave_excl_scan(msum);
+    uint64_t b = 0ull;
+#pragma unroll
+    for (int r = 0; r < kChainPer; r++) {
+        if (lane * kChainPer + r < f) {
+            after -= (int32_t)m[r];
+            if (after < 64) b |= 1ull << after;
+        }
+    }
+    bits = wave_or64(b);
+    tshift = (uint32_t)min(total, 64);
+}
+
+// One part of a long chain in this tile: records [j0, j0 + n) of the LDS
+// window (n <= kWalkSpan).  head: the chain starts here (state from the
+// context); else its state comes from the look-back.  out: the chain runs on
+// into the next tile (this tile publishes for it).
+// Where walk_long takes over a chain whose speculation broke in this tile.
+struct ChainFix {
+    uint32_t i0;      // sorted index of the first record it walks (kNoSlot: none)
+    CtxState st;      // the context state before that record
+};
+
+template <bool REV>
+__device__ ChainFix chain_part(const BundleArgs &a, uint32_t tile, uint32_t epoch, uint32_t base, uint32_t j0,
+                               int n, bool head, bool out, int32_t prev_seq_in, const WalkRec *s_rec,
+                               const uint32_t *s_g0, const uint32_t *s_ok) {
+    ChainFix fix;
+    fix.i0 = kNoSlot;
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t slot = a.sk_out[base + j0];
+    const CtxState st0 = a.ctx[slot];
+    const KeySet *ks = a.keysets + st0.ks;
+    WalkCtx c;
+    c.enc = ks->enc_type; c.auth = ks->auth_type; c.T = ks->tag_len; c.kind = ks->kind;
+    const bool mac = c.auth != SRTP_NULL_AUTHENTICATION;
+    const int32_t prev_seq = head ? st0.b : prev_seq_in;
+    // ---- local evaluation
+    int32_t dpre[kChainPer];
+    uint32_t m[kChainPer], xr[kChainPer];
+    int32_t seqv[kChainPer];
+    bool lok[kChainPer];
+    int32_t lsum = 0;
+#pragma unroll
+    for (int r = 0; r < kChainPer; r++) {
+        const int pos = lane * kChainPer + r;
+        dpre[r] = 0; m[r] = 0u; xr[r] = 0u; seqv[r] = 0; lok[r] = false;
+        if (pos >= n) continue;
+        const WalkRec rec = s_rec[j0 + pos];
+        const int32_t seq = (int32_t)(rec.word & 0xffffu);
+        const int32_t sl = pos ? (int32_t)(s_rec[j0 + pos - 1].word & 0xffffu) : prev_seq;
+        int32_t d;
+        if (sl < 32768) d = (seq - sl > 32768) ? -1 : 0;
+        else d = (sl - 32768 > seq) ? 1 : 0;
+        const int64_t delta = (int64_t)d * 65536 + seq - sl;
+        const int L = (int)(rec.lc & 0xffffu), C = (int)(rec.lc >> 16);
+        bool ok = delta > 0;
+        if (REV) {
+            const int newL = mac ? (L - c.T > 0 ? L - c.T : 0) : L;
+            if (!(rec.p & kRecSkipDec)) ok = ok && !enc_would_throw(c.enc, rec.h, newL - rec.h);
+            if (mac) ok = ok && (s_ok[j0 + pos] & 1u) != 0u;
+        } else {
+            ok = ok && L + (mac ? c.T : 0) <= C && !enc_would_throw(c.enc, rec.h, L - rec.h);
+        }
+        lok[r] = ok;
+        lsum += d;
+        dpre[r] = lsum;
+        m[r] = (uint32_t)((uint64_t)delta & 63u);
+        seqv[r] = seq;
+    }
+    const int32_t dex = wave_excl_scan(lsum);
+#pragma unroll
+    for (int r = 0; r < kChainPer; r++) {
+        dpre[r] += dex;
+        if (REV && mac && lane * kChainPer + r < n) xr[r] = s_g0[j0 + lane * kChainPer + r] - (uint32_t)dpre[r];
+    }
+    const bool hasx = REV && mac && n > 0;
+    const uint32_t x0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)xr[0]); // position 0's
+    int fb = kChainPer;
+#pragma unroll
+    for (int r = kChainPer - 1; r >= 0; r--)
+        if (lane * kChainPer + r < n && (!lok[r] || (hasx && xr[r] != x0))) fb = r;
+    int first_bad = n;
+    {
+        const unsigned long long bl = __ballot(fb < kChainPer);
+        if (bl) {
+            const int l = __ffsll((long long)bl) - 1;
+            first_bad = l * kChainPer + __builtin_amdgcn_readlane(fb, l);
+        }
+    }
+    auto at = [&](const int32_t v[kChainPer], int pos) -> int32_t { // position pos's value (uniform)
+        int32_t x = 0;
+#pragma unroll
+        for (int r = 0; r < kChainPer; r++)
+            if (pos % kChainPer == r) x = __builtin_amdgcn_readlane(v[r], pos / kChainPer);
+        return x;
+    };
+    if (out && !head) { // this tile's aggregate, before waiting on the tiles before it
+        ChainAgg g;
+        chain_window(m, first_bad, g.tshift, g.bits);
+        g.dsum = first_bad ? at(dpre, first_bad - 1) : 0;
+        g.s_l = first_bad ? at(seqv, first_bad - 1) : 0;
+        g.x = x0;
+        g.hasx = hasx;
+        g.broken = first_bad < n;
+        chain_publish_agg(a, tile, epoch, g);
+    }
+    // ---- the state the part starts from
+    ChainState in;
+    uint32_t g_in;
+    if (head) {
+        in.roc = (uint32_t)st0.a; in.s_l = st0.b; in.window = st0.window;
+        in.broken = c.kind != SRTP_KIND_RTP || !(st0.flags & 1u);
+        g_in = (uint32_t)st0.g;
+    } else {
+        in = chain_lookback(a, tile, epoch);
+        g_in = in.roc;
+    }
+    if (in.broken) { // an earlier tile handed the chain over (or SRTCP / first packet)
+        if (head) { // the whole chain goes to walk_long from its start
+            fix.i0 = base + j0;
+            fix.st = st0;
+        }
+        if (out) chain_publish_state(a, tile, epoch, in);
+        return fix;
+    }
+    int f = first_bad;
+    if (hasx && in.roc != x0) f = 0;
+    if (n > 0 && (int64_t)(int32_t)in.roc + at(dpre, n - 1) > (int64_t)0x7fffffff) f = 0;
+    // ---- commit the records before f
+#pragma unroll
+    for (int r = 0; r < kChainPer; r++) {
+        const int pos = lane * kChainPer + r;
+        if (pos < f) {
+            const WalkRec rec = s_rec[j0 + pos];
+            const uint32_t p = rec.p & kRecIdxMask;
+            const int L = (int)(rec.lc & 0xffffu);
+            a.w_cw[p] = in.roc + (uint32_t)dpre[r];
+            a.w_len[p] = (uint32_t)(REV ? (mac ? (L - c.T > 0 ? L - c.T : 0) : L) : L + (mac ? c.T : 0));
+            a.w_status[p] = SRTP_STATUS_OK;
+        }
+    }
+    ChainState st = in;
+    uint32_t g_out = g_in;
+    if (f > 0) {
+        uint32_t tsh;
+        uint64_t bits;
+        chain_window(m, f, tsh, bits);
+        st.roc = in.roc + (uint32_t)at(dpre, f - 1);
+        st.s_l = at(seqv, f - 1);
+        st.window = (tsh < 64u ? in.window << tsh : 0ull) | bits;
+        g_out = st.roc;
+    }
+    CtxState cs = st0;
+    cs.a = (int32_t)st.roc; cs.b = st.s_l; cs.g = (int32_t)g_out; cs.window = st.window;
+    if (f < n) { // the speculation breaks at record f: walk_long walks the rest
+        fix.i0 = base + j0 + (uint32_t)f;
+        fix.st = cs;
+        st.broken = true;
+        if (out) chain_publish_state(a, tile, epoch, st);
+        return fix;
+    }
+    if (out) chain_publish_state(a, tile, epoch, st);
+    else if (lane == 0) a.ctx[slot] = cs; // the chain ends in this tile
+    return fix;
+}
+
+// One wave per workgroup owns the context segments that START among kWalkSpan
+// consecutive sorted records, and stages those records plus a look-ahead of
+// kWalkAhead more in LDS with one coalesced pass (plus, for unprotect, the
+// verify pass's g0/auth_ok of each record, gathered in parallel); it compacts
+// the segment starts and lane l walks the l-th segment: the per-context chain
+// reads LDS (tens of cycles per record) instead of dependent HBM round trips.
+// Only a segment longer than the look-ahead reads its tail from global memory.
+
+// PASS 0: the first launch; PASS 1: the second (abort-on-throw's limit pass,
+// or the long chains) -- separate instances, so that the first pass's
+// registers do not pay for chain_part.
+template <bool REV, bool SK, int PASS>
+__global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
+    constexpr int limit_pass = PASS;
     __shared__ WalkRec s_rec[kWalkWin];
     __shared__ uint32_t s_key[kWalkWin];
     __shared__ uint32_t s_g0[REV ? kWalkWin : 1];
     __shared__ uint32_t s_ok[REV ? kWalkWin : 1];
-    __shared__ uint32_t s_start[kWalkSpan];
+    static_assert(kLongStep <= kWalkWin, "walk_long stages a step in the first pass's arrays");
+    __shared__ uint32_t s_start[kWalkSpan > kLongStep ? kWalkSpan : kLongStep];
     __shared__ uint32_t s_nstart;
+    __shared__ uint32_t s_pkey[kWalkSpan]; // keys of the tile before (long-chain test)
+    __shared__ uint32_t s_tile;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
-    if (limit_pass && !two_pass) {
-        // second pass without abort-on-throw work: the long chains the first
-        // pass handed over, one per wave until none is left
-        const uint32_t n_long = a.ctl->n_long;
-        if (n_long == 0u || blockIdx.x >= n_long) return; // nothing (more) to do: no atomics
-        for (;;) {
-            uint32_t q = 0u;
-            if (threadIdx.x == 0) q = atomicAdd(&a.ctl->long_cursor, 1u);
-            q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
-            if (q >= n_long) return;
-            LongLds sm;
-            sm.rec = s_rec;
-            sm.roc = s_key;
-            sm.g0 = REV ? s_g0 : s_start;
-            sm.ok = REV ? s_ok : s_start;
-            sm.info = s_start;
-            walk_long<REV, SK>(a, a.long_list[q], sm);
-        }
-    }
+    // Long chains (kWalkSpan records or more) are walked by the tiles they
+    // cross (chain_part) in the second launch, unless abort-on-throw needs the
+    // serial two-pass walk; the first pass only flags that there are some.
+    const bool chains = !two_pass && a.debug == 0;
+    const bool chain_pass = limit_pass && !two_pass;
+    if (chain_pass && a.ctl->n_long == 0u) return; // no long chain in this bundle
     if (!limit_pass) // the sort's last digit counts, zero again for the next bundle
         for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words;
              i += gridDim.x * kWalkBlock)
             a.sort_zero[i] = 0u;
-    const uint32_t base = blockIdx.x * kWalkSpan;
+    // The chain pass takes its tile from a ticket counter: a tile that waits on
+    // the tiles before it for a long chain's state only waits on tiles already
+    // running.
+    uint32_t tile = blockIdx.x;
+    if (chain_pass) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(&a.ctl->tile_ticket, 1u);
+        __syncthreads();
+        tile = s_tile;
+    }
+    const uint32_t base = tile * kWalkSpan;
     if (base >= a.n) return;
     const uint32_t span = min((uint32_t)kWalkSpan, a.n - base);
     const uint32_t win = min((uint32_t)kWalkWin, a.n - base);
     if (threadIdx.x == 0) s_nstart = 0;
+    if (chain_pass && base) {
+#pragma unroll
+        for (int k = 0; k < kWalkPer; k++) {
+            const uint32_t j = threadIdx.x + k * kWalkBlock;
+            s_pkey[j] = a.sk_out[base - kWalkSpan + j];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < kWalkWin / kWalkBlock; k++) {
         const uint32_t j = threadIdx.x + k * kWalkBlock;
@@ -1569,6 +1934,82 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
     __syncthreads();
     if (a.debug == 1) return;
     const uint32_t prev_key = base ? a.sk_out[base - 1] : ~0u;
+    // A chain of kWalkSpan records or more (it reaches the end of the tile it
+    // starts in): record j's chain, starting at j, is that long iff the record
+    // kLongMin - 1 places on carries its key.
+    auto long_from = [&](uint32_t j, uint32_t key) -> bool {
+        const uint32_t jl = j + kLongMin - 1u;
+        const uint32_t kl = jl < win ? s_key[jl] : (base + jl < a.n ? a.sk_out[base + jl] : ~0u);
+        return kl == key;
+    };
+    if constexpr (PASS == 1) if (chain_pass) {
+        const uint32_t epoch = a.serial + 1u;
+        // the part at the tile start that continues a chain from the tile before
+        const uint32_t key0 = s_key[0];
+        bool in_long = false;
+        if (base && key0 == prev_key && key0 <= a.ctx_mask) {
+            if (s_pkey[0] == key0) {
+                in_long = true; // already kWalkSpan + 1 records
+            } else {            // it starts at s in the tile before: long iff s + 255 has its key
+                uint32_t sj = kWalkSpan;
+#pragma unroll
+                for (int k = 0; k < kWalkPer; k++) {
+                    const uint32_t j = threadIdx.x * kWalkPer + k;
+                    if (s_pkey[j] == key0 && (j == 0 || s_pkey[j - 1] != key0)) sj = j;
+                }
+                sj = (uint32_t)__reduce_min_sync(~0ull, sj);
+                in_long = sj > 0 && sj < (uint32_t)kWalkSpan && s_key[sj - 1] == key0;
+            }
+        }
+        // the run holding the tile's last record, and where it starts in the tile
+        const uint32_t keyl = s_key[span - 1];
+        uint32_t runs = span; // first position of keyl's run in the tile
+#pragma unroll
+        for (int k = 0; k < kWalkPer; k++) {
+            const uint32_t j = threadIdx.x * kWalkPer + k;
+            if (j < span && s_key[j] == keyl && (j == 0 || s_key[j - 1] != keyl)) runs = j;
+        }
+        runs = (uint32_t)__reduce_min_sync(~0ull, runs);
+        const bool next_same = base + span < a.n &&
+                               (span < win ? s_key[span] : a.sk_out[base + span]) == keyl;
+        ChainFix fix_in, fix_head;
+        fix_in.i0 = fix_head.i0 = kNoSlot;
+        // a long chain that starts in this tile (it holds the tile's last record),
+        // first: its state for the tiles after needs no look-back
+        const bool head_long = keyl <= a.ctx_mask && !(in_long && runs == 0u) &&
+                               !(runs == 0u && base && keyl == prev_key) && long_from(runs, keyl);
+        if (head_long)
+            fix_head = chain_part<REV>(a, tile, epoch, base, runs, (int)(span - runs), true, next_same, 0,
+                                       s_rec, REV ? s_g0 : s_start, REV ? s_ok : s_start);
+        // the part of a chain from the tiles before
+        uint32_t e_in = 0u; // its end
+        if (in_long) {
+            uint32_t e = span;
+#pragma unroll
+            for (int k = 0; k < kWalkPer; k++) {
+                const uint32_t j = threadIdx.x * kWalkPer + k;
+                if (j < span && s_key[j] != key0) e = min(e, j);
+            }
+            e_in = (uint32_t)__reduce_min_sync(~0ull, e);
+            int32_t prev_seq = 0;
+            if (threadIdx.x == 0) prev_seq = (int32_t)(a.sv_out[base - 1].word & 0xffffu);
+            prev_seq = __builtin_amdgcn_readfirstlane(prev_seq);
+            fix_in = chain_part<REV>(a, tile, epoch, base, 0u, (int)e_in, false, e_in == span && next_same,
+                                     prev_seq, s_rec, REV ? s_g0 : s_start, REV ? s_ok : s_start);
+        }
+        // walk_long takes over where a chain's speculation broke (the staged
+        // window is no longer needed: its LDS is walk_long's)
+        LongLds sm;
+        sm.rec = s_rec;
+        sm.roc = s_key;
+        sm.g0 = REV ? s_g0 : s_start;
+        sm.ok = REV ? s_ok : s_start;
+        sm.info = s_start;
+        if (fix_in.i0 != kNoSlot) walk_long<REV, SK>(a, fix_in.i0, sm, fix_in.st);
+        if (fix_head.i0 != kNoSlot) walk_long<REV, SK>(a, fix_head.i0, sm, fix_head.st);
+
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kWalkPer; k++) {
         const uint32_t j = threadIdx.x + k * kWalkBlock;
@@ -1586,18 +2027,10 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a, int limit_pas
         const uint32_t j = s_start[q];
         const uint32_t key = s_key[j];
         const uint32_t slot = key;
-        // A chain of kLongMin records or more goes to the wave-parallel walk of
-        // the second pass (unless abort-on-throw needs this one): walked here,
-        // its records would take one serial step each on this lane.  A key's
-        // records are contiguous, so the chain is that long iff the record
-        // kLongMin - 1 places on carries the key.
-        if (!two_pass) {
-            const uint32_t jl = j + kLongMin - 1u;
-            const uint32_t kl = jl < win ? s_key[jl] : (base + jl < a.n ? a.sk_out[base + jl] : ~0u);
-            if (kl == key) {
-                a.long_list[atomicAdd(&a.ctl->n_long, 1u)] = base + j;
-                continue;
-            }
+        // long chains are the chain pass's, unless abort-on-throw needs the serial walk
+        if (chains && long_from(j, key)) {
+            atomicOr(&a.ctl->n_long, 1u);
+            continue;
         }
         CtxState st = a.ctx[slot];
         const KeySet *ks = a.keysets + st.ks;
@@ -2953,17 +3386,17 @@ hipError_t launch_skein(const BundleArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
-    // the second launch also walks the handed-over chains, one wave each: a
-    // grid of up to n / kLongMin waves (those beyond the chain count, and
-    // beyond the spans in the abort-on-throw limit pass, exit at once)
     const uint32_t spans = (a.n + kWalkSpan - 1) / kWalkSpan;
-    const dim3 grid(limit_pass ? max(spans, min((a.n + kLongMin - 1) / kLongMin, 8192u)) : spans);
+    const dim3 grid(spans);
     if (a.reverse && a.has_skein) {
-        hipLaunchKernelGGL((k_walk<true, true>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+        if (limit_pass) hipLaunchKernelGGL((k_walk<true, true, 1>), grid, dim3(kWalkBlock), 0, s, a);
+        else hipLaunchKernelGGL((k_walk<true, true, 0>), grid, dim3(kWalkBlock), 0, s, a);
     } else if (a.reverse) {
-        hipLaunchKernelGGL((k_walk<true, false>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+        if (limit_pass) hipLaunchKernelGGL((k_walk<true, false, 1>), grid, dim3(kWalkBlock), 0, s, a);
+        else hipLaunchKernelGGL((k_walk<true, false, 0>), grid, dim3(kWalkBlock), 0, s, a);
     } else {
-        hipLaunchKernelGGL((k_walk<false, false>), grid, dim3(kWalkBlock), 0, s, a, limit_pass);
+        if (limit_pass) hipLaunchKernelGGL((k_walk<false, false, 1>), grid, dim3(kWalkBlock), 0, s, a);
+        else hipLaunchKernelGGL((k_walk<false, false, 0>), grid, dim3(kWalkBlock), 0, s, a);
     }
     return hipGetLastError();
 }

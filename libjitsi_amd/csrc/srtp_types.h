@@ -108,7 +108,7 @@ struct BundleCtl {
     uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk
     uint32_t n_long;      // context chains longer than the walk's LDS window (long_list)
     uint32_t long_cursor; // next long chain to hand to a wave
-    uint32_t pad;
+    uint32_t tile_ticket; // next first-pass walk tile
 };
 
 // Cumulative per-engine event counters (srtp_engine_stats), 64-bit, kept in
@@ -119,6 +119,7 @@ constexpr int kCtrStatus = 0;        // [0, 16): final status counts (SRTP_STATU
 constexpr int kCtrRocRecheck = 16;   // unprotect tags re-checked under a walk ROC != the speculation
 constexpr int kCtrRepaired = 17;     // packets k_unprotect_fix re-ciphered
 constexpr int kCtrOverflow = 18;     // packets refused a new context (table full)
+constexpr int kCtrChainStall = 19;   // walk tiles that gave up waiting on a long chain's look-back (a bug)
 constexpr int kCtrStride = 32;       // u64 words per replica (one 256-B line)
 
 // internal walk statuses (beyond SRTP_STATUS_*)
