@@ -47,7 +47,7 @@ struct srtp_engine {
     WalkRec *sv_in = nullptr, *sv_out = nullptr;
     int32_t *w_status = nullptr;
     uint32_t *w_cw = nullptr, *w_len = nullptr, *g0 = nullptr, *auth_ok = nullptr, *mid = nullptr;
-    uint32_t *tailc = nullptr, *spec = nullptr, *long_list = nullptr;
+    uint32_t *tailc = nullptr, *spec = nullptr;
     uint64_t *tile_link = nullptr;
     uint32_t *spos = nullptr;
     void *sort_temp = nullptr;
@@ -217,13 +217,13 @@ uint32_t next_pow2(uint64_t x) {
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
                     e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp,
-                    e->long_list, e->spos, e->tile_link};
+                    e->spos, e->tile_link};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
     e->w_status = nullptr;
     e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
-    e->long_list = e->spos = nullptr;
+    e->spos = nullptr;
     e->tile_link = nullptr;
     e->sort_temp = nullptr;
     e->scratch_n = 0;
@@ -250,7 +250,6 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->mid, (size_t)5 * m));
     HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
     HIPCHK(e, dalloc(&e->spec, m));
-    HIPCHK(e, dalloc(&e->long_list, m / kLongMin + 2)); // long chains are disjoint runs of >= kLongMin records
     HIPCHK(e, dalloc(&e->spos, m));
     // walk tiles' long-chain links: granules tagged with the bundle serial + 1,
     // so zeroed memory never reads as published
@@ -672,7 +671,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
     a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
-    a.tailc = e->tailc; a.spec = e->spec; a.long_list = e->long_list;
+    a.tailc = e->tailc; a.spec = e->spec;
     a.tile_link = e->tile_link;
     a.spos = e->spos;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);

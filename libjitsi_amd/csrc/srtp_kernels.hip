@@ -14,8 +14,14 @@
 //   k_walk     one lane per context segment: the serial integer state machine of
 //              SRTPCryptoContext (guessIndex :457-475, checkReplay :279-323,
 //              update :719-744) / SRTCPCryptoContext (:106-120, :435-451), in
-//              array order, committing the context state in HBM.  A second
-//              "limit" pass reproduces SinglePacketTransformer's abort-on-throw.
+//              array order, committing the context state in HBM (in-order
+//              packets on a fast prefix).  The second launch walks chains of
+//              >= 256 packets with every tile they cross at once (chain_part),
+//              or is the "limit" pass reproducing SinglePacketTransformer's
+//              abort-on-throw.
+//   k_skein    [engines with Skein-MAC key sets] Skein-512 tag check / trailer.
+//   k_ext      [engines with F8 / AES-256 / Twofish / Skein key sets] their
+//              ciphers (and the F8 / AES-256 HMAC trailers).
 //   k_protect  [protect] one lane per packet: fused AES-CM keystream + XOR +
 //              HMAC-SHA1 (one read and one write of the packet bytes).
 //   k_unprotect_fix [unprotect] statuses/lengths out; undoes/redoes the rare
@@ -1273,8 +1279,8 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
 }
 
 // ----------------------------------------------------- wave-parallel walk
-// A context chain longer than k_walk's LDS window (a skewed bundle: a few
-// SSRCs carry most packets) is walked by a whole wave, 256 records per step,
+// The rest of a long chain (see chain_part below), from the record where the
+// tiles' speculation broke, is walked by a whole wave, 256 records per step,
 // by speculating that every packet is the context's new highest index -- the
 // steady state of an in-order stream.  Under that assumption each packet's
 // guessed ROC (guessIndex, SRTPCryptoContext.java:457-475) depends only on

@@ -106,9 +106,9 @@ constexpr uint32_t kLongRank = 1024; // k_unprotect: chain packets from this ran
 // bundle control block (zeroed per bundle)
 struct BundleCtl {
     uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk
-    uint32_t n_long;      // context chains longer than the walk's LDS window (long_list)
-    uint32_t long_cursor; // next long chain to hand to a wave
-    uint32_t tile_ticket; // next first-pass walk tile
+    uint32_t n_long;      // nonzero: the bundle has a context chain of >= kLongMin records
+    uint32_t tile_ticket; // next walk tile of the chain pass
+    uint32_t pad;
 };
 
 // Cumulative per-engine event counters (srtp_engine_stats), 64-bit, kept in

@@ -160,3 +160,50 @@ def test_multi_wrap_chain_with_loss(engine):
     _, _, st2 = twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap)
     assert (st2 == 0).sum() > 0.99 * keep.size
     assert engine.context_state(rcv.e, int(b.ssrc[0]))["roc"] == 2
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_chains_around_tile_size(engine, seed):
+    """Chains of 250..520 packets (around the walk's 256-record tile), so that
+    long chains start, end and break at every position of a tile, next to
+    short ones: the chain pass (per-tile speculation with look-back) against
+    the oracle in both directions, with first packets of new streams (no
+    seqNumSet yet), replays / tampering / reordering, a receiver that misses
+    every 97th packet, and a second bundle continuing the same streams."""
+    rng = np.random.default_rng(300 + seed)
+    twin = Twin(engine)
+    (k, s), = synth.keys(310 + seed, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    lens = [int(x) for x in rng.integers(250, 521, 14)] + [int(x) for x in rng.integers(1, 40, 30)]
+    ssrcs = rng.choice(1 << 30, len(lens), replace=False).astype(np.uint32) + 1000
+    for rnd in range(2):
+        parts = []
+        for i, L in enumerate(lens):
+            seq0 = np.array([int(rng.integers(0, 65536)) if rnd == 0 else 0], np.uint32)
+            parts.append(synth.rtp_bundle(L, 1, (40, 300), seed=int(rng.integers(1 << 30)),
+                                          ssrcs=ssrcs[i:i + 1], seq0=seq0))
+        if rnd == 1:  # continue each stream where the first bundle left it
+            for i, pb in enumerate(parts):
+                st = twin.engine.context_state(snd.e, int(ssrcs[i]))
+                q = (int(st["s_l"]) + 1 + np.arange(pb.n)) & 0xFFFF
+                for j in range(pb.n):
+                    pb.seg[pb.off[j] + 2] = q[j] >> 8
+                    pb.seg[pb.off[j] + 3] = q[j] & 0xFF
+        b = synth.concat(parts)
+        perm = rng.permutation(b.n)  # interleave streams, each in its own order
+        owner = np.concatenate([np.full(p.n, i) for i, p in enumerate(parts)])[perm]
+        base = np.cumsum([0] + [p.n for p in parts])
+        order = np.empty(b.n, int)
+        for i in range(len(parts)):
+            order[owner == i] = base[i] + np.arange(parts[i].n)
+        b = synth.select(b, order)
+        seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+        assert (st == 0).all()
+        pb = b.copy()
+        pb.seg, pb.length = seg, ln
+        keep = np.ones(pb.n, bool)
+        keep[::97] = False
+        fb = faults(synth.select(pb, np.nonzero(keep)[0]), rng, frac=0.003)
+        twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap)
+    assert engine.stats()["chain_stalls"] == 0
