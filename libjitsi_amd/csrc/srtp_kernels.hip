@@ -724,9 +724,13 @@ __device__ __forceinline__ uint32_t parse_one(const BundleArgs &a, uint32_t p) {
 
 // One lane per packet; the block also counts the first sort digit of its
 // packets' keys into their 2048-record tile (the radix sort's first pass).
-__global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
+#ifndef SRTP_PARSE_BLOCK
+#define SRTP_PARSE_BLOCK 256
+#endif
+constexpr int kParseBlock = SRTP_PARSE_BLOCK; // divides the sort's 2048-record tile
+__global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
     __shared__ uint32_t s_hist[256];
-    s_hist[threadIdx.x] = 0u;
+    if (threadIdx.x < 256) s_hist[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     // reset the next bundle's control block (the previous bundle, which used
@@ -737,8 +741,9 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
             a.e_min_next[i] = 0x7f7f7f7f;
     if (p < a.n) atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
     __syncthreads();
-    const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kBlock
-    if (s_hist[threadIdx.x]) atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
+    const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kParseBlock
+    if (threadIdx.x < 256 && s_hist[threadIdx.x])
+        atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
 }
 
 // ============================================================== radix sort
@@ -750,7 +755,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(BundleArgs a) {
 // two-digit sort and no memsets: pass q re-zeroes pass q-1's counts, k_walk
 // the last pass's.
 constexpr int kSortThreads = 512, kSortItems = 4, kSortTile = kSortThreads * kSortItems;
-static_assert(kSortTile == 2048 && kSortTile % kBlock == 0, "k_parse tiles");
+static_assert(kSortTile == 2048 && kSortTile % kParseBlock == 0 && kParseBlock >= 256, "k_parse tiles");
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -877,8 +882,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
             // record of a skipped / invalid packet unwritten (stale scratch,
             // whose index may lie anywhere)
             if (sp.spos && key[r] <= sp.walk_max) sp.spos[rec.p & kRecIdxMask] = pos;
+#ifndef SRTP_DIAG_NOATOM // diagnostic build: without the next pass's counts (results wrong)
             if (sp.next_counts)
                 atomicAdd(&sp.next_counts[(pos / kSortTile) * 256 + ((key[r] >> (sp.shift + 8)) & 255u)], 1u);
+#endif
         }
     }
 }
@@ -3378,7 +3385,7 @@ __global__ void k_rehash_insert(uint64_t *keys, CtxState *ctx, uint32_t mask,
 static inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_parse, grid_for(a.n), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(k_parse, dim3((a.n + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
