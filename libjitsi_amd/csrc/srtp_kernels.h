@@ -61,7 +61,7 @@ struct BundleArgs {
                            // under g0 - 1, bit 1 its result
     uint32_t *mid;         // [5n] unprotect: inner SHA-1 state before the ROC block
     uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
-    uint32_t *spec;        // [n] unprotect: 1 = decrypted in place under g0 by k_unprotect
+    uint32_t *spec;        // [n] unprotect: kSpec* summary of k_unprotect (bit 0: decrypted in place under g0)
     uint64_t *tile_link;   // [(n / 256 + 2) * 10] per walk tile: the published part of a long chain
     uint32_t *spos;        // [n] unprotect: each record's position in sort order (the last sort pass)
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer

@@ -1233,7 +1233,7 @@ __device__ __forceinline__ bool walk_one(const BundleArgs &a, const KeySet *ks, 
                     ReverifyArgs rv;
                     rv.pkt = a.seg + a.off[p];
                     rv.mid = a.mid + 5 * (size_t)p;
-                    rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
+                    rv.tailc = (a.spec[p] & kSpecDid) ? a.tailc + 16 * (size_t)p : nullptr;
                     ok = reverify_tag<SK>(a, rv, ks, L, g);
                     atomicAdd(&a.counters[kCtrRocRecheck], 1ull);
                 }
@@ -1459,7 +1459,7 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, c
                             ReverifyArgs rv;
                             rv.pkt = a.seg + a.off[p];
                             rv.mid = a.mid + 5 * (size_t)p;
-                            rv.tailc = a.spec[p] ? a.tailc + 16 * (size_t)p : nullptr;
+                            rv.tailc = (a.spec[p] & kSpecDid) ? a.tailc + 16 * (size_t)p : nullptr;
                             g = reverify_tag<SK>(a, rv, ks, L, (int32_t)roc);
                         }
                     }
@@ -2168,13 +2168,16 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
 // ====================================================== final status helper
 // Final status of packet p (abort-aware); writes the caller's status/len.
 __device__ __forceinline__ int32_t finish_status(const BundleArgs &a, uint32_t p) {
+    // loads issued together, before the stores
     int32_t st = a.w_status[p];
-    if (st != SRTP_STATUS_SKIPPED && a.abort_on_error && a.ctl->any_throw) {
+    const uint32_t wl = a.w_len[p];
+    const bool thrown = a.abort_on_error && a.ctl->any_throw;
+    if (st != SRTP_STATUS_SKIPPED && thrown) {
         const int32_t tid = packet_tid(a, p);
         if ((int32_t)p > a.e_min[tid]) st = SRTP_STATUS_NOT_PROCESSED;
     }
     a.status[p] = st;
-    if (st != SRTP_STATUS_NOT_PROCESSED && st != SRTP_STATUS_SKIPPED) a.len[p] = a.w_len[p];
+    if (st != SRTP_STATUS_NOT_PROCESSED && st != SRTP_STATUS_SKIPPED) a.len[p] = wl;
     return st;
 }
 
@@ -2592,7 +2595,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         }
     } else {
         const int io = L - 4 - T;
-        if (io < 0) { a.spec[p] = 0u; return; } // the reference throws here (k_walk)
+        if (io < 0) { a.spec[p] = 0u; return; } // the reference throws here (k_walk): no decryption due
         suffix = ld_be32(pkt + io);
         end = do_mac ? (io > 0 ? io : 0) : L;
         if (aes && (suffix & 0x80000000u) && end - 8 > 0) {
@@ -2602,7 +2605,10 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         }
     }
     if (a.debug == 5) spec = false; // diagnostics: MAC only (results wrong by design)
-    a.spec[p] = spec ? 1u : 0u;
+    // for k_unprotect_fix: decrypted here, AES-CM packet of the fused path,
+    // RTP, DISCARD/SILENCE (so it needs no key-set lookup to decide a repair)
+    a.spec[p] = (spec ? kSpecDid : 0u) | (aes ? kSpecAes : 0u) | (rtp ? kSpecRtp : 0u) |
+                (rtp && a.flags && (a.flags[p] & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ? kSpecSkip : 0u);
     if (!do_mac && !spec) return;
     cs.end = spec ? end : 0;
 #pragma unroll
@@ -2799,24 +2805,20 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     uint32_t ks_id = 0;
     int L0 = 0;
     if (p < a.n) {
+        // every per-packet word first, all in flight together (the status
+        // stores below would otherwise order the loads after them)
         L0 = (int)a.len[p];
+        const uint32_t slot = a.p_slot[p];
+        const uint32_t sw = a.spec[p]; // k_unprotect's summary: no context / key-set loads
+        const uint32_t cw = a.w_cw[p], g0 = a.g0[p];
         const int32_t st = finish_status(a, p);
         atomicAdd(&s_cnt[st & 15], 1u);
-        const uint32_t slot = a.p_slot[p];
         if (slot != kNoSlot) {
-            did = a.spec[p] != 0u;
-            ks_id = a.ctx[slot].ks;
-            const KeySet *ks = a.keysets + ks_id;
-            const bool rtp = ks->kind == SRTP_KIND_RTP;
-            if (st == SRTP_STATUS_OK && ks->enc_type == SRTP_AESCM_ENCRYPTION && !ks->ext) {
-                if (rtp) {
-                    const uint32_t fl = a.flags ? a.flags[p] : 0u;
-                    need = !(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE));
-                } else {
-                    need = (a.w_cw[p] & 0x80000000u) != 0;
-                }
-            }
-            repair = (did || need) && !(did && need && (!rtp || a.g0[p] == a.w_cw[p]));
+            did = (sw & kSpecDid) != 0u;
+            const bool rtp = (sw & kSpecRtp) != 0u;
+            if (st == SRTP_STATUS_OK && (sw & kSpecAes)) need = rtp ? !(sw & kSpecSkip) : (cw & 0x80000000u) != 0;
+            repair = (did || need) && !(did && need && (!rtp || g0 == cw));
+            if (repair) ks_id = a.ctx[slot].ks;
         }
     }
     const bool any_repair = __syncthreads_or(repair);

@@ -98,6 +98,13 @@ struct alignas(16) WalkRec {
     int32_t h;       // RTP: header length or kHdrThrow; RTCP unprotect: tag length used for `word`
 };
 constexpr uint32_t kRecSkipDec = 0x80000000u; // FLAG_DISCARD|FLAG_SILENCE: no decrypt
+
+// k_unprotect's per-packet summary (BundleArgs::spec), read by the walk's
+// tag re-check and by k_unprotect_fix to decide a repair without the key set
+constexpr uint32_t kSpecDid = 1u;  // decrypted in place under the ROC guess
+constexpr uint32_t kSpecAes = 2u;  // AES-128-CM key set of the fused path (not k_ext's)
+constexpr uint32_t kSpecRtp = 4u;  // SRTP (else SRTCP)
+constexpr uint32_t kSpecSkip = 8u; // SRTP packet flagged DISCARD / SILENCE: not deciphered
 constexpr uint32_t kRecIdxMask = 0x0FFFFFFFu;
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
 
