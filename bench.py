@@ -445,6 +445,13 @@ def main():
             t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = float(t.item())
+    # slow-path work per bundle over the whole run (run-in, warmup, timed steps)
+    slow = {"long_walked": 0, "repaired": 0, "roc_rechecks": 0, "bundles": 0}
+    for e in engines:
+        s = e.stats()
+        for k in slow:
+            slow[k] += s[k]
+    slow_per_bundle = {k: round(v / max(slow["bundles"], 1), 1) for k, v in slow.items() if k != "bundles"}
 
     total_pkts = n * args.steps * n_gpus
     pps = total_pkts / dt_max
@@ -529,6 +536,7 @@ def main():
             "goodput_gbps": round(pps * L * 2 / 1e9, 2),
             "all_accepted": ok,
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+            "slow_path_per_bundle": slow_per_bundle,
             "roofline": dominant,
             "roofline_other": other[0] if other else None,
             "cpu_baseline": cpu,

@@ -79,7 +79,7 @@ class Stats(C.Structure):
     _fields_ = ([("bundles", C.c_uint64), ("packets", C.c_uint64),
                  ("status", C.c_uint64 * 10)] +
                 [(n, C.c_uint64) for n in ("roc_rechecks", "repaired", "ctx_overflow", "ctx_live",
-                                           "ctx_tombstones", "ctx_slots", "rehashes", "chain_stalls")])
+                                           "ctx_tombstones", "ctx_slots", "rehashes", "chain_stalls", "long_walked")])
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "status"}

@@ -253,7 +253,7 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->spos, m));
     // walk tiles' long-chain links: granules tagged with the bundle serial + 1,
     // so zeroed memory never reads as published
-    const size_t link_words = (size_t)(m / 256 + 2) * 10;
+    const size_t link_words = (size_t)(m / kLongMin + 2) * 10; // per walk tile
     HIPCHK(e, dalloc(&e->tile_link, link_words));
     HIPCHK(e, hipMemset(e->tile_link, 0, link_words * sizeof(uint64_t)));
     e->sort_temp_bytes = sort_temp_bytes(m);
@@ -968,6 +968,7 @@ int srtp_engine_stats(srtp_engine *e, srtp_stats *out) {
     out->ctx_slots = e->ctx_cap;
     out->rehashes = e->n_rehash;
     out->chain_stalls = sum[kCtrChainStall];
+    out->long_walked = sum[kCtrLongWalked];
     return SRTP_OK;
 }
 

@@ -1377,7 +1377,7 @@ struct LongLds {
 };
 
 template <bool REV, bool SK>
-__device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, const CtxState &st_in) {
+__device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, const CtxState &st_in) {
     const int lane = (int)(threadIdx.x & 63u);
     const uint32_t key = a.sk_out[i0];
     const uint32_t slot = key;
@@ -1390,6 +1390,7 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, c
     const int32_t tid = (int32_t)(a.ctx_keys[slot] >> 32);
     const bool mac = c.auth != SRTP_NULL_AUTHENTICATION;
     uint32_t i = i0;
+    uint32_t walked = 0u;
     for (;;) {
         // stage the step's records (coalesced), count the chain's
         int nv = 0;
@@ -1517,6 +1518,7 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, c
                 if (lane == 0 && rc) atomicAdd(&a.counters[kCtrRocRecheck], (unsigned long long)rc);
             }
         }
+        walked += (uint32_t)(f < nvalid ? (c.kind == SRTP_KIND_RTP ? f + 1 : nvalid) : nvalid);
         if (f < nvalid) { // the breaking packet (or every SRTCP packet): exactly as the serial walk
             const int stop = c.kind == SRTP_KIND_RTP ? f + 1 : nvalid;
             if (lane == 0) {
@@ -1535,7 +1537,10 @@ __device__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, c
         __syncthreads(); // the step's LDS is reused by the next
         if (nvalid < kLongStep && f >= nvalid) break;
     }
-    if (lane == 0) a.ctx[slot] = st;
+    if (lane == 0) {
+        a.ctx[slot] = st;
+        atomicAdd(&a.counters[kCtrLongWalked], (unsigned long long)walked);
+    }
 }
 
 // k_walk's geometry (see k_walk): one wave per workgroup, a span of kWalkSpan
@@ -1648,7 +1653,7 @@ __device__ __forceinline__ void chain_publish_state(const BundleArgs &a, uint32_
 
 // The exact state before tile `tile`'s first record, for a chain that runs
 // into it from the tiles before (each of them published its part).
-__device__ ChainState chain_lookback(const BundleArgs &a, uint32_t tile, uint32_t epoch) {
+__device__ __forceinline__ ChainState chain_lookback(const BundleArgs &a, uint32_t tile, uint32_t epoch) {
     const int lane = (int)(threadIdx.x & 63u);
     ChainAgg acc = {};     // the composed parts of the tiles after the current window
     bool have_acc = false;
@@ -1686,22 +1691,52 @@ __device__ ChainState chain_lookback(const BundleArgs &a, uint32_t tile, uint32_
         }
         const unsigned long long pm = __ballot(isP);
         const int fp = pm ? __ffsll((long long)pm) - 1 : 64;
-        // aggregates of lanes fp-1 (earliest tile) .. 0 (tile - 1 - 64 steps back)
+        // aggregates of lanes fp-1 (earliest tile) .. 0 (the latest), composed
+        // by a wave reduction: lane l takes in lanes (l, l + 2o) at step o
+        const bool have_win = fp > 0;
         ChainAgg win = {};
-        bool have_win = false;
-        for (int i = min(fp, 64) - 1; i >= 0; i--) {
-            ChainAgg g;
-            g.dsum = __builtin_amdgcn_readlane((int)v[0], i);
-            g.x = (uint32_t)__builtin_amdgcn_readlane((int)v[1], i);
-            const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)v[2], i);
-            g.tshift = w2 & 0x7fu;
-            g.hasx = (w2 & 0x80u) != 0u;
-            g.broken = (w2 & 0x100u) != 0u;
-            g.s_l = (int32_t)(w2 >> 16);
-            g.bits = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v[3], i) |
-                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v[4], i) << 32);
-            win = have_win ? chain_compose(win, g) : g;
-            have_win = true;
+        if (have_win) {
+            bool gv = lane < fp;
+            ChainAgg g = {};
+            if (gv) {
+                g.dsum = (int32_t)v[0];
+                g.x = v[1];
+                g.tshift = v[2] & 0x7fu;
+                g.hasx = (v[2] & 0x80u) != 0u;
+                g.broken = (v[2] & 0x100u) != 0u;
+                g.s_l = (int32_t)(v[2] >> 16);
+                g.bits = (uint64_t)v[3] | ((uint64_t)v[4] << 32);
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t w = g.tshift | (g.hasx ? 0x80u : 0u) | (g.broken ? 0x100u : 0u) |
+                                   (gv ? 0x200u : 0u) | ((uint32_t)g.s_l << 16);
+                ChainAgg e;
+                e.dsum = __shfl_down(g.dsum, o, 64);
+                e.x = (uint32_t)__shfl_down((int)g.x, o, 64);
+                const uint32_t ew = (uint32_t)__shfl_down((int)w, o, 64);
+                const uint32_t elo = (uint32_t)__shfl_down((int)(uint32_t)g.bits, o, 64);
+                const uint32_t ehi = (uint32_t)__shfl_down((int)(uint32_t)(g.bits >> 32), o, 64);
+                e.tshift = ew & 0x7fu;
+                e.hasx = (ew & 0x80u) != 0u;
+                e.broken = (ew & 0x100u) != 0u;
+                e.s_l = (int32_t)(ew >> 16);
+                e.bits = (uint64_t)elo | ((uint64_t)ehi << 32);
+                if (lane + o < 64 && (ew & 0x200u)) { // lanes (l, l + 2o): earlier tiles
+                    g = gv ? chain_compose(e, g) : e;
+                    gv = true;
+                }
+            }
+            win.dsum = __builtin_amdgcn_readfirstlane(g.dsum);
+            win.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)g.x);
+            const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+                (int)(g.tshift | (g.hasx ? 0x80u : 0u) | (g.broken ? 0x100u : 0u) | ((uint32_t)g.s_l << 16)));
+            win.tshift = w0 & 0x7fu;
+            win.hasx = (w0 & 0x80u) != 0u;
+            win.broken = (w0 & 0x100u) != 0u;
+            win.s_l = (int32_t)(w0 >> 16);
+            win.bits = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g.bits) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g.bits >> 32)) << 32);
         }
         if (have_win) {
             acc = have_acc ? chain_compose(win, acc) : win;
@@ -1755,7 +1790,7 @@ struct ChainFix {
 };
 
 template <bool REV>
-__device__ ChainFix chain_part(const BundleArgs &a, uint32_t tile, uint32_t epoch, uint32_t base, uint32_t j0,
+__device__ __forceinline__ ChainFix chain_part(const BundleArgs &a, uint32_t tile, uint32_t epoch, uint32_t base, uint32_t j0,
                                int n, bool head, bool out, int32_t prev_seq_in, const WalkRec *s_rec,
                                const uint32_t *s_g0, const uint32_t *s_ok) {
     ChainFix fix;
