@@ -202,8 +202,9 @@ typedef struct {
     uint64_t rehashes;                   /* context-table rebuilds (tombstone cleanup) */
     uint64_t chain_stalls;               /* walk tiles that gave up waiting for a long chain's
                                             state from the tiles before (never expected) */
-    uint64_t long_walked;                /* packets of long context chains walked after the
-                                            tile-parallel speculation broke (the slow path) */
+    uint64_t long_walked;                /* packets of chains of 32+ packets that the wave-wide
+                                            speculation could not take and were walked one at
+                                            a time (the slow path) */
 } srtp_stats;
 int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
 

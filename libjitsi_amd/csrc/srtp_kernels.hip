@@ -1399,11 +1399,11 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
             const int j = lane + 64 * k;
             const uint32_t idx = i + (uint32_t)j;
             const bool v = idx < a.n && a.sk_out[idx] == key;
-            WalkRec r = WalkRec{0u, 0u, 0u, 0};
-            if (v) r = a.sv_out[idx];
-            sm.rec[j] = r;
+            uint4 r = make_uint4(0u, 0u, 0u, 0u); // the WalkRec as one 16-B word
+            if (v) r = reinterpret_cast<const uint4 *>(a.sv_out)[idx];
+            reinterpret_cast<uint4 *>(sm.rec)[j] = r;
             if (REV) {
-                const uint32_t p = r.p & kRecIdxMask;
+                const uint32_t p = r.x & kRecIdxMask;
                 sm.g0[j] = v ? a.g0[p] : 0u;
                 sm.ok[j] = v ? a.auth_ok[p] : 0u;
             }
@@ -1518,7 +1518,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
                 if (lane == 0 && rc) atomicAdd(&a.counters[kCtrRocRecheck], (unsigned long long)rc);
             }
         }
-        walked += (uint32_t)(f < nvalid ? (c.kind == SRTP_KIND_RTP ? f + 1 : nvalid) : nvalid);
+        walked += (uint32_t)(f < nvalid ? (c.kind == SRTP_KIND_RTP ? 1 : nvalid - f) : 0);
         if (f < nvalid) { // the breaking packet (or every SRTCP packet): exactly as the serial walk
             const int stop = c.kind == SRTP_KIND_RTP ? f + 1 : nvalid;
             if (lane == 0) {
@@ -1553,6 +1553,15 @@ constexpr int kWalkPer = SRTP_WALK_PER; // records per lane of a span
 constexpr int kWalkSpan = kWalkBlock * kWalkPer;
 constexpr int kWalkAhead = 256;
 constexpr int kWalkWin = kWalkSpan + kWalkAhead;
+// A chain of kMedMin records or more (and shorter than kLongMin) is walked by
+// the whole wave (walk_long) after the lanes' one-lane walks: a lane pays a
+// few hundred cycles per record, the wave's speculation a few per record.
+#ifndef SRTP_MED_MIN
+#define SRTP_MED_MIN 32
+#endif
+constexpr uint32_t kMedMin = SRTP_MED_MIN;
+constexpr int kMedMax = kWalkSpan / SRTP_MED_MIN + 1; // chains of kMedMin+ starting in a span
+static_assert(kMedMax <= 64, "one medium chain start per lane");
 
 // ------------------------------------------------ chains across walk tiles
 // A context chain of kWalkSpan or more records (a heavy SSRC in a skewed
@@ -1956,6 +1965,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     __shared__ uint32_t s_nstart;
     __shared__ uint32_t s_pkey[kWalkSpan]; // keys of the tile before (long-chain test)
     __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_med[kMedMax], s_nmed;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
     // Long chains (kWalkSpan records or more) are walked by the tiles they
     // cross (chain_part) in the second launch, unless abort-on-throw needs the
@@ -1980,7 +1990,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     if (base >= a.n) return;
     const uint32_t span = min((uint32_t)kWalkSpan, a.n - base);
     const uint32_t win = min((uint32_t)kWalkWin, a.n - base);
-    if (threadIdx.x == 0) s_nstart = 0;
+    if (threadIdx.x == 0) { s_nstart = 0; s_nmed = 0; }
     if (chain_pass && base) {
 #pragma unroll
         for (int k = 0; k < kWalkPer; k++) {
@@ -2106,6 +2116,11 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
             atomicOr(&a.ctl->n_long, 1u);
             continue;
         }
+        // medium chains: the whole wave walks them after the lanes' own
+        if (chains && j + kMedMin - 1u < win && s_key[j + kMedMin - 1u] == key) {
+            s_med[atomicAdd(&s_nmed, 1u)] = j;
+            continue;
+        }
         CtxState st = a.ctx[slot];
         const KeySet *ks = a.keysets + st.ks;
         WalkCtx c;
@@ -2197,6 +2212,25 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
             continue;
         }
         a.ctx[slot] = st;
+    }
+    if (!chains) return;
+    __syncthreads();
+    const uint32_t nmed = s_nmed;
+    if (nmed == 0u) return;
+    uint32_t med = threadIdx.x < nmed ? s_med[threadIdx.x] : 0u;
+    // walk_long's step arrays are the staging window's (no longer read)
+    LongLds sm;
+    sm.rec = s_rec;
+    sm.roc = s_key;
+    sm.g0 = REV ? s_g0 : s_start;
+    sm.ok = REV ? s_ok : s_start;
+    sm.info = s_start;
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t m = 0; m < nmed; m++) {
+        const uint32_t i0 = base + (uint32_t)__builtin_amdgcn_readlane((int)med, (int)m);
+        const CtxState st = a.ctx[a.sk_out[i0]];
+        walk_long<REV, SK>(a, i0, sm, st);
     }
 }
 

@@ -127,7 +127,7 @@ constexpr int kCtrRocRecheck = 16;   // unprotect tags re-checked under a walk R
 constexpr int kCtrRepaired = 17;     // packets k_unprotect_fix re-ciphered
 constexpr int kCtrOverflow = 18;     // packets refused a new context (table full)
 constexpr int kCtrChainStall = 19;   // walk tiles that gave up waiting on a long chain's look-back (a bug)
-constexpr int kCtrLongWalked = 20;   // records walk_long walked (a long chain's speculation broke)
+constexpr int kCtrLongWalked = 20;   // records walk_long walked one at a time (they broke the speculation)
 constexpr int kCtrStride = 32;       // u64 words per replica (one 256-B line)
 
 // internal walk statuses (beyond SRTP_STATUS_*)
