@@ -1375,11 +1375,19 @@ struct LongLds {
     uint32_t *ok;     // [kLongStep] unprotect: the verify pass's auth bits
     uint32_t *info;   // [kLongStep] bit 0: keeps the speculation; bits 1..: delta & 63
 };
+// A window already staged in LDS (k_walk's first pass): records [base, base +
+// win) of the sorted arrays, read in place instead of staged again.
+struct LongWin {
+    const WalkRec *rec;
+    const uint32_t *key, *g0, *ok;
+    uint32_t base, win;
+};
 
 template <bool REV, bool SK>
-__device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, const CtxState &st_in) {
+__device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, const LongLds &sm, const CtxState &st_in,
+                                          const LongWin *pw = nullptr) {
     const int lane = (int)(threadIdx.x & 63u);
-    const uint32_t key = a.sk_out[i0];
+    const uint32_t key = pw ? pw->key[i0 - pw->base] : a.sk_out[i0];
     const uint32_t slot = key;
     CtxState st = st_in;
     const KeySet *ks = a.keysets + st.ks;
@@ -1392,25 +1400,40 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
     uint32_t i = i0;
     uint32_t walked = 0u;
     for (;;) {
-        // stage the step's records (coalesced), count the chain's
-        int nv = 0;
+        const WalkRec *R = sm.rec;     // the step's records, block order
+        const uint32_t *G0 = sm.g0, *OK = sm.ok;
+        int nvalid;
+        if (pw) { // already staged: the records sit in the window at i - pw->base
+            const uint32_t jb = i - pw->base;
+            int nv = 0;
 #pragma unroll
-        for (int k = 0; k < kLongPer; k++) {
-            const int j = lane + 64 * k;
-            const uint32_t idx = i + (uint32_t)j;
-            const bool v = idx < a.n && a.sk_out[idx] == key;
-            uint4 r = make_uint4(0u, 0u, 0u, 0u); // the WalkRec as one 16-B word
-            if (v) r = reinterpret_cast<const uint4 *>(a.sv_out)[idx];
-            reinterpret_cast<uint4 *>(sm.rec)[j] = r;
-            if (REV) {
-                const uint32_t p = r.x & kRecIdxMask;
-                sm.g0[j] = v ? a.g0[p] : 0u;
-                sm.ok[j] = v ? a.auth_ok[p] : 0u;
+            for (int k = 0; k < kLongPer; k++) {
+                const uint32_t t = jb + (uint32_t)(lane + 64 * k);
+                nv += (t < pw->win && pw->key[t] == key) ? 1 : 0;
             }
-            nv += v ? 1 : 0;
+            nvalid = (int)__reduce_add_sync(~0ull, (unsigned)nv);
+            R = pw->rec + jb; G0 = pw->g0 + jb; OK = pw->ok + jb;
+        } else {
+            // stage the step's records (coalesced), count the chain's
+            int nv = 0;
+#pragma unroll
+            for (int k = 0; k < kLongPer; k++) {
+                const int j = lane + 64 * k;
+                const uint32_t idx = i + (uint32_t)j;
+                const bool v = idx < a.n && a.sk_out[idx] == key;
+                uint4 r = make_uint4(0u, 0u, 0u, 0u); // the WalkRec as one 16-B word
+                if (v) r = reinterpret_cast<const uint4 *>(a.sv_out)[idx];
+                reinterpret_cast<uint4 *>(sm.rec)[j] = r;
+                if (REV) {
+                    const uint32_t p = r.x & kRecIdxMask;
+                    sm.g0[j] = v ? a.g0[p] : 0u;
+                    sm.ok[j] = v ? a.auth_ok[p] : 0u;
+                }
+                nv += v ? 1 : 0;
+            }
+            nvalid = (int)__reduce_add_sync(~0ull, (unsigned)nv); // a prefix of the step
+            __syncthreads();
         }
-        const int nvalid = (int)__reduce_add_sync(~0ull, (unsigned)nv); // a prefix of the step
-        __syncthreads();
         if (nvalid == 0) break;
         int f = 0; // block position of the first packet that breaks the speculation
         if (c.kind == SRTP_KIND_RTP && (st.flags & 1u)) {
@@ -1421,8 +1444,8 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
             for (int r = 0; r < kLongPer; r++) {
                 const int pos = p0 + r;
                 if (pos >= nvalid) break;
-                const int32_t seq = (int32_t)(sm.rec[pos].word & 0xffffu);
-                const int32_t sl = pos ? (int32_t)(sm.rec[pos - 1].word & 0xffffu) : st.b;
+                const int32_t seq = (int32_t)(R[pos].word & 0xffffu);
+                const int32_t sl = pos ? (int32_t)(R[pos - 1].word & 0xffffu) : st.b;
                 int32_t d;
                 if (sl < 32768) d = (seq - sl > 32768) ? -1 : 0;
                 else d = (sl - 32768 > seq) ? 1 : 0;
@@ -1434,9 +1457,9 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
             for (int r = 0; r < kLongPer; r++) {
                 const int pos = p0 + r;
                 if (pos >= nvalid) { first_bad = min(first_bad, r); break; }
-                const WalkRec rec = sm.rec[pos];
+                const WalkRec rec = R[pos];
                 const int32_t seq = (int32_t)(rec.word & 0xffffu);
-                const int32_t sl = pos ? (int32_t)(sm.rec[pos - 1].word & 0xffffu) : st.b;
+                const int32_t sl = pos ? (int32_t)(R[pos - 1].word & 0xffffu) : st.b;
                 const uint32_t roc_prev = roc;
                 int32_t d;
                 if (sl < 32768) d = (seq - sl > 32768) ? -1 : 0;
@@ -1450,7 +1473,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
                     const int newL = mac ? (L - c.T > 0 ? L - c.T : 0) : L;
                     if (!(rec.p & kRecSkipDec)) g = g && !enc_would_throw(c.enc, rec.h, newL - rec.h);
                     if (g && mac) { // the tag under this ROC
-                        const uint32_t g0 = sm.g0[pos], okb = sm.ok[pos];
+                        const uint32_t g0 = G0[pos], okb = OK[pos];
                         if (roc == g0) {
                             g = (okb & 1u) != 0u;
                         } else if ((okb & 4u) && roc == g0 - 1u) {
@@ -1484,7 +1507,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
             for (int r = 0; r < kLongPer; r++) {
                 const int pos = p0 + r;
                 if (pos >= f) break;
-                const WalkRec rec = sm.rec[pos];
+                const WalkRec rec = R[pos];
                 const uint32_t p = rec.p & kRecIdxMask;
                 const int L = (int)(rec.lc & 0xffffu);
                 const uint32_t rr = sm.roc[pos];
@@ -1492,7 +1515,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
                 a.w_len[p] = (uint32_t)(REV ? (mac ? (L - c.T > 0 ? L - c.T : 0) : L) : L + (mac ? c.T : 0));
                 a.w_status[p] = SRTP_STATUS_OK;
                 if (REV && mac) {
-                    const uint32_t g0 = sm.g0[pos], okb = sm.ok[pos];
+                    const uint32_t g0 = G0[pos], okb = OK[pos];
                     if (rr != g0 && !((okb & 4u) && rr == g0 - 1u)) recheck++;
                 }
                 dsum += (int32_t)(sm.info[pos] >> 1);
@@ -1512,7 +1535,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
                 bits = wave_or64(bits);
                 st.window = (total < 64 ? st.window << total : 0ull) | bits;
                 st.a = (int32_t)sm.roc[f - 1];
-                st.b = (int32_t)(sm.rec[f - 1].word & 0xffffu);
+                st.b = (int32_t)(R[f - 1].word & 0xffffu);
                 st.g = st.a;
                 const uint32_t rc = (uint32_t)__reduce_add_sync(~0ull, recheck);
                 if (lane == 0 && rc) atomicAdd(&a.counters[kCtrRocRecheck], (unsigned long long)rc);
@@ -1523,9 +1546,9 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
             const int stop = c.kind == SRTP_KIND_RTP ? f + 1 : nvalid;
             if (lane == 0) {
                 for (int k = f; k < stop; k++) {
-                    const WalkRec r = sm.rec[k];
+                    const WalkRec r = R[k];
                     uint32_t g0 = 0u, ok = 0u;
-                    if (REV) { g0 = sm.g0[k]; ok = sm.ok[k]; }
+                    if (REV) { g0 = G0[k]; ok = OK[k]; }
                     (void)walk_one<SK>(a, ks, c, st, r, g0, ok, false, tid);
                 }
             }
@@ -1963,7 +1986,8 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     static_assert(kLongStep <= kWalkWin, "walk_long stages a step in the first pass's arrays");
     __shared__ uint32_t s_start[kWalkSpan > kLongStep ? kWalkSpan : kLongStep];
     __shared__ uint32_t s_nstart;
-    __shared__ uint32_t s_pkey[kWalkSpan]; // keys of the tile before (long-chain test)
+    __shared__ uint32_t s_pkey[kWalkSpan]; // keys of the tile before (long-chain test); medium chains: ROCs
+    static_assert(kLongStep <= kWalkSpan, "a medium chain's walk_long step keeps its ROCs in s_pkey");
     __shared__ uint32_t s_tile;
     __shared__ uint32_t s_med[kMedMax], s_nmed;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
@@ -2218,19 +2242,27 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     const uint32_t nmed = s_nmed;
     if (nmed == 0u) return;
     uint32_t med = threadIdx.x < nmed ? s_med[threadIdx.x] : 0u;
-    // walk_long's step arrays are the staging window's (no longer read)
+    // the chains' records are read from the staged window in place; walk_long's
+    // per-step results go to arrays the one-lane walks no longer use
+    LongWin pw;
+    pw.rec = s_rec;
+    pw.key = s_key;
+    pw.g0 = REV ? s_g0 : s_start;
+    pw.ok = REV ? s_ok : s_start;
+    pw.base = base;
+    pw.win = win;
     LongLds sm;
     sm.rec = s_rec;
-    sm.roc = s_key;
-    sm.g0 = REV ? s_g0 : s_start;
+    sm.roc = s_pkey;
+    sm.g0 = REV ? s_g0 : s_start; // unused in place
     sm.ok = REV ? s_ok : s_start;
     sm.info = s_start;
     __syncthreads();
 #pragma unroll 1
     for (uint32_t m = 0; m < nmed; m++) {
-        const uint32_t i0 = base + (uint32_t)__builtin_amdgcn_readlane((int)med, (int)m);
-        const CtxState st = a.ctx[a.sk_out[i0]];
-        walk_long<REV, SK>(a, i0, sm, st);
+        const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)med, (int)m);
+        const CtxState st = a.ctx[s_key[j]];
+        walk_long<REV, SK>(a, base + j, sm, st, &pw);
     }
 }
 

@@ -171,11 +171,26 @@ def test_chains_around_tile_size(engine, seed):
     seqNumSet yet), replays / tampering / reordering, a receiver that misses
     every 97th packet, and a second bundle continuing the same streams."""
     rng = np.random.default_rng(300 + seed)
+    lens = [int(x) for x in rng.integers(250, 521, 14)] + [int(x) for x in rng.integers(1, 40, 30)]
+    chains_roundtrip(engine, rng, 310 + seed, lens, 0.003)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_medium_chains(engine, seed):
+    """Chains of 24..260 packets: around the first pass's one-lane / whole-wave
+    threshold (32) and up to the chain pass's (256), several starting in one
+    tile, with the same first packets, faults and lost packets as above."""
+    rng = np.random.default_rng(400 + seed)
+    lens = ([int(x) for x in rng.integers(24, 40, 24)] + [int(x) for x in rng.integers(40, 261, 30)] +
+            [int(x) for x in rng.integers(1, 24, 30)])
+    chains_roundtrip(engine, rng, 410 + seed, lens, 0.01)
+
+
+def chains_roundtrip(engine, rng, key_seed, lens, frac):
     twin = Twin(engine)
-    (k, s), = synth.keys(310 + seed, 1)
+    (k, s), = synth.keys(key_seed, 1)
     fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
     snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
-    lens = [int(x) for x in rng.integers(250, 521, 14)] + [int(x) for x in rng.integers(1, 40, 30)]
     ssrcs = rng.choice(1 << 30, len(lens), replace=False).astype(np.uint32) + 1000
     for rnd in range(2):
         parts = []
@@ -204,6 +219,6 @@ def test_chains_around_tile_size(engine, seed):
         pb.seg, pb.length = seg, ln
         keep = np.ones(pb.n, bool)
         keep[::97] = False
-        fb = faults(synth.select(pb, np.nonzero(keep)[0]), rng, frac=0.003)
+        fb = faults(synth.select(pb, np.nonzero(keep)[0]), rng, frac=frac)
         twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap)
     assert engine.stats()["chain_stalls"] == 0
