@@ -799,6 +799,11 @@ struct SortPass {
     uint32_t walk_max;        // largest key of a walked record (the context table's mask)
 };
 
+#ifndef SRTP_SORT_COUNT_LOADS
+#define SRTP_SORT_COUNT_LOADS 64
+#endif
+constexpr int kSortCountLoads = SRTP_SORT_COUNT_LOADS;
+static_assert(kSortThreads == 512, "two threads per digit read the count table");
 __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
     __shared__ uint32_t s_base[256], s_run[256], s_wcnt[kSortThreads / 64][256];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -808,18 +813,19 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
         // + (records with digit d in earlier tiles).  Every tile re-reads the
         // whole [tiles][256] count table (128 KB at 2^18 records, L2-resident),
         // which costs less than a separate scan launch.  Thread (g, d) sums
-        // digit d over every other tile, 16 loads in flight.
+        // digit d over every other tile, kSortCountLoads loads in flight (one
+        // round up to 2 x kSortCountLoads tiles: 2^18 records at 64).
         const int d = t & 255, g = t >> 8;
         uint32_t before = 0u, total = 0u;
-        for (uint32_t u0 = (uint32_t)g; u0 < sp.tiles; u0 += 32u) {
-            uint32_t c[16];
+        for (uint32_t u0 = (uint32_t)g; u0 < sp.tiles; u0 += 2u * kSortCountLoads) {
+            uint32_t c[kSortCountLoads];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
+            for (int k = 0; k < kSortCountLoads; k++) {
                 const uint32_t u = u0 + 2u * k;
                 c[k] = u < sp.tiles ? sp.counts[u * 256u + d] : 0u;
             }
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
+            for (int k = 0; k < kSortCountLoads; k++) {
                 total += c[k];
                 before += u0 + 2u * k < tile ? c[k] : 0u;
             }
