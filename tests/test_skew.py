@@ -184,6 +184,8 @@ def test_medium_chains(engine, seed):
     lens = ([int(x) for x in rng.integers(24, 40, 24)] + [int(x) for x in rng.integers(40, 261, 30)] +
             [int(x) for x in rng.integers(1, 24, 30)])
     chains_roundtrip(engine, rng, 410 + seed, lens, 0.01)
+    # each new stream's first packet (no seqNumSet) is walked one at a time
+    assert engine.stats()["long_walked"] > 0
 
 
 def chains_roundtrip(engine, rng, key_seed, lens, frac):
