@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SRTP_MI355X_ABI_VERSION 1
+#define SRTP_MI355X_ABI_VERSION 2
 
 /* SRTPPolicy constants (transform/srtp/SRTPPolicy.java:29-63) */
 #define SRTP_NULL_ENCRYPTION 0
@@ -91,7 +91,9 @@ extern "C" {
 #define SRTP_STATUS_DROP_INVALID 7    /* len < 12 or len > cap (RawPacket.isInvalid) */
 #define SRTP_STATUS_NOT_PROCESSED 8   /* after an ERR_MALFORMED with abort_on_error */
 #define SRTP_STATUS_SKIPPED 9         /* SRTP_PKT_FLAG_SKIP (null element / predicate) */
-#define SRTP_NUM_STATUS 10
+#define SRTP_STATUS_ERR_INTERNAL 10   /* no walk reached the packet: an engine bug (never expected);
+                                         the packet and its context are left as they were */
+#define SRTP_NUM_STATUS 11
 
 /* per-packet flags (javax.media.Buffer values read at SRTPCryptoContext.java:609) */
 #define SRTP_PKT_FLAG_DISCARD 0x2u
@@ -201,12 +203,21 @@ typedef struct {
     uint64_t ctx_live, ctx_tombstones, ctx_slots;
     uint64_t rehashes;                   /* context-table rebuilds (tombstone cleanup) */
     uint64_t chain_stalls;               /* walk tiles that gave up waiting for a long chain's
-                                            state from the tiles before (never expected) */
+                                            state from the tiles before (never expected; the
+                                            chain is then walked serially from the exact state
+                                            by the last tile to finish, so results stay exact) */
     uint64_t long_walked;                /* packets of chains of 32+ packets that the wave-wide
                                             speculation could not take and were walked one at
                                             a time (the slow path) */
 } srtp_stats;
 int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
+
+/* Test hooks (0 in production): SRTP_DEBUG_FORCE_CHAIN_STALL makes every third
+ * chain-pass walk tile give up its look-back at once, which exercises the
+ * stall fix-up (srtp_stats.chain_stalls) that a tile preempted for seconds
+ * would take.  Results must not change. */
+#define SRTP_DEBUG_FORCE_CHAIN_STALL 0x1u
+int srtp_engine_set_debug(srtp_engine *e, uint32_t flags);
 
 /* Context-state export / import: lets a stream's ROC, s_l,
  * replay window and SRTCP indices follow it to another engine or GPU (SSRC
@@ -225,6 +236,23 @@ int srtp_export_contexts(srtp_engine *e, int32_t transformer, uint32_t *ssrcs,
                          srtp_ctx_state *states, uint32_t max, uint32_t *count);
 int srtp_set_context_state(srtp_engine *e, int32_t transformer, uint32_t ssrc, int32_t forward,
                            const srtp_ctx_state *st);
+
+/* Exact context snapshots (the dispatcher's abort rollback, dispatch.cpp):
+ * srtp_contexts_save copies the contexts (tids[i], ssrcs[i]) -- their whole
+ * record, key set included, as an opaque srtp_ctx_raw -- and sets present[i]
+ * to 0 where the transformer has no context for ssrcs[i].  srtp_contexts_restore
+ * puts such a snapshot back: the context is created or overwritten where
+ * present[i] != 0 and removed where present[i] == 0, so the table is as it
+ * was when the snapshot was taken.  The (tid, ssrc) pairs of one restore call
+ * must be distinct.  Both wait for the engine's enqueued bundles.  No
+ * reference API (SRTPCryptoContext's state is private). */
+typedef struct {
+    uint64_t w[4];
+} srtp_ctx_raw;
+int srtp_contexts_save(srtp_engine *e, uint32_t n, const int32_t *tids, const uint32_t *ssrcs,
+                       srtp_ctx_raw *out, int32_t *present);
+int srtp_contexts_restore(srtp_engine *e, uint32_t n, const int32_t *tids, const uint32_t *ssrcs,
+                          const srtp_ctx_raw *in, const int32_t *present);
 
 /* Per-stage kernel timing with HIP events recorded on the bundle's stream
  * (measurement hook for bench.py; off by default). */
@@ -296,7 +324,12 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
  * (srtp_aggregator_create returns SRTP_EINVAL otherwise).  When every slot is
  * sealed or in flight, submit blocks (backpressure).  flush seals the open
  * bundles and waits until every accepted packet has completed; destroy does
- * the same, then stops the threads. */
+ * the same, then stops the threads.  A submit copies its packet outside the
+ * aggregator's lock (producers only serialise on reserving its place).
+ * Callbacks may submit (e.g. forward a received packet), but a submit made
+ * from a callback never blocks: it returns SRTP_EFULL when no slot is free,
+ * since only the dispatch threads free slots.  flush from a callback returns
+ * SRTP_EINVAL and destroy from a callback does nothing. */
 typedef struct srtp_aggregator srtp_aggregator;
 typedef struct {
     uint32_t max_packets; /* per bundle, default 1<<14 */
@@ -326,20 +359,22 @@ void srtp_aggregator_destroy(srtp_aggregator *a);
  * place.  Results are identical to one engine processing the whole bundle,
  * including SinglePacketTransformer's abort-on-throw
  * (SinglePacketTransformer.java:134-155,190-210), which the dispatcher
- * reproduces across shards by running packets that could throw in phases of
- * their own (see dispatch.cpp).  Factories and transformers are created on
- * every shard with the same ids as one engine would assign.
- * srtp_dispatch_plan is the host-only split (no GPU needed): per packet its
- * shard (-1: handled without an engine) and phase; it returns the number of
- * phases.  kinds[t] = transformer t's kind, tag_mask bit T = some policy has
- * tag length T. */
+ * reproduces across shards by rolling back a throwing transformer's later
+ * packets and the contexts they touched (see dispatch.cpp): a bundle costs at
+ * most two runs per shard however many of its packets throw.  Factories and
+ * transformers are created on every shard with the same ids as one engine
+ * would assign.  srtp_dispatch_plan is the host-only split (no GPU needed):
+ * per packet its shard (-1: handled without an engine) and whether it could
+ * throw (may_throw, only with abort_on_error); it returns 2 if some packet
+ * could throw (the bundle needs context snapshots), else 1.  kinds[t] =
+ * transformer t's kind, tag_mask bit T = some policy has tag length T. */
 typedef struct srtp_dispatch srtp_dispatch;
 int32_t srtp_shard_of(uint32_t ssrc, int32_t n_shards);
 int32_t srtp_dispatch_plan(int32_t n_shards, int32_t abort_on_error, int32_t reverse,
                            const int32_t *kinds, int32_t n_transformers, uint32_t tag_mask,
                            const int32_t *tids, int32_t tid, const uint8_t *seg, size_t seg_bytes,
                            const uint32_t *off, const uint32_t *len, const uint32_t *cap,
-                           const uint32_t *flags, uint32_t n, int32_t *shard, int32_t *phase);
+                           const uint32_t *flags, uint32_t n, int32_t *shard, int32_t *may_throw);
 int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_engine_opts *opts,
                          srtp_dispatch **out);
 void srtp_dispatch_destroy(srtp_dispatch *d);
@@ -365,6 +400,19 @@ int srtp_dispatch_set_context_state(srtp_dispatch *d, int32_t transformer, uint3
                                     int32_t forward, const srtp_ctx_state *st);
 /* srtp_stats summed over the shards */
 int srtp_dispatch_stats(srtp_dispatch *d, srtp_stats *out);
+/* The shard a packet of transformer `tid` goes to (as srtp_dispatch_transform_host
+ * routes it: its SSRC's shard, shard 0 for a packet shorter than 12 bytes);
+ * -1 for an unknown transformer.  Does not wait for bundles in flight. */
+int32_t srtp_dispatch_route(srtp_dispatch *d, int32_t tid, const uint8_t *pkt, uint32_t len);
+/* The aggregator over a dispatcher: one lane per shard (its own pinned slots
+ * and dispatch thread); each packet goes to the lane of its shard, so
+ * per-packet submits from one process reach every GPU.  Callbacks of
+ * different shards run concurrently on the lanes' threads; the packets of
+ * one shard -- hence of one (transformer, SSRC) context -- and one direction
+ * complete in the order they were accepted.  opts apply per lane; every
+ * shard's engine must have abort_on_error = 0. */
+int srtp_aggregator_create_dispatch(srtp_dispatch *d, const srtp_aggregator_opts *opts,
+                                    srtp_aggregator_cb cb, void *user, srtp_aggregator **out);
 
 /* Control-plane crypto without a GPU (used by CPU-side tests): RFC 3711 4.3
  * session keys exactly as SRTPCryptoContext.deriveSrtpKeys (rtcp = 0) /

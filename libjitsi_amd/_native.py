@@ -20,12 +20,17 @@ NULL_AUTHENTICATION, HMACSHA1_AUTHENTICATION = 0, 1
 KIND_RTP, KIND_RTCP = 0, 1
 (STATUS_OK, STATUS_DROP_REPLAY, STATUS_DROP_AUTH, STATUS_DROP_VERSION, STATUS_DROP_NO_CONTEXT,
  STATUS_ERR_CAPACITY, STATUS_ERR_MALFORMED, STATUS_DROP_INVALID, STATUS_NOT_PROCESSED,
- STATUS_SKIPPED) = range(10)
+ STATUS_SKIPPED, STATUS_ERR_INTERNAL) = range(11)
 STATUS_NAMES = ["OK", "DROP_REPLAY", "DROP_AUTH", "DROP_VERSION", "DROP_NO_CONTEXT",
-                "ERR_CAPACITY", "ERR_MALFORMED", "DROP_INVALID", "NOT_PROCESSED", "SKIPPED"]
+                "ERR_CAPACITY", "ERR_MALFORMED", "DROP_INVALID", "NOT_PROCESSED", "SKIPPED",
+                "ERR_INTERNAL"]
+NUM_STATUS = len(STATUS_NAMES)
+DEBUG_FORCE_CHAIN_STALL = 0x1
+ABI_VERSION = 2
 PKT_FLAG_DISCARD, PKT_FLAG_SILENCE, PKT_FLAG_SKIP = 0x2, 0x4, 0x80000000
 RC = {0: "SRTP_OK", -1: "SRTP_EINVAL", -2: "SRTP_ENOMEM", -3: "SRTP_EFULL", -4: "SRTP_EDEVICE",
       -5: "SRTP_EPOLICY"}
+EFULL = -3
 
 EXPORTED = [
     "srtp_engine_opts_default", "srtp_engine_create", "srtp_engine_destroy",
@@ -47,6 +52,8 @@ EXPORTED = [
     "srtp_block_encrypt", "srtp_aggregator_opts_default", "srtp_aggregator_create",
     "srtp_aggregator_submit", "srtp_aggregator_flush", "srtp_aggregator_stats",
     "srtp_aggregator_destroy", "srtp_derive_session_keys_auth", "srtp_skein512_mac",
+    "srtp_engine_set_debug", "srtp_contexts_save", "srtp_contexts_restore",
+    "srtp_dispatch_route", "srtp_aggregator_create_dispatch",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -77,13 +84,13 @@ class CtxState(C.Structure):
 class Stats(C.Structure):
     """srtp_stats (include/srtp_mi355x.h)"""
     _fields_ = ([("bundles", C.c_uint64), ("packets", C.c_uint64),
-                 ("status", C.c_uint64 * 10)] +
+                 ("status", C.c_uint64 * NUM_STATUS)] +
                 [(n, C.c_uint64) for n in ("roc_rechecks", "repaired", "ctx_overflow", "ctx_live",
                                            "ctx_tombstones", "ctx_slots", "rehashes", "chain_stalls", "long_walked")])
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "status"}
-        d["status"] = {STATUS_NAMES[i]: int(self.status[i]) for i in range(10)}
+        d["status"] = {STATUS_NAMES[i]: int(self.status[i]) for i in range(NUM_STATUS)}
         return d
 
 
@@ -142,6 +149,7 @@ def lib() -> C.CDLL:
     L.srtp_engine_num_contexts.argtypes = [vp]
     L.srtp_engine_num_contexts.restype = C.c_int64
     L.srtp_engine_set_timing.argtypes = [vp, i32]
+    L.srtp_engine_set_debug.argtypes = [vp, u32]
     L.srtp_engine_read_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.srtp_derive_session_keys.argtypes = [pu8, pu8, i32, pu8, pu8, pu8]
     L.srtp_derive_session_keys_n.argtypes = [C.c_char_p, i32, C.c_char_p, i32, pu8, pu8, pu8]
@@ -151,6 +159,8 @@ def lib() -> C.CDLL:
     L.srtp_skein512_mac.argtypes = [C.c_char_p, i32, i32, C.c_char_p, C.c_size_t, pu8]
     L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
     L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
+    L.srtp_contexts_save.argtypes = [vp, u32, vp, vp, vp, vp]
+    L.srtp_contexts_restore.argtypes = [vp, u32, vp, vp, vp, vp]
     L.srtp_pipeline_create.argtypes = [vp, u32, C.c_size_t, i32, C.POINTER(vp)]
     L.srtp_pipeline_destroy.argtypes = [vp]
     L.srtp_pipeline_destroy.restype = None
@@ -161,6 +171,10 @@ def lib() -> C.CDLL:
     L.srtp_engine_get_opts.argtypes = [vp, C.POINTER(EngineOpts)]
     L.srtp_aggregator_opts_default.argtypes = [C.POINTER(AggregatorOpts)]
     L.srtp_aggregator_create.argtypes = [vp, C.POINTER(AggregatorOpts), AGG_CB, vp, C.POINTER(vp)]
+    L.srtp_aggregator_create_dispatch.argtypes = [vp, C.POINTER(AggregatorOpts), AGG_CB, vp,
+                                                   C.POINTER(vp)]
+    L.srtp_dispatch_route.argtypes = [vp, i32, C.c_char_p, u32]
+    L.srtp_dispatch_route.restype = i32
     L.srtp_aggregator_submit.argtypes = [vp, i32, i32, C.c_char_p, u32, u32, C.c_uint64]
     L.srtp_aggregator_flush.argtypes = [vp]
     L.srtp_aggregator_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),

@@ -15,17 +15,20 @@
 // cross-shard dependency is SinglePacketTransformer's rethrow
 // (SinglePacketTransformer.java:134-155,190-210): a packet that throws aborts
 // the later packets of the same transformer's array, on every shard.  The
-// host plan therefore marks every packet that could throw (a superset of the
-// engine's throws: RawPacket.getHeaderLength / SRTPCipherCTR.process /
-// RawPacket.getSRTCPIndex bounds, see may_throw) and cuts the bundle into
-// phases: phase 2k holds each transformer's packets after its k-th such
-// packet and before its (k+1)-th, phase 2k+1 the (k+1)-th itself.  Phases run
-// one after the other (transformers are independent, so packets of different
-// transformers may share a phase); a packet of phase 2k+1 that comes back
-// ERR_MALFORMED aborts its transformer: its later packets are never submitted
-// and get NOT_PROCESSED, exactly as one engine bundle would report them.
-// Without abort_on_error, or without any packet that could throw (the normal
-// case), the whole bundle is one phase.
+// whole bundle runs on every shard at once; when a packet of transformer t
+// came back ERR_MALFORMED, t's packets after the first such packet e_t (in
+// bundle order, over all shards) are rolled back: they get NOT_PROCESSED and
+// their original bytes and length, and every context they touched is reset to
+// its state before the bundle (srtp_contexts_save before the run,
+// srtp_contexts_restore after it; contexts they created are removed) and
+// then re-run with t's packets up to e_t -- which gives exactly the state one
+// engine leaves, because those packets see the same state and bytes as in the
+// first run.  Only transformers with a packet that could throw (a superset of
+// the engine's throws: RawPacket.getHeaderLength / SRTPCipherCTR.process /
+// RawPacket.getSRTCPIndex bounds, see may_throw) are snapshotted and stashed.
+// A bundle therefore costs at most two runs on each shard plus two context
+// copies, however many packets throw or could throw; without abort_on_error,
+// or without any packet that could throw (the normal case), one run.
 //
 // Data path per shard: a worker thread packs its packets into pinned slots of
 // an srtp_pipeline on its engine (H2D, kernels and D2H of consecutive chunks
@@ -41,6 +44,7 @@
 #include <thread>
 #include <vector>
 
+#include <stdint.h>
 #include <string.h>
 
 #include "../../include/srtp_mi355x.h"
@@ -90,27 +94,26 @@ bool cipher_may_throw(int32_t h, int32_t plen) {
 
 } // namespace
 
-// Plan of one bundle: the shard and phase of each packet (see the file
-// comment).  kinds[t] is transformer t's kind; tag_mask bit T is set when some
-// policy of the dispatcher has tag length T (0 for NULL authentication).
-// Packets that need no engine (SKIP flag, bad transformer id) get shard -1.
-// Returns the number of phases.
+// Plan of one bundle: the shard of each packet and whether it could throw
+// (see the file comment).  kinds[t] is transformer t's kind; tag_mask bit T
+// is set when some policy of the dispatcher has tag length T (0 for NULL
+// authentication).  Packets that need no engine (SKIP flag, bad transformer
+// id) get shard -1.  Returns 2 if some packet could throw, else 1.
 static int32_t plan_bundle(int32_t n_shards, int32_t abort_on_error, int32_t reverse,
                            const int32_t *kinds, int32_t n_transformers, uint32_t tag_mask,
                            const int32_t *tids, int32_t tid, const uint8_t *seg, const uint32_t *off,
                            const uint32_t *len, const uint32_t *cap, const uint32_t *flags, uint32_t n,
-                           int32_t *shard, int32_t *phase) {
+                           int32_t *shard, int32_t *may_throw) {
     int t_max = 0;
     for (int T = 0; T < 32; T++)
         if (tag_mask & (1u << T)) t_max = T;
-    std::vector<int32_t> rank((size_t)std::max(n_transformers, 1), 0);
-    int32_t n_phases = 1;
+    int32_t any = 0;
     for (uint32_t i = 0; i < n; i++) {
         const int32_t t = tids ? tids[i] : tid;
         const uint32_t fl = flags ? flags[i] : 0u;
+        may_throw[i] = 0;
         if ((fl & SRTP_PKT_FLAG_SKIP) || t < 0 || t >= n_transformers) {
             shard[i] = -1;
-            phase[i] = 0;
             continue;
         }
         const uint32_t L = len[i], C = cap[i];
@@ -139,20 +142,20 @@ static int32_t plan_bundle(int32_t n_shards, int32_t abort_on_error, int32_t rev
                 mt = (int32_t)L < 12 + t_max;
             }
         }
-        phase[i] = 2 * rank[t] + (mt ? 1 : 0);
-        if (mt) rank[t]++;
-        n_phases = std::max(n_phases, phase[i] + 1);
+        may_throw[i] = mt ? 1 : 0;
+        any |= may_throw[i];
     }
-    return n_phases;
+    return any ? 2 : 1;
 }
 
 struct srtp_dispatch {
     std::vector<srtp_engine *> engines;
     std::vector<srtp_pipeline *> pipes;
-    std::vector<int32_t> kinds;  // transformer kinds (replicated ids)
+    std::vector<int32_t> kinds;  // transformer kinds (replicated ids); written under mu and kmu
     uint32_t tag_mask = 0;
     int32_t abort_on_error = 1;
     std::mutex mu;
+    std::mutex kmu;              // kinds, for srtp_dispatch_route (which must not wait for a bundle)
     std::string last_error;
 
     // worker threads, one per shard
@@ -201,11 +204,12 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         if (!busy[k]) return;
         busy[k] = 0;
         const int rc = srtp_pipeline_wait(pl, k);
+        const std::vector<uint32_t> &ch = chunk_of[k];
         if (rc != SRTP_OK) {
             rc_all = rc;
+            for (uint32_t i : ch) d->b_status[i] = SRTP_STATUS_ERR_INTERNAL;
             return;
         }
-        const std::vector<uint32_t> &ch = chunk_of[k];
         for (size_t j = 0; j < ch.size(); j++) {
             const uint32_t i = ch[j];
             d->b_status[i] = sl[k].status[j];
@@ -236,13 +240,23 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             ch.push_back(i);
             pos++;
         }
-        if (ch.empty()) return SRTP_EINVAL; // a packet larger than a slot (cannot happen: cap <= 65535)
+        if (ch.empty()) { // a packet larger than a slot (cannot happen: cap <= 65535)
+            rc_all = SRTP_EINVAL;
+            break;
+        }
         const int rc = srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes);
-        if (rc != SRTP_OK) return rc;
+        if (rc != SRTP_OK) {
+            rc_all = rc;
+            for (uint32_t i : ch) d->b_status[i] = SRTP_STATUS_ERR_INTERNAL;
+            break;
+        }
         busy[k] = 1;
         k = (k + 1) % kDepth;
     }
+    // every chunk in flight comes back (its results are the caller's) even
+    // after an error; packets never submitted get an explicit status
     for (int q = 0; q < kDepth; q++) drain((k + q) % kDepth);
+    for (size_t q = pos; q < idx.size(); q++) d->b_status[idx[q]] = SRTP_STATUS_ERR_INTERNAL;
     return rc_all;
 }
 
@@ -314,19 +328,31 @@ int32_t srtp_shard_of(uint32_t ssrc, int32_t n_shards) {
     return n_shards > 0 ? (int32_t)(mix32(ssrc) % (uint32_t)n_shards) : -1;
 }
 
+int32_t srtp_dispatch_route(srtp_dispatch *d, int32_t tid, const uint8_t *pkt, uint32_t len) {
+    if (!d || (!pkt && len)) return -1;
+    int32_t kind;
+    {
+        std::lock_guard<std::mutex> kg(d->kmu);
+        if (tid < 0 || (size_t)tid >= d->kinds.size()) return -1;
+        kind = d->kinds[(size_t)tid];
+    }
+    if (len < 12) return 0; // RawPacket.isInvalid: shard 0 reports it (DROP_INVALID)
+    return (int32_t)(mix32(be32(pkt + (kind == SRTP_KIND_RTP ? 8 : 4))) % (uint32_t)d->engines.size());
+}
+
 int32_t srtp_dispatch_plan(int32_t n_shards, int32_t abort_on_error, int32_t reverse,
                            const int32_t *kinds, int32_t n_transformers, uint32_t tag_mask,
                            const int32_t *tids, int32_t tid, const uint8_t *seg, size_t seg_bytes,
                            const uint32_t *off, const uint32_t *len, const uint32_t *cap,
-                           const uint32_t *flags, uint32_t n, int32_t *shard, int32_t *phase) {
+                           const uint32_t *flags, uint32_t n, int32_t *shard, int32_t *may_throw) {
     if (n_shards < 1 || !kinds || n_transformers < 0 || (n && (!seg || !off || !len || !cap ||
-                                                               !shard || !phase)))
+                                                               !shard || !may_throw)))
         return SRTP_EINVAL;
     for (uint32_t i = 0; i < n; i++)
         if (off[i] % 16 != 0 || cap[i] > 65535u || (uint64_t)off[i] + region(cap[i]) > seg_bytes)
             return SRTP_EINVAL;
     return plan_bundle(n_shards, abort_on_error, reverse, kinds, n_transformers, tag_mask, tids, tid,
-                       seg, off, len, cap, flags, n, shard, phase);
+                       seg, off, len, cap, flags, n, shard, may_throw);
 }
 
 void srtp_dispatch_destroy(srtp_dispatch *d) {
@@ -422,6 +448,7 @@ int srtp_dispatch_transformer_create(srtp_dispatch *d, int32_t kind, int32_t fwd
         return srtp_transformer_create(e, kind, fwd, rev, x);
     }, &id);
     if (rc != SRTP_OK) return rc;
+    std::lock_guard<std::mutex> kg(d->kmu);
     if ((size_t)id >= d->kinds.size()) d->kinds.resize((size_t)id + 1, SRTP_KIND_RTP);
     d->kinds[(size_t)id] = kind;
     if (out) *out = id;
@@ -450,49 +477,128 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     if (!seg || !off || !len || !cap || !status) return dfail(d, SRTP_EINVAL, "null buffer");
     const int32_t nt = (int32_t)d->kinds.size();
     if (!tids && (tid < 0 || tid >= nt)) return dfail(d, SRTP_EINVAL, "bad transformer id");
-    std::vector<int32_t> shard(n), phase(n);
-    const int32_t n_phases = srtp_dispatch_plan((int32_t)d->engines.size(), d->abort_on_error, reverse,
-                                                d->kinds.data(), nt, d->tag_mask, tids, tid, seg,
-                                                seg_bytes, off, len, cap, flags, n, shard.data(),
-                                                phase.data());
-    if (n_phases < 0) return dfail(d, n_phases, "packet region outside the segment");
+    const size_t ns = d->engines.size();
+    std::vector<int32_t> shard(n), mt(n);
+    const int32_t plan = srtp_dispatch_plan((int32_t)ns, d->abort_on_error, reverse, d->kinds.data(), nt,
+                                            d->tag_mask, tids, tid, seg, seg_bytes, off, len, cap, flags,
+                                            n, shard.data(), mt.data());
+    if (plan < 0) return dfail(d, plan, "packet region outside the segment");
     d->b_tids = tids; d->b_tid = tid; d->b_seg = seg; d->b_off = off; d->b_len = len;
     d->b_cap = cap; d->b_flags = flags; d->b_status = status;
-    // packets grouped by phase (bundle order inside each)
-    std::vector<uint32_t> first((size_t)n_phases + 1, 0), by_phase(n);
-    for (uint32_t i = 0; i < n; i++) first[(size_t)phase[i] + 1]++;
-    for (int32_t ph = 0; ph < n_phases; ph++) first[(size_t)ph + 1] += first[(size_t)ph];
-    {
-        std::vector<uint32_t> fill(first.begin(), first.end() - 1);
-        for (uint32_t i = 0; i < n; i++) by_phase[fill[(size_t)phase[i]]++] = i;
+    auto tid_of = [&](uint32_t i) { return tids ? tids[i] : tid; };
+    std::vector<std::vector<uint32_t>> per_shard(ns);
+    for (uint32_t i = 0; i < n; i++) {
+        if (shard[i] < 0) status[i] = SRTP_STATUS_SKIPPED; // SKIP flag or no such transformer
+        else per_shard[(size_t)shard[i]].push_back(i);
     }
-    std::vector<char> aborted((size_t)std::max(nt, 1), 0);
-    std::vector<std::vector<uint32_t>> per_shard(d->engines.size());
-    std::vector<uint32_t> probes; // packets of an odd phase, for the abort check
-    int rc = SRTP_OK;
-    for (int32_t ph = 0; ph < n_phases && rc == SRTP_OK; ph++) {
-        for (auto &v : per_shard) v.clear();
-        probes.clear();
-        for (uint32_t q = first[(size_t)ph]; q < first[(size_t)ph + 1]; q++) {
-            const uint32_t i = by_phase[q];
-            if (shard[i] < 0) { // SKIP flag or no such transformer
-                status[i] = SRTP_STATUS_SKIPPED;
-                continue;
-            }
-            const int32_t t = tids ? tids[i] : tid;
-            if (aborted[(size_t)t]) { // an earlier packet of t threw
-                status[i] = SRTP_STATUS_NOT_PROCESSED;
-                continue;
-            }
-            per_shard[(size_t)shard[i]].push_back(i);
-            if (ph & 1) probes.push_back(i);
+    if (plan == 1) { // nothing can throw: one run
+        const int rc = run_phase(d, per_shard, reverse);
+        return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed");
+    }
+    // Transformers that could throw: their contexts in this bundle are
+    // snapshotted per shard and their packets' input bytes stashed.
+    std::vector<char> risky((size_t)nt, 0);
+    for (uint32_t i = 0; i < n; i++)
+        if (mt[i]) risky[(size_t)tid_of(i)] = 1;
+    auto valid = [&](uint32_t i) { return len[i] >= 12 && len[i] <= cap[i]; };
+    auto ssrc_of = [&](uint32_t i) {
+        return be32(seg + off[i] + (d->kinds[(size_t)tid_of(i)] == SRTP_KIND_RTP ? 8 : 4));
+    };
+    auto key_of = [&](uint32_t i) { return ((uint64_t)(uint32_t)tid_of(i) << 32) | ssrc_of(i); };
+    struct Snap {
+        std::vector<uint64_t> keys;
+        std::vector<srtp_ctx_raw> st;
+        std::vector<int32_t> present;
+    };
+    std::vector<Snap> snap(ns);
+    std::vector<uint8_t> stash;
+    std::vector<size_t> stash_at(n, SIZE_MAX);
+    std::vector<uint32_t> stash_len(n, 0);
+    for (size_t sh = 0; sh < ns; sh++) {
+        Snap &sn = snap[sh];
+        for (uint32_t i : per_shard[sh]) {
+            if (!risky[(size_t)tid_of(i)]) continue;
+            stash_at[i] = stash.size();
+            stash_len[i] = len[i];
+            stash.insert(stash.end(), seg + off[i], seg + off[i] + region(cap[i]));
+            if (valid(i)) sn.keys.push_back(key_of(i));
         }
-        rc = run_phase(d, per_shard, reverse);
-        for (uint32_t i : probes)
-            if (status[i] == SRTP_STATUS_ERR_MALFORMED) aborted[(size_t)(tids ? tids[i] : tid)] = 1;
+        std::sort(sn.keys.begin(), sn.keys.end());
+        sn.keys.erase(std::unique(sn.keys.begin(), sn.keys.end()), sn.keys.end());
+        if (sn.keys.empty()) continue;
+        std::vector<int32_t> kt(sn.keys.size());
+        std::vector<uint32_t> ks(sn.keys.size());
+        for (size_t q = 0; q < sn.keys.size(); q++) {
+            kt[q] = (int32_t)(sn.keys[q] >> 32);
+            ks[q] = (uint32_t)sn.keys[q];
+        }
+        sn.st.resize(sn.keys.size());
+        sn.present.resize(sn.keys.size());
+        const int rc = srtp_contexts_save(d->engines[sh], (uint32_t)kt.size(), kt.data(), ks.data(),
+                                          sn.st.data(), sn.present.data());
+        if (rc != SRTP_OK)
+            return dfail(d, rc, std::string("shard ") + std::to_string(sh) + ": " +
+                                    srtp_engine_last_error(d->engines[sh]));
     }
+    int rc = run_phase(d, per_shard, reverse);
     if (rc != SRTP_OK) return dfail(d, rc, "shard bundle failed");
-    return SRTP_OK;
+    // e_t: each risky transformer's first throw over all shards
+    std::vector<int64_t> e_first((size_t)nt, -1);
+    for (uint32_t i = 0; i < n; i++)
+        if (shard[i] >= 0 && status[i] == SRTP_STATUS_ERR_MALFORMED && e_first[(size_t)tid_of(i)] < 0)
+            e_first[(size_t)tid_of(i)] = i;
+    // Roll back t's packets after e_t; the contexts they touched are dirty.
+    std::vector<std::vector<uint64_t>> dirty(ns);
+    bool any_dirty = false;
+    for (uint32_t i = 0; i < n; i++) {
+        if (shard[i] < 0) continue;
+        const int64_t e = e_first[(size_t)tid_of(i)];
+        if (e < 0 || (int64_t)i <= e) continue;
+        if (status[i] != SRTP_STATUS_NOT_PROCESSED && valid(i)) {
+            dirty[(size_t)shard[i]].push_back(key_of(i));
+            any_dirty = true;
+        }
+        if (stash_at[i] == SIZE_MAX) return dfail(d, SRTP_EINVAL, "rollback: a throw the plan did not foresee");
+        status[i] = SRTP_STATUS_NOT_PROCESSED;
+        memcpy(seg + off[i], stash.data() + stash_at[i], region(cap[i]));
+        len[i] = stash_len[i];
+    }
+    if (!any_dirty) return SRTP_OK;
+    // Reset the dirty contexts, then re-run t's packets up to e_t on them.
+    std::vector<std::vector<uint32_t>> rerun(ns);
+    for (size_t sh = 0; sh < ns; sh++) {
+        std::vector<uint64_t> &dk = dirty[sh];
+        if (dk.empty()) continue;
+        std::sort(dk.begin(), dk.end());
+        dk.erase(std::unique(dk.begin(), dk.end()), dk.end());
+        const Snap &sn = snap[sh];
+        std::vector<int32_t> kt, pr;
+        std::vector<uint32_t> ks;
+        std::vector<srtp_ctx_raw> st;
+        for (uint64_t k : dk) {
+            const size_t q = (size_t)(std::lower_bound(sn.keys.begin(), sn.keys.end(), k) - sn.keys.begin());
+            if (q >= sn.keys.size() || sn.keys[q] != k) return dfail(d, SRTP_EINVAL, "rollback: context not in the snapshot");
+            kt.push_back((int32_t)(k >> 32));
+            ks.push_back((uint32_t)k);
+            st.push_back(sn.st[q]);
+            pr.push_back(sn.present[q]);
+        }
+        rc = srtp_contexts_restore(d->engines[sh], (uint32_t)kt.size(), kt.data(), ks.data(), st.data(),
+                                   pr.data());
+        if (rc != SRTP_OK)
+            return dfail(d, rc, std::string("shard ") + std::to_string(sh) + ": " +
+                                    srtp_engine_last_error(d->engines[sh]));
+        for (uint32_t i : per_shard[sh]) {
+            const int64_t e = e_first[(size_t)tid_of(i)];
+            if (e < 0 || (int64_t)i > e || !valid(i)) continue;
+            if (!std::binary_search(dk.begin(), dk.end(), key_of(i))) continue;
+            memcpy(seg + off[i], stash.data() + stash_at[i], region(cap[i]));
+            len[i] = stash_len[i];
+            rerun[sh].push_back(i);
+        }
+    }
+    rc = run_phase(d, rerun, reverse);
+    return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed (rollback re-run)");
 }
 
 int srtp_dispatch_get_context_state(srtp_dispatch *d, int32_t t, uint32_t ssrc, srtp_ctx_state *out) {

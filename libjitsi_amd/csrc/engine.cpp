@@ -85,6 +85,7 @@ struct srtp_engine {
 
     // optional per-stage timing (HIP events on the bundle stream)
     bool timing = false;
+    uint32_t dbg = 0;     // srtp_engine_set_debug test hooks
     struct Mark { int stage; hipEvent_t a, b; };
     std::vector<Mark> marks;
     std::vector<hipEvent_t> event_pool;
@@ -661,6 +662,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.serial = e->serial++;
     static const int debug_mode = getenv("SRTP_DEBUG") ? atoi(getenv("SRTP_DEBUG")) : 0;
     a.debug = debug_mode;
+    a.dbg = e->dbg;
     a.counters = e->d_counters;
 #ifdef SRTP_STAMPS
     if (!e->d_stamps[reverse ? 1 : 0])
@@ -933,6 +935,70 @@ int srtp_set_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, int32_t for
     return SRTP_OK;
 }
 
+// Snapshot / restore of (transformer, SSRC) contexts by key, on the device
+// (k_ctx_save / k_ctx_restore): one small kernel and two copies per call.
+static int contexts_io(srtp_engine *e, bool restore, uint32_t n, const int32_t *tids,
+                       const uint32_t *ssrcs, srtp_ctx_raw *out, const srtp_ctx_raw *in,
+                       int32_t *present_out, const int32_t *present_in) {
+    static_assert(sizeof(srtp_ctx_raw) == sizeof(CtxState), "srtp_ctx_raw holds one CtxState");
+    if (n == 0) return SRTP_OK;
+    std::vector<uint64_t> keys(n);
+    for (uint32_t i = 0; i < n; i++) keys[i] = ((uint64_t)(uint32_t)tids[i] << 32) | ssrcs[i];
+    GUARD(e);
+    int rc = quiesce(e);
+    if (rc != SRTP_OK) return rc;
+    uint64_t *d_keys = nullptr;
+    CtxState *d_st = nullptr;
+    int32_t *d_pr = nullptr;
+    unsigned int *d_fail = nullptr;
+    unsigned int failed = 0;
+    hipStream_t s = e->stream;
+    do {
+        if (dalloc(&d_keys, n) != hipSuccess || dalloc(&d_st, n) != hipSuccess ||
+            dalloc(&d_pr, n) != hipSuccess || dalloc(&d_fail, 1) != hipSuccess) {
+            rc = fail(e, SRTP_ENOMEM, "context snapshot scratch");
+            break;
+        }
+        bool ok = hipMemcpyAsync(d_keys, keys.data(), n * 8ull, hipMemcpyHostToDevice, s) == hipSuccess;
+        if (restore) {
+            ok = ok && hipMemcpyAsync(d_st, in, n * sizeof(CtxState), hipMemcpyHostToDevice, s) == hipSuccess &&
+                 hipMemcpyAsync(d_pr, present_in, n * 4ull, hipMemcpyHostToDevice, s) == hipSuccess &&
+                 hipMemsetAsync(d_fail, 0, 4, s) == hipSuccess &&
+                 launch_ctx_restore(e->d_ctx_keys, e->d_ctx, e->ctx_cap - 1, d_keys, n, d_st, d_pr, d_fail, s) ==
+                     hipSuccess &&
+                 hipMemcpyAsync(&failed, d_fail, 4, hipMemcpyDeviceToHost, s) == hipSuccess;
+        } else {
+            ok = ok && launch_ctx_save(e->d_ctx_keys, e->d_ctx, e->ctx_cap - 1, d_keys, n, d_st, d_pr, s) ==
+                           hipSuccess &&
+                 hipMemcpyAsync(out, d_st, n * sizeof(CtxState), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                 hipMemcpyAsync(present_out, d_pr, n * 4ull, hipMemcpyDeviceToHost, s) == hipSuccess;
+        }
+        if (!ok || hipStreamSynchronize(s) != hipSuccess) rc = fail(e, SRTP_EDEVICE, "context snapshot");
+        else if (failed) rc = fail(e, SRTP_EFULL, "context table full on restore");
+    } while (0);
+    if (d_st) (void)hipMemsetAsync(d_st, 0, n * sizeof(CtxState), s); // no key material is kept, but no state either
+    (void)hipStreamSynchronize(s);
+    dfree(d_keys);
+    dfree(d_st);
+    dfree(d_pr);
+    dfree(d_fail);
+    return rc;
+}
+
+int srtp_contexts_save(srtp_engine *e, uint32_t n, const int32_t *tids, const uint32_t *ssrcs,
+                       srtp_ctx_raw *out, int32_t *present) {
+    if (!e || (n && (!tids || !ssrcs || !out || !present))) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    return contexts_io(e, false, n, tids, ssrcs, out, nullptr, present, nullptr);
+}
+
+int srtp_contexts_restore(srtp_engine *e, uint32_t n, const int32_t *tids, const uint32_t *ssrcs,
+                          const srtp_ctx_raw *in, const int32_t *present) {
+    if (!e || (n && (!tids || !ssrcs || !in || !present))) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    return contexts_io(e, true, n, tids, ssrcs, nullptr, in, nullptr, present);
+}
+
 int64_t srtp_engine_num_contexts(srtp_engine *e) {
     if (!e) return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
@@ -969,6 +1035,13 @@ int srtp_engine_stats(srtp_engine *e, srtp_stats *out) {
     out->rehashes = e->n_rehash;
     out->chain_stalls = sum[kCtrChainStall];
     out->long_walked = sum[kCtrLongWalked];
+    return SRTP_OK;
+}
+
+int srtp_engine_set_debug(srtp_engine *e, uint32_t flags) {
+    if (!e || (flags & ~SRTP_DEBUG_FORCE_CHAIN_STALL)) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    e->dbg = flags;
     return SRTP_OK;
 }
 

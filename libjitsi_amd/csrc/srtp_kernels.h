@@ -44,6 +44,7 @@ struct BundleArgs {
     int32_t abort_on_error;
     uint32_t serial;       // bundle serial (context birth stamp)
     int32_t debug;         // diagnostics only (SRTP_DEBUG env): 0 in production
+    uint32_t dbg;          // kDbg* test hooks (srtp_engine_set_debug): 0 in production
     int32_t has_skein;     // the engine has Skein-MAC key sets (the walk's Skein re-check)
     unsigned long long *counters; // [kCountReplicas][kCtrStride] cumulative event counters
 #ifdef SRTP_STAMPS
@@ -104,6 +105,13 @@ hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 hipError_t launch_ext(const BundleArgs &a, hipStream_t s);
 hipError_t launch_remove_transformer(uint64_t *ctx_keys, CtxState *ctx, uint32_t cap,
                                      uint32_t tid, hipStream_t s);
+// Contexts by key (tid << 32 | ssrc): save -> out[i] / present[i]; restore ->
+// create or overwrite (present[i]) or remove (!present[i]); keys distinct.
+hipError_t launch_ctx_save(const uint64_t *tab, const CtxState *ctx, uint32_t mask, const uint64_t *keys,
+                           uint32_t n, CtxState *out, int32_t *present, hipStream_t s);
+hipError_t launch_ctx_restore(uint64_t *tab, CtxState *ctx, uint32_t mask, const uint64_t *keys, uint32_t n,
+                              const CtxState *in, const int32_t *present, unsigned int *failed,
+                              hipStream_t s);
 // out[0] += live contexts, out[1] += tombstones
 hipError_t launch_count_contexts(const uint64_t *ctx_keys, uint32_t cap, unsigned long long *out,
                                  hipStream_t s);

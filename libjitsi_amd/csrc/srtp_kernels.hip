@@ -1640,6 +1640,7 @@ struct ChainState {
     int32_t s_l;
     uint64_t window;
     bool broken;      // the speculation broke before (the rest is walk_long's)
+    bool stalled = false; // the look-back gave up: the part is left to the stall fix-up
 };
 
 __device__ __forceinline__ ChainState chain_apply(ChainState p, const ChainAgg &g) {
@@ -1705,6 +1706,12 @@ __device__ __forceinline__ ChainState chain_lookback(const BundleArgs &a, uint32
     const int lane = (int)(threadIdx.x & 63u);
     ChainAgg acc = {};     // the composed parts of the tiles after the current window
     bool have_acc = false;
+    if ((a.dbg & kDbgForceStall) && tile % 3u == 1u) { // test hook: give up at once
+        if (lane == 0) atomicAdd(&a.counters[kCtrChainStall], 1ull);
+        ChainState bad = {};
+        bad.broken = bad.stalled = true;
+        return bad;
+    }
     int32_t k0 = (int32_t)tile - 1;
     for (;;) {
         const int32_t k = k0 - lane;
@@ -1729,10 +1736,10 @@ __device__ __forceinline__ ChainState chain_lookback(const BundleArgs &a, uint32
             const int fp = pm ? __ffsll((long long)pm) - 1 : 64;
             const unsigned long long need = fp >= 63 ? ~0ull : ((2ull << fp) - 1ull);
             if ((dm & need) == need) break;
-            if (spin > (1u << 24)) { // never expected: report it and give up (results wrong, no hang)
+            if (spin > (1u << 24)) { // never expected: give up, the chain pass's last tile walks the part
                 if (lane == 0) atomicAdd(&a.counters[kCtrChainStall], 1ull);
                 ChainState bad = {};
-                bad.broken = true;
+                bad.broken = bad.stalled = true;
                 return bad;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -1927,6 +1934,7 @@ __device__ __forceinline__ ChainFix chain_part(const BundleArgs &a, uint32_t til
     if (head) {
         in.roc = (uint32_t)st0.a; in.s_l = st0.b; in.window = st0.window;
         in.broken = c.kind != SRTP_KIND_RTP || !(st0.flags & 1u);
+        in.stalled = false;
         g_in = (uint32_t)st0.g;
     } else {
         in = chain_lookback(a, tile, epoch);
@@ -1936,6 +1944,10 @@ __device__ __forceinline__ ChainFix chain_part(const BundleArgs &a, uint32_t til
         if (head) { // the whole chain goes to walk_long from its start
             fix.i0 = base + j0;
             fix.st = st0;
+        }
+        if (in.stalled && lane == 0) { // the fix-up walks the chain from this part on
+            gran_put(a.tile_link + (size_t)tile * kLinkWords + 9, epoch, base + j0);
+            atomicAdd(&a.ctl->n_stall, 1u);
         }
         if (out) chain_publish_state(a, tile, epoch, in);
         return fix;
@@ -1979,6 +1991,44 @@ __device__ __forceinline__ ChainFix chain_part(const BundleArgs &a, uint32_t til
     if (out) chain_publish_state(a, tile, epoch, st);
     else if (lane == 0) a.ctx[slot] = cs; // the chain ends in this tile
     return fix;
+}
+
+// The stall fix-up (run by the chain pass's last tile to finish, when some
+// tile's look-back gave up): the next tile from t on that left its part of a
+// chain unwalked (link word 9 = the part's first sorted record), with the
+// exact state the tile before it published -- every tile has finished, so it
+// is there.  walk_long then walks the chain from that record to its end,
+// exactly as after a speculation break; the tiles after the stalled one saw a
+// broken state and committed nothing.  A part whose predecessor's state is
+// itself broken is skipped: an earlier break or stall already hands that
+// chain's rest to walk_long.
+__device__ __forceinline__ ChainFix chain_stall_next(const BundleArgs &a, uint32_t epoch, uint32_t &t) {
+    ChainFix f;
+    f.i0 = kNoSlot;
+    for (; t < gridDim.x; t++) {
+        uint32_t i0 = 0u;
+        const bool st = gran_get(a.tile_link + (size_t)t * kLinkWords + 9, epoch, i0);
+        if (!__builtin_amdgcn_readfirstlane((int)st)) continue;
+        uint32_t v[4];
+        bool pr = true;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            pr &= gran_get(a.tile_link + (size_t)(t - 1u) * kLinkWords + 5 + i, epoch, v[i]);
+            v[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v[i]);
+        }
+        // not published would be a bug: the part stays unwalked (ERR_INTERNAL)
+        if (!__builtin_amdgcn_readfirstlane((int)pr) || (v[1] & 0x10000u)) continue;
+        i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i0);
+        f.st = a.ctx[a.sk_out[i0]];
+        f.st.a = (int32_t)v[0];
+        f.st.b = (int32_t)(v[1] & 0xffffu);
+        f.st.g = f.st.a;
+        f.st.window = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+        f.i0 = i0;
+        t++;
+        return f;
+    }
+    return f;
 }
 
 // One wave per workgroup owns the context segments that START among kWalkSpan
@@ -2129,9 +2179,37 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
         sm.g0 = REV ? s_g0 : s_start;
         sm.ok = REV ? s_ok : s_start;
         sm.info = s_start;
-        if (fix_in.i0 != kNoSlot) walk_long<REV, SK>(a, fix_in.i0, sm, fix_in.st);
-        if (fix_head.i0 != kNoSlot) walk_long<REV, SK>(a, fix_head.i0, sm, fix_head.st);
-
+        // One walk_long call site for the tile's two hand-overs and, in the
+        // last tile to finish, the stall fix-up's parts (chain_stall_next).
+        uint32_t t_fix = 1u;
+        bool fixup = false;
+#pragma unroll 1
+        for (int q = 0;; q++) {
+            ChainFix f;
+            if (q == 0) {
+                f = fix_in;
+            } else if (q == 1) {
+                f = fix_head;
+            } else {
+                if (q == 2) { // every tile counts itself done; the last one runs the fix-up
+                    uint32_t last = 0u;
+                    if (threadIdx.x == 0) {
+                        __threadfence();
+                        last = atomicAdd(&a.ctl->tiles_done, 1u) == gridDim.x - 1u ? 1u : 0u;
+                        if (last) {
+                            __threadfence();
+                            last = __hip_atomic_load(&a.ctl->n_stall, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) != 0u ? 1u : 0u;
+                        }
+                    }
+                    fixup = __builtin_amdgcn_readfirstlane((int)last) != 0;
+                }
+                if (!fixup) break;
+                f = chain_stall_next(a, epoch, t_fix);
+                if (f.i0 == kNoSlot) break;
+            }
+            if (f.i0 != kNoSlot) walk_long<REV, SK>(a, f.i0, sm, f.st);
+        }
         return;
     }
 #pragma unroll
@@ -2288,13 +2366,15 @@ __device__ __forceinline__ int32_t finish_status(const BundleArgs &a, uint32_t p
     // loads issued together, before the stores
     int32_t st = a.w_status[p];
     const uint32_t wl = a.w_len[p];
+    if (st == kStPending) st = SRTP_STATUS_ERR_INTERNAL; // a walked packet no walk reached: never expected
     const bool thrown = a.abort_on_error && a.ctl->any_throw;
     if (st != SRTP_STATUS_SKIPPED && thrown) {
         const int32_t tid = packet_tid(a, p);
         if ((int32_t)p > a.e_min[tid]) st = SRTP_STATUS_NOT_PROCESSED;
     }
     a.status[p] = st;
-    if (st != SRTP_STATUS_NOT_PROCESSED && st != SRTP_STATUS_SKIPPED) a.len[p] = wl;
+    if (st != SRTP_STATUS_NOT_PROCESSED && st != SRTP_STATUS_SKIPPED && st != SRTP_STATUS_ERR_INTERNAL)
+        a.len[p] = wl;
     return st;
 }
 
@@ -3486,6 +3566,49 @@ __global__ void k_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap
     }
 }
 
+// Context save / restore by key (srtp_contexts_save / _restore: the
+// dispatcher's rollback of a transformer whose packets ran past a throw on
+// another shard).  Restore keys are distinct, so concurrent inserts only race
+// with each other the way k_parse's do (ctx_lookup_insert).
+__global__ void k_ctx_save(const uint64_t *tab, const CtxState *ctx, uint32_t mask, const uint64_t *keys,
+                           uint32_t n, CtxState *out, int32_t *present) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t key = keys[i];
+    uint32_t h = (uint32_t)mix64(key) & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        const uint64_t cur = tab[h];
+        if (cur == key) {
+            out[i] = ctx[h];
+            present[i] = 1;
+            return;
+        }
+        if (cur == kEmptyKey) break;
+    }
+    out[i] = CtxState{};
+    present[i] = 0;
+}
+
+__global__ void k_ctx_restore(uint64_t *tab, CtxState *ctx, uint32_t mask, const uint64_t *keys, uint32_t n,
+                              const CtxState *in, const int32_t *present, unsigned int *failed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    BundleArgs a{};
+    a.ctx_keys = tab;
+    a.ctx = ctx;
+    a.ctx_mask = mask;
+    const CtxState st = in[i];
+    bool created = false;
+    const uint32_t slot = ctx_lookup_insert(a, keys[i], present[i] != 0, st.ks, &created);
+    if (present[i]) {
+        if (slot == kNoSlot) atomicAdd(failed, 1u);
+        else ctx[slot] = st;
+    } else if (slot != kNoSlot) {
+        __hip_atomic_store(&tab[slot], kTombKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ctx[slot] = CtxState{};
+    }
+}
+
 __global__ void k_count_contexts(const uint64_t *keys, uint32_t cap, unsigned long long *out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k = i < cap ? keys[i] : kEmptyKey;
@@ -3574,6 +3697,18 @@ hipError_t launch_ext(const BundleArgs &a, hipStream_t s) {
 hipError_t launch_remove_transformer(uint64_t *keys, CtxState *ctx, uint32_t cap, uint32_t tid,
                                      hipStream_t s) {
     hipLaunchKernelGGL(k_remove_transformer, grid_for(cap), dim3(kBlock), 0, s, keys, ctx, cap, tid);
+    return hipGetLastError();
+}
+hipError_t launch_ctx_save(const uint64_t *tab, const CtxState *ctx, uint32_t mask, const uint64_t *keys,
+                           uint32_t n, CtxState *out, int32_t *present, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctx_save, grid_for(n), dim3(kBlock), 0, s, tab, ctx, mask, keys, n, out, present);
+    return hipGetLastError();
+}
+hipError_t launch_ctx_restore(uint64_t *tab, CtxState *ctx, uint32_t mask, const uint64_t *keys, uint32_t n,
+                              const CtxState *in, const int32_t *present, unsigned int *failed,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_ctx_restore, grid_for(n), dim3(kBlock), 0, s, tab, ctx, mask, keys, n, in, present,
+                       failed);
     return hipGetLastError();
 }
 hipError_t launch_count_contexts(const uint64_t *keys, uint32_t cap, unsigned long long *out,

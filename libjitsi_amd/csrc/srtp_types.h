@@ -115,8 +115,13 @@ struct BundleCtl {
     uint32_t any_throw;   // some packet could make the reference throw -> two-pass walk
     uint32_t n_long;      // nonzero: the bundle has a context chain of >= kLongMin records
     uint32_t tile_ticket; // next walk tile of the chain pass
-    uint32_t pad;
+    uint32_t tiles_done;  // chain-pass tiles finished (the last one runs the stall fix-up)
+    uint32_t n_stall;     // chain-pass tiles whose look-back gave up (their parts left to the fix-up)
+    uint32_t pad[3];
 };
+
+// BundleArgs::dbg bits (srtp_engine_set_debug): test hooks, 0 in production
+constexpr uint32_t kDbgForceStall = 1u; // chain-pass tiles 1, 4, 7, ... give up their look-back at once
 
 // Cumulative per-engine event counters (srtp_engine_stats), 64-bit, kept in
 // kCountReplicas copies so that one bundle's wave-aggregated atomics spread
@@ -126,7 +131,8 @@ constexpr int kCtrStatus = 0;        // [0, 16): final status counts (SRTP_STATU
 constexpr int kCtrRocRecheck = 16;   // unprotect tags re-checked under a walk ROC != the speculation
 constexpr int kCtrRepaired = 17;     // packets k_unprotect_fix re-ciphered
 constexpr int kCtrOverflow = 18;     // packets refused a new context (table full)
-constexpr int kCtrChainStall = 19;   // walk tiles that gave up waiting on a long chain's look-back (a bug)
+constexpr int kCtrChainStall = 19;   // walk tiles that gave up waiting on a long chain's look-back
+                                     // (their chain is then walked by the fix-up; never expected)
 constexpr int kCtrLongWalked = 20;   // records walk_long walked one at a time (they broke the speculation)
 constexpr int kCtrStride = 32;       // u64 words per replica (one 256-B line)
 

@@ -10,8 +10,10 @@ their relative order inside a shard, which is all the per-context state
 machine depends on.
 
 ``plan`` calls the product's own split (``srtp_dispatch_plan``, C ABI, runs
-without a GPU): the shard of every packet and the phase that reproduces
-SinglePacketTransformer's abort-on-throw across shards.  ``split`` /
+without a GPU): the shard of every packet and whether it could throw, which
+decides the transformers whose contexts the dispatcher snapshots so that it
+can roll back their packets after a throw on another shard
+(SinglePacketTransformer's abort-on-throw, dispatch.cpp).  ``split`` /
 ``merge`` are the per-shard index lists and their inverse.
 """
 from __future__ import annotations
@@ -31,9 +33,11 @@ def shard_of_ssrc(ssrc: int, world: int) -> int:
 def plan(world: int, seg: np.ndarray, off: np.ndarray, length: np.ndarray, cap: np.ndarray,
          kinds: Sequence[int], tids=0, flags=None, reverse: bool = False,
          abort_on_error: bool = True, tag_lens: Sequence[int] = (10,)):
-    """(shard[n], phase[n], n_phases) of a bundle, as srtp_dispatch_transform_host
-    splits it.  ``tids`` is one transformer id or one per packet; ``kinds[t]``
-    is transformer t's kind; ``tag_lens`` the tag lengths of the policies in use."""
+    """(shard[n], may_throw[n], runs) of a bundle, as srtp_dispatch_transform_host
+    splits it (runs = 2 when some packet could throw: contexts are snapshotted
+    and a rollback re-run may follow).  ``tids`` is one transformer id or one
+    per packet; ``kinds[t]`` is transformer t's kind; ``tag_lens`` the tag
+    lengths of the policies in use."""
     n = len(off)
     seg = np.ascontiguousarray(seg, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
@@ -50,15 +54,15 @@ def plan(world: int, seg: np.ndarray, off: np.ndarray, length: np.ndarray, cap: 
     for t in tag_lens:
         mask |= 1 << int(t)
     shard = np.zeros(n, np.int32)
-    phase = np.zeros(n, np.int32)
+    may_throw = np.zeros(n, np.int32)
     rc = N.lib().srtp_dispatch_plan(int(world), int(abort_on_error), int(reverse),
                                     kinds_a.ctypes.data, len(kinds_a), mask, tids_p, tid0,
                                     seg.ctypes.data, seg.nbytes, off.ctypes.data,
                                     length.ctypes.data, cap.ctypes.data,
                                     None if fl is None else fl.ctypes.data, n,
-                                    shard.ctypes.data, phase.ctypes.data)
+                                    shard.ctypes.data, may_throw.ctypes.data)
     N.check(rc, None, "srtp_dispatch_plan")
-    return shard, phase, int(rc)
+    return shard, may_throw, int(rc)
 
 
 def split(shard: np.ndarray, world: int) -> List[np.ndarray]:

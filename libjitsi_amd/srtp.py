@@ -224,6 +224,10 @@ class SRTPEngine:
     def set_timing(self, enable: bool) -> None:
         N.check(N.lib().srtp_engine_set_timing(self.h, int(enable)), self.h, "set_timing")
 
+    def set_debug(self, flags: int) -> None:
+        """Test hooks (srtp_engine_set_debug), e.g. N.DEBUG_FORCE_CHAIN_STALL."""
+        N.check(N.lib().srtp_engine_set_debug(self.h, int(flags)), self.h, "set_debug")
+
     def read_timing(self) -> dict:
         """{stage: (total ms, bundles)} since the last read (HIP events)."""
         ms = (C.c_double * len(N.STAGES))()
@@ -455,14 +459,16 @@ class SRTPDispatcher:
 
 class SRTPAggregator:
     """Per-packet submits from many threads -> bundles (srtp_aggregator_*,
-    SURVEY.md 8f.2).  ``callback(cookie, status, data)`` runs on the
-    aggregator's dispatch thread once per packet, in bundle order; packets of
-    one direction complete in the order they were accepted.  The engine must
-    have abort_on_error=False: each packet is its own 1-element RawPacket[]
-    as in the reference's RTPConnector streams (RTPConnectorInputStream.java
+    SURVEY.md 8f.2).  ``callback(cookie, status, data)`` runs on a dispatch
+    thread once per packet, in bundle order; packets of one direction (and,
+    over a dispatcher, of one shard) complete in the order they were
+    accepted.  ``engine`` is an SRTPEngine or an SRTPDispatcher (one lane per
+    shard, srtp_aggregator_create_dispatch).  The engines must have
+    abort_on_error=False: each packet is its own 1-element RawPacket[] as in
+    the reference's RTPConnector streams (RTPConnectorInputStream.java
     :425-452, RTPConnectorOutputStream.java:268-300,652-830)."""
 
-    def __init__(self, engine: "SRTPEngine", callback, max_packets: int = 1 << 14,
+    def __init__(self, engine, callback, max_packets: int = 1 << 14,
                  max_bytes: int = 24 << 20, deadline_us: int = 1000, depth: int = 4):
         self.engine = engine
         o = N.AggregatorOpts(max_packets, max_bytes, deadline_us, depth)
@@ -472,18 +478,27 @@ class SRTPAggregator:
 
         self._cb = N.AGG_CB(_cb)  # kept alive with the aggregator
         h = C.c_void_p()
-        N.check(N.lib().srtp_aggregator_create(engine.h, C.byref(o), self._cb, None, C.byref(h)),
-                engine.h, "srtp_aggregator_create")
+        if isinstance(engine, SRTPDispatcher):
+            rc = N.lib().srtp_aggregator_create_dispatch(engine.h, C.byref(o), self._cb, None,
+                                                         C.byref(h))
+            N.check(rc, None, "srtp_aggregator_create_dispatch")
+        else:
+            N.check(N.lib().srtp_aggregator_create(engine.h, C.byref(o), self._cb, None, C.byref(h)),
+                    engine.h, "srtp_aggregator_create")
         self.h = h
 
     def submit(self, reverse: bool, transformer: "_SRTPBase", data: bytes, flags: int = 0,
-               cookie: int = 0) -> None:
+               cookie: int = 0) -> int:
+        """0, or N.EFULL for a submit from a callback that found no free slot."""
         data = bytes(data)
-        N.check(N.lib().srtp_aggregator_submit(self.h, int(reverse), transformer.tid, data,
-                                               len(data), flags, cookie), None, "submit")
+        rc = N.lib().srtp_aggregator_submit(self.h, int(reverse), transformer.tid, data, len(data),
+                                            flags, cookie)
+        if rc == N.EFULL:
+            return rc
+        return N.check(rc, None, "submit")
 
     def flush(self) -> None:
-        N.check(N.lib().srtp_aggregator_flush(self.h), self.engine.h, "flush")
+        N.check(N.lib().srtp_aggregator_flush(self.h), None, "flush")
 
     def stats(self) -> dict:
         a, c, b = C.c_uint64(), C.c_uint64(), C.c_uint64()

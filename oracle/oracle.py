@@ -78,6 +78,8 @@ def lib():
         L.orc_export_contexts.argtypes = [vp, u32p, C.POINTER(CtxState), C.c_uint32]
         L.orc_set_context_state.restype = C.c_int
         L.orc_set_context_state.argtypes = [vp, C.c_uint32, C.c_int, C.POINTER(CtxState)]
+        L.orc_remove_context.restype = C.c_int
+        L.orc_remove_context.argtypes = [vp, C.c_uint32]
         L.orc_aes128_encrypt_block.argtypes = [u8p, u8p, u8p]
         L.orc_hmac_sha1.argtypes = [u8p, C.c_int, u8p, C.c_size_t, u8p]
         L.orc_derive_keys.argtypes = [u8p, u8p, C.c_int, u8p, u8p, u8p]
@@ -251,6 +253,9 @@ class Transformer:
         st = CtxState(**{k: state.get(k, 0) for k, _ in CtxState._fields_})
         if lib().orc_set_context_state(self.h, ssrc & 0xFFFFFFFF, int(forward), C.byref(st)) != 0:
             raise ValueError("factory closed")
+
+    def remove_context(self, ssrc: int) -> bool:
+        return bool(lib().orc_remove_context(self.h, ssrc & 0xFFFFFFFF))
 
     def __del__(self):
         try:

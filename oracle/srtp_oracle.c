@@ -906,6 +906,34 @@ int orc_set_context_state(orc_transformer *t, uint32_t ssrc, int forward, const 
     return 0;
 }
 
+/* Removes the context for ssrc (backward-shift deletion keeps every probe
+ * path intact).  Returns 1 if there was one.  Test infrastructure: the
+ * sharded-dispatch rehearsal (tests/test_dispatch_dist.py) rolls contexts
+ * back to their state before a bundle, which may be "absent". */
+int orc_remove_context(orc_transformer *t, uint32_t ssrc) {
+    ctx_map *m = &t->map;
+    const uint32_t mask = m->cap - 1;
+    uint32_t i = mix32(ssrc) & mask;
+    for (;; i = (i + 1) & mask) {
+        if (!m->vals[i]) return 0;
+        if (m->keys[i] == ssrc) break;
+    }
+    ctx_free(m->vals[i]);
+    m->vals[i] = NULL;
+    m->count--;
+    for (uint32_t j = (i + 1) & mask; m->vals[j]; j = (j + 1) & mask) {
+        const uint32_t h = mix32(m->keys[j]) & mask;
+        /* entry j may move to the hole i unless its home h lies in (i, j] */
+        const int stays = i <= j ? (h > i && h <= j) : (h > i || h <= j);
+        if (stays) continue;
+        m->keys[i] = m->keys[j];
+        m->vals[i] = m->vals[j];
+        m->vals[j] = NULL;
+        i = j;
+    }
+    return 1;
+}
+
 /* RFC 5705 keying-material exporter (no context value) over the TLS PRF, via
  * OpenSSL's TLS1-PRF KDF: the checker for the engine's
  * srtp_tls_export_keying_material (what BouncyCastle's

@@ -117,6 +117,8 @@ uint32_t orc_num_contexts(orc_transformer *t);
  * private fields :96-135). */
 uint32_t orc_export_contexts(orc_transformer *t, uint32_t *ssrcs, orc_ctx_state *states, uint32_t max);
 int orc_set_context_state(orc_transformer *t, uint32_t ssrc, int forward, const orc_ctx_state *st);
+/* Remove the context for ssrc (1 if there was one). */
+int orc_remove_context(orc_transformer *t, uint32_t ssrc);
 
 /* Primitive helpers exposed for the KAT tests. */
 /* RFC 5705 exporter over the TLS PRF (OpenSSL TLS1-PRF KDF); prf 0 = TLS 1.0

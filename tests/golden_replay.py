@@ -62,7 +62,7 @@ def replay(path, backend_cls, **kw):
                 bad = np.nonzero(st != want_st)[0]
                 assert len(bad) == 0, (
                     f"{meta['name']} bundle {j}: status differs at {bad[:8].tolist()}: got "
-                    f"{[STATUS_NAMES[s] if 0 <= s < 10 else s for s in st[bad[:8]]]} want "
+                    f"{[STATUS_NAMES[s] if 0 <= s < len(STATUS_NAMES) else s for s in st[bad[:8]]]} want "
                     f"{[STATUS_NAMES[s] for s in want_st[bad[:8]]]}")
                 bad = np.nonzero(ln != z[p + "len_out"])[0]
                 assert len(bad) == 0, f"{meta['name']} bundle {j}: length differs at {bad[:8].tolist()}"

@@ -84,7 +84,7 @@ class Twin:
         assert len(bad) == 0, (
             f"status mismatch at {bad[:10].tolist()}: oracle "
             f"{[N.STATUS_NAMES[s] for s in st_o[bad[:10]]]} engine "
-            f"{[N.STATUS_NAMES[s] if 0 <= s < 10 else s for s in st_e[bad[:10]]]}")
+            f"{[N.STATUS_NAMES[s] if 0 <= s < N.NUM_STATUS else s for s in st_e[bad[:10]]]}")
         bad = np.nonzero(len_o != len_e)[0]
         assert len(bad) == 0, f"length mismatch at {bad[:10].tolist()}: {len_o[bad[:10]]} vs {len_e[bad[:10]]}"
         if not np.array_equal(seg_o, seg_e):

@@ -17,7 +17,7 @@ import time
 import numpy as np
 import pytest
 
-from libjitsi_amd import SRTPAggregator, profile_policies, synth
+from libjitsi_amd import SRTPAggregator, SRTPDispatcher, profile_policies, synth
 from libjitsi_amd import _native as N
 from oracle import oracle as O
 
@@ -69,19 +69,22 @@ def run_producers(agg, items, n_threads, reverse):
     agg.flush()
 
 
-def check_against_oracle(col, items, reverse, n_threads):
+def check_against_oracle(col, items, reverse, n_threads, lane_of=None):
+    """lane_of(item) -> shard, over a dispatcher: order holds per shard."""
     got = list(col.got)
     cookies = [c for c, _, _ in got]
     assert sorted(cookies) == list(range(len(items)))
     pos = {c: i for i, c in enumerate(cookies)}
-    for k in range(n_threads):  # each producer's packets complete in its order
-        mine = [pos[i] for i in range(k, len(items), n_threads)]
-        assert mine == sorted(mine)
+    for k in range(n_threads):  # each producer's packets complete in its order (per lane)
+        for lane in ({0} if lane_of is None else {lane_of(items[i]) for i in range(len(items))}):
+            mine = [pos[i] for i in range(k, len(items), n_threads)
+                    if lane_of is None or lane_of(items[i]) == lane]
+            assert mine == sorted(mine)
     outs = {}
     for c, st, data in got:  # the oracle, one packet at a time, in completion order
         t, inp, fl = items[c]
         st_o, out_o = oracle_one(t, reverse, inp, fl)
-        assert st == st_o, (c, N.STATUS_NAMES[st] if 0 <= st < 10 else st, N.STATUS_NAMES[st_o])
+        assert st == st_o, (c, N.STATUS_NAMES[st] if 0 <= st < N.NUM_STATUS else st, N.STATUS_NAMES[st_o])
         assert data == out_o, (c, len(data), len(out_o))
         outs[c] = (st, data)
     return outs
@@ -192,3 +195,115 @@ def test_refuses_abort_on_error_engine(engine_factory):
                        max_transformers=16)
     with pytest.raises(N.SrtpError):
         SRTPAggregator(E, lambda *a: None)
+
+
+def _lane_of(d):
+    def f(item):
+        t, data, _ = item
+        return N.lib().srtp_dispatch_route(d.h, t.tid, data, len(data))
+    return f
+
+
+def test_dispatch_lanes_concurrent_producers(oracle):
+    """The aggregator over a 4-shard dispatcher (srtp_aggregator_create_dispatch):
+    16 producer threads, 60 SSRCs of two transformers; every packet through
+    its shard's lane, each compared with the oracle as a 1-element array in
+    completion order, and each producer's packets of one shard complete in
+    its order."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    d = SRTPDispatcher([0] * 4, abort_on_error=False, max_contexts=4096, max_factories=64,
+                       max_transformers=64)
+    agg = None
+    try:
+        tw = Twin(d)
+        (k1, s1), (k2, s2) = synth.keys(81, 2)
+        A = tw.transformer(O.KIND_RTP, tw.factory(True, k1, s1, *P80))
+        B = tw.transformer(O.KIND_RTP, tw.factory(True, k2, s2, *P32))
+        ba = synth.rtp_bundle(1500, 40, (40, 1300), seed=82)
+        bb = synth.rtp_bundle(700, 20, (40, 600), seed=83)
+        # a random interleaving: streams are spread over producers and lanes
+        items = [None] * (ba.n + bb.n)
+        pa, pb = packets(ba), packets(bb)
+        order = np.random.default_rng(84).permutation(len(items))
+        srcs = [(A, x) for x in pa] + [(B, x) for x in pb]
+        for j, i in enumerate(order):
+            items[j] = (srcs[i][0], srcs[i][1], 0)
+        col = Collector()
+        agg = SRTPAggregator(d, col, max_packets=128, max_bytes=1 << 20, deadline_us=300, depth=4)
+        run_producers(agg, items, 16, False)
+        outs = check_against_oracle(col, items, False, 16, lane_of=_lane_of(d))
+        lanes = {_lane_of(d)(it) for it in items}
+        assert lanes == {0, 1, 2, 3}
+        assert sum(1 for st, _ in outs.values() if st == 0) > 0.9 * len(items)
+    finally:
+        if agg is not None:
+            agg.close()
+        d.close()
+
+
+@pytest.mark.parametrize("dispatch", [False, True], ids=["engine", "dispatch4"])
+def test_callback_forwards_packets(engine_factory, oracle, dispatch):
+    """An SFU's receive path: the callback of each unprotected packet submits
+    it again for protection toward another peer (from the aggregator's own
+    dispatch thread).  Such a submit never blocks (SRTP_EFULL when no slot is
+    free) and must not deadlock; every forwarded packet that was accepted
+    completes and matches the oracle."""
+    if dispatch:
+        import torch
+        if not torch.cuda.is_available():
+            pytest.skip("no GPU visible")
+        E = SRTPDispatcher([0] * 4, abort_on_error=False, max_contexts=4096, max_factories=64,
+                           max_transformers=64)
+    else:
+        E = engine_factory(abort_on_error=False, max_contexts=4096, max_factories=64,
+                           max_transformers=64)
+    agg = None
+    try:
+        tw = Twin(E)
+        (k1, s1), (k2, s2) = synth.keys(85, 2)
+        snd = tw.transformer(O.KIND_RTP, tw.factory(True, k1, s1, *P80))
+        rcv = tw.transformer(O.KIND_RTP, tw.factory(False, k1, s1, *P80))
+        fwd = tw.transformer(O.KIND_RTP, tw.factory(True, k2, s2, *P80))
+        b = synth.rtp_bundle(1200, 30, (60, 1000), seed=86)
+        seg, ln, st = tw.run(snd, False, b.seg, b.off, b.length, b.cap)
+        wire = [seg[b.off[i]:b.off[i] + ln[i]].tobytes() for i in range(b.n)]
+        got, lock, efull = [], threading.Lock(), [0]
+        F = 1 << 20
+
+        def cb(cookie, status, data):
+            with lock:
+                got.append((cookie, status, data))
+            if cookie < F and status == 0:
+                if agg.submit(False, fwd.e, data, cookie=F + cookie) == N.EFULL:
+                    with lock:
+                        efull[0] += 1
+
+        agg = SRTPAggregator(E, cb, max_packets=64, max_bytes=1 << 20, deadline_us=300, depth=6)
+        for i, x in enumerate(wire):
+            agg.submit(True, rcv.e, x, cookie=i)
+        t0 = time.time()
+        while True:  # forwarded packets are accepted while callbacks run
+            agg.flush()
+            s_ = agg.stats()
+            if s_["completed"] == s_["accepted"] or time.time() - t0 > 60:
+                break
+        assert agg.stats()["completed"] == agg.stats()["accepted"]
+        recv = [(c, st_, x) for c, st_, x in got if c < F]
+        sent = [(c - F, st_, x) for c, st_, x in got if c >= F]
+        assert sorted(c for c, _, _ in recv) == list(range(b.n))
+        for c, st_, x in recv:
+            st_o, out_o = oracle_one(rcv, True, wire[c])
+            assert st_ == st_o and x == out_o, c
+        assert len(sent) + efull[0] == sum(1 for _, st_, _ in recv if st_ == 0)
+        assert len(sent) > 0.5 * b.n
+        plain = {c: x for c, st_, x in recv}
+        for c, st_, x in sent:
+            st_o, out_o = oracle_one(fwd, False, plain[c])
+            assert st_ == st_o and x == out_o, c
+    finally:
+        if agg is not None:
+            agg.close()
+        if dispatch:
+            E.close()

@@ -2,15 +2,18 @@
 processing, with the product's own split.
 
 Each rank takes its shard of the same bundle from ``srtp_dispatch_plan`` (the
-C++ plan the in-process dispatcher runs, ``libjitsi_amd/csrc/dispatch.cpp``),
-and processes its packets phase by phase with its own transformers (the oracle
-stands in for the per-GPU engine).  Between phases the ranks exchange which
-transformers threw, as the dispatcher does between its shards, so that
-SinglePacketTransformer's abort-on-throw (SinglePacketTransformer.java:134-155,
-190-210) holds across shards.  Rank 0 checks the merged statuses, lengths and
-bytes against one oracle run of the whole bundle.  The bundle mixes two
-transformers, so one transformer's throw must stop only its own later
-packets."""
+C++ plan the in-process dispatcher runs, ``libjitsi_amd/csrc/dispatch.cpp``)
+and follows the dispatcher's abort-on-throw protocol with its own transformers
+(the oracle stands in for the per-GPU engine): snapshot the contexts of the
+transformers that could throw, run the whole shard, exchange each
+transformer's first throw (all_gather), roll back that transformer's later
+packets -- NOT_PROCESSED, original bytes -- and the contexts they touched,
+and re-run its earlier packets on those contexts.  That makes
+SinglePacketTransformer's abort-on-throw (SinglePacketTransformer.java
+:134-155,190-210) hold across shards.  Rank 0 checks the merged statuses,
+lengths and bytes against one oracle run of the whole bundle.  The bundle
+mixes two transformers, so one transformer's throw must stop only its own
+later packets."""
 import os
 import socket
 
@@ -75,21 +78,57 @@ def _process(O, ts, b, tids, idx, reverse, seg, ln, status):
 
 
 def _sharded(O, b, tids, reverse, seg, ln, rank, world, ts):
-    shard, phase, nph = dispatch.plan(world, seg, b.off, ln, b.cap, kinds=[0, 0], tids=tids,
-                                      reverse=reverse)
+    shard, may_throw, runs = dispatch.plan(world, seg, b.off, ln, b.cap, kinds=[0, 0], tids=tids,
+                                           reverse=reverse)
     status = np.full(b.n, NOT_PROCESSED, np.int32)
-    aborted = np.zeros(2, bool)
-    for ph in range(nph):
-        live = ~aborted[tids]
-        idx = np.nonzero((phase == ph) & (shard == rank) & live)[0]
-        _process(O, ts, b, tids, idx, reverse, seg, ln, status)
-        if ph & 1:  # probe phase: which transformers threw, on any rank
-            mine = sorted({int(tids[i]) for i in idx if status[i] == ERR_MALFORMED})
-            allt = [None] * world
-            dist.all_gather_object(allt, mine)
-            for lst in allt:
-                aborted[lst] = True
-    return status, shard, nph
+    mine = np.nonzero(shard == rank)[0]
+    risky = set(tids[may_throw == 1].tolist())
+    valid = (ln >= 12) & (ln <= b.cap)
+
+    def key(i):
+        o = int(b.off[i])
+        return int(tids[i]), int.from_bytes(seg[o + 8:o + 12].tobytes(), "big")
+
+    def tr(t):
+        return ts[t][1 if reverse else 0]
+
+    snap, stash = {}, {}
+    for i in mine:  # snapshot of the contexts that a rollback may reset
+        if int(tids[i]) in risky:
+            stash[i] = (seg[b.off[i]:b.off[i] + b.cap[i]].copy(), int(ln[i]))
+            if valid[i] and key(i) not in snap:
+                snap[key(i)] = tr(key(i)[0]).state(key(i)[1])
+    _process(O, ts, b, tids, mine, reverse, seg, ln, status)
+    first = {}
+    for i in mine:
+        if status[i] == ERR_MALFORMED and int(tids[i]) not in first:
+            first[int(tids[i])] = int(i)
+    allf = [None] * world
+    dist.all_gather_object(allf, first)
+    e_t = {}
+    for f in allf:
+        for t, i in f.items():
+            e_t[t] = min(i, e_t.get(t, i))
+    dirty = set()
+    for i in mine:  # roll back the packets after their transformer's first throw
+        e = e_t.get(int(tids[i]))
+        if e is None or i <= e:
+            continue
+        if status[i] != NOT_PROCESSED and valid[i]:
+            dirty.add(key(i))
+        status[i] = NOT_PROCESSED
+        seg[b.off[i]:b.off[i] + b.cap[i]], ln[i] = stash[i]
+    for t, ssrc in dirty:  # contexts back to their state before the bundle
+        if snap[(t, ssrc)] is None:
+            tr(t).remove_context(ssrc)
+        else:
+            tr(t).import_context(ssrc, snap[(t, ssrc)], forward=not reverse)
+    rerun = [i for i in mine if int(tids[i]) in e_t and i <= e_t[int(tids[i])] and valid[i]
+             and key(i) in dirty]
+    for i in rerun:
+        seg[b.off[i]:b.off[i] + b.cap[i]], ln[i] = stash[i]
+    _process(O, ts, b, tids, np.array(rerun, np.int64), reverse, seg, ln, status)
+    return status, shard, runs
 
 
 def _worker(rank, world, port, q):
@@ -99,7 +138,7 @@ def _worker(rank, world, port, q):
     b, tids = _bundle()
     ts = _transformers(O)
     seg, ln = b.seg.copy(), b.length.copy()
-    st1, shard, nph1 = _sharded(O, b, tids, False, seg, ln, rank, world, ts)
+    st1, shard, runs1 = _sharded(O, b, tids, False, seg, ln, rank, world, ts)
     hit = ((b.ssrc.astype(np.int64) + b.seq) % 13) == 0  # tamper a little on the wire
     seg[b.off[hit].astype(np.int64) + 30] ^= 1
     st2, _, _ = _sharded(O, b, tids, True, seg, ln, rank, world, ts)
@@ -126,7 +165,7 @@ def _worker(rank, world, port, q):
         ok = (np.array_equal(m1, r1) and np.array_equal(m2, r2) and np.array_equal(ml, l2)
               and pk == ref_pk and all(len(i) > 0 for i in idx)
               and (r1 == ERR_MALFORMED).sum() == 1 and (r1 == NOT_PROCESSED).sum() > 0
-              and nph1 > 1)
+              and runs1 == 2)
         q.put(bool(ok))
     dist.destroy_process_group()
 
@@ -155,13 +194,10 @@ def test_plan_is_stable_partition():
     for s in np.unique(b.ssrc):  # every SSRC lives on exactly one shard
         sh = set(shard[b.ssrc == s].tolist())
         assert sh == {dispatch.shard_of_ssrc(int(s), 3)}
-    # the two malformed packets of transformer 1 are its probe phases 1 and 3
-    assert nph == 5
-    assert phase[703] == 1 and phase[815] == 3
-    assert (phase[tids == 0] == 0).all()
-    t1 = np.nonzero(tids == 1)[0]
-    assert (phase[t1[t1 < 703]] == 0).all() and (phase[t1[(t1 > 703) & (t1 < 815)]] == 2).all()
-    # without abort-on-error there is a single phase
+    # the two malformed packets of transformer 1 are the ones that could throw
+    assert nph == 2
+    assert phase[703] == 1 and phase[815] == 1 and phase.sum() == 2
+    # without abort-on-error nothing needs a snapshot
     _, ph0, n0 = dispatch.plan(3, b.seg, b.off, b.length, b.cap, kinds=[0, 0], tids=tids,
                                abort_on_error=False)
     assert n0 == 1 and (ph0 == 0).all()

@@ -163,3 +163,54 @@ def test_dispatch_two_gpus_other_current_device(oracle):
             raise err[0]
     finally:
         d.close()
+
+
+def test_dispatch_many_throws_bounded_runs(oracle):
+    """200 packets that throw (or could: malformed headers, short SRTCP)
+    spread over 50 transformers interleaved on 4 shards, with abort-on-throw:
+    every bundle agrees with the oracle bit for bit, and the dispatcher runs
+    each shard at most twice per bundle (the whole bundle, then the rollback
+    re-run of the throwing transformers' earlier packets) -- the engines'
+    bundle counters bound the GPU round trips, however many packets throw
+    (SinglePacketTransformer.java:134-155,190-210)."""
+    if _gpus() < 1:
+        pytest.skip("no GPU visible")
+    shards = 4
+    d = SRTPDispatcher([0] * shards, max_contexts=1 << 14, max_factories=256, max_transformers=256)
+    try:
+        twin = Twin(d)
+        rng = np.random.default_rng(91)
+        (k, s), = synth.keys(90, 1)
+        f, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+        nt = 50
+        ts = [twin.transformer(O.KIND_RTP, f) for _ in range(nt)]
+        rs = [twin.transformer(O.KIND_RTP, fr) for _ in range(nt)]
+        b = synth.rtp_bundle(6000, 400, (40, 900), seed=92)
+        who = rng.integers(0, nt, b.n)
+        # SSRC i % 400 belongs to transformer who[...]: keep each SSRC on one transformer
+        who = who[np.arange(b.n) % 400]
+        o = b.off.astype(np.int64)
+        bad = rng.choice(np.arange(200, b.n), 200, replace=False)
+        for j, i in enumerate(bad):
+            if j % 2:
+                b.seg[o[i]] = 0x9F  # CC=15 with X: the header length runs past the packet
+            else:
+                b.seg[o[i]] = 0x8F  # CC=15: negative payload length on a short packet
+                b.length[i] = 40
+        n0 = d.stats()["bundles"]
+        seg, ln, st = twin.run([ts[w] for w in who], False, b.seg, b.off, b.length, b.cap)
+        n1 = d.stats()["bundles"]
+        assert (st == N.STATUS_ERR_MALFORMED).sum() >= 20 and (st == N.STATUS_NOT_PROCESSED).any()
+        assert n1 - n0 <= 2 * shards, (n1 - n0)
+        # receive side: the wire copy with the throws' transformers' traffic
+        twin.run([rs[w] for w in who], True, seg, b.off, ln, b.cap)
+        assert d.stats()["bundles"] - n1 <= 2 * shards
+        # SRTCP: short packets throw at the index offset before auth (50 transformers)
+        cts = [twin.transformer(O.KIND_RTCP, fr) for _ in range(nt)]
+        cb = synth.rtcp_bundle(3000, 200, len_range=(12, 60), seed=93)
+        cw = rng.integers(0, nt, cb.n)
+        n2 = d.stats()["bundles"]
+        twin.run([cts[w] for w in cw], True, cb.seg, cb.off, cb.length, cb.cap)
+        assert d.stats()["bundles"] - n2 <= 2 * shards
+    finally:
+        d.close()

@@ -188,7 +188,7 @@ def test_medium_chains(engine, seed):
     assert engine.stats()["long_walked"] > 0
 
 
-def chains_roundtrip(engine, rng, key_seed, lens, frac):
+def chains_roundtrip(engine, rng, key_seed, lens, frac, stalls_expected=False):
     twin = Twin(engine)
     (k, s), = synth.keys(key_seed, 1)
     fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
@@ -223,4 +223,48 @@ def chains_roundtrip(engine, rng, key_seed, lens, frac):
         keep[::97] = False
         fb = faults(synth.select(pb, np.nonzero(keep)[0]), rng, frac=frac)
         twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap)
-    assert engine.stats()["chain_stalls"] == 0
+    if not stalls_expected:
+        assert engine.stats()["chain_stalls"] == 0
+
+
+def test_forced_chain_stall_stays_exact(engine_factory, oracle):
+    """A chain-pass tile that gives up its look-back (a tile preempted for
+    seconds) leaves its part of the chain to the fix-up run by the last tile
+    to finish, which walks it from the exact state the tile before published.
+    The test hook makes every third tile give up at once; every bundle must
+    still match the oracle bit for bit, and the stall counter must show that
+    the fix-up ran.  Chains: one SSRC over many tiles with wraps, Zipf heads,
+    and chains around the tile size with faults."""
+    eng = engine_factory(max_contexts=1 << 15, max_factories=64, max_transformers=64,
+                         max_batch=1 << 17)
+    eng.set_debug(N.DEBUG_FORCE_CHAIN_STALL)
+    twin = Twin(eng)
+    (k, s), = synth.keys(501, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    b = synth.rtp_bundle(1 << 15, 1, (60, 300), seed=502, seq0=[50000])  # 128 tiles, one wrap
+    seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+    assert (st == 0).all()
+    pb = b.copy()
+    pb.seg, pb.length = seg, ln
+    fb = faults(pb, np.random.default_rng(503), frac=0.002)
+    _, _, st2 = twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap)
+    assert (st2 == 0).sum() > 0.99 * b.n
+    assert not (st2 == N.STATUS_ERR_INTERNAL).any()
+    zb = synth.rtp_bundle_skewed(1 << 16, 2000, (100, 600), seed=504, zipf_s=1.1)
+    zseg, zln, zst = twin.run(snd, False, zb.seg, zb.off, zb.length, zb.cap, check_state=False)
+    pz = zb.copy()
+    pz.seg, pz.length = zseg, zln
+    twin.run(rcv, True, pz.seg, pz.off, pz.length, pz.cap, check_state=False)
+    for ssrc in np.unique(zb.ssrc)[:300]:
+        for t in (snd, rcv):
+            so, se = t.o.state(int(ssrc)), eng.context_state(t.e, int(ssrc))
+            assert (so is None) == (se is None)
+            if so is not None:
+                for key in ("roc", "s_l", "seq_num_set", "guessed_roc", "replay_window"):
+                    assert int(so[key]) == int(se[key]), (hex(int(ssrc)), key, so, se)
+    rng = np.random.default_rng(505)
+    lens = [int(x) for x in rng.integers(250, 900, 10)] + [int(x) for x in rng.integers(1, 40, 20)]
+    chains_roundtrip(eng, rng, 506, lens, 0.003, stalls_expected=True)
+    assert eng.stats()["chain_stalls"] > 0
+    assert eng.stats()["status"]["ERR_INTERNAL"] == 0
