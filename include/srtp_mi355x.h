@@ -151,6 +151,10 @@ int srtp_transformer_create(srtp_engine *e, int32_t kind, int32_t fwd_factory,
 int srtp_transformer_set_factory(srtp_engine *e, int32_t transformer, int32_t factory,
                                  int32_t forward);
 int srtp_transformer_close(srtp_engine *e, int32_t transformer);
+/* The transformer's kind and its forward factory's SRTCP policy tag length
+ * (what RawPacket.grow sizes an SRTCP packet with, SRTCPCryptoContext.java:413). */
+int srtp_transformer_info(srtp_engine *e, int32_t transformer, int32_t *kind,
+                          int32_t *fwd_rtcp_tag_len);
 
 /* Process one bundle whose buffers are device (HBM) pointers on the engine's
  * device; asynchronous on `stream` (a hipStream_t of that device; NULL = its
@@ -413,6 +417,36 @@ int32_t srtp_dispatch_route(srtp_dispatch *d, int32_t tid, const uint8_t *pkt, u
  * shard's engine must have abort_on_error = 0. */
 int srtp_aggregator_create_dispatch(srtp_dispatch *d, const srtp_aggregator_opts *opts,
                                     srtp_aggregator_cb cb, void *user, srtp_aggregator **out);
+
+/* RawPacket[] marshalling for the Java drop-in (the JNI shim
+ * src/native/srtp_mi355x/ calls exactly this).  PacketTransformer.transform /
+ * reverseTransform(RawPacket[]) as SinglePacketTransformer.java:121-216 runs
+ * it: element i is bufs[i] (NULL: a null element, skipped) with the RawPacket's
+ * buffer length, offset, length and flags (SRTP_PKT_FLAG_SKIP: the packet
+ * predicate rejected it; FLAG_DISCARD / FLAG_SILENCE as RawPacket.getFlags).
+ * Packs the elements into a bundle of transformer tids[i] (tids == NULL: tid),
+ * runs it, and writes each result back into its buffer in place, as the
+ * reference leaves it: status[i] (drops: the caller replaces the element with
+ * null; the RawPacket keeps what was done to it -- e.g. the shrink of a failed
+ * tag check), length[i] updated.  need_len[i] != 0 where the reference
+ * allocates a new buffer -- RawPacket.append without room after the payload
+ * (RawPacket.java:203-220), and RawPacket.grow for every SRTCP protect
+ * (:885-893): the caller allocates need_len[i] bytes, copies the result from
+ * srtp_rawpacket_result to offset 0, and sets buffer / offset 0 / length.
+ * *thrown = the first element the reference throws on (SRTP_STATUS_ERR_MALFORMED;
+ * -1: none): every element was written back, the thrower keeps its partial
+ * mutation, its transformer's later packets are NOT_PROCESSED and untouched,
+ * and the caller rethrows.  A batch is the staging of one calling thread
+ * (pinned memory for an engine); results stay valid until its next call. */
+typedef struct srtp_rawpacket_batch srtp_rawpacket_batch;
+int srtp_rawpacket_batch_create(srtp_engine *e, srtp_rawpacket_batch **out);
+int srtp_rawpacket_batch_create_dispatch(srtp_dispatch *d, srtp_rawpacket_batch **out);
+void srtp_rawpacket_batch_destroy(srtp_rawpacket_batch *b);
+int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int32_t *tids, int32_t tid,
+                             uint8_t *const *bufs, const uint32_t *buf_len, const uint32_t *offset,
+                             uint32_t *length, const uint32_t *flags, int32_t *status,
+                             uint32_t *need_len, uint32_t n, int32_t *thrown);
+int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **data, uint32_t *len);
 
 /* Control-plane crypto without a GPU (used by CPU-side tests): RFC 3711 4.3
  * session keys exactly as SRTPCryptoContext.deriveSrtpKeys (rtcp = 0) /

@@ -53,7 +53,9 @@ EXPORTED = [
     "srtp_aggregator_submit", "srtp_aggregator_flush", "srtp_aggregator_stats",
     "srtp_aggregator_destroy", "srtp_derive_session_keys_auth", "srtp_skein512_mac",
     "srtp_engine_set_debug", "srtp_contexts_save", "srtp_contexts_restore",
-    "srtp_dispatch_route", "srtp_aggregator_create_dispatch",
+    "srtp_dispatch_route", "srtp_aggregator_create_dispatch", "srtp_transformer_info",
+    "srtp_rawpacket_batch_create", "srtp_rawpacket_batch_create_dispatch",
+    "srtp_rawpacket_batch_destroy", "srtp_rawpacket_transform", "srtp_rawpacket_result",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -160,6 +162,13 @@ def lib() -> C.CDLL:
     L.srtp_export_contexts.argtypes = [vp, i32, pu32, C.POINTER(CtxState), u32, pu32]
     L.srtp_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_contexts_save.argtypes = [vp, u32, vp, vp, vp, vp]
+    L.srtp_transformer_info.argtypes = [vp, i32, pi32, pi32]
+    L.srtp_rawpacket_batch_create.argtypes = [vp, C.POINTER(vp)]
+    L.srtp_rawpacket_batch_create_dispatch.argtypes = [vp, C.POINTER(vp)]
+    L.srtp_rawpacket_batch_destroy.argtypes = [vp]
+    L.srtp_rawpacket_batch_destroy.restype = None
+    L.srtp_rawpacket_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, u32, pi32]
+    L.srtp_rawpacket_result.argtypes = [vp, u32, C.POINTER(C.POINTER(C.c_uint8)), pu32]
     L.srtp_contexts_restore.argtypes = [vp, u32, vp, vp, vp, vp]
     L.srtp_pipeline_create.argtypes = [vp, u32, C.c_size_t, i32, C.POINTER(vp)]
     L.srtp_pipeline_destroy.argtypes = [vp]

@@ -34,6 +34,7 @@ struct srtp_engine {
     uint32_t n_keysets = 0, max_keysets = 0;
     FactoryRec *d_factories = nullptr;
     std::vector<FactoryRec> factories;
+    std::vector<int32_t> f_rtcp_tag; // per factory: its SRTCP policy's tag length (RawPacket.grow)
     TransformerRec *d_transformers = nullptr;
     std::vector<TransformerRec> transformers;
     uint64_t *d_ctx_keys = nullptr;
@@ -551,6 +552,7 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
     f.sender = sender;
     e->n_keysets += 2;
     e->factories.push_back(f);
+    e->f_rtcp_tag.push_back(srtcp_pol->auth_tag_len);
     int32_t id = (int32_t)e->factories.size() - 1;
     int rc = sync_factory(e, id);
     if (rc != SRTP_OK) return rc;
@@ -602,6 +604,16 @@ int srtp_transformer_set_factory(srtp_engine *e, int32_t t, int32_t f, int32_t f
     }
     slot = f;
     return sync_transformer(e, t);
+}
+
+int srtp_transformer_info(srtp_engine *e, int32_t t, int32_t *kind, int32_t *fwd_rtcp_tag_len) {
+    if (!e) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (t < 0 || (size_t)t >= e->transformers.size()) return fail(e, SRTP_EINVAL, "bad id");
+    const TransformerRec &tr = e->transformers[(size_t)t];
+    if (kind) *kind = tr.kind;
+    if (fwd_rtcp_tag_len) *fwd_rtcp_tag_len = tr.fwd >= 0 ? e->f_rtcp_tag[(size_t)tr.fwd] : 0;
+    return SRTP_OK;
 }
 
 int srtp_transformer_close(srtp_engine *e, int32_t t) {

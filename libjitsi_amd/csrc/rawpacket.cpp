@@ -1,0 +1,234 @@
+// rawpacket.cpp -- RawPacket[] marshalling for the Java drop-in.
+//
+// What a JNI shim under PacketTransformer.transform / reverseTransform(RawPacket[])
+// needs, in C: each element's buffer, offset, length and flags are packed
+// into a bundle segment, the bundle runs on the engine (or the multi-GPU
+// dispatcher), and the results are written back into the callers' buffers in
+// place -- exactly where the reference's per-packet calls leave them:
+//
+//   * SinglePacketTransformer.java:121-216: array order; a null element (or one
+//     the packet predicate rejects: SRTP_PKT_FLAG_SKIP) is not touched; a drop
+//     is reported so the caller can null the element; a throw is reported with
+//     the index of the first throwing element, after every packet was written
+//     back -- the earlier packets transformed, the thrower keeping the
+//     mutations made before its throw (e.g. authenticatePacket's shrink),
+//     its transformer's later packets untouched (NOT_PROCESSED);
+//   * RawPacket.append (RawPacket.java:203-220): SRTP protect appends the tag in
+//     place when the buffer has room after the payload, else into a new buffer
+//     of exactly length + tag at offset 0;
+//   * RawPacket.grow (:885-893): SRTCP protect always moves to a new buffer of
+//     length + 4 + tag at offset 0 (SRTCPCryptoContext.java:413);
+//   * RawPacket.shrink (:1284-1292): unprotect shrinks in place, also for a
+//     packet whose tag check fails.
+//
+// A new buffer cannot be allocated here (it is a Java byte[]): such an
+// element gets need_len[i] = the new buffer's length, its result stays in
+// the batch (srtp_rawpacket_result), and the shim allocates the array, copies
+// the result to offset 0 and sets buffer / offset = 0 / length.  Everything
+// else is written in place while the shim holds the arrays
+// (GetPrimitiveArrayCritical).  The Python mirror (libjitsi_amd/srtp.py
+// SRTPTransformer.transform) calls these same functions.
+#include <algorithm>
+#include <new>
+#include <string.h>
+#include <vector>
+
+#include "../../include/srtp_mi355x.h"
+
+struct srtp_rawpacket_batch {
+    srtp_engine *e = nullptr;   // engine mode: a pinned pipeline slot is the staging
+    srtp_dispatch *d = nullptr; // dispatch mode: host staging (the dispatcher pins per shard)
+    srtp_pipeline *pl = nullptr;
+    uint32_t pl_packets = 0;
+    size_t pl_bytes = 0;
+    std::vector<uint8_t> seg;   // dispatch-mode staging
+    std::vector<uint32_t> off, len, cap, flags;
+    std::vector<int32_t> tids, status;
+    // the current call's arrays (pipeline slot or the vectors above)
+    uint8_t *s_seg = nullptr;
+    uint32_t *s_off = nullptr, *s_len = nullptr, *s_cap = nullptr, *s_flags = nullptr;
+    int32_t *s_tids = nullptr, *s_status = nullptr;
+    uint32_t n = 0;
+};
+
+namespace {
+
+constexpr uint32_t kTrailerRoom = 16; // SRTCP E|index (4) + a 12-byte tag: the most protect appends
+
+size_t region(uint32_t cap) { return ((size_t)cap + 15) & ~(size_t)15; }
+
+srtp_engine *engine_of(const srtp_rawpacket_batch *b) {
+    return b->e ? b->e : srtp_dispatch_engine(b->d, 0);
+}
+
+// Staging for n packets / bytes: the pipeline slot (grown by recreating the
+// pipeline) or the host vectors.
+int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
+    if (b->e) {
+        if (!b->pl || n > b->pl_packets || bytes > b->pl_bytes) {
+            if (b->pl) srtp_pipeline_destroy(b->pl);
+            b->pl = nullptr;
+            const uint32_t np = std::max<uint32_t>(std::max<uint32_t>(n, 64), b->pl_packets * 2);
+            const size_t nb = std::max<size_t>(std::max<size_t>(bytes, (size_t)1 << 16), b->pl_bytes * 2);
+            const int rc = srtp_pipeline_create(b->e, np, nb, 1, &b->pl);
+            if (rc != SRTP_OK) return rc;
+            b->pl_packets = np;
+            b->pl_bytes = nb;
+        }
+        srtp_pipeline_slot sl;
+        const int rc = srtp_pipeline_slot_get(b->pl, 0, &sl);
+        if (rc != SRTP_OK) return rc;
+        b->s_seg = sl.seg; b->s_off = sl.off; b->s_len = sl.len; b->s_cap = sl.cap;
+        b->s_flags = sl.flags; b->s_tids = sl.tids; b->s_status = sl.status;
+    } else {
+        try {
+            b->seg.resize(std::max<size_t>(bytes, 16));
+            b->off.resize(n); b->len.resize(n); b->cap.resize(n); b->flags.resize(n);
+            b->tids.resize(n); b->status.resize(n);
+        } catch (...) {
+            return SRTP_ENOMEM;
+        }
+        b->s_seg = b->seg.data(); b->s_off = b->off.data(); b->s_len = b->len.data();
+        b->s_cap = b->cap.data(); b->s_flags = b->flags.data(); b->s_tids = b->tids.data();
+        b->s_status = b->status.data();
+    }
+    return SRTP_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int srtp_rawpacket_batch_create(srtp_engine *e, srtp_rawpacket_batch **out) {
+    if (!e || !out) return SRTP_EINVAL;
+    srtp_rawpacket_batch *b = new (std::nothrow) srtp_rawpacket_batch();
+    if (!b) return SRTP_ENOMEM;
+    b->e = e;
+    *out = b;
+    return SRTP_OK;
+}
+
+int srtp_rawpacket_batch_create_dispatch(srtp_dispatch *d, srtp_rawpacket_batch **out) {
+    if (!d || !out) return SRTP_EINVAL;
+    srtp_rawpacket_batch *b = new (std::nothrow) srtp_rawpacket_batch();
+    if (!b) return SRTP_ENOMEM;
+    b->d = d;
+    *out = b;
+    return SRTP_OK;
+}
+
+void srtp_rawpacket_batch_destroy(srtp_rawpacket_batch *b) {
+    if (!b) return;
+    if (b->pl) srtp_pipeline_destroy(b->pl);
+    delete b;
+}
+
+int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int32_t *tids, int32_t tid,
+                             uint8_t *const *bufs, const uint32_t *buf_len, const uint32_t *offset,
+                             uint32_t *length, const uint32_t *flags, int32_t *status,
+                             uint32_t *need_len, uint32_t n, int32_t *thrown) {
+    if (!b || (n && (!bufs || !buf_len || !offset || !length || !status || !need_len)) || !thrown)
+        return SRTP_EINVAL;
+    *thrown = -1;
+    b->n = 0;
+    if (n == 0) return SRTP_OK;
+    srtp_engine *eng = engine_of(b);
+    // Packing (the JNI shim's GetPrimitiveArrayCritical view of each buffer):
+    // region i holds the buffer's bytes from the packet's offset on, so the
+    // reference's reads past `length` (getHeaderLength's extension field,
+    // readRegionToBuff) see the same bytes; cap is the buffer's length after
+    // the offset (RawPacket.isInvalid compares against it), plus room for the
+    // trailer on protect -- the in-place form of append / grow.
+    std::vector<uint32_t> avail(n), ccap(n);
+    size_t bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const bool skip = !bufs[i] || (flags && (flags[i] & SRTP_PKT_FLAG_SKIP));
+        if (skip) {
+            avail[i] = 0;
+            ccap[i] = 16;
+        } else {
+            avail[i] = offset[i] <= buf_len[i] ? buf_len[i] - offset[i] : 0u;
+            const bool fits = length[i] <= avail[i];
+            uint64_t c = (fits && !reverse) ? std::max<uint64_t>(avail[i], (uint64_t)length[i] + kTrailerRoom)
+                                            : avail[i];
+            ccap[i] = (uint32_t)std::min<uint64_t>(c, 65535u);
+        }
+        bytes += region(ccap[i]);
+    }
+    int rc = stage(b, n, bytes);
+    if (rc != SRTP_OK) return rc;
+    size_t pos = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const bool skip = !bufs[i] || (flags && (flags[i] & SRTP_PKT_FLAG_SKIP));
+        const size_t r = region(ccap[i]);
+        b->s_off[i] = (uint32_t)pos;
+        b->s_cap[i] = ccap[i];
+        b->s_tids[i] = tids ? tids[i] : tid;
+        if (skip) {
+            b->s_len[i] = 0;
+            b->s_flags[i] = SRTP_PKT_FLAG_SKIP;
+            memset(b->s_seg + pos, 0, r);
+        } else {
+            b->s_len[i] = length[i];
+            b->s_flags[i] = flags ? (flags[i] & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) : 0u;
+            const size_t c = std::min<size_t>(avail[i], ccap[i]);
+            memcpy(b->s_seg + pos, bufs[i] + offset[i], c);
+            memset(b->s_seg + pos + c, 0, r - c);
+        }
+        pos += r;
+    }
+    if (b->e) {
+        rc = srtp_pipeline_submit(b->pl, 0, reverse, 1, -1, 1, n, pos);
+        if (rc == SRTP_OK) rc = srtp_pipeline_wait(b->pl, 0);
+    } else {
+        rc = srtp_dispatch_transform_host(b->d, reverse, b->s_tids, -1, b->s_seg, pos, b->s_off, b->s_len,
+                                          b->s_cap, b->s_flags, b->s_status, n);
+    }
+    if (rc != SRTP_OK) return rc;
+    b->n = n;
+    // Write-back (SinglePacketTransformer + RawPacket.append / grow / shrink).
+    int32_t info_tid = -1, kind = SRTP_KIND_RTP, rtcp_tag = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        need_len[i] = 0;
+        const int32_t st = b->s_status[i];
+        status[i] = st;
+        if (!bufs[i] || st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED) continue;
+        const uint8_t *res = b->s_seg + b->s_off[i];
+        const uint32_t old = length[i], nl = b->s_len[i];
+        if (!reverse && st == SRTP_STATUS_OK) {
+            const int32_t t = tids ? tids[i] : tid;
+            if (t != info_tid) {
+                rc = srtp_transformer_info(eng, t, &kind, &rtcp_tag);
+                if (rc != SRTP_OK) return rc;
+                info_tid = t;
+            }
+        }
+        if (!reverse && st == SRTP_STATUS_OK && (nl != old || kind == SRTP_KIND_RTCP)) {
+            // grow(4 + tag) then append(E|index, tag): a new buffer of exactly the
+            // new length; with NULL authentication nothing is appended and the
+            // buffer is length + 4 + the policy's tag length (the forward
+            // factory's SRTCP policy: a context kept across an SDES rekey with a
+            // different tag length is the one case this does not cover)
+            if (kind == SRTP_KIND_RTCP)
+                need_len[i] = nl != old ? nl : old + 4u + (uint32_t)rtcp_tag;
+            else if (nl > avail[i]) // append reallocates: exactly length + tag
+                need_len[i] = nl;
+            else
+                memcpy(bufs[i] + offset[i], res, nl);
+        } else {
+            memcpy(bufs[i] + offset[i], res, std::min(old, avail[i]));
+        }
+        length[i] = nl;
+        if (st == SRTP_STATUS_ERR_MALFORMED && *thrown < 0) *thrown = (int32_t)i;
+    }
+    return SRTP_OK;
+}
+
+int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **data, uint32_t *len) {
+    if (!b || !data || !len || i >= b->n) return SRTP_EINVAL;
+    *data = b->s_seg + b->s_off[i];
+    *len = b->s_len[i];
+    return SRTP_OK;
+}
+
+} // extern "C"

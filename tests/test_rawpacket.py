@@ -1,7 +1,8 @@
-"""GPU: the RawPacket[] marshalling a JNI shim mirrors (libjitsi_amd/srtp.py
-pack / _apply behind SRTPTransformer.transform / reverseTransform and
-transform_bundle), against the oracle on the same bytes and against the Java
-buffer rules:
+"""GPU: the RawPacket[] marshalling of the Java drop-in -- the C functions a
+JNI shim calls (srtp_rawpacket_transform, libjitsi_amd/csrc/rawpacket.cpp),
+driven through SRTPTransformer.transform / reverseTransform and
+transform_bundle on one engine and on a 3-shard dispatcher -- against the
+oracle on the same bytes and against the Java buffer rules:
 
 * SinglePacketTransformer.java:121-216 -- array order, null elements skipped,
   each element replaced by the result or null, the same array returned, a
@@ -21,6 +22,7 @@ import pytest
 
 from libjitsi_amd import (RawPacket, SRTCPTransformer, SRTPContextFactory, SRTPTransformer,
                           SRTPTransformException, pack, profile_policies, synth, transform_bundle)
+from libjitsi_amd.srtp import _rp_batch
 from libjitsi_amd import _native as N
 from oracle import oracle as O
 
@@ -31,9 +33,15 @@ P80 = profile_policies("AES_CM_128_HMAC_SHA1_80")
 RNG = np.random.default_rng(5150)
 
 
-@pytest.fixture(scope="module")
-def eng(engine_factory, oracle):
-    return engine_factory(max_contexts=4096, max_factories=256, max_transformers=256)
+@pytest.fixture(scope="module", params=["engine", "dispatch3"])
+def eng(request, engine_factory, oracle):
+    if request.param == "engine":
+        yield engine_factory(max_contexts=4096, max_factories=256, max_transformers=256)
+        return
+    from libjitsi_amd import SRTPDispatcher
+    d = SRTPDispatcher([0] * 3, max_contexts=4096, max_factories=256, max_transformers=256)
+    yield d
+    d.close()
 
 
 def rtp(seq, ssrc, L, b0=0x80, room=0, offset=0, cc_ext=None):
@@ -225,3 +233,70 @@ def test_transform_bundle_many_transformers_and_predicate(eng):
             assert p.length == 210
         else:
             assert snapshot(p) == raw[i]
+
+
+def test_c_marshalling_raw_abi(eng):
+    """srtp_rawpacket_transform called directly (as the JNI shim does), with
+    null elements, a predicate-skipped element, DISCARD / SILENCE flags, a
+    packet past its buffer (RawPacket.isInvalid), and an element whose
+    protect needs a new buffer: statuses, need_len, lengths and bytes against
+    the oracle run of the same RawPacket[]."""
+    import ctypes as C
+    (k, s), = synth.keys(506, 1)
+    snd = SRTPTransformer(SRTPContextFactory(True, k, s, *P80, engine=eng))
+    of = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+    ot = O.Transformer(O.KIND_RTP, of, of)
+    pkts = [rtp(40 + i, 0x5000 + i % 3, int(RNG.integers(40, 500)), room=(0 if i % 4 == 0 else 20),
+                offset=int(RNG.integers(0, 9))) for i in range(24)]
+    pkts[3] = None
+    pkts[9] = RawPacket(bytes(pkts[9].buffer), pkts[9].offset, len(pkts[9].buffer) + 5)  # invalid
+    skip = np.zeros(len(pkts), np.uint32)
+    skip[11] = N.PKT_FLAG_SKIP
+    pkts[14].flags = N.PKT_FLAG_DISCARD
+    ref = copy.deepcopy(pkts)
+    seg_o, off_o, ln_o, cap_o, fl_o = pack([None if skip[i] else p for i, p in enumerate(ref)])
+    st_o = O.process(ot, False, seg_o, off_o, ln_o, cap_o, fl_o)
+    n = len(pkts)
+    L = N.lib()
+    bufs = (C.c_void_p * n)()
+    views = []
+    buf_len = np.zeros(n, np.uint32)
+    offset = np.zeros(n, np.uint32)
+    length = np.zeros(n, np.uint32)
+    flags = skip.copy()
+    for i, p in enumerate(pkts):
+        if p is None:
+            continue
+        v = (C.c_char * len(p.buffer)).from_buffer(p.buffer)
+        views.append(v)
+        bufs[i] = C.addressof(v)
+        buf_len[i], offset[i], length[i] = len(p.buffer), p.offset, p.length
+        flags[i] |= p.flags
+    status = np.zeros(n, np.int32)
+    need = np.zeros(n, np.uint32)
+    thrown = C.c_int32(7)
+    before = [snapshot(p) for p in pkts]
+    rc = L.srtp_rawpacket_transform(_rp_batch(eng), 0, None, snd.tid, bufs, buf_len.ctypes.data,
+                                    offset.ctypes.data, length.ctypes.data, flags.ctypes.data,
+                                    status.ctypes.data, need.ctypes.data, n, C.byref(thrown))
+    del views
+    assert rc == 0 and thrown.value == -1
+    exp = st_o.copy()
+    exp[3] = N.STATUS_SKIPPED
+    assert status.tolist() == exp.tolist()
+    assert status[9] == N.STATUS_DROP_INVALID and status[11] == N.STATUS_SKIPPED
+    for i, p in enumerate(pkts):
+        if p is None or status[i] == N.STATUS_SKIPPED:
+            assert snapshot(p) == before[i]
+            continue
+        assert length[i] == ln_o[i]
+        want = seg_o[off_o[i]:off_o[i] + ln_o[i]].tobytes()
+        if need[i]:
+            assert need[i] == ln_o[i] and length[i] > buf_len[i] - offset[i]
+            data, dl = C.POINTER(C.c_uint8)(), C.c_uint32()
+            assert L.srtp_rawpacket_result(_rp_batch(eng), i, C.byref(data), C.byref(dl)) == 0
+            assert C.string_at(data, dl.value) == want
+            assert bytes(p.buffer) == before[i][0]  # the caller moves it to a new buffer
+        elif status[i] == 0:
+            assert bytes(p.buffer[p.offset:p.offset + length[i]]) == want
+    assert (need > 0).sum() >= 3
