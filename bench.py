@@ -18,9 +18,11 @@ step i = protect(i) then unprotect(i).
 Multi-GPU: one process per GPU (torchrun), contexts sharded by SSRC (each rank
 owns its own SSRCs), no collective on the data path ("scaling": "weak").
 Without torchrun, ``--gpus N`` drives N GPUs from this one process (the
-in-process dispatcher deployment: one engine pair per GPU, one host thread
-enqueueing on all of them).  value = packets protected AND unprotected by all
-GPUs / wall time (max over ranks).
+in-process deployment: one engine pair per GPU, each GPU's steps enqueued by a
+host thread of its own; ``SRTP_BENCH_ONE_DEVICE=1`` puts all N on device 0, a
+rehearsal on a one-GPU box).  value = packets protected AND unprotected by all
+GPUs / wall time (max over ranks).  The line also reports the host time spent
+enqueueing a step, per GPU.
 
 Also reported: the dominant kernel's roofline (HIP events on the bundle
 stream, algorithmic bytes L + (L+T) per packet), and a CPU baseline: the
@@ -65,6 +67,12 @@ def parse_args():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned-host end-to-end leg")
     ap.add_argument("--e2e-bundles", type=int, default=24)
+    ap.add_argument("--no-dispatch", action="store_true",
+                    help="skip the dispatcher leg (host bundles through srtp_dispatch_transform_host)")
+    ap.add_argument("--dispatch-shards", default="",
+                    help="comma-separated shard counts of the dispatcher leg (default: 1,2,4 on one "
+                         "GPU, else the GPU count)")
+    ap.add_argument("--dispatch-bundles", type=int, default=8)
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for the barrier/timing reduction (nccl = RCCL)")
     ap.add_argument("--serial", action="store_true",
@@ -124,69 +132,130 @@ def cpu_baseline(seconds: float, threads: int, L: int, nssrc: int, T: int):
         return o
 
     ref, tuned = obj("ref"), obj("tuned")
-    return {"value": ref["value"], "unit": "packets/s", "cores": threads, "kind": "port",
+    return {"value": ref["value"], "unit": "packets/s", "cores": threads, "threads": threads,
+            "kind": "port",
             "sample": f"oracle/oracle_bench.c pinned C loop, {threads} threads (the box's CPU "
                       f"share) and 1 thread, {seconds:.0f} s each: 4096-packet bundles of {L}-B "
                       f"RTP over {nssrc} SSRCs split across threads, protect then unprotect "
                       f"(reference call structure; 'tuned' = EVP AES-CTR per packet + pre-keyed "
                       f"HMAC)",
             "ref": ref, "tuned": tuned, **info,
-            "note": "per_core_x_physical_cores scales the 1-thread rate to every physical "
-                    "core of the host (an upper bound; this run may use only the box's share)"}
+            "note": "cores = threads used (min(16, the affinity set): the box's CPU share, not "
+                    "a count of physical cores); per_core_x_physical_cores is an extrapolation "
+                    "of the 1-thread rate to every physical core, not a measurement"}
 
 
-def e2e_leg(b, pols, keys, n, L, device, bundles, depth=3):
+class E2E:
     """End-to-end through PCIe (SURVEY.md 8d "end-to-end: pinned host buffers,
-    H2D + kernels + D2H"): the same workload's bundles held in pinned host
-    slots of an SRTPPipeline, each bundle copied to HBM, processed, copied
-    back.  Each slot alternates protect (sender) and unprotect (receiver) of
-    its bundle, so its content returns to the original RTP every two bundles;
-    the engine runs with checkReplay off (SRTPCryptoContext's config flag) so
-    the repeated sequence numbers are processed in full, not dropped.
-    Returns directional packets/s (one bundle = one direction) and PCIe GB/s."""
-    from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPPipeline, SRTPTransformer
-    eng = SRTPEngine(device=device, check_replay=False, max_contexts=1 << 15,
-                     max_factories=8, max_transformers=8, max_batch=n)
-    k, s = keys
-    snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=eng))
-    rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=eng))
-    nb = len(b.seg)
-    pl = SRTPPipeline(eng, max_packets=n, max_seg_bytes=nb, depth=depth)
-    for j in range(depth):
-        sl = pl.slot(j)
-        sl["seg"][:nb] = b.seg
-        sl["off"][:n] = b.off
-        sl["len"][:n] = b.length
-        sl["cap"][:n] = b.cap
-    use = [0] * depth
+    H2D + kernels + D2H") on one GPU: the same workload's bundles held in
+    pinned host slots of an SRTPPipeline, each bundle copied to HBM,
+    processed, copied back.  Each slot alternates protect (sender) and
+    unprotect (receiver) of its bundle, so its content returns to the original
+    RTP every two bundles; the engine runs with checkReplay off
+    (SRTPCryptoContext's config flag) so the repeated sequence numbers are
+    processed in full, not dropped.  Several GPUs run it at once (one E2E per
+    GPU, started together), which is the PCIe / host-memory bound scaling
+    curve of the north star's deployment."""
 
-    def submit(i):
-        j = i % depth
-        rev = use[j] % 2 == 1
-        pl.submit(j, rev, n, nb, tid=(rcv if rev else snd).tid)
-        use[j] += 1
+    def __init__(self, b, pols, keys, n, device, depth=3):
+        from libjitsi_amd import SRTPContextFactory, SRTPEngine, SRTPPipeline, SRTPTransformer
+        self.eng = SRTPEngine(device=device, check_replay=False, max_contexts=1 << 15,
+                              max_factories=8, max_transformers=8, max_batch=n)
+        k, s = keys
+        self.snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=self.eng))
+        self.rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=self.eng))
+        self.nb = nb = len(b.seg)
+        self.n, self.depth = n, depth
+        self.pl = SRTPPipeline(self.eng, max_packets=n, max_seg_bytes=nb, depth=depth)
+        for j in range(depth):
+            sl = self.pl.slot(j)
+            sl["seg"][:nb] = b.seg
+            sl["off"][:n] = b.off
+            sl["len"][:n] = b.length
+            sl["cap"][:n] = b.cap
+        self.use = [0] * depth
+        self.i = 0
 
-    warm = 2 * depth
-    for i in range(warm):
-        submit(i)
-    for j in range(depth):
-        pl.wait(j)
-    t0 = time.perf_counter()
-    for i in range(warm, warm + bundles):
-        submit(i)
-    for j in range(depth):
-        pl.wait(j)
-    dt = time.perf_counter() - t0
-    ok = all(int((pl.slot(j)["status"][:n] != 0).sum()) == 0 for j in range(depth))
-    pps = bundles * n / dt
-    pcie = bundles * 2 * nb / dt / 1e9
-    pl.close()
-    eng.close()
+    def _submit(self):
+        j = self.i % self.depth
+        rev = self.use[j] % 2 == 1
+        self.pl.submit(j, rev, self.n, self.nb, tid=(self.rcv if rev else self.snd).tid)
+        self.use[j] += 1
+        self.i += 1
+
+    def _drain(self):
+        for j in range(self.depth):
+            self.pl.wait(j)
+
+    def warm(self):
+        for _ in range(2 * self.depth):
+            self._submit()
+        self._drain()
+
+    def run(self, bundles):
+        """(seconds, packets, H2D + D2H bytes, all accepted) of `bundles` bundles."""
+        t0 = time.perf_counter()
+        for _ in range(bundles):
+            self._submit()
+        self._drain()
+        dt = time.perf_counter() - t0
+        ok = all(int((self.pl.slot(j)["status"][:self.n] != 0).sum()) == 0 for j in range(self.depth))
+        return dt, bundles * self.n, bundles * 2 * self.nb, ok
+
+    def close(self):
+        self.pl.close()
+        self.eng.close()
+
+
+def e2e_summary(dt, pkts, nbytes, ok, n_gpus, bundles, depth):
+    pps = pkts / dt
     return {"directional_pps": round(pps, 1), "round_trip_pps": round(pps / 2, 1),
-            "pcie_gbps_h2d_plus_d2h": round(pcie, 2), "bundles": bundles, "depth": depth,
-            "all_accepted": ok,
+            "pcie_gbps_h2d_plus_d2h": round(nbytes / dt / 1e9, 2), "bundles_per_gpu": bundles,
+            "depth": depth, "n_gpus": n_gpus, "all_accepted": ok,
             "note": "pinned host slots -> H2D -> protect or unprotect -> D2H, bundles of the "
-                    "same workload; checkReplay off so repeated bundles are processed in full"}
+                    "same workload, every GPU at once; checkReplay off so repeated bundles are "
+                    "processed in full; rates are whole-job (all GPUs)"}
+
+
+def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
+    """Host bundles through the in-process dispatcher (srtp_dispatch_transform_host):
+    the deployment path of one JVM driving every GPU.  For each shard count G
+    (devices_for(G) = the device of each shard), protect then unprotect the
+    same bundle (checkReplay off), and report packets/s per direction and the
+    dispatcher's host time per bundle: plan + split, packing into the shards'
+    pinned slots, waiting for the shards (H2D + kernels + D2H), scattering
+    back (the last three summed over the shards' worker threads)."""
+    from libjitsi_amd import SRTPContextFactory, SRTPDispatcher, SRTPTransformer
+    out = {}
+    for G in shard_counts:
+        d = SRTPDispatcher(devices_for(G), check_replay=False, max_contexts=1 << 15,
+                           max_factories=8, max_transformers=8)
+        try:
+            k, s = keys
+            snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=d))
+            rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=d))
+            seg, ln = b.seg.copy(), b.length.copy()
+            for _ in range(2):  # warm: both directions once
+                d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
+                d.transform_host(True, rcv.tid, seg, b.off, ln, b.cap)
+            h0 = d.host_times()
+            ok = True
+            t0 = time.perf_counter()
+            for _ in range(bundles):
+                st = d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
+                st2 = d.transform_host(True, rcv.tid, seg, b.off, ln, b.cap)
+                ok = ok and not st.any() and not st2.any()
+            dt = time.perf_counter() - t0
+            h1 = d.host_times()
+            calls = max(h1["calls"] - h0["calls"], 1)
+            per = {k2: round((h1[k2] - h0[k2]) / calls, 3) for k2 in h1 if k2 != "calls"}
+            out[str(G)] = {"directional_pps": round(2 * bundles * n / dt, 1),
+                           "ms_per_bundle": round(dt / (2 * bundles) * 1e3, 3),
+                           "host_ms_per_bundle": per, "all_accepted": bool(ok),
+                           "devices": sorted(set(devices_for(G)))}
+        finally:
+            d.close()
+    return out
 
 
 class Side:
@@ -235,6 +304,8 @@ class Side:
             self.end_a, self.end_b = torch.cuda.Event(), torch.cuda.Event()
             self.ev_b = [torch.cuda.Event() for _ in range(3)]  # receiver step ends (lag modes)
             self.ring = min(total + 1, RING)
+            # ring slot j is free again once the unprotect of its last bundle ran
+            self.ev_free = [torch.cuda.Event() for _ in range(self.ring)]
             self.pending = None  # join mode: protected bundle whose unprotect is due
             base = torch.from_numpy(b.seg).to(dev)
             len0 = torch.from_numpy(b.length.view(np.int32)).to(dev)
@@ -261,7 +332,8 @@ class Side:
 
     def protect(self, i, stream):
         j = i % self.ring
-        if i >= self.ring:  # reuse a staged bundle: its unprotect finished steps ago
+        if i >= self.ring:  # reuse a staged bundle once its unprotect has run
+            stream.wait_event(self.ev_free[j])
             with self.torch.cuda.stream(stream):
                 self.advance_seq(self.segs[j], self.ring)
         self.eng.transform_device(False, self.snd.tid, self.segs[j], self.off, self.lens[j],
@@ -271,6 +343,7 @@ class Side:
         j = i % self.ring
         self.eng_r.transform_device(True, self.rcv.tid, self.segs[j], self.off, self.lens[j],
                                     self.cap, self.st_r, stream=stream)
+        self.ev_free[j].record(stream)
 
     def step(self, i):
         """free: protect(i) on stream A, unprotect(i) on stream B after it; the
@@ -323,6 +396,59 @@ class Side:
     def bad(self):
         return int((self.st != 0).sum()) + int((self.st_r != 0).sum())
 
+    def engines(self):
+        return [self.eng] if self.eng_r is self.eng else [self.eng, self.eng_r]
+
+
+def status_counts(sides):
+    """(packets submitted, packets finished OK) over every engine of every GPU
+    (srtp_engine_stats), so that every step's statuses are checked, not only
+    the last one's."""
+    sub = ok = 0
+    for sd in sides:
+        for e in sd.engines():
+            st = e.stats()
+            sub += st["packets"]
+            ok += st["status"]["OK"]
+    return sub, ok
+
+
+def run_steps(torch, sides, g0, warmup, steps, barrier=None):
+    """Warmup then `steps` timed steps on every side.  One side: this thread.
+    Several (in-process mode): one host thread per GPU, started together
+    behind a barrier.  Returns (t_start, t_end, host seconds spent enqueueing
+    the timed steps, per side)."""
+    import threading
+
+    def body(i, sd, res):
+        torch.cuda.set_device(sd.dev)
+        for w in range(warmup):
+            sd.step(g0 + w)
+        torch.cuda.synchronize(sd.dev)
+        if barrier is not None:
+            barrier.wait()
+        t0 = time.perf_counter()
+        enq = 0.0
+        for k in range(steps):
+            a = time.perf_counter()
+            sd.step(g0 + warmup + k)
+            enq += time.perf_counter() - a
+        torch.cuda.synchronize(sd.dev)
+        res[i] = (t0, time.perf_counter(), enq)
+
+    res = [None] * len(sides)
+    if len(sides) == 1:
+        body(0, sides[0], res)
+    else:
+        bar = threading.Barrier(len(sides))
+        barrier = bar
+        th = [threading.Thread(target=body, args=(i, sd, res)) for i, sd in enumerate(sides)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    return min(r[0] for r in res), max(r[1] for r in res), [r[2] for r in res]
+
 
 def main():
     args = parse_args()
@@ -345,7 +471,9 @@ def main():
         devices = [local_rank]
         mode = "process"
     elif args.gpus > 1:
-        devices = list(range(args.gpus))  # in-process: this process drives every GPU
+        # in-process: this process drives every GPU (all on device 0 for a rehearsal)
+        one = os.environ.get("SRTP_BENCH_ONE_DEVICE") == "1"
+        devices = [0] * args.gpus if one else list(range(args.gpus))
         mode = "inproc"
     else:
         devices = [local_rank]
@@ -413,32 +541,27 @@ def main():
 
     # 2. Warmup, straight into the timed steps: no host work between them but
     # the synchronisation the timing needs (an idle GPU lowers its clocks, and
-    # the first steps after a gap run slow).
-    for _ in range(args.warmup):
-        for sd in sides:
-            sd.step(g)
-        g += 1
+    # the first steps after a gap run slow).  Every step's statuses are checked
+    # through the engines' counters (before / after), not only the last one's.
+    sub0, ok0 = status_counts(sides)
     if world > 1:
         dist.barrier()
     for sd in sides:
         torch.cuda.synchronize(sd.dev)
     if world > 1:
         dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        for sd in sides:
-            sd.step(g)
-        g += 1
-    for sd in sides:
-        torch.cuda.synchronize(sd.dev)
+    t_start, t_end, enq = run_steps(torch, sides, g, args.warmup, args.steps)
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    ok = ok and all(sd.bad() == 0 for sd in sides)
+    g += args.warmup + args.steps
+    dt = t_end - t_start
     for sd in sides:
         sd.finish()
+    sub1, ok1 = status_counts(sides)
+    ok = ok and sub1 - sub0 == ok1 - ok0 and sub1 > sub0
     ok = ok and all(sd.bad() == 0 and all(int((x != L).sum()) == 0 for x in sd.lens[:min(g, sd.ring)])
                     for sd in sides)
+    enqueue_us = [round(x / args.steps * 1e6, 1) for x in enq]
     t = torch.tensor([dt], dtype=torch.float64, device=sd0.dev)
     if world > 1:
         if args.backend != "nccl":
@@ -447,7 +570,7 @@ def main():
     dt_max = float(t.item())
     # slow-path work per bundle over the whole run (run-in, warmup, timed steps)
     slow = {"long_walked": 0, "repaired": 0, "roc_rechecks": 0, "bundles": 0}
-    for e in engines:
+    for e in engines:  # the first GPU's engines
         s = e.stats()
         for k in slow:
             slow[k] += s[k]
@@ -498,13 +621,63 @@ def main():
         share = args.cpu_threads or max(1, min(16, len(os.sched_getaffinity(0))))
         cpu = cpu_baseline(args.cpu_seconds, share, L, args.ssrcs, T)
 
+    # 3. The PCIe-inclusive legs (never `value`): every GPU's pinned pipeline at
+    # once, and the dispatcher's host-bundle path.
+    b0, keys0 = sd0.b, sd0.keys
+    del sides, sd0
+    torch.cuda.empty_cache()
     e2e = None
-    if rank == 0 and n_gpus == 1 and not args.no_e2e:
-        b = sd0.b
-        keys = sd0.keys
-        del sides, sd0
-        torch.cuda.empty_cache()
-        e2e = e2e_leg(b, pols, keys, n, L, devices[0], args.e2e_bundles)
+    if not args.no_e2e:
+        legs = [E2E(b0, pols, keys0, n, d) for d in devices]
+        for x in legs:
+            x.warm()
+        if world > 1:
+            dist.barrier()
+        if len(legs) == 1:
+            res = [legs[0].run(args.e2e_bundles)]
+        else:
+            import threading
+            res = [None] * len(legs)
+            bar = threading.Barrier(len(legs))
+
+            def e2e_body(i):
+                torch.cuda.set_device(devices[i])
+                bar.wait()
+                res[i] = legs[i].run(args.e2e_bundles)
+            th = [threading.Thread(target=e2e_body, args=(i,)) for i in range(len(legs))]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+        e_dt = max(r[0] for r in res)
+        e_pk = sum(r[1] for r in res)
+        e_by = sum(r[2] for r in res)
+        e_ok = all(r[3] for r in res)
+        if world > 1:
+            v = torch.tensor([e_dt, -float(e_ok)], dtype=torch.float64, device=devices[0])
+            w = torch.tensor([e_pk, e_by], dtype=torch.float64, device=devices[0])
+            if args.backend != "nccl":
+                v, w = v.cpu(), w.cpu()
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            dist.all_reduce(w, op=dist.ReduceOp.SUM)
+            e_dt, e_ok = float(v[0]), float(v[1]) < 0
+            e_pk, e_by = float(w[0]), float(w[1])
+        for x in legs:
+            x.close()
+        e2e = e2e_summary(e_dt, e_pk, e_by, e_ok, n_gpus, args.e2e_bundles, legs[0].depth)
+    disp = None
+    if rank == 0 and not args.no_dispatch and world == 1:
+        if args.dispatch_shards:
+            counts = [int(x) for x in args.dispatch_shards.split(",")]
+        else:
+            counts = [1, 2, 4] if len(devices) == 1 else [len(devices)]
+        if len(devices) == 1:
+            def devs_for(G):
+                return [devices[0]] * G
+        else:
+            def devs_for(G):
+                return [devices[i % len(devices)] for i in range(G)]
+        disp = dispatch_leg(b0, pols, keys0, n, devs_for, counts, args.dispatch_bundles)
 
     if rank == 0:
         line = {
@@ -537,10 +710,12 @@ def main():
             "all_accepted": ok,
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
             "slow_path_per_bundle": slow_per_bundle,
+            "host_enqueue_us_per_step": enqueue_us,
             "roofline": dominant,
             "roofline_other": other[0] if other else None,
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "dispatch": disp,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

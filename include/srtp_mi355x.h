@@ -404,6 +404,12 @@ int srtp_dispatch_set_context_state(srtp_dispatch *d, int32_t transformer, uint3
                                     int32_t forward, const srtp_ctx_state *st);
 /* srtp_stats summed over the shards */
 int srtp_dispatch_stats(srtp_dispatch *d, srtp_stats *out);
+/* Host time of srtp_dispatch_transform_host since creation, in ns: [0] plan
+ * and split, [1] packing into the shards' pinned slots, [2] waiting for the
+ * shards' bundles (H2D + kernels + D2H), [3] scattering results back (1-3
+ * summed over the shards' worker threads), [4] wall time of the calls, [5]
+ * number of calls. */
+int srtp_dispatch_host_times(srtp_dispatch *d, uint64_t ns[6]);
 /* The shard a packet of transformer `tid` goes to (as srtp_dispatch_transform_host
  * routes it: its SSRC's shard, shard 0 for a packet shorter than 12 bytes);
  * -1 for an unknown transformer.  Does not wait for bundles in flight. */

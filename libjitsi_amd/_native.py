@@ -56,6 +56,7 @@ EXPORTED = [
     "srtp_dispatch_route", "srtp_aggregator_create_dispatch", "srtp_transformer_info",
     "srtp_rawpacket_batch_create", "srtp_rawpacket_batch_create_dispatch",
     "srtp_rawpacket_batch_destroy", "srtp_rawpacket_transform", "srtp_rawpacket_result",
+    "srtp_dispatch_host_times",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -221,6 +222,7 @@ def lib() -> C.CDLL:
     L.srtp_dispatch_get_context_state.argtypes = [vp, i32, u32, C.POINTER(CtxState)]
     L.srtp_dispatch_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_dispatch_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.srtp_dispatch_host_times.argtypes = [vp, C.POINTER(C.c_uint64)]
     _lib = L
     return L
 

@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -156,6 +158,8 @@ struct srtp_dispatch {
     int32_t abort_on_error = 1;
     std::mutex mu;
     std::mutex kmu;              // kinds, for srtp_dispatch_route (which must not wait for a bundle)
+    // host time per phase of a bundle, summed over shards (srtp_dispatch_host_times)
+    std::atomic<uint64_t> t_plan{0}, t_pack{0}, t_wait{0}, t_scatter{0}, t_total{0}, n_calls{0};
     std::string last_error;
 
     // worker threads, one per shard
@@ -182,6 +186,11 @@ struct srtp_dispatch {
 
 namespace {
 
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int dfail(srtp_dispatch *d, int code, const std::string &msg) {
     d->last_error = msg;
     return code;
@@ -203,7 +212,10 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
     auto drain = [&](int k) {
         if (!busy[k]) return;
         busy[k] = 0;
+        const uint64_t tw = now_ns();
         const int rc = srtp_pipeline_wait(pl, k);
+        const uint64_t ts = now_ns();
+        d->t_wait += ts - tw;
         const std::vector<uint32_t> &ch = chunk_of[k];
         if (rc != SRTP_OK) {
             rc_all = rc;
@@ -216,6 +228,7 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             d->b_len[i] = sl[k].len[j];
             memcpy(d->b_seg + d->b_off[i], sl[k].seg + sl[k].off[j], region(d->b_cap[i]));
         }
+        d->t_scatter += now_ns() - ts;
     };
     size_t pos = 0;
     int k = 0;
@@ -225,6 +238,7 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         std::vector<uint32_t> &ch = chunk_of[k];
         ch.clear();
         size_t bytes = 0;
+        const uint64_t tp = now_ns();
         while (pos < idx.size() && ch.size() < sl[k].max_packets) {
             const uint32_t i = idx[pos];
             const size_t r = region(d->b_cap[i]);
@@ -240,6 +254,7 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             ch.push_back(i);
             pos++;
         }
+        d->t_pack += now_ns() - tp;
         if (ch.empty()) { // a packet larger than a slot (cannot happen: cap <= 65535)
             rc_all = SRTP_EINVAL;
             break;
@@ -475,6 +490,15 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     std::lock_guard<std::mutex> g(d->mu);
     if (n == 0) return SRTP_OK;
     if (!seg || !off || !len || !cap || !status) return dfail(d, SRTP_EINVAL, "null buffer");
+    const uint64_t t0 = now_ns();
+    struct Done { // the call's total host time, however it returns
+        srtp_dispatch *d;
+        uint64_t t0;
+        ~Done() {
+            d->t_total += now_ns() - t0;
+            d->n_calls++;
+        }
+    } done{d, t0};
     const int32_t nt = (int32_t)d->kinds.size();
     if (!tids && (tid < 0 || tid >= nt)) return dfail(d, SRTP_EINVAL, "bad transformer id");
     const size_t ns = d->engines.size();
@@ -491,6 +515,7 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
         if (shard[i] < 0) status[i] = SRTP_STATUS_SKIPPED; // SKIP flag or no such transformer
         else per_shard[(size_t)shard[i]].push_back(i);
     }
+    d->t_plan += now_ns() - t0;
     if (plan == 1) { // nothing can throw: one run
         const int rc = run_phase(d, per_shard, reverse);
         return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed");
@@ -599,6 +624,13 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     }
     rc = run_phase(d, rerun, reverse);
     return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed (rollback re-run)");
+}
+
+int srtp_dispatch_host_times(srtp_dispatch *d, uint64_t ns[6]) {
+    if (!d || !ns) return SRTP_EINVAL;
+    ns[0] = d->t_plan; ns[1] = d->t_pack; ns[2] = d->t_wait; ns[3] = d->t_scatter;
+    ns[4] = d->t_total; ns[5] = d->n_calls;
+    return SRTP_OK;
 }
 
 int srtp_dispatch_get_context_state(srtp_dispatch *d, int32_t t, uint32_t ssrc, srtp_ctx_state *out) {

@@ -397,6 +397,15 @@ class SRTPDispatcher:
         self._chk(N.lib().srtp_dispatch_stats(self.h, C.byref(st)), "stats")
         return st.as_dict()
 
+    def host_times(self) -> dict:
+        """srtp_dispatch_host_times in ms (plan, pack, wait, scatter, total) and calls."""
+        ns = (C.c_uint64 * 6)()
+        self._chk(N.lib().srtp_dispatch_host_times(self.h, ns), "host_times")
+        d = {k: ns[i] / 1e6 for i, k in enumerate(("plan_ms", "pack_ms", "wait_ms", "scatter_ms",
+                                                    "total_ms"))}
+        d["calls"] = int(ns[5])
+        return d
+
     def context_state(self, transformer: "_SRTPBase", ssrc: int) -> Optional[dict]:
         st = N.CtxState()
         rc = self._chk(N.lib().srtp_dispatch_get_context_state(self.h, transformer.tid,
