@@ -525,7 +525,10 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     std::vector<char> risky((size_t)nt, 0);
     for (uint32_t i = 0; i < n; i++)
         if (mt[i]) risky[(size_t)tid_of(i)] = 1;
-    auto valid = [&](uint32_t i) { return len[i] >= 12 && len[i] <= cap[i]; };
+    // RawPacket.isInvalid of the packet as handed in (the lengths change in the run)
+    std::vector<char> valid0(n);
+    for (uint32_t i = 0; i < n; i++) valid0[i] = len[i] >= 12 && len[i] <= cap[i];
+    auto valid = [&](uint32_t i) { return valid0[i] != 0; };
     auto ssrc_of = [&](uint32_t i) {
         return be32(seg + off[i] + (d->kinds[(size_t)tid_of(i)] == SRTP_KIND_RTP ? 8 : 4));
     };
