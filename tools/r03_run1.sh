@@ -20,4 +20,5 @@ t c5 600 $PT -x -v -s tests/test_config5_sharded.py --timeout 550
 t gpu 900 $PT -q tests -m gpu --deselect tests/test_config5_sharded.py
 t bench 600 python bench.py
 SRTP_BENCH_ONE_DEVICE=1 t bench_inproc2 600 python bench.py --gpus 2 --steps 20 --no-cpu
+t split 120 ./tools/split_bench 20
 echo done
