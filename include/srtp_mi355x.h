@@ -332,7 +332,10 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
  * aggregator's lock (producers only serialise on reserving its place).
  * Callbacks may submit (e.g. forward a received packet), but a submit made
  * from a callback never blocks: it returns SRTP_EFULL when no slot is free,
- * since only the dispatch threads free slots.  flush from a callback returns
+ * since only the dispatch threads free slots.  Producers outside callbacks
+ * leave one slot of each lane (depth - 1 usable) for callback submits, so the
+ * callbacks of a completed bundle can forward all of its packets unless they
+ * outgrow max_bytes.  flush from a callback returns
  * SRTP_EINVAL and destroy from a callback does nothing. */
 typedef struct srtp_aggregator srtp_aggregator;
 typedef struct {

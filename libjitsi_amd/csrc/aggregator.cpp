@@ -27,7 +27,13 @@
 // callback may submit (an SFU forwarding what it just received), but such a
 // submit never waits for a free slot -- only the dispatch threads free slots,
 // so waiting could deadlock -- and returns SRTP_EFULL instead; flush and
-// destroy from a callback return SRTP_EINVAL.
+// destroy from a callback return SRTP_EINVAL.  So that callbacks rarely see
+// SRTP_EFULL, producers leave one slot of each lane free: only a callback's
+// submit opens a lane's last free slot.  A bundle holds at most max_packets
+// packets, so the callbacks of one completed bundle can forward all of its
+// packets (a bundle's worth fits the reserved slot, and the completed slot
+// restores the reserve once its callbacks have run) unless the forwarded
+// packets outgrow max_bytes.
 //
 // Per-packet semantics: each submitted packet is its own 1-element
 // RawPacket[] in the reference, so one packet's exception must not stop
@@ -105,10 +111,16 @@ void seal_locked(srtp_aggregator *a, Lane &ln, int dir) {
     (void)a;
 }
 
-int free_slot_locked(Lane &ln) {
+// a free slot of the lane; producers (not in a callback) only take one when
+// another stays free for callbacks
+int free_slot_locked(Lane &ln, bool in_cb) {
+    int first = -1, n_free = 0;
     for (size_t i = 0; i < ln.slots.size(); i++)
-        if (ln.slots[i].state == kFree) return (int)i;
-    return -1;
+        if (ln.slots[i].state == kFree) {
+            if (first < 0) first = (int)i;
+            n_free++;
+        }
+    return (in_cb ? n_free >= 1 : n_free >= 2) ? first : -1;
 }
 
 void lane_loop(srtp_aggregator *a, Lane *ln) {
@@ -289,7 +301,7 @@ int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, con
             if (sl.n < a->opts.max_packets && sl.bytes + need <= a->opts.max_bytes) break;
             seal_locked(a, ln, dir);
         }
-        s = free_slot_locked(ln);
+        s = free_slot_locked(ln, in_cb);
         if (s >= 0) {
             Slot &sl = ln.slots[(size_t)s];
             sl.state = kOpen;

@@ -297,7 +297,9 @@ def test_callback_forwards_packets(engine_factory, oracle, dispatch):
             st_o, out_o = oracle_one(rcv, True, wire[c])
             assert st_ == st_o and x == out_o, c
         assert len(sent) + efull[0] == sum(1 for _, st_, _ in recv if st_ == 0)
-        assert len(sent) > 0.5 * b.n
+        # a lane keeps a slot free for callback submits, and a forwarded
+        # bundle fits it (64 packets, far below max_bytes): none is refused
+        assert efull[0] == 0 and len(sent) > 0.9 * b.n
         plain = {c: x for c, st_, x in recv}
         for c, st_, x in sent:
             st_o, out_o = oracle_one(fwd, False, plain[c])

@@ -127,7 +127,7 @@ def test_stats_count_every_status_and_overflow(engine_factory, oracle):
         rb.seg[rb.off[j]:rb.off[j] + rb.cap[j]] = seg[b.off[i]:b.off[i] + b.cap[i]]
     rb.length = ln[np.r_[0:b.n, 0:300]].copy()
     _, _, st2 = twin.run(rcv, True, rb.seg, rb.off, rb.length, rb.cap)
-    want = np.bincount(np.concatenate([st, st2]), minlength=10)
+    want = np.bincount(np.concatenate([st, st2]), minlength=N.NUM_STATUS)
     got = eng.stats()
     assert [got["status"][n] for n in N.STATUS_NAMES] == want.tolist()
     assert got["bundles"] == 2 and got["packets"] == b.n + rb.n
