@@ -20,26 +20,26 @@
 // bundle order -- so packets of one lane (one shard, hence one context) and
 // one direction complete in the order they were accepted.
 //
-// Concurrency.  A submit reserves its packet's place (slot, index, bytes)
-// under the aggregator's lock and copies the packet outside it; a sealed
-// slot is handed to the engine only when the copies into it have finished
-// (Slot::writers).  Callbacks run on the lanes' dispatch threads.  A
-// callback may submit (an SFU forwarding what it just received), but such a
-// submit never waits for a free slot -- only the dispatch threads free slots,
-// so waiting could deadlock -- and returns SRTP_EFULL instead; flush and
-// destroy from a callback return SRTP_EINVAL.  So that callbacks rarely see
-// SRTP_EFULL, producers leave one slot of each lane free: only a callback's
-// submit opens a lane's last free slot.  A bundle holds at most max_packets
-// packets, so the callbacks of one completed bundle can forward all of its
-// packets (a bundle's worth fits the reserved slot, and the completed slot
-// restores the reserve once its callbacks have run) unless the forwarded
-// packets outgrow max_bytes.
+// Concurrency.  A submit reserves its packet's place (index, bytes) in the
+// open slot of its lane and direction with one compare-and-swap on a packed
+// reservation word -- no lock -- and copies the packet; only opening,
+// sealing and freeing slots take the aggregator's lock (once per bundle, not
+// per packet).  A sealed slot is handed to the engine once every reserved
+// copy into it has finished (Slot::done == n).  Callbacks run on the lanes'
+// dispatch threads.  A callback may submit (an SFU forwarding what it just
+// received); such a submit never waits for a slot -- only the dispatch
+// threads free slots, so waiting could deadlock.  When no slot is free it
+// parks a copy of the packet in the lane's overflow queue, which the lane's
+// thread moves into the first slot it frees, ahead of other producers, so a
+// forwarded packet is never refused.  flush and destroy from a callback
+// return SRTP_EINVAL.
 //
 // Per-packet semantics: each submitted packet is its own 1-element
 // RawPacket[] in the reference, so one packet's exception must not stop
 // later packets of the same transformer in the bundle.  The engines therefore
 // run with abort_on_error = 0 (creation refuses otherwise); a packet the
 // reference would throw on completes with SRTP_STATUS_ERR_MALFORMED.
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -56,24 +56,45 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 enum SlotState { kFree, kOpen, kSealed, kInflight };
+constexpr uint32_t kNotSealed = 0xffffffffu;
+
+// Reservation word of a lane direction's open slot: slot + 1 (0 = none) in
+// bits 56-63, packets reserved in bits 32-55, segment bytes in bits 0-31.
+constexpr uint64_t resv_pack(uint32_t slot1, uint32_t n, uint32_t bytes) {
+    return ((uint64_t)slot1 << 56) | ((uint64_t)n << 32) | bytes;
+}
+constexpr uint32_t resv_slot1(uint64_t r) { return (uint32_t)(r >> 56); }
+constexpr uint32_t resv_n(uint64_t r) { return (uint32_t)(r >> 32) & 0xffffffu; }
+constexpr uint32_t resv_bytes(uint64_t r) { return (uint32_t)r; }
 
 struct Slot {
-    SlotState state = kFree;
+    SlotState state = kFree;                 // under the aggregator's lock
     int32_t reverse = 0;
-    uint32_t n = 0;         // packets reserved
-    size_t bytes = 0;       // segment bytes reserved
-    uint32_t writers = 0;   // submits still copying into the slot
+    uint32_t n = 0;                          // packets, final once sealed
+    size_t bytes = 0;                        // segment bytes, final once sealed
+    std::atomic<uint32_t> done{0};           // reserved copies that have finished
+    std::atomic<uint32_t> sealed_n{kNotSealed};
     Clock::time_point first;
     std::vector<uint64_t> cookies;
     srtp_pipeline_slot h{};
 };
 
+// a callback's packet parked until a slot frees (see the file comment)
+struct Parked {
+    int32_t reverse, tid;
+    uint32_t flags;
+    uint64_t cookie;
+    std::vector<uint8_t> pkt;
+};
+
 struct Lane {
     srtp_engine *e = nullptr;
     srtp_pipeline *pl = nullptr;
-    std::vector<Slot> slots;
-    int open[2] = {-1, -1}; // open slot per direction
+    std::unique_ptr<Slot[]> slots;
+    int n_slots = 0;
+    std::atomic<uint64_t> resv[2] = {{0}, {0}}; // open slot per direction
     std::deque<int> sealed, inflight;
+    std::deque<Parked> parked;
     std::condition_variable cv_work;  // the lane's dispatch thread: something to do
     std::condition_variable cv_space; // producers: a slot of this lane became free
     std::thread thread;
@@ -93,7 +114,8 @@ struct srtp_aggregator {
     std::condition_variable cv_idle;  // flush(): everything completed
     std::vector<std::unique_ptr<Lane>> lanes;
     bool stop = false;
-    uint64_t accepted = 0, completed = 0, bundles = 0;
+    std::atomic<uint64_t> accepted{0};
+    uint64_t completed = 0, bundles = 0;
     int error = SRTP_OK;
     std::string last_error;
     std::thread flusher;
@@ -101,43 +123,133 @@ struct srtp_aggregator {
 
 namespace {
 
-void seal_locked(srtp_aggregator *a, Lane &ln, int dir) {
-    const int s = ln.open[dir];
-    if (s < 0) return;
-    ln.open[dir] = -1;
-    ln.slots[(size_t)s].state = kSealed;
-    ln.sealed.push_back(s);
+// Seals direction dir's open slot of the lane (no more reservations); a slot
+// nobody reserved in goes back to the free list.
+void seal_locked(Lane &ln, int dir) {
+    const uint64_t r = ln.resv[dir].exchange(0);
+    if (!resv_slot1(r)) return;
+    Slot &sl = ln.slots[resv_slot1(r) - 1];
+    sl.n = resv_n(r);
+    sl.bytes = resv_bytes(r);
+    if (sl.n == 0) {
+        sl.state = kFree;
+        ln.cv_space.notify_all();
+        return;
+    }
+    sl.state = kSealed;
+    sl.sealed_n.store(sl.n);
+    ln.sealed.push_back(resv_slot1(r) - 1);
     ln.cv_work.notify_all();
-    (void)a;
 }
 
-// a free slot of the lane; producers (not in a callback) only take one when
-// another stays free for callbacks
+// A free slot of the lane; producers (not in a callback) only take one when
+// another stays free, so a callback's submit usually finds a slot at once.
 int free_slot_locked(Lane &ln, bool in_cb) {
     int first = -1, n_free = 0;
-    for (size_t i = 0; i < ln.slots.size(); i++)
+    for (int i = 0; i < ln.n_slots; i++)
         if (ln.slots[i].state == kFree) {
-            if (first < 0) first = (int)i;
+            if (first < 0) first = i;
             n_free++;
         }
     return (in_cb ? n_free >= 1 : n_free >= 2) ? first : -1;
 }
 
+void open_locked(srtp_aggregator *a, Lane &ln, int dir, int s) {
+    Slot &sl = ln.slots[s];
+    sl.state = kOpen;
+    sl.reverse = dir;
+    sl.n = 0;
+    sl.bytes = 0;
+    sl.done.store(0);
+    sl.sealed_n.store(kNotSealed);
+    sl.first = Clock::now();
+    ln.resv[dir].store(resv_pack((uint32_t)s + 1u, 0, 0));
+    a->cv_flush.notify_all(); // the flusher learns the new deadline
+}
+
+// Fast path: reserve (index, offset) in the open slot of direction dir.
+// False when there is none or it has no room.
+bool try_reserve(const srtp_aggregator *a, Lane &ln, int dir, size_t need, int &s, uint32_t &i,
+                 size_t &off) {
+    uint64_t r = ln.resv[dir].load();
+    for (;;) {
+        const uint32_t s1 = resv_slot1(r);
+        if (!s1 || resv_n(r) >= a->opts.max_packets || resv_bytes(r) + need > a->opts.max_bytes)
+            return false;
+        const uint64_t nr = resv_pack(s1, resv_n(r) + 1u, resv_bytes(r) + (uint32_t)need);
+        if (ln.resv[dir].compare_exchange_weak(r, nr)) {
+            s = (int)s1 - 1;
+            i = resv_n(r);
+            off = resv_bytes(r);
+            return true;
+        }
+    }
+}
+
+// Copies the packet into its reserved place and counts it done; the copy
+// that completes a sealed slot wakes the lane's thread.
+// (`locked`: the caller holds the lock, and no one else can have sealed the slot)
+void fill(srtp_aggregator *a, Lane &ln, int s, uint32_t i, size_t off, int32_t tid, const uint8_t *pkt,
+          uint32_t len, uint32_t cap, size_t need, uint32_t flags, uint64_t cookie, bool locked = false) {
+    Slot &sl = ln.slots[s];
+    if (len) memcpy(sl.h.seg + off, pkt, len);
+    if (need > len) memset(sl.h.seg + off + len, 0, need - len);
+    sl.h.off[i] = (uint32_t)off;
+    sl.h.len[i] = len;
+    sl.h.cap[i] = cap;
+    sl.h.flags[i] = flags;
+    sl.h.tids[i] = tid;
+    sl.cookies[i] = cookie;
+    const uint32_t d = sl.done.fetch_add(1) + 1u;
+    if (!locked && d == sl.sealed_n.load()) {
+        std::lock_guard<std::mutex> lk(a->mu);
+        ln.cv_work.notify_all();
+    }
+}
+
+size_t need_of(uint32_t cap) { return ((size_t)cap + 15u) & ~(size_t)15u; }
+
+// Places parked callback packets into slots (the lane's thread, after it
+// freed one); stops when no slot is left.
+void place_parked_locked(srtp_aggregator *a, Lane &ln) {
+    while (!ln.parked.empty()) {
+        Parked &pk = ln.parked.front();
+        const int dir = pk.reverse ? 1 : 0;
+        const uint32_t len = (uint32_t)pk.pkt.size();
+        const uint32_t cap = pk.reverse ? len : len + 16u;
+        const size_t need = need_of(cap);
+        int s;
+        uint32_t i;
+        size_t off;
+        if (!try_reserve(a, ln, dir, need, s, i, off)) {
+            seal_locked(ln, dir);
+            const int f = free_slot_locked(ln, true);
+            if (f < 0) return;
+            open_locked(a, ln, dir, f);
+            if (!try_reserve(a, ln, dir, need, s, i, off)) return; // cannot happen: need <= max_bytes
+        }
+        fill(a, ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie, true);
+        if (i + 1u == a->opts.max_packets) seal_locked(ln, dir);
+        ln.parked.pop_front();
+    }
+}
+
 void lane_loop(srtp_aggregator *a, Lane *ln) {
     std::unique_lock<std::mutex> lk(a->mu);
     // keep up to depth - 2 bundles in flight (one slot per open direction)
-    const size_t max_inflight = ln->slots.size() > 2 ? ln->slots.size() - 2 : 1;
+    const size_t max_inflight = ln->n_slots > 2 ? (size_t)ln->n_slots - 2 : 1;
     for (;;) {
         auto can_submit = [&] {
-            return !ln->sealed.empty() && ln->inflight.size() < max_inflight &&
-                   ln->slots[(size_t)ln->sealed.front()].writers == 0;
+            if (ln->sealed.empty() || ln->inflight.size() >= max_inflight) return false;
+            const Slot &sl = ln->slots[ln->sealed.front()];
+            return sl.done.load() == sl.n;
         };
         ln->cv_work.wait(lk, [&] { return a->stop || can_submit() || !ln->inflight.empty(); });
-        if (a->stop && ln->sealed.empty() && ln->inflight.empty()) return;
+        if (a->stop && ln->sealed.empty() && ln->inflight.empty() && ln->parked.empty()) return;
         if (can_submit()) {
             const int s = ln->sealed.front();
             ln->sealed.pop_front();
-            Slot &sl = ln->slots[(size_t)s];
+            Slot &sl = ln->slots[s];
             sl.state = kInflight;
             ln->inflight.push_back(s);
             const uint32_t n = sl.n;
@@ -155,7 +267,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln) {
         }
         if (ln->inflight.empty()) continue; // stop requested with sealed slots still being written
         const int s = ln->inflight.front();
-        Slot &sl = ln->slots[(size_t)s];
+        Slot &sl = ln->slots[s];
         lk.unlock();
         (void)srtp_pipeline_wait(ln->pl, s);
         // callbacks outside the lock, in bundle order
@@ -172,6 +284,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln) {
         sl.state = kFree;
         sl.n = 0;
         sl.bytes = 0;
+        place_parked_locked(a, *ln);
         ln->cv_space.notify_all();
         a->cv_idle.notify_all();
     }
@@ -184,10 +297,10 @@ void flush_loop(srtp_aggregator *a) {
         Clock::time_point wake = Clock::now() + std::chrono::milliseconds(50);
         for (auto &ln : a->lanes) {
             for (int d = 0; d < 2; d++) {
-                const int s = ln->open[d];
-                if (s < 0) continue;
-                const Clock::time_point due = ln->slots[(size_t)s].first + deadline;
-                if (due <= Clock::now()) seal_locked(a, *ln, d);
+                const uint32_t s1 = resv_slot1(ln->resv[d].load());
+                if (!s1) continue;
+                const Clock::time_point due = ln->slots[s1 - 1].first + deadline;
+                if (due <= Clock::now()) seal_locked(*ln, d);
                 else if (due < wake) wake = due;
             }
         }
@@ -197,8 +310,8 @@ void flush_loop(srtp_aggregator *a) {
 
 void seal_all_locked(srtp_aggregator *a) {
     for (auto &ln : a->lanes) {
-        seal_locked(a, *ln, 0);
-        seal_locked(a, *ln, 1);
+        seal_locked(*ln, 0);
+        seal_locked(*ln, 1);
     }
 }
 
@@ -215,7 +328,10 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
     srtp_aggregator_opts o;
     if (opts) o = *opts;
     else srtp_aggregator_opts_default(&o);
-    if (o.max_packets == 0 || o.max_bytes < 64 || o.depth < 3 || o.depth > 16) return SRTP_EINVAL;
+    // the reservation word holds 24 bits of packets and 32 of bytes
+    if (o.max_packets == 0 || o.max_packets > 0xffffffu || o.max_bytes < 64 ||
+        o.max_bytes > 0xffffffffull || o.depth < 3 || o.depth > 16)
+        return SRTP_EINVAL;
     for (size_t l = 0; l < n_lanes; l++) {
         srtp_engine_opts eo;
         if (!engines[l] || srtp_engine_get_opts(engines[l], &eo) != SRTP_OK || eo.abort_on_error)
@@ -237,10 +353,11 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
             delete a;
             return rc;
         }
-        ln.slots.resize((size_t)o.depth);
+        ln.n_slots = o.depth;
+        ln.slots.reset(new Slot[(size_t)o.depth]);
         for (int i = 0; i < o.depth; i++) {
-            srtp_pipeline_slot_get(ln.pl, i, &ln.slots[(size_t)i].h);
-            ln.slots[(size_t)i].cookies.resize(o.max_packets);
+            srtp_pipeline_slot_get(ln.pl, i, &ln.slots[i].h);
+            ln.slots[i].cookies.resize(o.max_packets);
         }
     }
     for (auto &ln : a->lanes) ln->thread = std::thread(lane_loop, a, ln.get());
@@ -283,7 +400,7 @@ int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, con
     // protect appends up to 16 bytes (SRTCP E|index + a 12-byte tag): the
     // in-place form of RawPacket.append / grow; unprotect only shrinks
     const uint32_t cap = reverse ? len : len + 16u;
-    const size_t need = ((size_t)cap + 15u) & ~(size_t)15u;
+    const size_t need = need_of(cap);
     if (need > a->opts.max_bytes) return SRTP_EINVAL;
     size_t lane = 0;
     if (a->d) {
@@ -292,52 +409,35 @@ int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, con
     }
     Lane &ln = *a->lanes[lane];
     const bool in_cb = tl_in_callback == a;
-    std::unique_lock<std::mutex> lk(a->mu);
-    if (a->stop) return SRTP_EINVAL;
-    for (;;) {
-        int s = ln.open[dir];
-        if (s >= 0) {
-            Slot &sl = ln.slots[(size_t)s];
-            if (sl.n < a->opts.max_packets && sl.bytes + need <= a->opts.max_bytes) break;
-            seal_locked(a, ln, dir);
+    int s;
+    uint32_t i;
+    size_t off;
+    if (!try_reserve(a, ln, dir, need, s, i, off)) {
+        std::unique_lock<std::mutex> lk(a->mu);
+        for (;;) {
+            if (a->stop) return SRTP_EINVAL;
+            if (try_reserve(a, ln, dir, need, s, i, off)) break;
+            seal_locked(ln, dir); // full (or none open)
+            const int f = free_slot_locked(ln, in_cb);
+            if (f >= 0) {
+                open_locked(a, ln, dir, f);
+                continue;
+            }
+            if (in_cb) { // never wait for a slot from a callback: park the packet
+                ln.parked.push_back(Parked{dir, tid, flags, cookie, std::vector<uint8_t>(pkt, pkt + len)});
+                a->accepted.fetch_add(1);
+                return SRTP_OK;
+            }
+            ln.cv_space.wait(lk); // backpressure: every slot is sealed or in flight
         }
-        s = free_slot_locked(ln, in_cb);
-        if (s >= 0) {
-            Slot &sl = ln.slots[(size_t)s];
-            sl.state = kOpen;
-            sl.reverse = reverse ? 1 : 0;
-            sl.n = 0;
-            sl.bytes = 0;
-            sl.writers = 0;
-            sl.first = Clock::now();
-            ln.open[dir] = s;
-            a->cv_flush.notify_all(); // the flusher learns the new deadline
-            break;
-        }
-        if (in_cb) return SRTP_EFULL; // only the dispatch threads free slots: never wait on one
-        ln.cv_space.wait(lk); // backpressure: every slot is sealed or in flight
-        if (a->stop) return SRTP_EINVAL;
     }
-    const int s = ln.open[dir];
-    Slot &sl = ln.slots[(size_t)s];
-    const uint32_t i = sl.n++;
-    const size_t off = sl.bytes;
-    sl.bytes += need;
-    sl.writers++;
-    a->accepted++;
-    if (sl.n == a->opts.max_packets) seal_locked(a, ln, dir);
-    lk.unlock();
-    // the packet's place is reserved: copy it without the lock
-    if (len) memcpy(sl.h.seg + off, pkt, len);
-    if (need > len) memset(sl.h.seg + off + len, 0, need - len);
-    sl.h.off[i] = (uint32_t)off;
-    sl.h.len[i] = len;
-    sl.h.cap[i] = cap;
-    sl.h.flags[i] = flags;
-    sl.h.tids[i] = tid;
-    sl.cookies[i] = cookie;
-    lk.lock();
-    if (--sl.writers == 0 && sl.state == kSealed) ln.cv_work.notify_all();
+    a->accepted.fetch_add(1);
+    fill(a, ln, s, i, off, tid, pkt, len, cap, need, flags, cookie);
+    if (i + 1u == a->opts.max_packets) { // the reservation that filled the slot seals it
+        std::lock_guard<std::mutex> lk(a->mu);
+        const uint64_t r = ln.resv[dir].load();
+        if (resv_slot1(r) == (uint32_t)s + 1u && resv_n(r) == a->opts.max_packets) seal_locked(ln, dir);
+    }
     return SRTP_OK;
 }
 
@@ -346,8 +446,12 @@ int srtp_aggregator_flush(srtp_aggregator *a) {
     if (tl_in_callback == a) return SRTP_EINVAL; // would wait for its own callback
     std::unique_lock<std::mutex> lk(a->mu);
     seal_all_locked(a);
-    const uint64_t target = a->accepted;
-    a->cv_idle.wait(lk, [&] { return a->completed >= target; });
+    const uint64_t target = a->accepted.load();
+    a->cv_idle.wait(lk, [&] {
+        if (a->completed >= target) return true;
+        seal_all_locked(a); // parked callback packets placed since then
+        return false;
+    });
     return a->error;
 }
 
@@ -355,7 +459,7 @@ int srtp_aggregator_stats(srtp_aggregator *a, uint64_t *accepted, uint64_t *comp
                           uint64_t *bundles) {
     if (!a) return SRTP_EINVAL;
     std::lock_guard<std::mutex> lk(a->mu);
-    if (accepted) *accepted = a->accepted;
+    if (accepted) *accepted = a->accepted.load();
     if (completed) *completed = a->completed;
     if (bundles) *bundles = a->bundles;
     return a->error;
@@ -366,8 +470,12 @@ void srtp_aggregator_destroy(srtp_aggregator *a) {
     {
         std::unique_lock<std::mutex> lk(a->mu);
         seal_all_locked(a);
-        const uint64_t target = a->accepted;
-        a->cv_idle.wait(lk, [&] { return a->completed >= target; });
+        const uint64_t target = a->accepted.load();
+        a->cv_idle.wait(lk, [&] {
+            if (a->completed >= target) return true;
+            seal_all_locked(a);
+            return false;
+        });
         a->stop = true;
         a->cv_flush.notify_all();
         for (auto &ln : a->lanes) {

@@ -40,6 +40,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -157,7 +158,11 @@ struct srtp_dispatch {
     uint32_t tag_mask = 0;
     int32_t abort_on_error = 1;
     std::mutex mu;
-    std::mutex kmu;              // kinds, for srtp_dispatch_route (which must not wait for a bundle)
+    std::mutex kmu;              // kinds (the vector)
+    // transformer kinds for srtp_dispatch_route, read without a lock (it is
+    // called once per packet by the aggregator's producers): -1 = no such id
+    std::unique_ptr<std::atomic<int32_t>[]> route_kind;
+    uint32_t n_route_kind = 0;
     // host time per phase of a bundle, summed over shards (srtp_dispatch_host_times)
     std::atomic<uint64_t> t_plan{0}, t_pack{0}, t_wait{0}, t_scatter{0}, t_total{0}, n_calls{0};
     std::string last_error;
@@ -345,12 +350,9 @@ int32_t srtp_shard_of(uint32_t ssrc, int32_t n_shards) {
 
 int32_t srtp_dispatch_route(srtp_dispatch *d, int32_t tid, const uint8_t *pkt, uint32_t len) {
     if (!d || (!pkt && len)) return -1;
-    int32_t kind;
-    {
-        std::lock_guard<std::mutex> kg(d->kmu);
-        if (tid < 0 || (size_t)tid >= d->kinds.size()) return -1;
-        kind = d->kinds[(size_t)tid];
-    }
+    if (tid < 0 || (uint32_t)tid >= d->n_route_kind) return -1;
+    const int32_t kind = d->route_kind[(size_t)tid].load(std::memory_order_acquire);
+    if (kind < 0) return -1;
     if (len < 12) return 0; // RawPacket.isInvalid: shard 0 reports it (DROP_INVALID)
     return (int32_t)(mix32(be32(pkt + (kind == SRTP_KIND_RTP ? 8 : 4))) % (uint32_t)d->engines.size());
 }
@@ -394,6 +396,13 @@ int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_en
     if (opts) o = *opts;
     else srtp_engine_opts_default(&o);
     d->abort_on_error = o.abort_on_error;
+    d->n_route_kind = o.max_transformers;
+    d->route_kind.reset(new (std::nothrow) std::atomic<int32_t>[o.max_transformers]);
+    if (!d->route_kind) {
+        delete d;
+        return SRTP_ENOMEM;
+    }
+    for (uint32_t t = 0; t < o.max_transformers; t++) d->route_kind[t].store(-1);
     int rc = SRTP_OK;
     for (int32_t s = 0; s < n_shards && rc == SRTP_OK; s++) {
         srtp_engine_opts os = o;
@@ -466,6 +475,7 @@ int srtp_dispatch_transformer_create(srtp_dispatch *d, int32_t kind, int32_t fwd
     std::lock_guard<std::mutex> kg(d->kmu);
     if ((size_t)id >= d->kinds.size()) d->kinds.resize((size_t)id + 1, SRTP_KIND_RTP);
     d->kinds[(size_t)id] = kind;
+    if ((uint32_t)id < d->n_route_kind) d->route_kind[(size_t)id].store(kind, std::memory_order_release);
     if (out) *out = id;
     return SRTP_OK;
 }

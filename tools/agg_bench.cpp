@@ -73,15 +73,19 @@ int main(int argc, char **argv) {
         if (G == 0) {
             check(srtp_engine_create(&o, &e), "engine");
             check(srtp_factory_create(e, 1, key, 16, salt, 14, &pol, &pol, &f), "factory");
-            check(srtp_transformer_create(e, SRTP_KIND_RTP, f, f, &t), "transformer");
         } else {
             std::vector<int32_t> devs((size_t)G);
             for (int s = 0; s < G; s++) devs[(size_t)s] = distinct_devices ? s : 0;
             check(srtp_dispatch_create(devs.data(), G, &o, &d), "dispatch");
             check(srtp_dispatch_factory_create(d, 1, key, 16, salt, 14, &pol, &pol, &f), "factory");
-            check(srtp_dispatch_transformer_create(d, SRTP_KIND_RTP, f, f, &t), "transformer");
         }
         for (int P : producer_counts) {
+            // a fresh sender transformer per point: the SSRCs and sequence
+            // numbers of the producers repeat from point to point, and the
+            // sender's replay check (SRTPCryptoContext.java:279-323) would drop
+            // them in a transformer that has seen them
+            check(d ? srtp_dispatch_transformer_create(d, SRTP_KIND_RTP, f, f, &t)
+                    : srtp_transformer_create(e, SRTP_KIND_RTP, f, f, &t), "transformer");
             srtp_aggregator_opts ao;
             srtp_aggregator_opts_default(&ao);
             srtp_aggregator *a = nullptr;
