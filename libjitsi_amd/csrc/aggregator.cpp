@@ -22,10 +22,12 @@
 //
 // Concurrency.  A submit reserves its packet's place (index, bytes) in the
 // open slot of its lane and direction with one compare-and-swap on a packed
-// reservation word -- no lock -- and copies the packet; only opening,
-// sealing and freeing slots take the aggregator's lock (once per bundle, not
-// per packet).  A sealed slot is handed to the engine once every reserved
-// copy into it has finished (Slot::done == n).  Callbacks run on the lanes'
+// reservation word -- no lock, and the only read-modify-write a submit makes
+// on memory other threads write -- and copies the packet, storing its length
+// last; only opening, sealing and freeing slots take the aggregator's lock
+// (once per bundle, not per packet).  A sealed slot is handed to the engine
+// once every reserved packet's length has been stored (lengths start as a
+// sentinel).  Callbacks run on the lanes'
 // dispatch threads.  A callback may submit (an SFU forwarding what it just
 // received); such a submit never waits for a slot -- only the dispatch
 // threads free slots, so waiting could deadlock.  When no slot is free it
@@ -56,7 +58,7 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 enum SlotState { kFree, kOpen, kSealed, kInflight };
-constexpr uint32_t kNotSealed = 0xffffffffu;
+constexpr uint32_t kNoLen = 0xffffffffu; // h.len[i] until packet i's copy has finished
 
 // Reservation word of a lane direction's open slot: slot + 1 (0 = none) in
 // bits 56-63, packets reserved in bits 32-55, segment bytes in bits 0-31.
@@ -72,8 +74,7 @@ struct Slot {
     int32_t reverse = 0;
     uint32_t n = 0;                          // packets, final once sealed
     size_t bytes = 0;                        // segment bytes, final once sealed
-    std::atomic<uint32_t> done{0};           // reserved copies that have finished
-    std::atomic<uint32_t> sealed_n{kNotSealed};
+    uint32_t ready = 0;                      // h.len[0 .. ready) seen stored (lane thread)
     Clock::time_point first;
     std::vector<uint64_t> cookies;
     srtp_pipeline_slot h{};
@@ -114,7 +115,6 @@ struct srtp_aggregator {
     std::condition_variable cv_idle;  // flush(): everything completed
     std::vector<std::unique_ptr<Lane>> lanes;
     bool stop = false;
-    std::atomic<uint64_t> accepted{0};
     uint64_t completed = 0, bundles = 0;
     int error = SRTP_OK;
     std::string last_error;
@@ -137,7 +137,7 @@ void seal_locked(Lane &ln, int dir) {
         return;
     }
     sl.state = kSealed;
-    sl.sealed_n.store(sl.n);
+    sl.ready = 0;
     ln.sealed.push_back(resv_slot1(r) - 1);
     ln.cv_work.notify_all();
 }
@@ -160,8 +160,6 @@ void open_locked(srtp_aggregator *a, Lane &ln, int dir, int s) {
     sl.reverse = dir;
     sl.n = 0;
     sl.bytes = 0;
-    sl.done.store(0);
-    sl.sealed_n.store(kNotSealed);
     sl.first = Clock::now();
     ln.resv[dir].store(resv_pack((uint32_t)s + 1u, 0, 0));
     a->cv_flush.notify_all(); // the flusher learns the new deadline
@@ -186,25 +184,37 @@ bool try_reserve(const srtp_aggregator *a, Lane &ln, int dir, size_t need, int &
     }
 }
 
-// Copies the packet into its reserved place and counts it done; the copy
-// that completes a sealed slot wakes the lane's thread.
-// (`locked`: the caller holds the lock, and no one else can have sealed the slot)
-void fill(srtp_aggregator *a, Lane &ln, int s, uint32_t i, size_t off, int32_t tid, const uint8_t *pkt,
-          uint32_t len, uint32_t cap, size_t need, uint32_t flags, uint64_t cookie, bool locked = false) {
+// Copies the packet into its reserved place; its length, stored last, marks
+// it complete for the lane's thread.
+void fill(Lane &ln, int s, uint32_t i, size_t off, int32_t tid, const uint8_t *pkt, uint32_t len, uint32_t cap,
+          size_t need, uint32_t flags, uint64_t cookie) {
     Slot &sl = ln.slots[s];
     if (len) memcpy(sl.h.seg + off, pkt, len);
     if (need > len) memset(sl.h.seg + off + len, 0, need - len);
     sl.h.off[i] = (uint32_t)off;
-    sl.h.len[i] = len;
     sl.h.cap[i] = cap;
     sl.h.flags[i] = flags;
     sl.h.tids[i] = tid;
     sl.cookies[i] = cookie;
-    const uint32_t d = sl.done.fetch_add(1) + 1u;
-    if (!locked && d == sl.sealed_n.load()) {
-        std::lock_guard<std::mutex> lk(a->mu);
-        ln.cv_work.notify_all();
+    __atomic_store_n(&sl.h.len[i], len, __ATOMIC_RELEASE);
+}
+
+// True when every packet reserved in sealed slot sl has been copied.
+bool slot_ready(Slot &sl) {
+    while (sl.ready < sl.n && __atomic_load_n(&sl.h.len[sl.ready], __ATOMIC_ACQUIRE) != kNoLen) sl.ready++;
+    return sl.ready == sl.n;
+}
+
+// Packets accepted and not yet completed (under the lock).
+uint64_t pending_locked(const srtp_aggregator *a) {
+    uint64_t n = 0;
+    for (const auto &ln : a->lanes) {
+        for (int s = 0; s < ln->n_slots; s++)
+            if (ln->slots[s].state == kSealed || ln->slots[s].state == kInflight) n += ln->slots[s].n;
+        for (int d = 0; d < 2; d++) n += resv_n(ln->resv[d].load());
+        n += ln->parked.size();
     }
+    return n;
 }
 
 size_t need_of(uint32_t cap) { return ((size_t)cap + 15u) & ~(size_t)15u; }
@@ -228,7 +238,7 @@ void place_parked_locked(srtp_aggregator *a, Lane &ln) {
             open_locked(a, ln, dir, f);
             if (!try_reserve(a, ln, dir, need, s, i, off)) return; // cannot happen: need <= max_bytes
         }
-        fill(a, ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie, true);
+        fill(ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie);
         if (i + 1u == a->opts.max_packets) seal_locked(ln, dir);
         ln.parked.pop_front();
     }
@@ -239,12 +249,18 @@ void lane_loop(srtp_aggregator *a, Lane *ln) {
     // keep up to depth - 2 bundles in flight (one slot per open direction)
     const size_t max_inflight = ln->n_slots > 2 ? (size_t)ln->n_slots - 2 : 1;
     for (;;) {
+        bool straggler = false; // a sealed slot still being copied into
         auto can_submit = [&] {
+            straggler = false;
             if (ln->sealed.empty() || ln->inflight.size() >= max_inflight) return false;
-            const Slot &sl = ln->slots[ln->sealed.front()];
-            return sl.done.load() == sl.n;
+            straggler = !slot_ready(ln->slots[ln->sealed.front()]);
+            return !straggler;
         };
-        ln->cv_work.wait(lk, [&] { return a->stop || can_submit() || !ln->inflight.empty(); });
+        auto go = [&] { return a->stop || can_submit() || !ln->inflight.empty(); };
+        while (!go()) {
+            if (straggler) ln->cv_work.wait_for(lk, std::chrono::microseconds(20)); // copies take ~0.1 us
+            else ln->cv_work.wait(lk);
+        }
         if (a->stop && ln->sealed.empty() && ln->inflight.empty() && ln->parked.empty()) return;
         if (can_submit()) {
             const int s = ln->sealed.front();
@@ -281,6 +297,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln) {
         ln->inflight.pop_front();
         a->completed += sl.n;
         a->bundles++;
+        for (uint32_t i = 0; i < sl.n; i++) sl.h.len[i] = kNoLen;
         sl.state = kFree;
         sl.n = 0;
         sl.bytes = 0;
@@ -358,6 +375,7 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
         for (int i = 0; i < o.depth; i++) {
             srtp_pipeline_slot_get(ln.pl, i, &ln.slots[i].h);
             ln.slots[i].cookies.resize(o.max_packets);
+            for (uint32_t k = 0; k < o.max_packets; k++) ln.slots[i].h.len[k] = kNoLen;
         }
     }
     for (auto &ln : a->lanes) ln->thread = std::thread(lane_loop, a, ln.get());
@@ -425,14 +443,12 @@ int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, con
             }
             if (in_cb) { // never wait for a slot from a callback: park the packet
                 ln.parked.push_back(Parked{dir, tid, flags, cookie, std::vector<uint8_t>(pkt, pkt + len)});
-                a->accepted.fetch_add(1);
                 return SRTP_OK;
             }
             ln.cv_space.wait(lk); // backpressure: every slot is sealed or in flight
         }
     }
-    a->accepted.fetch_add(1);
-    fill(a, ln, s, i, off, tid, pkt, len, cap, need, flags, cookie);
+    fill(ln, s, i, off, tid, pkt, len, cap, need, flags, cookie);
     if (i + 1u == a->opts.max_packets) { // the reservation that filled the slot seals it
         std::lock_guard<std::mutex> lk(a->mu);
         const uint64_t r = ln.resv[dir].load();
@@ -446,7 +462,7 @@ int srtp_aggregator_flush(srtp_aggregator *a) {
     if (tl_in_callback == a) return SRTP_EINVAL; // would wait for its own callback
     std::unique_lock<std::mutex> lk(a->mu);
     seal_all_locked(a);
-    const uint64_t target = a->accepted.load();
+    const uint64_t target = a->completed + pending_locked(a);
     a->cv_idle.wait(lk, [&] {
         if (a->completed >= target) return true;
         seal_all_locked(a); // parked callback packets placed since then
@@ -459,7 +475,7 @@ int srtp_aggregator_stats(srtp_aggregator *a, uint64_t *accepted, uint64_t *comp
                           uint64_t *bundles) {
     if (!a) return SRTP_EINVAL;
     std::lock_guard<std::mutex> lk(a->mu);
-    if (accepted) *accepted = a->accepted.load();
+    if (accepted) *accepted = a->completed + pending_locked(a);
     if (completed) *completed = a->completed;
     if (bundles) *bundles = a->bundles;
     return a->error;
@@ -470,7 +486,7 @@ void srtp_aggregator_destroy(srtp_aggregator *a) {
     {
         std::unique_lock<std::mutex> lk(a->mu);
         seal_all_locked(a);
-        const uint64_t target = a->accepted.load();
+        const uint64_t target = a->completed + pending_locked(a);
         a->cv_idle.wait(lk, [&] {
             if (a->completed >= target) return true;
             seal_all_locked(a);

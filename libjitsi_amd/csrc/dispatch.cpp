@@ -32,13 +32,16 @@
 //
 // Data path per shard: a worker thread packs its packets into pinned slots of
 // an srtp_pipeline on its engine (H2D, kernels and D2H of consecutive chunks
-// overlap), then scatters statuses, lengths and packet bytes back.
+// overlap), then scatters statuses, lengths and packet bytes back.  The packet
+// copies of a chunk are split over the worker and a pool of copy helpers
+// shared by the shards (one host thread copies ~12 GB/s, below the PCIe rate).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -47,7 +50,9 @@
 #include <thread>
 #include <vector>
 
+#include <sched.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/srtp_mi355x.h"
@@ -151,7 +156,84 @@ static int32_t plan_bundle(int32_t n_shards, int32_t abort_on_error, int32_t rev
     return any ? 2 : 1;
 }
 
+namespace {
+// Fork-join helpers for the packet copies (pack / scatter).  run(parts, f)
+// calls f(0..parts-1): the caller takes parts itself while helpers take the
+// rest from the queue, so it never waits on a busy pool.
+class CopyPool {
+  public:
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    void run(int parts, const std::function<void(int)> &f) {
+        if (parts <= 1 || th_.empty()) {
+            for (int i = 0; i < parts; i++) f(i);
+            return;
+        }
+        struct Job {
+            std::atomic<int> next{0}, done{0};
+        };
+        auto job = std::make_shared<Job>();
+        auto body = [job, parts, &f] {
+            int i;
+            while ((i = job->next.fetch_add(1)) < parts) {
+                f(i);
+                job->done.fetch_add(1);
+            }
+        };
+        const int helpers = std::min(parts - 1, (int)th_.size());
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            for (int h = 0; h < helpers; h++) q_.push_back(body);
+        }
+        cv_.notify_all();
+        body();
+        while (job->done.load() < parts) std::this_thread::yield();
+    }
+
+  private:
+    void loop() {
+        for (;;) {
+            std::function<void()> t;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                t = std::move(q_.front());
+                q_.pop_front();
+            }
+            t();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+};
+
+// copy helpers: SRTP_DISPATCH_COPY_THREADS, else the CPUs this process may
+// run on beyond one per shard worker, at most 8
+int copy_threads(int n_shards) {
+    if (const char *e = getenv("SRTP_DISPATCH_COPY_THREADS")) return std::max(0, atoi(e));
+    cpu_set_t cs;
+    int ncpu = 4;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) ncpu = CPU_COUNT(&cs);
+    return std::max(0, std::min(8, ncpu - n_shards));
+}
+} // namespace
+
 struct srtp_dispatch {
+    std::unique_ptr<CopyPool> pool;
     std::vector<srtp_engine *> engines;
     std::vector<srtp_pipeline *> pipes;
     std::vector<int32_t> kinds;  // transformer kinds (replicated ids); written under mu and kmu
@@ -227,12 +309,16 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             for (uint32_t i : ch) d->b_status[i] = SRTP_STATUS_ERR_INTERNAL;
             return;
         }
-        for (size_t j = 0; j < ch.size(); j++) {
-            const uint32_t i = ch[j];
-            d->b_status[i] = sl[k].status[j];
-            d->b_len[i] = sl[k].len[j];
-            memcpy(d->b_seg + d->b_off[i], sl[k].seg + sl[k].off[j], region(d->b_cap[i]));
-        }
+        const size_t nch = ch.size();
+        const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
+        d->pool->run(parts, [&](int q) {
+            for (size_t j = nch * q / parts; j < nch * (q + 1) / parts; j++) {
+                const uint32_t i = ch[j];
+                d->b_status[i] = sl[k].status[j];
+                d->b_len[i] = sl[k].len[j];
+                memcpy(d->b_seg + d->b_off[i], sl[k].seg + sl[k].off[j], region(d->b_cap[i]));
+            }
+        });
         d->t_scatter += now_ns() - ts;
     };
     size_t pos = 0;
@@ -244,7 +330,7 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         ch.clear();
         size_t bytes = 0;
         const uint64_t tp = now_ns();
-        while (pos < idx.size() && ch.size() < sl[k].max_packets) {
+        while (pos < idx.size() && ch.size() < sl[k].max_packets) { // the chunk's layout
             const uint32_t i = idx[pos];
             const size_t r = region(d->b_cap[i]);
             if (bytes + r > sl[k].seg_cap) break;
@@ -254,10 +340,19 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             sl[k].cap[j] = d->b_cap[i];
             sl[k].flags[j] = d->b_flags ? d->b_flags[i] : 0u;
             sl[k].tids[j] = d->b_tids ? d->b_tids[i] : d->b_tid;
-            memcpy(sl[k].seg + bytes, d->b_seg + d->b_off[i], r);
             bytes += r;
             ch.push_back(i);
             pos++;
+        }
+        {   // the packet bytes, split over the copy helpers
+            const size_t nch = ch.size();
+            const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
+            d->pool->run(parts, [&](int q) {
+                for (size_t j = nch * q / parts; j < nch * (q + 1) / parts; j++) {
+                    const uint32_t i = ch[j];
+                    memcpy(sl[k].seg + sl[k].off[j], d->b_seg + d->b_off[i], region(d->b_cap[i]));
+                }
+            });
         }
         d->t_pack += now_ns() - tp;
         if (ch.empty()) { // a packet larger than a slot (cannot happen: cap <= 65535)
@@ -381,6 +476,7 @@ void srtp_dispatch_destroy(srtp_dispatch *d) {
     d->cv_go.notify_all();
     for (auto &w : d->workers)
         if (w.joinable()) w.join();
+    d->pool.reset();
     for (auto *p : d->pipes) srtp_pipeline_destroy(p);
     for (auto *e : d->engines) srtp_engine_destroy(e);
     delete d;
@@ -404,6 +500,11 @@ int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_en
     }
     for (uint32_t t = 0; t < o.max_transformers; t++) d->route_kind[t].store(-1);
     int rc = SRTP_OK;
+    try {
+        d->pool.reset(new CopyPool(copy_threads(n_shards)));
+    } catch (...) {
+        rc = SRTP_ENOMEM;
+    }
     for (int32_t s = 0; s < n_shards && rc == SRTP_OK; s++) {
         srtp_engine_opts os = o;
         os.device = devices[s];

@@ -2587,7 +2587,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
             ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
-#if SRTP_COALESCE
+#if SRTP_COALESCE == 1
             const bool full = quad_full();
             load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
 #else
@@ -2596,14 +2596,16 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
             ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-#if SRTP_COALESCE
+#if SRTP_COALESCE == 1
             load_chunk_quad_finish(full, d);
 #endif
             ctr_apply_wave(cs, b, K, d);
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k];
-#if SRTP_COALESCE
+#if SRTP_COALESCE == 1
             store_chunk_quad(a.seg, a.off[p], b, full, d);
+#elif SRTP_COALESCE == 2
+            store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
 #else
             store_chunk_full(pkt, b, d);
 #endif
@@ -2846,7 +2848,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
             ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
-#if SRTP_COALESCE
+#if SRTP_COALESCE == 1
             const bool full = quad_full();
             load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
 #else
@@ -2855,14 +2857,16 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-#if SRTP_COALESCE
+#if SRTP_COALESCE == 1
             load_chunk_quad_finish(full, d);
 #endif
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k]; // ciphertext of chunk b, hashed next
             ctr_apply_wave(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
-#if SRTP_COALESCE
+#if SRTP_COALESCE == 1
             store_chunk_quad(a.seg, a.off[p], b, full, d);
+#elif SRTP_COALESCE == 2
+            store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
 #else
             store_chunk_full(pkt, b, d);
 #endif
