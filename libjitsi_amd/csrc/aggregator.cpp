@@ -20,27 +20,32 @@
 // bundle order -- so packets of one lane (one shard, hence one context) and
 // one direction complete in the order they were accepted.
 //
-// Concurrency.  A submit reserves its packet's place (index, bytes) in the
-// open slot of its lane and direction with one compare-and-swap on a packed
-// reservation word -- no lock, and the only read-modify-write a submit makes
-// on memory other threads write -- and copies the packet, storing its length
-// last; only opening, sealing and freeing slots take the aggregator's lock
-// (once per bundle, not per packet).  A sealed slot is handed to the engine
-// once every reserved packet's length has been stored (lengths start as a
-// sentinel).  Callbacks run on the lanes'
-// dispatch threads.  A callback may submit (an SFU forwarding what it just
-// received); such a submit never waits for a slot -- only the dispatch
-// threads free slots, so waiting could deadlock.  When no slot is free it
-// parks a copy of the packet in the lane's overflow queue, which the lane's
-// thread moves into the first slot it frees, ahead of other producers, so a
-// forwarded packet is never refused.  flush and destroy from a callback
-// return SRTP_EINVAL.
+// Concurrency.  Each producer thread fills blocks of 16 consecutive packet
+// entries of the open slot of its lane and direction (with a byte range of
+// the segment): it takes a block with one compare-and-swap on the slot's
+// reservation word, then claims the block's entries one at a time with a
+// compare-and-swap on the block's own cache line, which no other thread
+// touches until the slot is sealed.  So producers share no written cache
+// line per packet (the entries' metadata of a block fill whole lines), and
+// the aggregator's lock is taken only to open, seal and free slots.  A packet
+// is copied with its length stored last; a sealed slot goes to the engine once
+// every claimed entry's length has been stored (lengths start as a
+// sentinel).  Sealing closes every block: entries nobody claimed become holes
+// (SRTP_PKT_FLAG_SKIP, no callback), at most 15 per producer per bundle.
+// Callbacks run on the lanes' dispatch threads.  A callback may submit (an SFU
+// forwarding what it just received); such a submit never waits for a slot --
+// only the dispatch threads free slots, so waiting could deadlock.  When no
+// slot is free it parks a copy of the packet in the lane's overflow queue,
+// which the lane's thread moves into the first slot it frees, ahead of other
+// producers, so a forwarded packet is never refused.  flush and destroy from
+// a callback return SRTP_EINVAL.
 //
 // Per-packet semantics: each submitted packet is its own 1-element
 // RawPacket[] in the reference, so one packet's exception must not stop
 // later packets of the same transformer in the bundle.  The engines therefore
 // run with abort_on_error = 0 (creation refuses otherwise); a packet the
 // reference would throw on completes with SRTP_STATUS_ERR_MALFORMED.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -59,9 +64,10 @@ using Clock = std::chrono::steady_clock;
 
 enum SlotState { kFree, kOpen, kSealed, kInflight };
 constexpr uint32_t kNoLen = 0xffffffffu; // h.len[i] until packet i's copy has finished
+constexpr uint32_t kBlock = 16;          // entries per producer block (a cache line of u32s)
 
 // Reservation word of a lane direction's open slot: slot + 1 (0 = none) in
-// bits 56-63, packets reserved in bits 32-55, segment bytes in bits 0-31.
+// bits 56-63, blocks handed out in bits 32-55, segment bytes in bits 0-31.
 constexpr uint64_t resv_pack(uint32_t slot1, uint32_t n, uint32_t bytes) {
     return ((uint64_t)slot1 << 56) | ((uint64_t)n << 32) | bytes;
 }
@@ -69,13 +75,32 @@ constexpr uint32_t resv_slot1(uint64_t r) { return (uint32_t)(r >> 56); }
 constexpr uint32_t resv_n(uint64_t r) { return (uint32_t)(r >> 32) & 0xffffffu; }
 constexpr uint32_t resv_bytes(uint64_t r) { return (uint32_t)r; }
 
+// Claim word of a block: entries claimed in bits 0-7, bytes used in bits
+// 8-39, the slot's generation (mod 2^23) in bits 40-62, closed (sealed) in bit
+// 63.  The generation keeps a thread that cached a block from claiming in a
+// later opening of the same slot.
+constexpr uint64_t kClosed = 1ull << 63;
+constexpr uint32_t blk_used(uint64_t w) { return (uint32_t)(w & 0xffu); }
+constexpr uint32_t blk_bytes(uint64_t w) { return (uint32_t)(w >> 8); }
+constexpr uint64_t blk_tag(uint32_t gen) { return (uint64_t)(gen & 0x7fffffu) << 40; }
+constexpr uint64_t kTagMask = 0x7fffffull << 40;
+
+struct alignas(64) Block {
+    std::atomic<uint64_t> w{0};
+    uint32_t b0 = 0, size = 0; // byte range (written by the block's owner)
+};
+
 struct Slot {
     SlotState state = kFree;                 // under the aggregator's lock
+    std::atomic<uint32_t> gen{0};            // opened how often (producers' cached blocks)
     int32_t reverse = 0;
-    uint32_t n = 0;                          // packets, final once sealed
+    uint32_t n = 0;                          // entries (with holes), final once sealed
+    uint32_t n_real = 0;                     // packets, final once sealed
     size_t bytes = 0;                        // segment bytes, final once sealed
     uint32_t ready = 0;                      // h.len[0 .. ready) seen stored (lane thread)
     Clock::time_point first;
+    std::unique_ptr<Block[]> blocks;
+    std::vector<uint8_t> hole;
     std::vector<uint64_t> cookies;
     srtp_pipeline_slot h{};
 };
@@ -102,6 +127,16 @@ struct Lane {
 };
 
 thread_local const void *tl_in_callback = nullptr; // the aggregator whose callback runs here
+
+// The block a thread is filling, per (aggregator, lane, direction).
+struct TlBlock {
+    uint64_t a = 0; // srtp_aggregator::id (0: unused)
+    uint32_t lane = 0, dir = 0, slot = 0, gen = 0, blk = 0;
+};
+constexpr int kTlBlocks = 8;
+thread_local TlBlock tl_blocks[kTlBlocks];
+thread_local unsigned tl_victim = 0;
+std::atomic<uint64_t> g_next_id{1};
 } // namespace
 
 struct srtp_aggregator {
@@ -109,6 +144,10 @@ struct srtp_aggregator {
     srtp_aggregator_opts opts{};
     srtp_aggregator_cb cb = nullptr;
     void *user = nullptr;
+    uint64_t id = g_next_id.fetch_add(1); // keys the threads' cached blocks (never reused)
+    uint32_t blk = kBlock;      // entries per block (max_packets if smaller)
+    uint32_t n_blk = 0;         // blocks per slot
+    uint32_t blk_bytes = 0;     // default byte range of a block
 
     std::mutex mu;
     std::condition_variable cv_flush; // the flusher: a new deadline
@@ -123,15 +162,36 @@ struct srtp_aggregator {
 
 namespace {
 
-// Seals direction dir's open slot of the lane (no more reservations); a slot
-// nobody reserved in goes back to the free list.
-void seal_locked(Lane &ln, int dir) {
+// Seals direction dir's open slot of the lane: no more blocks, every block
+// closed, unclaimed entries become holes.  A slot without packets goes back
+// to the free list.
+void seal_locked(srtp_aggregator *a, Lane &ln, int dir) {
     const uint64_t r = ln.resv[dir].exchange(0);
     if (!resv_slot1(r)) return;
     Slot &sl = ln.slots[resv_slot1(r) - 1];
-    sl.n = resv_n(r);
+    const uint32_t nb = resv_n(r);
+    uint32_t real = 0;
+    for (uint32_t k = 0; k < nb; k++) {
+        const uint32_t u = blk_used(sl.blocks[k].w.fetch_or(kClosed));
+        real += u;
+        for (uint32_t i = k * a->blk + u; i < (k + 1) * a->blk; i++) {
+            sl.hole[i] = 1;
+            sl.h.off[i] = 0;
+            sl.h.cap[i] = 0;
+            sl.h.flags[i] = SRTP_PKT_FLAG_SKIP;
+            sl.h.tids[i] = -1;
+            sl.h.len[i] = 0;
+        }
+    }
+    sl.n = nb * a->blk;
+    sl.n_real = real;
     sl.bytes = resv_bytes(r);
-    if (sl.n == 0) {
+    if (real == 0) {
+        for (uint32_t i = 0; i < sl.n; i++) {
+            sl.h.len[i] = kNoLen;
+            sl.hole[i] = 0;
+        }
+        sl.n = 0;
         sl.state = kFree;
         ln.cv_space.notify_all();
         return;
@@ -142,8 +202,6 @@ void seal_locked(Lane &ln, int dir) {
     ln.cv_work.notify_all();
 }
 
-// A free slot of the lane; producers (not in a callback) only take one when
-// another stays free, so a callback's submit usually finds a slot at once.
 int free_slot_locked(Lane &ln, bool in_cb) {
     int first = -1, n_free = 0;
     for (int i = 0; i < ln.n_slots; i++)
@@ -158,29 +216,78 @@ void open_locked(srtp_aggregator *a, Lane &ln, int dir, int s) {
     Slot &sl = ln.slots[s];
     sl.state = kOpen;
     sl.reverse = dir;
-    sl.n = 0;
+    sl.n = sl.n_real = 0;
     sl.bytes = 0;
     sl.first = Clock::now();
+    const uint32_t g = sl.gen.load() + 1u;
+    for (uint32_t k = 0; k < a->n_blk; k++) sl.blocks[k].w.store(blk_tag(g), std::memory_order_relaxed);
+    sl.gen.store(g, std::memory_order_release);
     ln.resv[dir].store(resv_pack((uint32_t)s + 1u, 0, 0));
     a->cv_flush.notify_all(); // the flusher learns the new deadline
 }
 
-// Fast path: reserve (index, offset) in the open slot of direction dir.
-// False when there is none or it has no room.
-bool try_reserve(const srtp_aggregator *a, Lane &ln, int dir, size_t need, int &s, uint32_t &i,
+// Fast path: an entry (index, offset) in the calling thread's block of the
+// open slot of direction dir, taking a new block when it has none or its
+// block is full or closed.  False when the slot has no room (or none is open).
+bool try_reserve(srtp_aggregator *a, Lane &ln, uint32_t lane, int dir, size_t need, int &s, uint32_t &i,
                  size_t &off) {
+    TlBlock *tb = nullptr;
+    for (auto &t : tl_blocks)
+        if (t.a == a->id && t.lane == lane && t.dir == (uint32_t)dir) tb = &t;
+    if (tb) {
+        Slot &sl = ln.slots[tb->slot];
+        Block &bk = sl.blocks[tb->blk];
+        uint64_t w = bk.w.load(std::memory_order_acquire);
+        if ((w & kTagMask) == blk_tag(tb->gen)) {
+            // (b0 and size are this thread's own writes when the tag matches)
+            while (!(w & kClosed) && blk_used(w) < a->blk && blk_bytes(w) + need <= bk.size) {
+                const uint64_t nw = blk_tag(tb->gen) | ((uint64_t)(blk_bytes(w) + need) << 8) | (blk_used(w) + 1u);
+                if (bk.w.compare_exchange_weak(w, nw, std::memory_order_acq_rel)) {
+                    s = (int)tb->slot;
+                    i = tb->blk * a->blk + blk_used(w);
+                    off = bk.b0 + blk_bytes(w);
+                    return true;
+                }
+            }
+        }
+    } else {
+        tb = &tl_blocks[tl_victim++ % kTlBlocks];
+        tb->a = a->id;
+        tb->lane = lane;
+        tb->dir = (uint32_t)dir;
+    }
+    // a new block
     uint64_t r = ln.resv[dir].load();
     for (;;) {
         const uint32_t s1 = resv_slot1(r);
-        if (!s1 || resv_n(r) >= a->opts.max_packets || resv_bytes(r) + need > a->opts.max_bytes)
+        const size_t size = need > a->blk_bytes ? need : a->blk_bytes;
+        if (!s1 || resv_n(r) >= a->n_blk || resv_bytes(r) + size > a->opts.max_bytes) {
+            tb->a = 0;
             return false;
-        const uint64_t nr = resv_pack(s1, resv_n(r) + 1u, resv_bytes(r) + (uint32_t)need);
-        if (ln.resv[dir].compare_exchange_weak(r, nr)) {
-            s = (int)s1 - 1;
-            i = resv_n(r);
-            off = resv_bytes(r);
-            return true;
         }
+        Slot &sl = ln.slots[s1 - 1];
+        const uint32_t g = sl.gen.load(std::memory_order_acquire); // before the CAS (see below)
+        const uint64_t nr = resv_pack(s1, resv_n(r) + 1u, resv_bytes(r) + (uint32_t)size);
+        if (!ln.resv[dir].compare_exchange_weak(r, nr)) continue;
+        const uint32_t k = resv_n(r);
+        Block &bk = sl.blocks[k];
+        // The first entry -- unless the slot was sealed meanwhile (closed), or
+        // sealed and reopened between reading g and the CAS (tag of a later
+        // generation: the block is then a run of holes in that opening).
+        uint64_t w = blk_tag(g);
+        if (!bk.w.compare_exchange_strong(w, blk_tag(g) | ((uint64_t)need << 8) | 1u, std::memory_order_acq_rel)) {
+            r = ln.resv[dir].load();
+            continue;
+        }
+        bk.b0 = resv_bytes(r);
+        bk.size = (uint32_t)size;
+        tb->slot = s1 - 1;
+        tb->gen = g;
+        tb->blk = k;
+        s = (int)(s1 - 1);
+        i = k * a->blk;
+        off = bk.b0;
+        return true;
     }
 }
 
@@ -210,8 +317,13 @@ uint64_t pending_locked(const srtp_aggregator *a) {
     uint64_t n = 0;
     for (const auto &ln : a->lanes) {
         for (int s = 0; s < ln->n_slots; s++)
-            if (ln->slots[s].state == kSealed || ln->slots[s].state == kInflight) n += ln->slots[s].n;
-        for (int d = 0; d < 2; d++) n += resv_n(ln->resv[d].load());
+            if (ln->slots[s].state == kSealed || ln->slots[s].state == kInflight) n += ln->slots[s].n_real;
+        for (int d = 0; d < 2; d++) {
+            const uint64_t r = ln->resv[d].load();
+            if (!resv_slot1(r)) continue;
+            const Slot &sl = ln->slots[resv_slot1(r) - 1];
+            for (uint32_t k = 0; k < resv_n(r); k++) n += blk_used(sl.blocks[k].w.load());
+        }
         n += ln->parked.size();
     }
     return n;
@@ -221,7 +333,7 @@ size_t need_of(uint32_t cap) { return ((size_t)cap + 15u) & ~(size_t)15u; }
 
 // Places parked callback packets into slots (the lane's thread, after it
 // freed one); stops when no slot is left.
-void place_parked_locked(srtp_aggregator *a, Lane &ln) {
+void place_parked_locked(srtp_aggregator *a, Lane &ln, uint32_t lane) {
     while (!ln.parked.empty()) {
         Parked &pk = ln.parked.front();
         const int dir = pk.reverse ? 1 : 0;
@@ -231,20 +343,19 @@ void place_parked_locked(srtp_aggregator *a, Lane &ln) {
         int s;
         uint32_t i;
         size_t off;
-        if (!try_reserve(a, ln, dir, need, s, i, off)) {
-            seal_locked(ln, dir);
+        if (!try_reserve(a, ln, lane, dir, need, s, i, off)) {
+            seal_locked(a, ln, dir);
             const int f = free_slot_locked(ln, true);
             if (f < 0) return;
             open_locked(a, ln, dir, f);
-            if (!try_reserve(a, ln, dir, need, s, i, off)) return; // cannot happen: need <= max_bytes
+            if (!try_reserve(a, ln, lane, dir, need, s, i, off)) return; // cannot happen: need <= max_bytes
         }
         fill(ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie);
-        if (i + 1u == a->opts.max_packets) seal_locked(ln, dir);
         ln.parked.pop_front();
     }
 }
 
-void lane_loop(srtp_aggregator *a, Lane *ln) {
+void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
     std::unique_lock<std::mutex> lk(a->mu);
     // keep up to depth - 2 bundles in flight (one slot per open direction)
     const size_t max_inflight = ln->n_slots > 2 ? (size_t)ln->n_slots - 2 : 1;
@@ -289,19 +400,23 @@ void lane_loop(srtp_aggregator *a, Lane *ln) {
         // callbacks outside the lock, in bundle order
         tl_in_callback = a;
         for (uint32_t i = 0; i < sl.n; i++) {
+            if (sl.hole[i]) continue;
             const int32_t st = sl.h.status[i];
             a->cb(a->user, sl.cookies[i], st, sl.h.seg + sl.h.off[i], sl.h.len[i]);
         }
         tl_in_callback = nullptr;
         lk.lock();
         ln->inflight.pop_front();
-        a->completed += sl.n;
+        a->completed += sl.n_real;
         a->bundles++;
-        for (uint32_t i = 0; i < sl.n; i++) sl.h.len[i] = kNoLen;
+        for (uint32_t i = 0; i < sl.n; i++) {
+            sl.h.len[i] = kNoLen;
+            sl.hole[i] = 0;
+        }
         sl.state = kFree;
-        sl.n = 0;
+        sl.n = sl.n_real = 0;
         sl.bytes = 0;
-        place_parked_locked(a, *ln);
+        place_parked_locked(a, *ln, lane);
         ln->cv_space.notify_all();
         a->cv_idle.notify_all();
     }
@@ -317,7 +432,7 @@ void flush_loop(srtp_aggregator *a) {
                 const uint32_t s1 = resv_slot1(ln->resv[d].load());
                 if (!s1) continue;
                 const Clock::time_point due = ln->slots[s1 - 1].first + deadline;
-                if (due <= Clock::now()) seal_locked(*ln, d);
+                if (due <= Clock::now()) seal_locked(a, *ln, d);
                 else if (due < wake) wake = due;
             }
         }
@@ -327,8 +442,8 @@ void flush_loop(srtp_aggregator *a) {
 
 void seal_all_locked(srtp_aggregator *a) {
     for (auto &ln : a->lanes) {
-        seal_locked(*ln, 0);
-        seal_locked(*ln, 1);
+        seal_locked(a, *ln, 0);
+        seal_locked(a, *ln, 1);
     }
 }
 
@@ -360,6 +475,9 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
     a->opts = o;
     a->cb = cb;
     a->user = user;
+    a->blk = o.max_packets < kBlock ? o.max_packets : kBlock;
+    a->n_blk = o.max_packets / a->blk;
+    a->blk_bytes = (uint32_t)std::max<size_t>(64, (o.max_bytes / a->n_blk) & ~(size_t)15);
     for (size_t l = 0; l < n_lanes; l++) {
         a->lanes.emplace_back(new Lane());
         Lane &ln = *a->lanes.back();
@@ -373,12 +491,15 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
         ln.n_slots = o.depth;
         ln.slots.reset(new Slot[(size_t)o.depth]);
         for (int i = 0; i < o.depth; i++) {
-            srtp_pipeline_slot_get(ln.pl, i, &ln.slots[i].h);
-            ln.slots[i].cookies.resize(o.max_packets);
-            for (uint32_t k = 0; k < o.max_packets; k++) ln.slots[i].h.len[k] = kNoLen;
+            Slot &sl = ln.slots[i];
+            srtp_pipeline_slot_get(ln.pl, i, &sl.h);
+            sl.cookies.resize(o.max_packets);
+            sl.hole.assign(o.max_packets, 0);
+            sl.blocks.reset(new Block[a->n_blk]);
+            for (uint32_t k = 0; k < o.max_packets; k++) sl.h.len[k] = kNoLen;
         }
     }
-    for (auto &ln : a->lanes) ln->thread = std::thread(lane_loop, a, ln.get());
+    for (size_t l = 0; l < a->lanes.size(); l++) a->lanes[l]->thread = std::thread(lane_loop, a, a->lanes[l].get(), (uint32_t)l);
     a->flusher = std::thread(flush_loop, a);
     *out = a;
     return SRTP_OK;
@@ -430,12 +551,12 @@ int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, con
     int s;
     uint32_t i;
     size_t off;
-    if (!try_reserve(a, ln, dir, need, s, i, off)) {
+    if (!try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) {
         std::unique_lock<std::mutex> lk(a->mu);
         for (;;) {
             if (a->stop) return SRTP_EINVAL;
-            if (try_reserve(a, ln, dir, need, s, i, off)) break;
-            seal_locked(ln, dir); // full (or none open)
+            if (try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) break;
+            seal_locked(a, ln, dir); // full (or none open)
             const int f = free_slot_locked(ln, in_cb);
             if (f >= 0) {
                 open_locked(a, ln, dir, f);
@@ -449,11 +570,6 @@ int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, con
         }
     }
     fill(ln, s, i, off, tid, pkt, len, cap, need, flags, cookie);
-    if (i + 1u == a->opts.max_packets) { // the reservation that filled the slot seals it
-        std::lock_guard<std::mutex> lk(a->mu);
-        const uint64_t r = ln.resv[dir].load();
-        if (resv_slot1(r) == (uint32_t)s + 1u && resv_n(r) == a->opts.max_packets) seal_locked(ln, dir);
-    }
     return SRTP_OK;
 }
 
