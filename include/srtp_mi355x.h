@@ -322,21 +322,25 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
  * packet's cookie, final status (SRTP_STATUS_*; -1 if the bundle could not be
  * submitted) and processed bytes, valid only during the call.  So packets
  * of one direction -- and thus of one transformer -- complete in the order
- * they were accepted.  Every packet is its own 1-element array, as in the
- * reference: one packet's exception (SRTP_STATUS_ERR_MALFORMED) does not stop
- * the others, which requires an engine with abort_on_error = 0
- * (srtp_aggregator_create returns SRTP_EINVAL otherwise).  When every slot is
- * sealed or in flight, submit blocks (backpressure).  flush seals the open
- * bundles and waits until every accepted packet has completed; destroy does
- * the same, then stops the threads.  A submit copies its packet outside the
- * aggregator's lock (producers only serialise on reserving its place).
- * Callbacks may submit (e.g. forward a received packet), but a submit made
- * from a callback never blocks: it returns SRTP_EFULL when no slot is free,
- * since only the dispatch threads free slots.  Producers outside callbacks
- * leave one slot of each lane (depth - 1 usable) for callback submits, so the
- * callbacks of a completed bundle can forward all of its packets unless they
- * outgrow max_bytes.  flush from a callback returns
- * SRTP_EINVAL and destroy from a callback does nothing. */
+ * they were accepted (per submitting thread when several threads submit).
+ * Every packet is its own 1-element array, as in the reference: one packet's
+ * exception (SRTP_STATUS_ERR_MALFORMED) does not stop the others, which
+ * requires an engine with abort_on_error = 0 (srtp_aggregator_create returns
+ * SRTP_EINVAL otherwise).  When every slot is sealed or in flight, submit
+ * blocks (backpressure).  flush seals the open bundles and waits until every
+ * packet accepted before it has completed; destroy does the same, then stops
+ * the threads.  Submits take no lock: each thread fills its own block of 16
+ * entries of the open bundle (one compare-and-swap per block on the bundle,
+ * one per packet on the thread's own block), so producers do not share a
+ * written cache line per packet; entries of a block left unclaimed when the
+ * bundle is sealed go to the engine as SRTP_PKT_FLAG_SKIP holes (counted as
+ * SKIPPED in srtp_engine_stats, no callback).  Callbacks may submit (e.g.
+ * forward a received packet); a submit made from a callback never blocks: when
+ * no slot is free the packet is parked and placed in the first slot the
+ * aggregator frees, ahead of other producers.  Producers outside callbacks
+ * leave one slot of each lane (depth - 1 usable) for callback submits.  flush
+ * from a callback returns SRTP_EINVAL and destroy from a callback does
+ * nothing. */
 typedef struct srtp_aggregator srtp_aggregator;
 typedef struct {
     uint32_t max_packets; /* per bundle, default 1<<14 */
