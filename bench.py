@@ -604,8 +604,12 @@ def main():
              "algorithmic_bytes_per_launch": alg_launch,
              "copy_measured_gbps": copy_gbs}
         if r["traffic"]:
-            r["traffic_source"] = f"rocprofv3 FETCH_SIZE/WRITE_SIZE per {kernel} launch, profiles/pmc_traffic.json"
+            r["traffic_source"] = (f"rocprofv3 FETCH_SIZE/WRITE_SIZE per {kernel} launch, profiles/pmc_traffic.json: "
+                                   + pmc.get("method", ""))
             r["traffic_over_algorithmic"] = round(r["traffic"] / alg_launch, 3)
+            g = (pmc.get("guide_correction_bytes_per_launch") or {}).get(kernel)
+            if g:  # the guide's stream correction (FETCH x 2), kept for comparison
+                r["traffic_guide_correction"] = g
         if util_key and pmc.get(util_key):
             r["utilisation"] = pmc.get(util_key)
         return r

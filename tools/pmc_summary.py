@@ -8,11 +8,15 @@ for the passes gpu_run.sh `prof` writes (fetch, write, sq, sq2).  Prints, per
 kernel of the SRTP pipeline, the average duration and every counter averaged
 over dispatches, then derived figures for k_protect / k_unprotect:
 
-* HBM traffic per launch = FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024 bytes.
-  FETCH_SIZE (KB) is TCC_EA0_RDREQ x 64 B and counts half the bytes of a
-  16-B-per-lane read stream on gfx950 (MI355X_MICROARCH.md, HBM section);
-  tools/pmc_calib.hip checks the factor on this kernel's access pattern
-  (one lane per packet, 16-B loads walking a 1200-B packet).
+* HBM traffic per launch.  FETCH_SIZE (KB) is TCC_EA0_RDREQ x 64 B and counts
+  half the bytes of a 16-B-per-lane coalesced read stream on gfx950
+  (MI355X_MICROARCH.md, HBM section): the guide's correction is FETCH_SIZE x 2
+  + WRITE_SIZE x 1.  The kernels' own pattern (one lane per packet, 16-B
+  accesses walking each packet in 64-B chunks) is calibrated separately by
+  tools/pmc_calib.hip (its k_lane_rw4 moves every byte of 2^18 such packets
+  exactly once): with --calib <factor.json> (tools/pmc_calib_factor.py)
+  traffic = FETCH_SIZE x read_factor + WRITE_SIZE x write_factor of k_lane_rw4,
+  and the guide's figure is kept beside it.
 * VALU / LDS issue: instructions per wave, LDS-array cycles, bank conflicts,
   effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration).
 
@@ -65,7 +69,11 @@ def main():
     ap.add_argument("--len", type=int, default=1200)
     ap.add_argument("--tag", type=int, default=10)
     ap.add_argument("--out")
+    ap.add_argument("--calib", help="factor.json of tools/pmc_calib_factor.py")
     a = ap.parse_args()
+    calib = None
+    if a.calib:
+        calib = json.load(open(a.calib)).get("k_lane_rw4")
     lines = []
     P = lines.append
     trace = load_trace(os.path.join(a.prof_dir, "trace", "run_kernel_trace.csv"))
@@ -98,9 +106,15 @@ def main():
         avg_us = sum(trace[k]) / len(trace[k]) / 1e3
         d = {"avg_us_trace": round(avg_us, 2)}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            rd = c["FETCH_SIZE"] * 1024 * 2
-            wr = c["WRITE_SIZE"] * 1024
             alg = a.packets * (a.len + a.len + a.tag)
+            rd_g, wr_g = c["FETCH_SIZE"] * 1024 * 2, c["WRITE_SIZE"] * 1024
+            d.update(guide_read_bytes=rd_g, guide_write_bytes=wr_g,
+                     guide_traffic_over_algorithmic=round((rd_g + wr_g) / alg, 3))
+            if calib:
+                rd = c["FETCH_SIZE"] * 1024 * calib["read_factor"]
+                wr = c["WRITE_SIZE"] * 1024 * calib["write_factor"]
+            else:
+                rd, wr = rd_g, wr_g
             d.update(hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes=rd + wr,
                      algorithmic_bytes=alg, traffic_over_algorithmic=round((rd + wr) / alg, 3))
         for name in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
@@ -141,8 +155,14 @@ def main():
         kp = derived.get("k_protect", {})
         if "hbm_bytes" in kp:
             js = {"packets": a.packets, "len": a.len, "source": os.path.join(a.out, "pmc_summary.txt"),
-                  "method": "FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024 per k_protect dispatch "
-                            "(separate --pmc passes; gfx950 half-count correction on reads)",
+                  "method": (("FETCH_SIZE x %.3f + WRITE_SIZE x %.3f (x 1024) per dispatch: the factors "
+                              "tools/pmc_calib.hip measures for the kernels' access pattern (k_lane_rw4); "
+                              "separate --pmc passes" % (calib["read_factor"], calib["write_factor"]))
+                             if calib else
+                             "FETCH_SIZE x 2 x 1024 + WRITE_SIZE x 1024 per dispatch (separate --pmc passes; "
+                             "gfx950 half-count correction on reads)"),
+                  "guide_correction_bytes_per_launch": {
+                      "k_protect": round(kp["guide_read_bytes"] + kp["guide_write_bytes"])},
                   "k_protect_bytes_per_launch": round(kp["hbm_bytes"]),
                   "k_protect_read_bytes": round(kp["hbm_read_bytes"]),
                   "k_protect_write_bytes": round(kp["hbm_write_bytes"])}
@@ -154,6 +174,8 @@ def main():
                 k: ku.get(k) for k in ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac",
                                        "eff_clock_ghz")}
             if "hbm_bytes" in ku:
+                js["guide_correction_bytes_per_launch"]["k_unprotect"] = round(
+                    ku["guide_read_bytes"] + ku["guide_write_bytes"])
                 js.update({"k_unprotect_bytes_per_launch": round(ku["hbm_bytes"]),
                            "k_unprotect_read_bytes": round(ku["hbm_read_bytes"]),
                            "k_unprotect_write_bytes": round(ku["hbm_write_bytes"])})

@@ -23,11 +23,11 @@ run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/fetch -o run 
 run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -o run -- $S &&
 run sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $P/sq -o run -- $S &&
 run sq2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $P/sq2 -o run -- $S &&
-run pmc_summary 120 python tools/pmc_summary.py $P --out $P/summary &&
 run calib_trace 120 rocprofv3 --kernel-trace --stats --output-format csv -d $P/calib/trace -o run -- ./tools/pmc_calib &&
 run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/calib/fetch -o run -- ./tools/pmc_calib &&
 run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/calib/write -o run -- ./tools/pmc_calib &&
 run calib_factor 60 python tools/pmc_calib_factor.py $P/calib &&
+run pmc_summary 120 python tools/pmc_summary.py $P --calib $P/calib/factor.json --out $P/summary &&
 run trace_default 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace_default -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu --no-e2e --no-dispatch &&
 python tools/timeline.py $(find $P/trace_default -name "*kernel_trace.csv" | head -1) 10 > $P/timeline.txt && head -12 $P/timeline.txt
 echo done
