@@ -2442,6 +2442,11 @@ __device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint
 #ifndef SRTP_COALESCE
 #define SRTP_COALESCE 0
 #endif
+// SRTP_TAIL_STEP: the fused loops take the packet's last chunk (protect: the
+// partial one; unprotect: the ROC-carrying one) in one more fused step
+#ifndef SRTP_TAIL_STEP
+#define SRTP_TAIL_STEP 1
+#endif
 template <int CTRL>
 __device__ __forceinline__ uint32_t qdpp(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
@@ -2611,8 +2616,50 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #endif
         }
 
-        inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
-        sha1_compress(h, c);
+        // The last, partial chunk B (payload bytes 64B .. L-1) in one more
+        // fused step -- its keystream beside the hash of block B-1 -- instead
+        // of the generic loop's unoverlapped AES and a reload of the chunk;
+        // then block B (it carries the suffix) is hashed here.
+        const bool ext = SRTP_TAIL_STEP && b == B && 64 * B < L && !ctr_pre_exhausted(4 * b - hq);
+        if (ext) {
+            uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
+            uint32_t K[16], d[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
+            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+            load_chunk(pkt, b, L, d);
+            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
+#pragma unroll
+            for (int k = 0; k < 5; k++) h[k] += v[k];
+            ctr_apply(cs, b, K, d);
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = d[k];
+            store_chunk(pkt, b, cs, d);
+            // the rest of the MAC and the trailer here, so that nothing of the
+            // AES state stays live past this step (the generic loop below
+            // would otherwise keep it, and the step spills)
+            inner_words(c, b, L, suffix);
+            sha1_compress(h, c);
+            for (b = b + 1; b <= nb_inner; b++) {
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) w[k] = 0u;
+                if (b < nb_inner) inner_words(w, b, L, suffix);
+                else outer_words(w, h, ks);
+                sha1_compress(h, w);
+            }
+            int o = L;
+            if (rtcp) {
+                pkt[o] = (uint8_t)(suffix >> 24); pkt[o + 1] = (uint8_t)(suffix >> 16);
+                pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
+                o += 4;
+            }
+            tag_write(h, pkt + o, T);
+            return;
+        } else {
+            inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
+            sha1_compress(h, c);
+        }
     }
     // One AES site and one SHA-1 site: 64-B chunk b is loaded, encrypted in
     // place, stored, then hashed (inner blocks, then the outer block).
@@ -2871,9 +2918,57 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             store_chunk_full(pkt, b, d);
 #endif
         }
+        // The ROC-carrying chunk nb_full (MAC'd bytes up to end) in one more
+        // fused step: its keystream beside the hash of block nb_full-1, the
+        // midstate and ciphertext saved for the walk, decrypted in place --
+        // instead of the MAC loop's reload and the decryption loop's
+        // unoverlapped AES below.
+        const bool ext = SRTP_TAIL_STEP && b == nb_full && 64 * nb_full < end &&
+                         !ctr_pre_exhausted(4 * b - hq);
+        if (ext) {
+            uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
+            uint32_t K[16], d[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
-        sha1_compress(h, c); // block b-1, a full block before the ROC-carrying one
+            for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
+            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+            load_chunk(pkt, b, end, d);
+            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
+#pragma unroll
+            for (int k = 0; k < 5; k++) h[k] += v[k];
+            if (rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
+                uint32_t *mp = a.mid + 5 * (size_t)p;
+#pragma unroll
+                for (int k = 0; k < 5; k++) mp[k] = h[k];
+                if (spec) {
+                    uint4 *tp = reinterpret_cast<uint4 *>(a.tailc + 16 * (size_t)p);
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+                        tp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = d[k]; // ciphertext of block nb_full
+            ctr_apply(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
+            store_chunk(pkt, b, cs, d);
+            // the rest of the MAC here (nothing is left to decrypt: end lies in
+            // this chunk), so that no AES state stays live past this step
+            inner_words(c, b, end, suffix);
+            sha1_compress(h, c);
+            for (b = b + 1; b <= nb_inner; b++) {
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) w[k] = 0u;
+                if (b < nb_inner) inner_words(w, b, end, suffix);
+                else outer_words(w, h, ks);
+                sha1_compress(h, w);
+            }
+            a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+            return;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
+            sha1_compress(h, c); // block b-1, a full block before the ROC-carrying one
+        }
     }
     // The blocks left after the fused loop: first the MAC over their
     // ciphertext, then their decryption -- two loops, so that no AES state
