@@ -2442,10 +2442,16 @@ __device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint
 #ifndef SRTP_COALESCE
 #define SRTP_COALESCE 0
 #endif
-// SRTP_TAIL_STEP: the fused loops take the packet's last chunk (protect: the
-// partial one; unprotect: the ROC-carrying one) in one more fused step
+// SRTP_TAIL_STEP (unprotect) / SRTP_TAIL_STEP_PROTECT: the fused loop takes
+// the packet's last chunk (unprotect: the ROC-carrying one; protect: the
+// partial one) in one more fused step.  Measured (profiles/r03/
+// kernel_experiments.md): k_unprotect 0.301 -> 0.295 ms; k_protect 0.283 ->
+// 0.299 ms (its extra step spills), so off for protect.
 #ifndef SRTP_TAIL_STEP
 #define SRTP_TAIL_STEP 1
+#endif
+#ifndef SRTP_TAIL_STEP_PROTECT
+#define SRTP_TAIL_STEP_PROTECT 0
 #endif
 template <int CTRL>
 __device__ __forceinline__ uint32_t qdpp(uint32_t x) {
@@ -2582,8 +2588,11 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         ctr_chunk_pre(lds, tb, rk, cp, cs, 0, c);
         store_chunk(pkt, 0, cs, c);
         const int hq = cs.off >> 4;
-        const int nbw = SRTP_PRIO ? wave_max_i(B) : 0;
-        for (b = 1; b < B; b++) {
+        // SRTP_TAIL_STEP_PROTECT == 2: the loop also takes the last, partial
+        // chunk B (masked loads and stores in every iteration)
+        const int Bx = (SRTP_TAIL_STEP_PROTECT == 2 && 64 * B < L) ? B + 1 : B;
+        const int nbw = SRTP_PRIO ? wave_max_i(Bx) : 0;
+        for (b = 1; b < Bx; b++) {
             // packets past ~4 KB: the generic loop below finishes them
             if (ctr_pre_exhausted(4 * b - hq)) break;
             progress_prio(b, nbw);
@@ -2595,6 +2604,8 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #if SRTP_COALESCE == 1
             const bool full = quad_full();
             load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
+#elif SRTP_TAIL_STEP_PROTECT == 2
+            load_chunk(pkt, b, L, d);
 #else
             load_chunk_full(pkt, b, d);
 #endif
@@ -2611,6 +2622,8 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
             store_chunk_quad(a.seg, a.off[p], b, full, d);
 #elif SRTP_COALESCE == 2
             store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
+#elif SRTP_TAIL_STEP_PROTECT == 2
+            store_chunk(pkt, b, cs, d);
 #else
             store_chunk_full(pkt, b, d);
 #endif
@@ -2620,7 +2633,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         // fused step -- its keystream beside the hash of block B-1 -- instead
         // of the generic loop's unoverlapped AES and a reload of the chunk;
         // then block B (it carries the suffix) is hashed here.
-        const bool ext = SRTP_TAIL_STEP && b == B && 64 * B < L && !ctr_pre_exhausted(4 * b - hq);
+        const bool ext = SRTP_TAIL_STEP_PROTECT && b == B && 64 * B < L && !ctr_pre_exhausted(4 * b - hq);
         if (ext) {
             uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
             uint32_t K[16], d[16];
