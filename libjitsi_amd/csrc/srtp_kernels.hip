@@ -2442,16 +2442,14 @@ __device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint
 #ifndef SRTP_COALESCE
 #define SRTP_COALESCE 0
 #endif
-// SRTP_TAIL_STEP (unprotect) / SRTP_TAIL_STEP_PROTECT: the fused loop takes
-// the packet's last chunk (unprotect: the ROC-carrying one; protect: the
-// partial one) in one more fused step.  Measured (profiles/r03/
-// kernel_experiments.md): k_unprotect 0.301 -> 0.295 ms; k_protect 0.283 ->
-// 0.299 ms (its extra step spills), so off for protect.
+// SRTP_TAIL_STEP: k_unprotect's fused loop takes the packet's ROC-carrying
+// chunk in one more fused step (0.301 -> 0.296 ms per bundle).  The same for
+// k_protect's last partial chunk was measured slower either way -- as a step
+// after the loop (0.283 -> 0.299 ms: it spills) and as one more loop iteration
+// with masked loads and stores (0.322 ms) -- and is not built
+// (profiles/r03/kernel_experiments.md).
 #ifndef SRTP_TAIL_STEP
 #define SRTP_TAIL_STEP 1
-#endif
-#ifndef SRTP_TAIL_STEP_PROTECT
-#define SRTP_TAIL_STEP_PROTECT 0
 #endif
 template <int CTRL>
 __device__ __forceinline__ uint32_t qdpp(uint32_t x) {
@@ -2588,11 +2586,8 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         ctr_chunk_pre(lds, tb, rk, cp, cs, 0, c);
         store_chunk(pkt, 0, cs, c);
         const int hq = cs.off >> 4;
-        // SRTP_TAIL_STEP_PROTECT == 2: the loop also takes the last, partial
-        // chunk B (masked loads and stores in every iteration)
-        const int Bx = (SRTP_TAIL_STEP_PROTECT == 2 && 64 * B < L) ? B + 1 : B;
-        const int nbw = SRTP_PRIO ? wave_max_i(Bx) : 0;
-        for (b = 1; b < Bx; b++) {
+        const int nbw = SRTP_PRIO ? wave_max_i(B) : 0;
+        for (b = 1; b < B; b++) {
             // packets past ~4 KB: the generic loop below finishes them
             if (ctr_pre_exhausted(4 * b - hq)) break;
             progress_prio(b, nbw);
@@ -2604,8 +2599,6 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #if SRTP_COALESCE == 1
             const bool full = quad_full();
             load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
-#elif SRTP_TAIL_STEP_PROTECT == 2
-            load_chunk(pkt, b, L, d);
 #else
             load_chunk_full(pkt, b, d);
 #endif
@@ -2622,57 +2615,13 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
             store_chunk_quad(a.seg, a.off[p], b, full, d);
 #elif SRTP_COALESCE == 2
             store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
-#elif SRTP_TAIL_STEP_PROTECT == 2
-            store_chunk(pkt, b, cs, d);
 #else
             store_chunk_full(pkt, b, d);
 #endif
         }
 
-        // The last, partial chunk B (payload bytes 64B .. L-1) in one more
-        // fused step -- its keystream beside the hash of block B-1 -- instead
-        // of the generic loop's unoverlapped AES and a reload of the chunk;
-        // then block B (it carries the suffix) is hashed here.
-        const bool ext = SRTP_TAIL_STEP_PROTECT && b == B && 64 * B < L && !ctr_pre_exhausted(4 * b - hq);
-        if (ext) {
-            uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-            uint32_t K[16], d[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
-            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
-            load_chunk(pkt, b, L, d);
-            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
-#pragma unroll
-            for (int k = 0; k < 5; k++) h[k] += v[k];
-            ctr_apply(cs, b, K, d);
-#pragma unroll
-            for (int k = 0; k < 16; k++) c[k] = d[k];
-            store_chunk(pkt, b, cs, d);
-            // the rest of the MAC and the trailer here, so that nothing of the
-            // AES state stays live past this step (the generic loop below
-            // would otherwise keep it, and the step spills)
-            inner_words(c, b, L, suffix);
-            sha1_compress(h, c);
-            for (b = b + 1; b <= nb_inner; b++) {
-                uint32_t w[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) w[k] = 0u;
-                if (b < nb_inner) inner_words(w, b, L, suffix);
-                else outer_words(w, h, ks);
-                sha1_compress(h, w);
-            }
-            int o = L;
-            if (rtcp) {
-                pkt[o] = (uint8_t)(suffix >> 24); pkt[o + 1] = (uint8_t)(suffix >> 16);
-                pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
-                o += 4;
-            }
-            tag_write(h, pkt + o, T);
-            return;
-        } else {
-            inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
-            sha1_compress(h, c);
-        }
+        inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
+        sha1_compress(h, c);
     }
     // One AES site and one SHA-1 site: 64-B chunk b is loaded, encrypted in
     // place, stored, then hashed (inner blocks, then the outer block).
