@@ -240,7 +240,10 @@ def config4(torch, K, seed):
             ts += [snd[2 * j + 1].tid] * n_rtcp
             tr += [rcv[2 * j + 1].tid] * n_rtcp
         cb = synth.concat(parts)
-        perm = rng.permutation(cb.n)  # interleave the streams
+        # interleave the six sources, each keeping its own order (a random
+        # permutation would reorder a stream past the sender's replay window)
+        keys_t = np.concatenate([(np.arange(p.n) + rng.random(p.n)) / p.n for p in parts])
+        perm = np.argsort(keys_t, kind="stable")
         bundles.append(synth.select(cb, perm))
         tids_s.append(np.asarray(ts, np.int32)[perm])
         tids_r.append(np.asarray(tr, np.int32)[perm])
