@@ -190,6 +190,8 @@ def config3(torch, K, seed):
     tm = er.read_timing()
     er.set_timing(False)
     stages = {k: round(v[0] / max(v[1], 1), 4) for k, v in tm.items() if v[1]}
+    est = er.stats()
+    slow = {k: est[k] for k in ("long_walked", "repaired", "roc_rechecks")}
     stc = np.bincount(np.concatenate([d.st.cpu().numpy() for d in dev]), minlength=N.NUM_STATUS)
     pkts = sum(x.n for x in fb)
     # CPU: the oracle receiver over a sample of the last faulted bundle, after
@@ -208,7 +210,7 @@ def config3(torch, K, seed):
             "packets": pkts, "unprotect_pps": round(pkts / tu, 1),
             "gbps_algorithmic": round(sum(float((2 * x.length.astype(np.int64) - 10).sum()) for x in fb) / tu / 1e9, 1),
             "statuses": {N.STATUS_NAMES[i]: int(c) for i, c in enumerate(stc) if c},
-            "stage_ms_per_bundle": stages, "slow_path": {k: er.stats()[k] for k in ("long_walked", "repaired", "roc_rechecks") if k in er.stats()},
+            "stage_ms_per_bundle": stages, "slow_path_total": slow,
             "cpu": {"value": round(sb.n / dt, 1), "unit": "packets/s (unprotect)", "threads": 1, "kind": "port",
                     "sample": f"{sb.n} packets of the last faulted bundle, oracle unprotect"}}
 
