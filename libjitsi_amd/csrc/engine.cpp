@@ -51,6 +51,7 @@ struct srtp_engine {
     uint32_t *tailc = nullptr, *spec = nullptr;
     uint64_t *tile_link = nullptr;
     uint32_t *spos = nullptr;
+    uint32_t *lord = nullptr; // [n] crypto kernels' lane order (k_lenperm)
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     // Two control blocks (BundleCtl + e_min row), alternating per bundle: each
@@ -219,13 +220,14 @@ uint32_t next_pow2(uint64_t x) {
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
                     e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp,
-                    e->spos, e->tile_link};
+                    e->spos, e->tile_link, e->lord};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
     e->w_status = nullptr;
     e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
     e->spos = nullptr;
+    e->lord = nullptr;
     e->tile_link = nullptr;
     e->sort_temp = nullptr;
     e->scratch_n = 0;
@@ -253,6 +255,7 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
     HIPCHK(e, dalloc(&e->spec, m));
     HIPCHK(e, dalloc(&e->spos, m));
+    HIPCHK(e, dalloc(&e->lord, m));
     // walk tiles' long-chain links: granules tagged with the bundle serial + 1,
     // so zeroed memory never reads as published
     const size_t link_words = (size_t)(m / kLongMin + 2) * 10; // per walk tile
@@ -688,6 +691,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.tailc = e->tailc; a.spec = e->spec;
     a.tile_link = e->tile_link;
     a.spos = e->spos;
+    a.lord = e->lord;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     a.sort_counts = ss.counts[0];
@@ -708,6 +712,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     {
         StageTimer t(e, s, SRTP_STAGE_PARSE);
         HIPCHK(e, launch_parse(a, s)); // also resets control block c ^ 1
+        HIPCHK(e, launch_lenperm(a, s)); // returns at once for a bundle of one length class
     }
     e->ctl_clean[c ^ 1] = true;
     e->emin_filled[c ^ 1] = a.n_transformers;

@@ -65,6 +65,7 @@ struct BundleArgs {
     uint32_t *spec;        // [n] unprotect: kSpec* summary of k_unprotect (bit 0: decrypted in place under g0)
     uint64_t *tile_link;   // [(n / 256 + 2) * 10] per walk tile: the published part of a long chain
     uint32_t *spos;        // [n] unprotect: each record's position in sort order (the last sort pass)
+    uint32_t *lord;        // [n] packets grouped by length class (k_lenperm), for the crypto kernels
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse
     int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse
@@ -85,6 +86,7 @@ struct SortScratch {
 };
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
+hipError_t launch_lenperm(const BundleArgs &a, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n_max);
 SortScratch sort_scratch(void *temp, uint32_t n_max);
 // Stable LSD radix sort of (sk_in, sv_in) by key into (sk_out, sv_out),

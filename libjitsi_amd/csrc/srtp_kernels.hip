@@ -738,9 +738,16 @@ __device__ __forceinline__ uint32_t parse_one(const BundleArgs &a, uint32_t p) {
 #define SRTP_PARSE_BLOCK 256
 #endif
 constexpr int kParseBlock = SRTP_PARSE_BLOCK; // divides the sort's 2048-record tile
+// Length class of a packet for the crypto kernels' lane order: its number of
+// 64-B chunks (31: 31 or more).  One lane walks one packet chunk by chunk, so a
+// wave lasts as long as its longest packet; grouping packets by class keeps the
+// lanes of a wave busy on mixed-size bundles (k_lenperm).
+__device__ __forceinline__ uint32_t len_class(uint32_t L) { return min((L + 63u) >> 6, 31u); }
+
 __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
-    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_hist[256], s_cls[32];
     if (threadIdx.x < 256) s_hist[threadIdx.x] = 0u;
+    if (threadIdx.x < 32) s_cls[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     // reset the next bundle's control block (the previous bundle, which used
@@ -749,11 +756,62 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
     if (a.abort_on_error)
         for (uint32_t i = p; i < a.n_transformers; i += gridDim.x * blockDim.x)
             a.e_min_next[i] = 0x7f7f7f7f;
-    if (p < a.n) atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
+    if (p < a.n) {
+        atomicAdd(&s_cls[len_class(a.len[p])], 1u);
+        atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
+    }
     __syncthreads();
     const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kParseBlock
     if (threadIdx.x < 256 && s_hist[threadIdx.x])
         atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
+    if (threadIdx.x < 32) {
+        const uint32_t c = s_cls[threadIdx.x];
+        if (c) atomicAdd(&a.ctl->cls_count[threadIdx.x], c);
+        const unsigned long long m = __ballot(c != 0u);
+        if (threadIdx.x == 0 && (uint32_t)m) atomicOr(&a.ctl->len_classes, (uint32_t)m);
+    }
+}
+
+// Lane order of the crypto kernels (k_protect, k_unprotect): with packets of
+// more than one length class in the bundle, lord[] lists the packets grouped
+// by class, the longest class first, so that the lanes of a wave walk packets
+// of about the same length.  Within a class the order is whatever the
+// workgroups' reservations give: the crypto kernels treat every packet on its
+// own.  A bundle of one class (the fixed-size case) keeps lane = packet, and
+// this kernel returns at once.
+#ifndef SRTP_LEN_ORDER
+#define SRTP_LEN_ORDER 1
+#endif
+constexpr int kLenPermBlock = 256;
+__global__ __launch_bounds__(kLenPermBlock) void k_lenperm(BundleArgs a) {
+    __shared__ uint32_t s_base[32], s_cnt[32], s_off[32];
+    if (__popc(a.ctl->len_classes) <= 1) return;
+    if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0u;
+        for (int c = 31; c >= 0; c--) {
+            s_base[c] = acc;
+            acc += a.ctl->cls_count[c];
+        }
+    }
+    __syncthreads();
+    const uint32_t p = blockIdx.x * kLenPermBlock + threadIdx.x;
+    uint32_t cls = 0u, r = 0u;
+    if (p < a.n) {
+        cls = len_class(a.len[p]);
+        r = atomicAdd(&s_cnt[cls], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 32 && s_cnt[threadIdx.x])
+        s_off[threadIdx.x] = atomicAdd(&a.ctl->cls_cursor[threadIdx.x], s_cnt[threadIdx.x]);
+    __syncthreads();
+    if (p < a.n) a.lord[s_base[cls] + s_off[cls] + r] = p;
+}
+
+// The packet lane i of a crypto kernel takes (i < a.n).
+__device__ __forceinline__ uint32_t lane_packet(const BundleArgs &a, uint32_t i) {
+    if (SRTP_LEN_ORDER && __popc(a.ctl->len_classes) > 1) return a.lord[i];
+    return i;
 }
 
 // ============================================================== radix sort
@@ -2706,17 +2764,18 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     STAMP(0);
     STAMP_XCC();
     if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t p = i < a.n ? lane_packet(a, i) : i;
     fill_te4(s_te); // ends with a barrier
     STAMP(1);
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     int32_t fs = -1;
-    if (p < a.n) {
+    if (i < a.n) {
         fs = finish_status(a, p);
         atomicAdd(&s_cnt[fs & 15], 1u);
     }
     __syncthreads();
     flush_status_counts(a, s_cnt);
-    if (p >= a.n) return;
+    if (i >= a.n) return;
     const bool todo = fs == SRTP_STATUS_OK;
     const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
     const TeBase tb = te_base();
@@ -2999,8 +3058,9 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     // the packet's context state and whether it lies deep in a long chain
     // (its kLongRank-th predecessor in sort order has its context), loaded
     // while the T-tables fill
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = p < a.n;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < a.n;
+    const uint32_t p = live ? lane_packet(a, i) : i;
     uint32_t slot = kNoSlot, pos = 0u;
     if (live) {
         slot = a.p_slot[p];
@@ -3715,6 +3775,11 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock)
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_parse, dim3((a.n + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_lenperm(const BundleArgs &a, hipStream_t s) {
+    if (!SRTP_LEN_ORDER) return hipSuccess;
+    hipLaunchKernelGGL(k_lenperm, dim3((a.n + kLenPermBlock - 1) / kLenPermBlock), dim3(kLenPermBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
