@@ -51,7 +51,7 @@ struct srtp_engine {
     uint32_t *tailc = nullptr, *spec = nullptr;
     uint64_t *tile_link = nullptr;
     uint32_t *spos = nullptr;
-    uint32_t *lord = nullptr; // [n] crypto kernels' lane order (k_lenperm)
+    uint32_t *lord = nullptr; // [n] crypto kernels' lane order (the sort's first pass)
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     // Two control blocks (BundleCtl + e_min row), alternating per bundle: each
@@ -712,7 +712,6 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     {
         StageTimer t(e, s, SRTP_STAGE_PARSE);
         HIPCHK(e, launch_parse(a, s)); // also resets control block c ^ 1
-        HIPCHK(e, launch_lenperm(a, s)); // returns at once for a bundle of one length class
     }
     e->ctl_clean[c ^ 1] = true;
     e->emin_filled[c ^ 1] = a.n_transformers;

@@ -86,7 +86,6 @@ struct SortScratch {
 };
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
-hipError_t launch_lenperm(const BundleArgs &a, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n_max);
 SortScratch sort_scratch(void *temp, uint32_t n_max);
 // Stable LSD radix sort of (sk_in, sv_in) by key into (sk_out, sv_out),

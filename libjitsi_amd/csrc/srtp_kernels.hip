@@ -757,7 +757,15 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
         for (uint32_t i = p; i < a.n_transformers; i += gridDim.x * blockDim.x)
             a.e_min_next[i] = 0x7f7f7f7f;
     if (p < a.n) {
-        atomicAdd(&s_cls[len_class(a.len[p])], 1u);
+        // one LDS atomic per distinct class of the wave (a fixed-size bundle
+        // would otherwise send all 256 lanes to one word)
+        const uint32_t cls = len_class(a.len[p]);
+        const unsigned long long act = __ballot(1);
+        const int leader = __ffsll((long long)act) - 1;
+        const uint32_t lc = (uint32_t)__builtin_amdgcn_readlane((int)cls, leader);
+        const unsigned long long same = __ballot(cls == lc);
+        if (cls != lc) atomicAdd(&s_cls[cls], 1u);
+        else if ((int)(threadIdx.x & 63u) == leader) atomicAdd(&s_cls[cls], (uint32_t)__popcll(same));
         atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
     }
     __syncthreads();
@@ -775,38 +783,13 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
 // Lane order of the crypto kernels (k_protect, k_unprotect): with packets of
 // more than one length class in the bundle, lord[] lists the packets grouped
 // by class, the longest class first, so that the lanes of a wave walk packets
-// of about the same length.  Within a class the order is whatever the
-// workgroups' reservations give: the crypto kernels treat every packet on its
-// own.  A bundle of one class (the fixed-size case) keeps lane = packet, and
-// this kernel returns at once.
+// of about the same length.  The radix sort's first scatter pass writes it
+// (k_sort_scatter, SortPass::lord); within a class the order is whatever its
+// tiles' reservations give, since the crypto kernels treat every packet on its
+// own.  A bundle of one class (the fixed-size case) keeps lane = packet.
 #ifndef SRTP_LEN_ORDER
 #define SRTP_LEN_ORDER 1
 #endif
-constexpr int kLenPermBlock = 256;
-__global__ __launch_bounds__(kLenPermBlock) void k_lenperm(BundleArgs a) {
-    __shared__ uint32_t s_base[32], s_cnt[32], s_off[32];
-    if (__popc(a.ctl->len_classes) <= 1) return;
-    if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0u;
-        for (int c = 31; c >= 0; c--) {
-            s_base[c] = acc;
-            acc += a.ctl->cls_count[c];
-        }
-    }
-    __syncthreads();
-    const uint32_t p = blockIdx.x * kLenPermBlock + threadIdx.x;
-    uint32_t cls = 0u, r = 0u;
-    if (p < a.n) {
-        cls = len_class(a.len[p]);
-        r = atomicAdd(&s_cnt[cls], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 32 && s_cnt[threadIdx.x])
-        s_off[threadIdx.x] = atomicAdd(&a.ctl->cls_cursor[threadIdx.x], s_cnt[threadIdx.x]);
-    __syncthreads();
-    if (p < a.n) a.lord[s_base[cls] + s_off[cls] + r] = p;
-}
 
 // The packet lane i of a crypto kernel takes (i < a.n).
 __device__ __forceinline__ uint32_t lane_packet(const BundleArgs &a, uint32_t i) {
@@ -855,6 +838,11 @@ struct SortPass {
     uint32_t *zero;           // the previous pass's counts (this tile's row is re-zeroed), or null
     uint32_t *spos;           // last unprotect pass: spos[packet] = its sorted position, or null
     uint32_t walk_max;        // largest key of a walked record (the context table's mask)
+    // first pass only (else null): the crypto kernels' lane order by length
+    // class (see lane_packet); its input records are in packet order
+    uint32_t *lord;
+    const uint32_t *len;
+    BundleCtl *ctl;
 };
 
 #ifndef SRTP_SORT_COUNT_LOADS
@@ -962,6 +950,38 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
 #endif
         }
     }
+    if (SRTP_LEN_ORDER && sp.lord && __popc(sp.ctl->len_classes) > 1) {
+        // the lane order of the crypto kernels: this tile's packets by length
+        // class, at the class bases (longest first) plus a reserved range
+        __syncthreads(); // s_base / s_run are free again
+        uint32_t *s_cb = s_base, *s_cc = s_run, *s_co = s_run + 32;
+        if (t < 32) s_cc[t] = 0u;
+        if (t == 0) {
+            uint32_t acc = 0u;
+            for (int c = 31; c >= 0; c--) {
+                s_cb[c] = acc;
+                acc += sp.ctl->cls_count[c];
+            }
+        }
+        __syncthreads();
+        uint32_t cls[kSortItems], rk[kSortItems];
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            const uint32_t i = base + r * kSortThreads + t;
+            if (i < sp.n) {
+                cls[r] = len_class(sp.len[i]);
+                rk[r] = atomicAdd(&s_cc[cls[r]], 1u);
+            }
+        }
+        __syncthreads();
+        if (t < 32 && s_cc[t]) s_co[t] = atomicAdd(&sp.ctl->cls_cursor[t], s_cc[t]);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            const uint32_t i = base + r * kSortThreads + t;
+            if (i < sp.n) sp.lord[s_cb[cls[r]] + s_co[cls[r]] + rk[r]] = i;
+        }
+    }
 }
 
 // The next pass's digit counts per tile of this pass's output: one workgroup
@@ -1008,6 +1028,9 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
         sp.zero = q ? ss.counts[q - 1] : nullptr;
         sp.spos = last && a.reverse ? a.spos : nullptr;
         sp.walk_max = a.ctx_mask;
+        sp.lord = q == 0 ? a.lord : nullptr;
+        sp.len = a.len;
+        sp.ctl = a.ctl;
         hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
         if (!last)
             hipLaunchKernelGGL(k_sort_count, dim3(tiles), dim3(kSortThreads), 0, s, (const uint32_t *)sp.dk,
@@ -3775,11 +3798,6 @@ static inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock)
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_parse, dim3((a.n + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, s, a);
-    return hipGetLastError();
-}
-hipError_t launch_lenperm(const BundleArgs &a, hipStream_t s) {
-    if (!SRTP_LEN_ORDER) return hipSuccess;
-    hipLaunchKernelGGL(k_lenperm, dim3((a.n + kLenPermBlock - 1) / kLenPermBlock), dim3(kLenPermBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
