@@ -3136,37 +3136,64 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
 // some do (replays, forged tags, ROC guesses overturned in-bundle -- a flood of
 // them must not cost more than a decryption), the workgroup builds the LDS
 // T-tables and repairs at full AES speed.
+// Repairs are compacted within the workgroup first: the packets to repair
+// are listed in LDS and taken by the first lanes, so that a few scattered
+// repairs (replays and forgeries of a faulty link: ~2.5 % of the packets)
+// keep one wave busy instead of every wave that holds one (which costs almost
+// an AES pass over the whole bundle).
 __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords + kTeCounters];
+    __shared__ uint2 s_rep[kAesBlock]; // {packet | did << 30 | need << 31, original length}
+    __shared__ uint32_t s_nrep;
     uint32_t *s_cnt = s_te + kTeWords;
     if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_nrep = 0u;
     __syncthreads();
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t p0 = blockIdx.x * blockDim.x + threadIdx.x;
     bool repair = false, did = false, need = false;
-    uint32_t ks_id = 0;
     int L0 = 0;
-    if (p < a.n) {
+    if (p0 < a.n) {
         // every per-packet word first, all in flight together (the status
         // stores below would otherwise order the loads after them)
-        L0 = (int)a.len[p];
-        const uint32_t slot = a.p_slot[p];
-        const uint32_t sw = a.spec[p]; // k_unprotect's summary: no context / key-set loads
-        const uint32_t cw = a.w_cw[p], g0 = a.g0[p];
-        const int32_t st = finish_status(a, p);
+        L0 = (int)a.len[p0];
+        const uint32_t slot = a.p_slot[p0];
+        const uint32_t sw = a.spec[p0]; // k_unprotect's summary: no context / key-set loads
+        const uint32_t cw = a.w_cw[p0], g0 = a.g0[p0];
+        const int32_t st = finish_status(a, p0);
         atomicAdd(&s_cnt[st & 15], 1u);
         if (slot != kNoSlot) {
             did = (sw & kSpecDid) != 0u;
             const bool rtp = (sw & kSpecRtp) != 0u;
             if (st == SRTP_STATUS_OK && (sw & kSpecAes)) need = rtp ? !(sw & kSpecSkip) : (cw & 0x80000000u) != 0;
             repair = (did || need) && !(did && need && (!rtp || g0 == cw));
-            if (repair) ks_id = a.ctx[slot].ks;
         }
     }
-    const bool any_repair = __syncthreads_or(repair);
+    {   // list this wave's repairs (one LDS atomic per wave)
+        const unsigned long long m = __ballot(repair);
+        if (m) {
+            const uint32_t lane = threadIdx.x & 63u;
+            const int first = __ffsll((long long)m) - 1;
+            uint32_t base = 0u;
+            if ((int)lane == first) base = atomicAdd(&s_nrep, (uint32_t)__popcll(m));
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);
+            if (repair) {
+                const uint32_t k = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                s_rep[k] = make_uint2(p0 | (did ? 1u << 30 : 0u) | (need ? 1u << 31 : 0u), (uint32_t)L0);
+            }
+        }
+    }
+    __syncthreads();
     flush_status_counts(a, s_cnt);
-    if (!any_repair) return; // the common case: speculation was right
+    const uint32_t nrep = s_nrep;
+    if (nrep == 0u) return; // the common case: speculation was right
     fill_te4(s_te);
-    if (!repair) return;
+    if (threadIdx.x >= nrep) return;
+    const uint2 job = s_rep[threadIdx.x];
+    const uint32_t p = job.x & 0x3fffffffu;
+    did = (job.x >> 30) & 1u;
+    need = (job.x >> 31) != 0u;
+    L0 = (int)job.y;
+    const uint32_t ks_id = a.ctx[a.p_slot[p]].ks;
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
     for_each_keyset(true, ks_id, [&](uint32_t ks_u) {
