@@ -3137,10 +3137,11 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
 // them must not cost more than a decryption), the workgroup builds the LDS
 // T-tables and repairs at full AES speed.
 // Repairs are compacted within the workgroup first: the packets to repair
-// are listed in LDS and taken by the first lanes, so that a few scattered
+// are listed in LDS and their 64-B chunks spread over the lanes, one chunk
+// per lane (counter-mode blocks are independent), so that a few scattered
 // repairs (replays and forgeries of a faulty link: ~2.5 % of the packets)
-// keep one wave busy instead of every wave that holds one (which costs almost
-// an AES pass over the whole bundle).
+// cost one short AES step instead of every wave that holds one walking its
+// packet chunk by chunk (which cost almost an AES pass over the bundle).
 __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords + kTeCounters];
     __shared__ uint2 s_rep[kAesBlock]; // {packet | did << 30 | need << 31, original length}
@@ -3186,57 +3187,121 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
     flush_status_counts(a, s_cnt);
     const uint32_t nrep = s_nrep;
     if (nrep == 0u) return; // the common case: speculation was right
+    // Each listed packet's chunks become jobs, one chunk per lane: a packet's
+    // keystream blocks are independent, so no lane walks a whole packet.
+    // s_pref[k] = jobs of the packets before k (the T-table image is built
+    // after this scan; its LDS is not used yet).
+    uint32_t *s_pref = s_te; // [kAesBlock + 1]
+    if (threadIdx.x < nrep) {
+        const uint2 job = s_rep[threadIdx.x];
+        s_pref[threadIdx.x + 1] = (job.y + 63u) >> 6; // chunks of [0, L0)
+    }
+    if (threadIdx.x == 0) s_pref[0] = 0u;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (uint32_t k = 1; k <= nrep; k++) s_pref[k] += s_pref[k - 1];
+    __syncthreads();
+    const uint32_t n_jobs = s_pref[nrep];
+    // the job list is kept in registers (one round of up to 4 jobs per lane),
+    // since the table fill below overwrites s_pref
+    constexpr int kJobsPerLane = 4;
+    uint32_t jk[kJobsPerLane], jc[kJobsPerLane];
+    int n_mine = 0;
+#pragma unroll
+    for (int q = 0; q < kJobsPerLane; q++) {
+        const uint32_t j = threadIdx.x + (uint32_t)q * kAesBlock;
+        jk[q] = 0u;
+        jc[q] = 0u;
+        if (j < n_jobs) {
+            uint32_t lo = 0u, hi = nrep; // last k with s_pref[k] <= j
+            while (hi - lo > 1u) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pref[mid] <= j) lo = mid;
+                else hi = mid;
+            }
+            jk[q] = lo;
+            jc[q] = j - s_pref[lo];
+            n_mine = q + 1;
+        }
+    }
+    const bool overflow = n_jobs > (uint32_t)kJobsPerLane * kAesBlock; // > 4096 chunks: whole packets
+    __syncthreads();
     fill_te4(s_te);
-    if (threadIdx.x >= nrep) return;
-    const uint2 job = s_rep[threadIdx.x];
-    const uint32_t p = job.x & 0x3fffffffu;
-    did = (job.x >> 30) & 1u;
-    need = (job.x >> 31) != 0u;
-    L0 = (int)job.y;
-    const uint32_t ks_id = a.ctx[a.p_slot[p]].ks;
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
-    for_each_keyset(true, ks_id, [&](uint32_t ks_u) {
-        const KeySet *ks = a.keysets + ks_u;
-        RoundKeys rk;
-        load_round_keys_uniform(ks, rk);
-        uint8_t *pkt = a.seg + a.off[p];
-        const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
-        const int T = ks->tag_len;
-        const bool mac = ks->auth_type != SRTP_NULL_AUTHENTICATION;
-        Ctr spec, real;
-        if (ks->kind == SRTP_KIND_RTP) {
-            real.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-            real.end = mac ? (L0 - T > 0 ? L0 - T : 0) : L0;
-            make_iv_rtp(ks, hdr, a.g0[p], spec.iv);
-            make_iv_rtp(ks, hdr, a.w_cw[p], real.iv);
+    // (rare) more chunks than jobs: lane k < nrep walks packet k whole
+    const int rounds = overflow ? 1 : n_mine;
+    for (int q = 0; q < (overflow ? 1 : kJobsPerLane); q++) {
+        bool act;
+        uint32_t k, c_first, c_last;
+        if (overflow) {
+            act = threadIdx.x < nrep;
+            k = threadIdx.x;
+            c_first = 0u;
+            c_last = 0xffffu;
         } else {
-            real.off = 8;
-            real.end = mac ? (L0 - T - 4 > 0 ? L0 - T - 4 : 0) : L0;
-            const uint32_t sidx = ld_be32(pkt + L0 - 4 - T) & 0x7FFFFFFFu;
-            make_iv_rtcp(ks, hdr, sidx, spec.iv);
-            make_iv_rtcp(ks, hdr, a.w_cw[p] & 0x7FFFFFFFu, real.iv);
+            act = q < rounds;
+            k = jk[q];
+            c_first = c_last = jc[q];
         }
-        if (real.off < 0 || real.off > real.end) real.off = real.end; // nothing to cipher
-        spec.off = real.off;
-        spec.end = did ? real.end : 0;
-        const int end = real.end;
-        if (!need) real.end = 0;
+        const uint2 job = act ? s_rep[k] : make_uint2(0u, 0u);
+        const uint32_t p = job.x & 0x3fffffffu;
+        const bool jdid = (job.x >> 30) & 1u;
+        const bool jneed = (job.x >> 31) != 0u;
+        const int jL0 = (int)job.y;
+        const uint32_t ks_id = act ? a.ctx[a.p_slot[p]].ks : 0u;
+        for_each_keyset(act, ks_id, [&](uint32_t ks_u) {
+            const KeySet *ks = a.keysets + ks_u;
+            RoundKeys rk;
+            load_round_keys_uniform(ks, rk);
+            uint8_t *pkt = a.seg + a.off[p];
+            const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+            const int T = ks->tag_len;
+            const bool mac = ks->auth_type != SRTP_NULL_AUTHENTICATION;
+            Ctr spec, real;
+            if (ks->kind == SRTP_KIND_RTP) {
+                real.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+                real.end = mac ? (jL0 - T > 0 ? jL0 - T : 0) : jL0;
+                make_iv_rtp(ks, hdr, a.g0[p], spec.iv);
+                make_iv_rtp(ks, hdr, a.w_cw[p], real.iv);
+            } else {
+                real.off = 8;
+                real.end = mac ? (jL0 - T - 4 > 0 ? jL0 - T - 4 : 0) : jL0;
+                const uint32_t sidx = ld_be32(pkt + jL0 - 4 - T) & 0x7FFFFFFFu;
+                make_iv_rtcp(ks, hdr, sidx, spec.iv);
+                make_iv_rtcp(ks, hdr, a.w_cw[p] & 0x7FFFFFFFu, real.iv);
+            }
+            if (real.off < 0 || real.off > real.end) real.off = real.end; // nothing to cipher
+            spec.off = real.off;
+            spec.end = jdid ? real.end : 0;
+            const int end = real.end;
+            if (!jneed) real.end = 0;
+            Ctr span = real;
+            span.end = end;
+            const int c0 = max((int)c_first, span.off >> 6);
+            // keystream carry into chunk c0: block 4 c0 - off/16 - 1 (zero when
+            // c0 holds `off`: the words before it are masked)
+            const int hq = span.off >> 4;
 #pragma unroll
-        for (int k = 0; k < 4; k++) spec.carry[k] = real.carry[k] = 0u;
-        Ctr span = real;
-        span.end = end;
-        // chunks from the one holding `off` (words before it are masked, so
-        // the keystream carry may start at zero there)
-        for (int c = span.off >> 6; 64 * c < end; c++) {
-            uint32_t d[16];
-            load_chunk(pkt, c, end, d);
-            if (did) ctr_chunk(lds, tb, rk, spec, c, d);
-            if (need) ctr_chunk(lds, tb, rk, real, c, d);
-            store_chunk(pkt, c, span, d);
-        }
-    });
-    atomicAdd(&a.counters[kCtrRepaired], 1ull);
+            for (int k2 = 0; k2 < 4; k2++) spec.carry[k2] = real.carry[k2] = 0u;
+            if (c0 > (span.off >> 6) && 64 * c0 < end) {
+                uint32_t x[4], y[4];
+                ctr_input(spec.iv, 4 * c0 - hq - 1, x);
+                ctr_input(real.iv, 4 * c0 - hq - 1, y);
+                aes_encrypt2(lds, tb, rk, x, y);
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++) { spec.carry[k2] = x[k2]; real.carry[k2] = y[k2]; }
+            }
+            for (int c = c0; c <= (int)c_last && 64 * c < end; c++) {
+                uint32_t d[16];
+                load_chunk(pkt, c, end, d);
+                if (jdid) ctr_chunk(lds, tb, rk, spec, c, d);
+                if (jneed) ctr_chunk(lds, tb, rk, real, c, d);
+                store_chunk(pkt, c, span, d);
+            }
+        });
+        if (act && c_first == 0u) atomicAdd(&a.counters[kCtrRepaired], 1ull);
+    }
 }
 
 // ============================================================== k_ext
