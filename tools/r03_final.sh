@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-3 final evidence of the committed tree: the GPU suite, smoke, the
+# bench line as the driver runs it and at the default step count, every
+# BASELINE config, aggregator throughput, then the profile passes
+# (tools/r03_prof.sh: kernel traces, PMC, calibration, timeline).
+# A crash or time limit (exit >= 124) ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${R03_TAG:-r03z}
+mkdir -p $O
+t() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?
+  echo "== $name exit $rc"; tail -2 $O/$name.log | cut -c1-400
+  if [ $rc -ge 124 ]; then echo "STOP after $name ($rc)"; exit $rc; fi
+  return 0
+}
+t gpu 300 python -u -m pytest -q --timeout 150 --timeout-method thread -p no:cacheprovider tests -m gpu
+t smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
+t bench20 180 python bench.py --gpus 1 --steps 20 --warmup 5
+t bench100 180 python bench.py
+t configs 300 python -u tools/config_bench.py --out $O/configs.json
+t agg_bench 120 ./tools/agg_bench 1.5
+R03_TAG=${R03_TAG:-r03z}/prof ./tools/r03_prof.sh
