@@ -52,6 +52,7 @@ struct srtp_engine {
     uint64_t *tile_link = nullptr;
     uint32_t *spos = nullptr;
     uint32_t *lord = nullptr; // [n] crypto kernels' lane order (the sort's first pass)
+    uint32_t *cls_tile = nullptr; // [tiles][33] length classes per sort tile (k_parse, zeroed by k_walk)
     void *sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     // Two control blocks (BundleCtl + e_min row), alternating per bundle: each
@@ -220,7 +221,7 @@ uint32_t next_pow2(uint64_t x) {
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
                     e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp,
-                    e->spos, e->tile_link, e->lord};
+                    e->spos, e->tile_link, e->lord, e->cls_tile};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
@@ -228,6 +229,7 @@ void free_scratch(srtp_engine *e) {
     e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
     e->spos = nullptr;
     e->lord = nullptr;
+    e->cls_tile = nullptr;
     e->tile_link = nullptr;
     e->sort_temp = nullptr;
     e->scratch_n = 0;
@@ -256,6 +258,11 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->spec, m));
     HIPCHK(e, dalloc(&e->spos, m));
     HIPCHK(e, dalloc(&e->lord, m));
+    {
+        const size_t words = (size_t)((m + 2047u) / 2048u) * 33u;
+        HIPCHK(e, dalloc(&e->cls_tile, words));
+        HIPCHK(e, hipMemset(e->cls_tile, 0, words * 4));
+    }
     // walk tiles' long-chain links: granules tagged with the bundle serial + 1,
     // so zeroed memory never reads as published
     const size_t link_words = (size_t)(m / kLongMin + 2) * 10; // per walk tile
@@ -692,6 +699,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.tile_link = e->tile_link;
     a.spos = e->spos;
     a.lord = e->lord;
+    a.cls_tile = e->cls_tile;
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     a.sort_counts = ss.counts[0];

@@ -65,7 +65,9 @@ struct BundleArgs {
     uint32_t *spec;        // [n] unprotect: kSpec* summary of k_unprotect (bit 0: decrypted in place under g0)
     uint64_t *tile_link;   // [(n / 256 + 2) * 10] per walk tile: the published part of a long chain
     uint32_t *spos;        // [n] unprotect: each record's position in sort order (the last sort pass)
-    uint32_t *lord;        // [n] packets grouped by length class (k_lenperm), for the crypto kernels
+    uint32_t *lord;        // [n] packets grouped by length class (the sort's first pass), for the crypto kernels
+    uint32_t *cls_tile;    // [tiles][33] per 2048-packet tile: packets per length class, the class mask
+                           // (k_parse; zeroed again by k_walk)
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse
     int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse

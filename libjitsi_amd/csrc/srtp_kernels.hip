@@ -743,6 +743,7 @@ constexpr int kParseBlock = SRTP_PARSE_BLOCK; // divides the sort's 2048-record 
 // wave lasts as long as its longest packet; grouping packets by class keeps the
 // lanes of a wave busy on mixed-size bundles (k_lenperm).
 __device__ __forceinline__ uint32_t len_class(uint32_t L) { return min((L + 63u) >> 6, 31u); }
+constexpr uint32_t kClsWords = 33; // per tile: 32 class counts + the class mask
 
 __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
     __shared__ uint32_t s_hist[256], s_cls[32];
@@ -772,11 +773,11 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
     const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kParseBlock
     if (threadIdx.x < 256 && s_hist[threadIdx.x])
         atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
-    if (threadIdx.x < 32) {
+    if (threadIdx.x < 32) { // per 2048-packet tile: at most 8 parse blocks share a word
         const uint32_t c = s_cls[threadIdx.x];
-        if (c) atomicAdd(&a.ctl->cls_count[threadIdx.x], c);
+        if (c) atomicAdd(&a.cls_tile[tile * kClsWords + threadIdx.x], c);
         const unsigned long long m = __ballot(c != 0u);
-        if (threadIdx.x == 0 && (uint32_t)m) atomicOr(&a.ctl->len_classes, (uint32_t)m);
+        if (threadIdx.x == 0 && (uint32_t)m) atomicOr(&a.cls_tile[tile * kClsWords + 32], (uint32_t)m);
     }
 }
 
@@ -843,6 +844,7 @@ struct SortPass {
     uint32_t *lord;
     const uint32_t *len;
     BundleCtl *ctl;
+    const uint32_t *cls_tile;
 };
 
 #ifndef SRTP_SORT_COUNT_LOADS
@@ -950,17 +952,36 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
 #endif
         }
     }
-    if (SRTP_LEN_ORDER && sp.lord && __popc(sp.ctl->len_classes) > 1) {
+    if (SRTP_LEN_ORDER && sp.lord) {
         // the lane order of the crypto kernels: this tile's packets by length
-        // class, at the class bases (longest first) plus a reserved range
-        __syncthreads(); // s_base / s_run are free again
-        uint32_t *s_cb = s_base, *s_cc = s_run, *s_co = s_run + 32;
-        if (t < 32) s_cc[t] = 0u;
+        // class, at the class bases (longest first) plus a reserved range --
+        // when the bundle has more than one class (k_parse's per-tile masks)
+        __syncthreads(); // s_base / s_run / s_wcnt are free again
+        uint32_t *s_cb = s_base, *s_cc = s_run, *s_co = s_run + 32, *s_tot = s_run + 64;
+        if (t < 64) {
+            uint32_t m = 0u;
+            for (uint32_t u = (uint32_t)t; u < sp.tiles; u += 64u) m |= sp.cls_tile[u * kClsWords + 32];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+            if (t == 0) {
+                s_run[96] = m;
+                if (tile == 0u) sp.ctl->len_classes = m; // read by the crypto kernels' lane_packet
+            }
+        }
+        __syncthreads();
+        if (__popc(s_run[96]) <= 1) return; // one class: lane = packet
+        if (t < 32) {
+            uint32_t tot = 0u;
+            for (uint32_t u = 0u; u < sp.tiles; u++) tot += sp.cls_tile[u * kClsWords + t];
+            s_tot[t] = tot;
+            s_cc[t] = 0u;
+        }
+        __syncthreads();
         if (t == 0) {
             uint32_t acc = 0u;
             for (int c = 31; c >= 0; c--) {
                 s_cb[c] = acc;
-                acc += sp.ctl->cls_count[c];
+                acc += s_tot[c];
             }
         }
         __syncthreads();
@@ -1031,6 +1052,7 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
         sp.lord = q == 0 ? a.lord : nullptr;
         sp.len = a.len;
         sp.ctl = a.ctl;
+        sp.cls_tile = a.cls_tile;
         hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
         if (!last)
             hipLaunchKernelGGL(k_sort_count, dim3(tiles), dim3(kSortThreads), 0, s, (const uint32_t *)sp.dk,
@@ -2144,10 +2166,14 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     const bool chains = !two_pass && a.debug == 0;
     const bool chain_pass = limit_pass && !two_pass;
     if (chain_pass && a.ctl->n_long == 0u) return; // no long chain in this bundle
-    if (!limit_pass) // the sort's last digit counts, zero again for the next bundle
+    if (!limit_pass) { // the sort's last digit counts and k_parse's class counts, zero again for the next bundle
         for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words;
              i += gridDim.x * kWalkBlock)
             a.sort_zero[i] = 0u;
+        for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words / 256u * kClsWords;
+             i += gridDim.x * kWalkBlock)
+            a.cls_tile[i] = 0u;
+    }
     // The chain pass takes its tile from a ticket counter: a tile that waits on
     // the tiles before it for a long chain's state only waits on tiles already
     // running.
