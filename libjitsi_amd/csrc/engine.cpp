@@ -259,7 +259,8 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->spos, m));
     HIPCHK(e, dalloc(&e->lord, m));
     {
-        const size_t words = (size_t)((m + 2047u) / 2048u) * 33u;
+        const uint32_t st = sort_tile_records();
+        const size_t words = (size_t)((m + st - 1u) / st) * 33u;
         HIPCHK(e, dalloc(&e->cls_tile, words));
         HIPCHK(e, hipMemset(e->cls_tile, 0, words * 4));
     }
@@ -704,7 +705,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.sort_passes = (e->ctx_bits + 1 + 7) / 8; // keys: slot or ctx_cap (= not walked)
     a.sort_counts = ss.counts[0];
     a.sort_zero = ss.counts[a.sort_passes - 1];
-    a.sort_zero_words = ((n + 2047u) / 2048u) * 256u; // tiles of this bundle x 256 digits
+    a.sort_zero_words = ((n + sort_tile_records() - 1u) / sort_tile_records()) * 256u; // tiles of this bundle x 256 digits
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;
     a.ctl = e->ctl + c;

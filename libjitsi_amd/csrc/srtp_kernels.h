@@ -66,14 +66,14 @@ struct BundleArgs {
     uint64_t *tile_link;   // [(n / 256 + 2) * 10] per walk tile: the published part of a long chain
     uint32_t *spos;        // [n] unprotect: each record's position in sort order (the last sort pass)
     uint32_t *lord;        // [n] packets grouped by length class (the sort's first pass), for the crypto kernels
-    uint32_t *cls_tile;    // [tiles][33] per 2048-packet tile: packets per length class, the class mask
+    uint32_t *cls_tile;    // [tiles][33] per sort tile: packets per length class, the class mask
                            // (k_parse; zeroed again by k_walk)
     int32_t *e_min;        // [n_transformers] first throwing packet per transformer
     BundleCtl *ctl_next;   // the next bundle's control block, reset by k_parse
     int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse
     BundleCtl *ctl;
     // radix sort of the walk records (srtp_kernels.hip "radix sort")
-    uint32_t *sort_counts; // [tiles][256] first-digit counts per 2048-record tile, by k_parse
+    uint32_t *sort_counts; // [tiles][256] first-digit counts per sort tile, by k_parse
     int32_t sort_passes;   // 8-bit digits to sort (key width / 8, rounded up)
     uint32_t *sort_zero;   // the last pass's digit counts, re-zeroed by k_walk
     uint32_t sort_zero_words;
@@ -89,6 +89,7 @@ struct SortScratch {
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n_max);
+uint32_t sort_tile_records(); // records per sort tile (k_parse's class and digit counts, the sort's tiles)
 SortScratch sort_scratch(void *temp, uint32_t n_max);
 // Stable LSD radix sort of (sk_in, sv_in) by key into (sk_out, sv_out),
 // a.sort_passes passes of 8 bits; zeroes the other parity's histograms.

@@ -744,6 +744,13 @@ constexpr int kParseBlock = SRTP_PARSE_BLOCK; // divides the sort's 2048-record 
 // lanes of a wave busy on mixed-size bundles (k_lenperm).
 __device__ __forceinline__ uint32_t len_class(uint32_t L) { return min((L + 63u) >> 6, 31u); }
 constexpr uint32_t kClsWords = 33; // per tile: 32 class counts + the class mask
+// The radix sort's tile (see "radix sort" below): 512 threads x kSortItems records.
+#ifndef SRTP_SORT_ITEMS
+#define SRTP_SORT_ITEMS 4
+#endif
+constexpr int kSortThreads = 512, kSortItems = SRTP_SORT_ITEMS, kSortTile = kSortThreads * kSortItems;
+static_assert(kSortTile % kParseBlock == 0 && kParseBlock >= 256, "k_parse tiles");
+uint32_t sort_tile_records() { return (uint32_t)kSortTile; }
 
 __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
     __shared__ uint32_t s_hist[256], s_cls[32];
@@ -770,10 +777,10 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
         atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
     }
     __syncthreads();
-    const uint32_t tile = (blockIdx.x * blockDim.x) / 2048u; // kSortTile, a multiple of kParseBlock
+    const uint32_t tile = (blockIdx.x * blockDim.x) / (uint32_t)kSortTile; // a multiple of kParseBlock
     if (threadIdx.x < 256 && s_hist[threadIdx.x])
         atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
-    if (threadIdx.x < 32) { // per 2048-packet tile: at most 8 parse blocks share a word
+    if (threadIdx.x < 32) { // per sort tile: at most kSortTile / kParseBlock parse blocks share a word
         const uint32_t c = s_cls[threadIdx.x];
         if (c) atomicAdd(&a.cls_tile[tile * kClsWords + threadIdx.x], c);
         const unsigned long long m = __ballot(c != 0u);
@@ -806,8 +813,6 @@ __device__ __forceinline__ uint32_t lane_packet(const BundleArgs &a, uint32_t i)
 // bases and ranks the tile's digits stably in LDS.  Two launches for a
 // two-digit sort and no memsets: pass q re-zeroes pass q-1's counts, k_walk
 // the last pass's.
-constexpr int kSortThreads = 512, kSortItems = 4, kSortTile = kSortThreads * kSortItems;
-static_assert(kSortTile == 2048 && kSortTile % kParseBlock == 0 && kParseBlock >= 256, "k_parse tiles");
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
