@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SRTP_MI355X_ABI_VERSION 2
+#define SRTP_MI355X_ABI_VERSION 3
 
 /* SRTPPolicy constants (transform/srtp/SRTPPolicy.java:29-63) */
 #define SRTP_NULL_ENCRYPTION 0
@@ -213,6 +213,9 @@ typedef struct {
     uint64_t long_walked;                /* packets of chains of 32+ packets that the wave-wide
                                             speculation could not take and were walked one at
                                             a time (the slow path) */
+    uint64_t holes;                      /* bundle-former holes: SRTP_PKT_FLAG_SKIP entries of no
+                                            transformer (tid < 0) that srtp_aggregator_* seals
+                                            unclaimed; not in status[SRTP_STATUS_SKIPPED] */
 } srtp_stats;
 int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
 
@@ -305,6 +308,14 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
 int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                          int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes);
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
+/* srtp_pipeline_submit with the bundle's abort-on-throw chosen per bundle:
+ * abort_on_error = -1 the engine's option, 1 SinglePacketTransformer's abort of
+ * a throwing transformer's later packets (one RawPacket[] call), 0 none (every
+ * packet its own 1-element array: the bundle former's bundles).  One engine
+ * can so serve both kinds of call with the same contexts. */
+int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                            int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                            int32_t abort_on_error);
 
 /* Bundle aggregator over the pipeline: per-packet submits
  * from any number of threads become bundles.  Replaces the reference's
@@ -324,12 +335,13 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
  * of one direction -- and thus of one transformer -- complete in the order
  * they were accepted (per submitting thread when several threads submit).
  * Every packet is its own 1-element array, as in the reference: one packet's
- * exception (SRTP_STATUS_ERR_MALFORMED) does not stop the others, which
- * requires an engine with abort_on_error = 0 (srtp_aggregator_create returns
- * SRTP_EINVAL otherwise).  When every slot is sealed or in flight, submit
- * blocks (backpressure).  flush seals the open bundles and waits until every
- * packet accepted before it has completed; destroy does the same, then stops
- * the threads.  Submits take no lock: each thread fills its own block of 16
+ * exception (SRTP_STATUS_ERR_MALFORMED) does not stop the others (the bundles
+ * run without abort-on-throw whatever the engine's abort_on_error, so one
+ * engine or dispatcher serves this and srtp_rawpacket_transform alike).  When
+ * every slot is sealed or in flight, submit blocks (backpressure).  flush
+ * seals the open bundles and waits until every packet accepted before it has
+ * completed; destroy refuses new submits (SRTP_EINVAL, also from callbacks),
+ * waits until every accepted packet has completed, then stops the threads.  Submits take no lock: each thread fills its own block of 16
  * entries of the open bundle (one compare-and-swap per block on the bundle,
  * one per packet on the thread's own block), so producers do not share a
  * written cache line per packet; entries of a block left unclaimed when the
@@ -340,13 +352,18 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
  * aggregator frees, ahead of other producers.  Producers outside callbacks
  * leave one slot of each lane (depth - 1 usable) for callback submits.  flush
  * from a callback returns SRTP_EINVAL and destroy from a callback does
- * nothing. */
+ * nothing.  cb may be NULL for an aggregator that serves only synchronous
+ * calls (srtp_aggregator_transform); srtp_aggregator_submit then returns
+ * SRTP_EINVAL. */
 typedef struct srtp_aggregator srtp_aggregator;
+#define SRTP_AGG_SEAL_IDLE 0x1 /* seal a lane's open bundle at once while the lane has no
+                                  bundle in flight (adaptive: bundles grow with the load) */
 typedef struct {
     uint32_t max_packets; /* per bundle, default 1<<14 */
     size_t max_bytes;     /* per bundle (segment), default 24 MB */
     uint32_t deadline_us; /* default 1000 */
     int32_t depth;        /* pipeline slots (3..16), default 4 */
+    uint32_t flags;       /* SRTP_AGG_*, default SRTP_AGG_SEAL_IDLE */
 } srtp_aggregator_opts;
 typedef void (*srtp_aggregator_cb)(void *user, uint64_t cookie, int32_t status, const uint8_t *data,
                                    uint32_t len);
@@ -359,6 +376,28 @@ int srtp_aggregator_flush(srtp_aggregator *a);
 int srtp_aggregator_stats(srtp_aggregator *a, uint64_t *accepted, uint64_t *completed,
                           uint64_t *bundles);
 void srtp_aggregator_destroy(srtp_aggregator *a);
+/* The synchronous per-packet call: SinglePacketTransformer.transform /
+ * reverseTransform(RawPacket) (SinglePacketTransformer.java:113,169 as
+ * SRTPTransformer.java:185-219 / SRTCPTransformer.java:175-207 implement
+ * it) from any number of threads at once.  The packet -- copy_len bytes of
+ * pkt (what lies behind its length, e.g. an extension header the reference
+ * reads past it), RTP/RTCP length len, buffer room cap >= len (in-place
+ * protect needs 16 bytes behind the packet) -- joins the lane's open bundle
+ * like a submit, so concurrent callers share bundles; the call returns when
+ * its bundle has completed, with the packet's final status, length and bytes
+ * (max(len, *out_len) bytes to out, which holds at least cap bytes).  It
+ * never calls the aggregator's callback.  With SRTP_AGG_SEAL_IDLE a call into
+ * an idle lane is sealed at once, so a lone caller waits one GPU round trip
+ * and concurrent callers coalesce behind the bundle in flight; deadline_us
+ * bounds the wait for a seal otherwise.  Not from a callback (SRTP_EINVAL). */
+int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt,
+                              uint32_t copy_len, uint32_t len, uint32_t cap, uint32_t flags,
+                              uint8_t *out, int32_t *status, uint32_t *out_len);
+/* Transformer t's kind (read without a lock after the first call) and, when
+ * fwd_rtcp_tag_len != NULL, its forward factory's SRTCP tag length
+ * (srtp_transformer_info on the first shard). */
+int srtp_aggregator_transformer_info(srtp_aggregator *a, int32_t t, int32_t *kind,
+                                     int32_t *fwd_rtcp_tag_len);
 
 /* In-process multi-GPU dispatcher (SURVEY.md 8b engine_create(devices, opts),
  * 8e): one engine per shard, shard i on device devices[i] (a device may host
@@ -460,6 +499,26 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
                              uint32_t *length, const uint32_t *flags, int32_t *status,
                              uint32_t *need_len, uint32_t n, int32_t *thrown);
 int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **data, uint32_t *len);
+/* One RawPacket through SinglePacketTransformer.transform / reverseTransform
+ * (RawPacket) (SinglePacketTransformer.java:113,169; every
+ * RTPConnector*Stream call and DtlsPacketTransformer.transformSrtp,
+ * DtlsPacketTransformer.java:1544-1564, hands the transformer one packet at
+ * a time), coalesced with concurrent callers' packets through the aggregator
+ * (srtp_aggregator_transform).  The element marshalling and write-back are
+ * srtp_rawpacket_transform's for an array of one: buf (NULL: a null element)
+ * of buf_len bytes holds the packet at offset with *length bytes; *status,
+ * *length and the bytes in buf are updated in place; *need_len != 0 where the
+ * reference reallocates (RawPacket.append / grow), the result then being the
+ * first *need_len bytes of grow, which must hold grow_cap >= *length + 16
+ * bytes and at least the bytes from offset to the end of buf (min 65535).
+ * SRTP_STATUS_ERR_MALFORMED: the reference throws (the packet keeps its
+ * partial mutation); the caller rethrows. */
+int srtp_rawpacket_transform_one(srtp_aggregator *a, int32_t reverse, int32_t tid, uint8_t *buf,
+                                 uint32_t buf_len, uint32_t offset, uint32_t *length, uint32_t flags,
+                                 int32_t *status, uint32_t *need_len, uint8_t *grow, uint32_t grow_cap);
+/* Devices the engine can use (hipGetDeviceCount; 0 without a GPU): what the
+ * Java drop-in sizes its dispatcher with. */
+int32_t srtp_device_count(void);
 
 /* Control-plane crypto without a GPU (used by CPU-side tests): RFC 3711 4.3
  * session keys exactly as SRTPCryptoContext.deriveSrtpKeys (rtcp = 0) /

@@ -26,7 +26,8 @@ STATUS_NAMES = ["OK", "DROP_REPLAY", "DROP_AUTH", "DROP_VERSION", "DROP_NO_CONTE
                 "ERR_INTERNAL"]
 NUM_STATUS = len(STATUS_NAMES)
 DEBUG_FORCE_CHAIN_STALL = 0x1
-ABI_VERSION = 2
+ABI_VERSION = 3
+AGG_SEAL_IDLE = 0x1
 PKT_FLAG_DISCARD, PKT_FLAG_SILENCE, PKT_FLAG_SKIP = 0x2, 0x4, 0x80000000
 RC = {0: "SRTP_OK", -1: "SRTP_EINVAL", -2: "SRTP_ENOMEM", -3: "SRTP_EFULL", -4: "SRTP_EDEVICE",
       -5: "SRTP_EPOLICY"}
@@ -56,7 +57,8 @@ EXPORTED = [
     "srtp_dispatch_route", "srtp_aggregator_create_dispatch", "srtp_transformer_info",
     "srtp_rawpacket_batch_create", "srtp_rawpacket_batch_create_dispatch",
     "srtp_rawpacket_batch_destroy", "srtp_rawpacket_transform", "srtp_rawpacket_result",
-    "srtp_dispatch_host_times",
+    "srtp_dispatch_host_times", "srtp_pipeline_submit_ex", "srtp_aggregator_transform",
+    "srtp_aggregator_transformer_info", "srtp_rawpacket_transform_one", "srtp_device_count",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -89,7 +91,8 @@ class Stats(C.Structure):
     _fields_ = ([("bundles", C.c_uint64), ("packets", C.c_uint64),
                  ("status", C.c_uint64 * NUM_STATUS)] +
                 [(n, C.c_uint64) for n in ("roc_rechecks", "repaired", "ctx_overflow", "ctx_live",
-                                           "ctx_tombstones", "ctx_slots", "rehashes", "chain_stalls", "long_walked")])
+                                           "ctx_tombstones", "ctx_slots", "rehashes", "chain_stalls", "long_walked",
+                                           "holes")])
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "status"}
@@ -107,7 +110,7 @@ class DtlsKeys(C.Structure):
 
 class AggregatorOpts(C.Structure):
     _fields_ = [("max_packets", C.c_uint32), ("max_bytes", C.c_size_t), ("deadline_us", C.c_uint32),
-                ("depth", C.c_int32)]
+                ("depth", C.c_int32), ("flags", C.c_uint32)]
 
 
 AGG_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(C.c_uint8), C.c_uint32)
@@ -177,6 +180,12 @@ def lib() -> C.CDLL:
     L.srtp_pipeline_slot_get.argtypes = [vp, i32, C.POINTER(PipelineSlot)]
     L.srtp_pipeline_submit.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t]
     L.srtp_pipeline_wait.argtypes = [vp, i32]
+    L.srtp_pipeline_submit_ex.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t, i32]
+    L.srtp_aggregator_transform.argtypes = [vp, i32, i32, vp, u32, u32, u32, u32, vp, pi32, pu32]
+    L.srtp_aggregator_transformer_info.argtypes = [vp, i32, pi32, pi32]
+    L.srtp_rawpacket_transform_one.argtypes = [vp, i32, i32, vp, u32, u32, pu32, u32, pi32, pu32, vp, u32]
+    L.srtp_device_count.argtypes = []
+    L.srtp_device_count.restype = i32
     L.srtp_engine_stats.argtypes = [vp, C.POINTER(Stats)]
     L.srtp_engine_get_opts.argtypes = [vp, C.POINTER(EngineOpts)]
     L.srtp_aggregator_opts_default.argtypes = [C.POINTER(AggregatorOpts)]

@@ -42,11 +42,29 @@
 //
 // Per-packet semantics: each submitted packet is its own 1-element
 // RawPacket[] in the reference, so one packet's exception must not stop
-// later packets of the same transformer in the bundle.  The engines therefore
-// run with abort_on_error = 0 (creation refuses otherwise); a packet the
-// reference would throw on completes with SRTP_STATUS_ERR_MALFORMED.
+// later packets of the same transformer in the bundle.  The lanes therefore
+// submit their bundles without abort-on-throw (srtp_pipeline_submit_ex with
+// abort_on_error = 0), whatever the engines' option -- so the same engines
+// (contexts) also serve srtp_rawpacket_transform's RawPacket[] calls, which
+// keep it; a packet the reference would throw on completes with
+// SRTP_STATUS_ERR_MALFORMED.
+//
+// Adaptive sealing (SRTP_AGG_SEAL_IDLE).  A lane with no bundle in flight
+// seals its open bundle as soon as a packet lands in it; while a bundle is in
+// flight the next one fills, and is sealed when the one in flight completes.
+// So a lone packet waits one GPU round trip, not the deadline, and under load
+// bundles grow to what arrives during a round trip -- the group commit of a
+// database log.  The lane thread and the producers meet through `idle`:
+// the lane stores idle = 1 and then looks at its open slot, a producer
+// reserves its entry and then looks at idle, both sequentially consistent,
+// so at least one of them sees the other and seals.
+//
+// Synchronous calls (srtp_aggregator_transform): the entry carries a waiter
+// instead of a cookie; the lane thread copies the packet's result to the
+// caller's buffer and wakes it (a futex), in bundle order like a callback.
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -56,6 +74,10 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../../include/srtp_mi355x.h"
 
@@ -85,6 +107,21 @@ constexpr uint32_t blk_bytes(uint64_t w) { return (uint32_t)(w >> 8); }
 constexpr uint64_t blk_tag(uint32_t gen) { return (uint64_t)(gen & 0x7fffffu) << 40; }
 constexpr uint64_t kTagMask = 0x7fffffull << 40;
 
+// A synchronous caller waiting for its packet (srtp_aggregator_transform).
+struct Waiter {
+    std::atomic<uint32_t> done{0};
+    int32_t status = 0;
+    uint32_t len = 0;
+    uint8_t *out = nullptr;
+};
+
+void futex_wait(std::atomic<uint32_t> *w, uint32_t v) {
+    syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+void futex_wake(std::atomic<uint32_t> *w) {
+    syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+}
+
 struct alignas(64) Block {
     std::atomic<uint64_t> w{0};
     uint32_t b0 = 0, size = 0; // byte range (written by the block's owner)
@@ -102,6 +139,7 @@ struct Slot {
     std::unique_ptr<Block[]> blocks;
     std::vector<uint8_t> hole;
     std::vector<uint64_t> cookies;
+    std::vector<Waiter *> waiters;           // non-null: a synchronous caller's entry
     srtp_pipeline_slot h{};
 };
 
@@ -123,6 +161,7 @@ struct Lane {
     std::deque<Parked> parked;
     std::condition_variable cv_work;  // the lane's dispatch thread: something to do
     std::condition_variable cv_space; // producers: a slot of this lane became free
+    std::atomic<int> idle{1};         // SRTP_AGG_SEAL_IDLE: nothing sealed or in flight
     std::thread thread;
 };
 
@@ -153,7 +192,11 @@ struct srtp_aggregator {
     std::condition_variable cv_flush; // the flusher: a new deadline
     std::condition_variable cv_idle;  // flush(): everything completed
     std::vector<std::unique_ptr<Lane>> lanes;
+    std::atomic<bool> closing{false}; // destroy has begun: submits are refused
     bool stop = false;
+    // transformer kinds, read without a lock (-2: not looked up yet)
+    std::unique_ptr<std::atomic<int32_t>[]> kinds;
+    uint32_t n_kinds = 0;
     uint64_t completed = 0, bundles = 0;
     int error = SRTP_OK;
     std::string last_error;
@@ -199,7 +242,18 @@ void seal_locked(srtp_aggregator *a, Lane &ln, int dir) {
     sl.state = kSealed;
     sl.ready = 0;
     ln.sealed.push_back(resv_slot1(r) - 1);
+    ln.idle.store(0);
     ln.cv_work.notify_all();
+}
+
+// SRTP_AGG_SEAL_IDLE, the lane thread's side (see the file comment): with
+// nothing sealed or in flight, mark the lane idle, then seal an open bundle
+// that has packets (which clears idle again).
+void seal_if_idle_locked(srtp_aggregator *a, Lane &ln) {
+    if (!(a->opts.flags & SRTP_AGG_SEAL_IDLE) || !ln.sealed.empty() || !ln.inflight.empty()) return;
+    ln.idle.store(1);
+    for (int d = 0; d < 2; d++)
+        if (resv_n(ln.resv[d].load()) > 0) seal_locked(a, ln, d);
 }
 
 int free_slot_locked(Lane &ln, bool in_cb) {
@@ -294,16 +348,24 @@ bool try_reserve(srtp_aggregator *a, Lane &ln, uint32_t lane, int dir, size_t ne
 // Copies the packet into its reserved place; its length, stored last, marks
 // it complete for the lane's thread.
 void fill(Lane &ln, int s, uint32_t i, size_t off, int32_t tid, const uint8_t *pkt, uint32_t len, uint32_t cap,
-          size_t need, uint32_t flags, uint64_t cookie) {
+          size_t need, uint32_t flags, uint64_t cookie, uint32_t copy_len) {
     Slot &sl = ln.slots[s];
-    if (len) memcpy(sl.h.seg + off, pkt, len);
-    if (need > len) memset(sl.h.seg + off + len, 0, need - len);
+    if (copy_len) memcpy(sl.h.seg + off, pkt, copy_len);
+    if (need > copy_len) memset(sl.h.seg + off + copy_len, 0, need - copy_len);
     sl.h.off[i] = (uint32_t)off;
     sl.h.cap[i] = cap;
     sl.h.flags[i] = flags;
     sl.h.tids[i] = tid;
     sl.cookies[i] = cookie;
     __atomic_store_n(&sl.h.len[i], len, __ATOMIC_RELEASE);
+}
+
+// SRTP_AGG_SEAL_IDLE, the producer's side: after its entry is reserved (and
+// filled), an idle lane's open bundle is sealed by the producer.
+void producer_seal_if_idle(srtp_aggregator *a, Lane &ln, int dir) {
+    if (!(a->opts.flags & SRTP_AGG_SEAL_IDLE) || !ln.idle.load()) return;
+    std::lock_guard<std::mutex> lk(a->mu);
+    if (ln.idle.load() && ln.sealed.empty() && ln.inflight.empty()) seal_locked(a, ln, dir);
 }
 
 // True when every packet reserved in sealed slot sl has been copied.
@@ -350,7 +412,8 @@ void place_parked_locked(srtp_aggregator *a, Lane &ln, uint32_t lane) {
             open_locked(a, ln, dir, f);
             if (!try_reserve(a, ln, lane, dir, need, s, i, off)) return; // cannot happen: need <= max_bytes
         }
-        fill(ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie);
+        ln.slots[s].waiters[i] = nullptr;
+        fill(ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie, len);
         ln.parked.pop_front();
     }
 }
@@ -383,7 +446,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
             const size_t bytes = sl.bytes;
             const int32_t rev = sl.reverse;
             lk.unlock(); // the slot is ours: producers only touch open slots
-            const int rc = srtp_pipeline_submit(ln->pl, s, rev, 1, -1, 1, n, bytes);
+            const int rc = srtp_pipeline_submit_ex(ln->pl, s, rev, 1, -1, 1, n, bytes, 0);
             lk.lock();
             if (rc != SRTP_OK) {
                 a->error = rc;
@@ -397,12 +460,24 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
         Slot &sl = ln->slots[s];
         lk.unlock();
         (void)srtp_pipeline_wait(ln->pl, s);
-        // callbacks outside the lock, in bundle order
+        // callbacks outside the lock, in bundle order; synchronous callers get
+        // their packet's bytes (as much as it occupied before or after) and wake
         tl_in_callback = a;
         for (uint32_t i = 0; i < sl.n; i++) {
             if (sl.hole[i]) continue;
             const int32_t st = sl.h.status[i];
-            a->cb(a->user, sl.cookies[i], st, sl.h.seg + sl.h.off[i], sl.h.len[i]);
+            if (Waiter *w = sl.waiters[i]) {
+                sl.waiters[i] = nullptr;
+                const uint32_t nl = sl.h.len[i];
+                const uint32_t ol = (uint32_t)(uintptr_t)sl.cookies[i]; // the length submitted
+                memcpy(w->out, sl.h.seg + sl.h.off[i], std::max(nl, ol));
+                w->status = st;
+                w->len = nl;
+                w->done.store(1, std::memory_order_release);
+                futex_wake(&w->done);
+                continue;
+            }
+            if (a->cb) a->cb(a->user, sl.cookies[i], st, sl.h.seg + sl.h.off[i], sl.h.len[i]);
         }
         tl_in_callback = nullptr;
         lk.lock();
@@ -417,6 +492,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
         sl.n = sl.n_real = 0;
         sl.bytes = 0;
         place_parked_locked(a, *ln, lane);
+        seal_if_idle_locked(a, *ln);
         ln->cv_space.notify_all();
         a->cv_idle.notify_all();
     }
@@ -455,20 +531,18 @@ void destroy_lanes(srtp_aggregator *a) {
 
 int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const srtp_aggregator_opts *opts,
            srtp_aggregator_cb cb, void *user, srtp_aggregator **out) {
-    if (!cb || !out || n_lanes == 0) return SRTP_EINVAL;
+    if (!out || n_lanes == 0) return SRTP_EINVAL; // cb NULL: only synchronous calls (srtp_aggregator_transform)
     *out = nullptr;
     srtp_aggregator_opts o;
     if (opts) o = *opts;
     else srtp_aggregator_opts_default(&o);
     // the reservation word holds 24 bits of packets and 32 of bytes
     if (o.max_packets == 0 || o.max_packets > 0xffffffu || o.max_bytes < 64 ||
-        o.max_bytes > 0xffffffffull || o.depth < 3 || o.depth > 16)
+        o.max_bytes > 0xffffffffull || o.depth < 3 || o.depth > 16 || (o.flags & ~(uint32_t)SRTP_AGG_SEAL_IDLE))
         return SRTP_EINVAL;
-    for (size_t l = 0; l < n_lanes; l++) {
-        srtp_engine_opts eo;
-        if (!engines[l] || srtp_engine_get_opts(engines[l], &eo) != SRTP_OK || eo.abort_on_error)
-            return SRTP_EINVAL;
-    }
+    srtp_engine_opts eo{};
+    for (size_t l = 0; l < n_lanes; l++)
+        if (!engines[l] || srtp_engine_get_opts(engines[l], &eo) != SRTP_OK) return SRTP_EINVAL;
     srtp_aggregator *a = new (std::nothrow) srtp_aggregator();
     if (!a) return SRTP_ENOMEM;
     a->d = d;
@@ -478,6 +552,13 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
     a->blk = o.max_packets < kBlock ? o.max_packets : kBlock;
     a->n_blk = o.max_packets / a->blk;
     a->blk_bytes = (uint32_t)std::max<size_t>(64, (o.max_bytes / a->n_blk) & ~(size_t)15);
+    a->n_kinds = eo.max_transformers;
+    a->kinds.reset(new (std::nothrow) std::atomic<int32_t>[a->n_kinds]);
+    if (!a->kinds) {
+        delete a;
+        return SRTP_ENOMEM;
+    }
+    for (uint32_t t = 0; t < a->n_kinds; t++) a->kinds[t].store(-2, std::memory_order_relaxed);
     for (size_t l = 0; l < n_lanes; l++) {
         a->lanes.emplace_back(new Lane());
         Lane &ln = *a->lanes.back();
@@ -494,6 +575,7 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
             Slot &sl = ln.slots[i];
             srtp_pipeline_slot_get(ln.pl, i, &sl.h);
             sl.cookies.resize(o.max_packets);
+            sl.waiters.assign(o.max_packets, nullptr);
             sl.hole.assign(o.max_packets, 0);
             sl.blocks.reset(new Block[a->n_blk]);
             for (uint32_t k = 0; k < o.max_packets; k++) sl.h.len[k] = kNoLen;
@@ -502,6 +584,49 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
     for (size_t l = 0; l < a->lanes.size(); l++) a->lanes[l]->thread = std::thread(lane_loop, a, a->lanes[l].get(), (uint32_t)l);
     a->flusher = std::thread(flush_loop, a);
     *out = a;
+    return SRTP_OK;
+}
+
+// A packet into its lane's open bundle (srtp_aggregator_submit / _transform):
+// copy_len bytes of pkt, length len, room cap; w != nullptr: a synchronous
+// caller's entry.
+int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt, uint32_t copy_len,
+                 uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie, Waiter *w) {
+    if (a->closing.load()) return SRTP_EINVAL; // destroy has begun
+    const int dir = reverse ? 1 : 0;
+    const size_t need = need_of(cap);
+    if (need > a->opts.max_bytes) return SRTP_EINVAL;
+    size_t lane = 0;
+    if (a->d) {
+        const int32_t sh = srtp_dispatch_route(a->d, tid, pkt, copy_len < len ? copy_len : len);
+        lane = sh < 0 ? 0 : (size_t)sh; // an unknown transformer: the engine reports it SKIPPED
+    }
+    Lane &ln = *a->lanes[lane];
+    const bool in_cb = tl_in_callback == a;
+    int s;
+    uint32_t i;
+    size_t off;
+    if (!try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) {
+        std::unique_lock<std::mutex> lk(a->mu);
+        for (;;) {
+            if (a->stop || a->closing.load()) return SRTP_EINVAL;
+            if (try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) break;
+            seal_locked(a, ln, dir); // full (or none open)
+            const int f = free_slot_locked(ln, in_cb);
+            if (f >= 0) {
+                open_locked(a, ln, dir, f);
+                continue;
+            }
+            if (in_cb) { // never wait for a slot from a callback: park the packet
+                ln.parked.push_back(Parked{dir, tid, flags, cookie, std::vector<uint8_t>(pkt, pkt + len)});
+                return SRTP_OK;
+            }
+            ln.cv_space.wait(lk); // backpressure: every slot is sealed or in flight
+        }
+    }
+    ln.slots[s].waiters[i] = w;
+    fill(ln, s, i, off, tid, pkt, len, cap, need, flags, cookie, copy_len);
+    producer_seal_if_idle(a, ln, dir);
     return SRTP_OK;
 }
 
@@ -515,6 +640,7 @@ int srtp_aggregator_opts_default(srtp_aggregator_opts *o) {
     o->max_bytes = (size_t)24 << 20;
     o->deadline_us = 1000;
     o->depth = 4;
+    o->flags = SRTP_AGG_SEAL_IDLE;
     return SRTP_OK;
 }
 
@@ -534,42 +660,41 @@ int srtp_aggregator_create_dispatch(srtp_dispatch *d, const srtp_aggregator_opts
 
 int srtp_aggregator_submit(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt,
                            uint32_t len, uint32_t flags, uint64_t cookie) {
-    if (!a || (!pkt && len) || len > 65535u - 16u) return SRTP_EINVAL;
-    const int dir = reverse ? 1 : 0;
+    if (!a || !a->cb || (!pkt && len) || len > 65535u - 16u) return SRTP_EINVAL;
     // protect appends up to 16 bytes (SRTCP E|index + a 12-byte tag): the
     // in-place form of RawPacket.append / grow; unprotect only shrinks
     const uint32_t cap = reverse ? len : len + 16u;
-    const size_t need = need_of(cap);
-    if (need > a->opts.max_bytes) return SRTP_EINVAL;
-    size_t lane = 0;
-    if (a->d) {
-        const int32_t sh = srtp_dispatch_route(a->d, tid, pkt, len);
-        lane = sh < 0 ? 0 : (size_t)sh; // an unknown transformer: the engine reports it SKIPPED
+    return submit_entry(a, reverse, tid, pkt, len, len, cap, flags, cookie, nullptr);
+}
+
+int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt,
+                              uint32_t copy_len, uint32_t len, uint32_t cap, uint32_t flags,
+                              uint8_t *out, int32_t *status, uint32_t *out_len) {
+    if (!a || !out || !status || !out_len || (!pkt && copy_len) || copy_len > cap || len > 65535u ||
+        cap > 65535u)
+        return SRTP_EINVAL;
+    if (tl_in_callback == a) return SRTP_EINVAL; // would wait for its own lane
+    Waiter w;
+    w.out = out;
+    // the waiter's entry keeps the submitted length in its cookie word
+    const int rc = submit_entry(a, reverse, tid, pkt, copy_len, len, cap, flags, (uint64_t)len, &w);
+    if (rc != SRTP_OK) return rc;
+    while (w.done.load(std::memory_order_acquire) == 0) futex_wait(&w.done, 0);
+    *status = w.status;
+    *out_len = w.len;
+    return SRTP_OK;
+}
+
+int srtp_aggregator_transformer_info(srtp_aggregator *a, int32_t t, int32_t *kind, int32_t *fwd_rtcp_tag_len) {
+    if (!a || t < 0 || (uint32_t)t >= a->n_kinds) return SRTP_EINVAL;
+    srtp_engine *e = a->lanes[0]->e;
+    int32_t k = a->kinds[(size_t)t].load(std::memory_order_acquire);
+    if (k < 0 || fwd_rtcp_tag_len) {
+        const int rc = srtp_transformer_info(e, t, &k, fwd_rtcp_tag_len);
+        if (rc != SRTP_OK) return rc;
+        a->kinds[(size_t)t].store(k, std::memory_order_release); // a transformer's kind never changes
     }
-    Lane &ln = *a->lanes[lane];
-    const bool in_cb = tl_in_callback == a;
-    int s;
-    uint32_t i;
-    size_t off;
-    if (!try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) {
-        std::unique_lock<std::mutex> lk(a->mu);
-        for (;;) {
-            if (a->stop) return SRTP_EINVAL;
-            if (try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) break;
-            seal_locked(a, ln, dir); // full (or none open)
-            const int f = free_slot_locked(ln, in_cb);
-            if (f >= 0) {
-                open_locked(a, ln, dir, f);
-                continue;
-            }
-            if (in_cb) { // never wait for a slot from a callback: park the packet
-                ln.parked.push_back(Parked{dir, tid, flags, cookie, std::vector<uint8_t>(pkt, pkt + len)});
-                return SRTP_OK;
-            }
-            ln.cv_space.wait(lk); // backpressure: every slot is sealed or in flight
-        }
-    }
-    fill(ln, s, i, off, tid, pkt, len, cap, need, flags, cookie);
+    if (kind) *kind = k;
     return SRTP_OK;
 }
 
@@ -601,11 +726,13 @@ void srtp_aggregator_destroy(srtp_aggregator *a) {
     if (!a || tl_in_callback == a) return; // from its own callback: refused (see the header)
     {
         std::unique_lock<std::mutex> lk(a->mu);
+        // refuse new submits (callbacks' forwards included), then drain every
+        // accepted packet: a packet accepted is always delivered
+        a->closing.store(true);
         seal_all_locked(a);
-        const uint64_t target = a->completed + pending_locked(a);
         a->cv_idle.wait(lk, [&] {
-            if (a->completed >= target) return true;
-            seal_all_locked(a);
+            if (pending_locked(a) == 0) return true;
+            seal_all_locked(a); // parked callback packets placed since, stragglers' slots
             return false;
         });
         a->stop = true;

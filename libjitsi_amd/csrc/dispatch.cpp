@@ -686,18 +686,38 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     for (uint32_t i = 0; i < n; i++)
         if (shard[i] >= 0 && status[i] == SRTP_STATUS_ERR_MALFORMED && e_first[(size_t)tid_of(i)] < 0)
             e_first[(size_t)tid_of(i)] = i;
-    // Roll back t's packets after e_t; the contexts they touched are dirty.
+    // t's packets after e_t are rolled back; the contexts they touched are
+    // dirty.  Everything the rollback needs is checked before anything is
+    // changed, so a failure (a throw the plan did not foresee: cannot happen
+    // by construction) returns the bundle as the run left it -- packets and
+    // contexts consistent with each other -- never half rolled back.
     std::vector<std::vector<uint64_t>> dirty(ns);
-    bool any_dirty = false;
+    std::vector<uint32_t> undo;
     for (uint32_t i = 0; i < n; i++) {
         if (shard[i] < 0) continue;
         const int64_t e = e_first[(size_t)tid_of(i)];
         if (e < 0 || (int64_t)i <= e) continue;
-        if (status[i] != SRTP_STATUS_NOT_PROCESSED && valid(i)) {
-            dirty[(size_t)shard[i]].push_back(key_of(i));
+        if (stash_at[i] == SIZE_MAX) return dfail(d, SRTP_EINVAL, "rollback: a throw the plan did not foresee");
+        if (status[i] != SRTP_STATUS_NOT_PROCESSED && valid(i)) dirty[(size_t)shard[i]].push_back(key_of(i));
+        undo.push_back(i);
+    }
+    // the snapshot entries of the dirty contexts, per shard
+    std::vector<std::vector<size_t>> snap_at(ns);
+    bool any_dirty = false;
+    for (size_t sh = 0; sh < ns; sh++) {
+        std::vector<uint64_t> &dk = dirty[sh];
+        std::sort(dk.begin(), dk.end());
+        dk.erase(std::unique(dk.begin(), dk.end()), dk.end());
+        const Snap &sn = snap[sh];
+        for (uint64_t k : dk) {
+            const size_t q = (size_t)(std::lower_bound(sn.keys.begin(), sn.keys.end(), k) - sn.keys.begin());
+            if (q >= sn.keys.size() || sn.keys[q] != k)
+                return dfail(d, SRTP_EINVAL, "rollback: context not in the snapshot");
+            snap_at[sh].push_back(q);
             any_dirty = true;
         }
-        if (stash_at[i] == SIZE_MAX) return dfail(d, SRTP_EINVAL, "rollback: a throw the plan did not foresee");
+    }
+    for (uint32_t i : undo) {
         status[i] = SRTP_STATUS_NOT_PROCESSED;
         memcpy(seg + off[i], stash.data() + stash_at[i], region(cap[i]));
         len[i] = stash_len[i];
@@ -708,15 +728,13 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     for (size_t sh = 0; sh < ns; sh++) {
         std::vector<uint64_t> &dk = dirty[sh];
         if (dk.empty()) continue;
-        std::sort(dk.begin(), dk.end());
-        dk.erase(std::unique(dk.begin(), dk.end()), dk.end());
         const Snap &sn = snap[sh];
         std::vector<int32_t> kt, pr;
         std::vector<uint32_t> ks;
         std::vector<srtp_ctx_raw> st;
-        for (uint64_t k : dk) {
-            const size_t q = (size_t)(std::lower_bound(sn.keys.begin(), sn.keys.end(), k) - sn.keys.begin());
-            if (q >= sn.keys.size() || sn.keys[q] != k) return dfail(d, SRTP_EINVAL, "rollback: context not in the snapshot");
+        for (size_t j = 0; j < dk.size(); j++) {
+            const uint64_t k = dk[j];
+            const size_t q = snap_at[sh][j];
             kt.push_back((int32_t)(k >> 32));
             ks.push_back((uint32_t)k);
             st.push_back(sn.st[q]);

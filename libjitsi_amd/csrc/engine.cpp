@@ -652,9 +652,12 @@ int srtp_transformer_close(srtp_engine *e, int32_t t) {
     return SRTP_OK;
 }
 
+// abort: SinglePacketTransformer's abort-on-throw for this bundle (-1: the
+// engine's abort_on_error; 0: every packet is its own 1-element array)
 static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
                             uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
-                            const uint32_t *flags, int32_t *status, uint32_t n, hipStream_t s) {
+                            const uint32_t *flags, int32_t *status, uint32_t n, hipStream_t s,
+                            int32_t abort = -1) {
     if (n == 0) return SRTP_OK;
     if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
     if (n > kRecIdxMask) return fail(e, SRTP_EINVAL, "bundle too large");
@@ -681,7 +684,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.tids = tids; a.tid = tid; a.n = n;
     a.reverse = reverse ? 1 : 0;
     a.check_replay = e->opts.check_replay;
-    a.abort_on_error = e->opts.abort_on_error;
+    a.abort_on_error = abort < 0 ? e->opts.abort_on_error : (abort ? 1 : 0);
     a.serial = e->serial++;
     static const int debug_mode = getenv("SRTP_DEBUG") ? atoi(getenv("SRTP_DEBUG")) : 0;
     a.debug = debug_mode;
@@ -715,7 +718,9 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     const bool need_ctl = !e->ctl_clean[c];
     const bool need_emin = a.abort_on_error && e->emin_filled[c] < a.n_transformers;
     e->ctl_clean[c] = false; // this bundle's atomics dirty it
-    e->emin_filled[c] = 0u;
+    // e_min is written (and the next bundle's reset by k_parse) only by bundles
+    // with abort-on-throw; a bundle without it leaves both tables as they are
+    if (a.abort_on_error) e->emin_filled[c] = 0u;
     if (need_ctl) HIPCHK(e, hipMemsetAsync(a.ctl, 0, sizeof(BundleCtl), s));
     if (need_emin) HIPCHK(e, hipMemsetAsync(a.e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
     {
@@ -723,7 +728,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         HIPCHK(e, launch_parse(a, s)); // also resets control block c ^ 1
     }
     e->ctl_clean[c ^ 1] = true;
-    e->emin_filled[c ^ 1] = a.n_transformers;
+    if (a.abort_on_error) e->emin_filled[c ^ 1] = a.n_transformers;
     e->ctl_cur = c ^ 1;
     {
         StageTimer t(e, s, SRTP_STAGE_SORT);
@@ -1060,7 +1065,13 @@ int srtp_engine_stats(srtp_engine *e, srtp_stats *out) {
     out->rehashes = e->n_rehash;
     out->chain_stalls = sum[kCtrChainStall];
     out->long_walked = sum[kCtrLongWalked];
+    out->holes = sum[kCtrStatus + kStatusHole];
     return SRTP_OK;
+}
+
+int32_t srtp_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? (int32_t)n : 0;
 }
 
 int srtp_engine_set_debug(srtp_engine *e, uint32_t flags) {
@@ -1276,6 +1287,12 @@ static int pipeline_wait_locked(srtp_pipeline *pl, srtp_pipeline::Slot &sl) {
 
 int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                          int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes) {
+    return srtp_pipeline_submit_ex(pl, slot, reverse, use_tids, tid, use_flags, n, seg_bytes, -1);
+}
+
+int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                            int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                            int32_t abort_on_error) {
     if (!pl || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
     std::lock_guard<std::mutex> gp(pl->mu);
     srtp_pipeline::Slot &sl = pl->slots[(size_t)slot];
@@ -1300,7 +1317,8 @@ int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32
     HIPCHK(e, hipEventRecord(sl.ev_in, si));
     HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
     sl.rc = transform_locked(e, reverse, use_tids ? sl.d_tids : nullptr, tid, sl.d_seg, sl.d_off,
-                             sl.d_len, sl.d_cap, use_flags ? sl.d_flags : nullptr, sl.d_status, n, s);
+                             sl.d_len, sl.d_cap, use_flags ? sl.d_flags : nullptr, sl.d_status, n, s,
+                             abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0));
     if (sl.rc != SRTP_OK) return sl.rc;
     HIPCHK(e, hipEventRecord(sl.ev_done, s));
     HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));

@@ -95,6 +95,48 @@ int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
     return SRTP_OK;
 }
 
+// The region an element gets (RawPacket.isInvalid compares the length with
+// it): the buffer after the offset, plus room for the trailer on protect --
+// the in-place form of append / grow.  avail = the buffer's bytes after offset.
+uint32_t element_cap(int32_t reverse, uint32_t avail, uint32_t length) {
+    const bool fits = length <= avail;
+    const uint64_t c = (fits && !reverse) ? std::max<uint64_t>(avail, (uint64_t)length + kTrailerRoom) : avail;
+    return (uint32_t)std::min<uint64_t>(c, 65535u);
+}
+
+// Write-back of one processed element (SinglePacketTransformer + RawPacket.append
+// / grow / shrink): res / nl = the engine's bytes and length of the packet,
+// dst = buffer + offset with avail bytes.  Returns need_len (0: written in
+// place) or a negative SRTP_E*.  info(kind, rtcp_tag) gives the transformer's
+// kind and, when rtcp_tag != nullptr, its forward factory's SRTCP tag length.
+template <class Info>
+int64_t write_back(int32_t reverse, int32_t st, uint8_t *dst, uint32_t avail, uint32_t old, const uint8_t *res,
+                   uint32_t nl, Info &&info) {
+    if (!reverse && st == SRTP_STATUS_OK) {
+        int32_t kind = SRTP_KIND_RTP, rtcp_tag = 0;
+        int rc = info(&kind, nullptr);
+        if (rc != SRTP_OK) return rc;
+        if (kind == SRTP_KIND_RTCP) {
+            // grow(4 + tag) then append(E|index, tag): a new buffer of exactly the
+            // new length; with NULL authentication nothing is appended and the
+            // buffer is length + 4 + the policy's tag length (the forward
+            // factory's SRTCP policy: a context kept across an SDES rekey with a
+            // different tag length is the one case this does not cover)
+            if (nl != old) return nl;
+            rc = info(&kind, &rtcp_tag);
+            if (rc != SRTP_OK) return rc;
+            return (int64_t)old + 4 + rtcp_tag;
+        }
+        if (nl != old) {
+            if (nl > avail) return nl; // append reallocates: exactly length + tag
+            memcpy(dst, res, nl);
+            return 0;
+        }
+    }
+    memcpy(dst, res, std::min(old, avail));
+    return 0;
+}
+
 } // namespace
 
 extern "C" {
@@ -148,10 +190,7 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
             ccap[i] = 16;
         } else {
             avail[i] = offset[i] <= buf_len[i] ? buf_len[i] - offset[i] : 0u;
-            const bool fits = length[i] <= avail[i];
-            uint64_t c = (fits && !reverse) ? std::max<uint64_t>(avail[i], (uint64_t)length[i] + kTrailerRoom)
-                                            : avail[i];
-            ccap[i] = (uint32_t)std::min<uint64_t>(c, 65535u);
+            ccap[i] = element_cap(reverse, avail[i], length[i]);
         }
         bytes += region(ccap[i]);
     }
@@ -187,38 +226,29 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
     if (rc != SRTP_OK) return rc;
     b->n = n;
     // Write-back (SinglePacketTransformer + RawPacket.append / grow / shrink).
-    int32_t info_tid = -1, kind = SRTP_KIND_RTP, rtcp_tag = 0;
+    int32_t info_tid = -1, info_kind = SRTP_KIND_RTP;
     for (uint32_t i = 0; i < n; i++) {
         need_len[i] = 0;
         const int32_t st = b->s_status[i];
         status[i] = st;
         if (!bufs[i] || st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED) continue;
-        const uint8_t *res = b->s_seg + b->s_off[i];
-        const uint32_t old = length[i], nl = b->s_len[i];
-        if (!reverse && st == SRTP_STATUS_OK) {
-            const int32_t t = tids ? tids[i] : tid;
-            if (t != info_tid) {
-                rc = srtp_transformer_info(eng, t, &kind, &rtcp_tag);
-                if (rc != SRTP_OK) return rc;
-                info_tid = t;
+        const int32_t t = tids ? tids[i] : tid;
+        const int64_t need = write_back(reverse, st, bufs[i] + offset[i], avail[i], length[i],
+                                        b->s_seg + b->s_off[i], b->s_len[i], [&](int32_t *kind, int32_t *tag) {
+            if (!tag && t == info_tid) {
+                *kind = info_kind;
+                return SRTP_OK;
             }
-        }
-        if (!reverse && st == SRTP_STATUS_OK && (nl != old || kind == SRTP_KIND_RTCP)) {
-            // grow(4 + tag) then append(E|index, tag): a new buffer of exactly the
-            // new length; with NULL authentication nothing is appended and the
-            // buffer is length + 4 + the policy's tag length (the forward
-            // factory's SRTCP policy: a context kept across an SDES rekey with a
-            // different tag length is the one case this does not cover)
-            if (kind == SRTP_KIND_RTCP)
-                need_len[i] = nl != old ? nl : old + 4u + (uint32_t)rtcp_tag;
-            else if (nl > avail[i]) // append reallocates: exactly length + tag
-                need_len[i] = nl;
-            else
-                memcpy(bufs[i] + offset[i], res, nl);
-        } else {
-            memcpy(bufs[i] + offset[i], res, std::min(old, avail[i]));
-        }
-        length[i] = nl;
+            const int rc = srtp_transformer_info(eng, t, kind, tag);
+            if (rc == SRTP_OK) {
+                info_tid = t;
+                info_kind = *kind;
+            }
+            return rc;
+        });
+        if (need < 0) return (int)need;
+        need_len[i] = (uint32_t)need;
+        length[i] = b->s_len[i];
         if (st == SRTP_STATUS_ERR_MALFORMED && *thrown < 0) *thrown = (int32_t)i;
     }
     return SRTP_OK;
@@ -228,6 +258,39 @@ int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **d
     if (!b || !data || !len || i >= b->n) return SRTP_EINVAL;
     *data = b->s_seg + b->s_off[i];
     *len = b->s_len[i];
+    return SRTP_OK;
+}
+
+int srtp_rawpacket_transform_one(srtp_aggregator *a, int32_t reverse, int32_t tid, uint8_t *buf,
+                                 uint32_t buf_len, uint32_t offset, uint32_t *length, uint32_t flags,
+                                 int32_t *status, uint32_t *need_len, uint8_t *grow, uint32_t grow_cap) {
+    if (!a || !length || !status || !need_len || !grow) return SRTP_EINVAL;
+    *need_len = 0;
+    if (!buf || (flags & SRTP_PKT_FLAG_SKIP)) { // a null element / the predicate said no: untouched
+        *status = SRTP_STATUS_SKIPPED;
+        return SRTP_OK;
+    }
+    const uint32_t avail = offset <= buf_len ? buf_len - offset : 0u;
+    const uint32_t old = *length;
+    if (old > 65535u) { // longer than any region: RawPacket.isInvalid, as the array path reports it
+        *status = SRTP_STATUS_DROP_INVALID;
+        return SRTP_OK;
+    }
+    const uint32_t cap = element_cap(reverse, avail, old);
+    if (grow_cap < cap) return SRTP_EINVAL;
+    uint32_t nl = 0;
+    int rc = srtp_aggregator_transform(a, reverse, tid, buf + offset, std::min(avail, cap), old, cap,
+                                       flags & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE), grow, status, &nl);
+    if (rc != SRTP_OK) return rc;
+    const int32_t st = *status;
+    if (st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED) return SRTP_OK;
+    const int64_t need = write_back(reverse, st, buf + offset, avail, old, grow, nl,
+                                    [&](int32_t *kind, int32_t *tag) {
+                                        return srtp_aggregator_transformer_info(a, tid, kind, tag);
+                                    });
+    if (need < 0) return (int)need;
+    *need_len = (uint32_t)need;
+    *length = nl;
     return SRTP_OK;
 }
 

@@ -588,6 +588,14 @@ __device__ __forceinline__ int32_t packet_tid(const BundleArgs &a, uint32_t p) {
     return a.tids ? a.tids[p] : a.tid;
 }
 
+// Index of a final status in the engine's status counters: a bundle former's
+// hole (SKIPPED, no transformer: srtp_aggregator_* seals unclaimed entries so)
+// is counted apart from the packets the caller skipped (srtp_stats.holes).
+__device__ __forceinline__ uint32_t status_counter(const BundleArgs &a, uint32_t p, int32_t st) {
+    if (st == SRTP_STATUS_SKIPPED && packet_tid(a, p) < 0) return kStatusHole;
+    return (uint32_t)st & 15u;
+}
+
 // ------------------------------------------------------- context hash table
 // Linear probing over (transformer << 32 | SSRC) keys.  A key absent from the
 // table is inserted into the first tombstone of its probe path (slots freed by
@@ -801,7 +809,7 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
 
 // The packet lane i of a crypto kernel takes (i < a.n).
 __device__ __forceinline__ uint32_t lane_packet(const BundleArgs &a, uint32_t i) {
-    if (SRTP_LEN_ORDER && __popc(a.ctl->len_classes) > 1) return a.lord[i];
+    if (SRTP_LEN_ORDER && __popc(a.ctl->len_classes & ~1u) > 1) return a.lord[i];
     return i;
 }
 
@@ -974,7 +982,9 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
             }
         }
         __syncthreads();
-        if (__popc(s_run[96]) <= 1) return; // one class: lane = packet
+        // one class: lane = packet.  Class 0 (length 0: a bundle former's holes,
+        // null elements) runs no crypto and does not count.
+        if (__popc(s_run[96] & ~1u) <= 1) return;
         if (t < 32) {
             uint32_t tot = 0u;
             for (uint32_t u = 0u; u < sp.tiles; u++) tot += sp.cls_tile[u * kClsWords + t];
@@ -2635,6 +2645,63 @@ __device__ __forceinline__ void store_chunk_quad(uint8_t *seg, uint32_t off, int
     }
 }
 
+// ------------------------------------------- stores staged through LDS
+// SRTP_STAGE_STORES: the fused loops' 64-B chunk stores leave the wave
+// quad-coalesced -- four lanes write the four 16-B pieces of one packet's
+// chunk, so a store instruction covers 16 whole chunks instead of touching 64
+// lines -- after a transpose through a 2-KB wave buffer in LDS behind the
+// T-table image (16 waves x 2 KB: the image and the buffers fill the 160 KB).
+// Two passes of 32 lanes: the pass's lanes write their chunks (4 x
+// ds_write_b128), then every lane reads one 16-B piece (2 x ds_read_b128) and
+// stores it.  The LDS, not the VALU, pays for the transpose (the DPP form of
+// round 3 cost 48 VALU per chunk).  Only when every lane of the wave is at the
+// same chunk; otherwise each lane stores its own chunk.
+#ifndef SRTP_STAGE_STORES
+#define SRTP_STAGE_STORES 0
+#endif
+constexpr int kStageWordsPerWave = SRTP_STAGE_STORES ? 512 : 0; // 2 KB
+constexpr int kStageWords = kStageWordsPerWave * (kAesBlock / 64);
+
+// the calling wave's store buffer, behind the T-table image at LDS 0
+__device__ __forceinline__ uint4 *stage_buf(const char *lds) {
+    return reinterpret_cast<uint4 *>(const_cast<char *>(lds) + 4 * kTeWords) +
+           (threadIdx.x >> 6) * (kStageWordsPerWave / 4);
+}
+
+// Chunk b of every lane's packet (d[16]; own_off = the lane's packet offset in
+// seg) to HBM, quad-coalesced, through the wave's buffer wb.  Every lane of the
+// wave must be active.  Peer offsets are fetched per store (ds_bpermute) rather
+// than held across the loop: the fused loops have no VGPRs to spare.
+__device__ __forceinline__ void store_chunk_staged(uint8_t *seg, uint32_t own_off, int b, uint4 *wb,
+                                                   const uint32_t d[16]) {
+    const uint32_t lane = __lane_id();
+    const int q = (int)(lane >> 2);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        if ((lane >> 5) == (uint32_t)h) {
+            uint4 *dst = wb + 4 * (lane & 31u);
+#pragma unroll
+            for (int m = 0; m < 4; m++) dst[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+        }
+        // the LDS runs one wave's instructions in order: only the compiler
+        // must not move the other lanes' writes and reads across (no s_waitcnt)
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t po = (uint32_t)__shfl((int)own_off, 32 * h + 16 * r + q);
+            const uint4 v = wb[64 * r + lane];
+            *reinterpret_cast<uint4 *>(seg + po + 64u * (uint32_t)b + 16u * (lane & 3u)) = v;
+        }
+        // the LDS runs one wave's instructions in order: only the compiler
+        // must not move the other lanes' writes and reads across (no s_waitcnt)
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+}
+
 // Store the 16-B pieces of chunk b that overlap the ciphered range [off, end).
 __device__ __forceinline__ void store_chunk(uint8_t *pkt, int b, const Ctr &cs, const uint32_t d[16]) {
     uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
@@ -2727,6 +2794,9 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
             store_chunk_quad(a.seg, a.off[p], b, full, d);
 #elif SRTP_COALESCE == 2
             store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
+#elif SRTP_STAGE_STORES
+            if (__builtin_amdgcn_read_exec() == ~0ull) store_chunk_staged(a.seg, (uint32_t)(pkt - a.seg), b, stage_buf(lds), d);
+            else store_chunk_full(pkt, b, d);
 #else
             store_chunk_full(pkt, b, d);
 #endif
@@ -2813,7 +2883,9 @@ __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const u
 }
 
 __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
-    __shared__ uint32_t s_te[kTeWords + kTeCounters];
+    // the status counts sit at the start of wave 0's store buffer, which wave 0
+    // first writes after flushing them
+    __shared__ uint32_t s_te[kTeWords + (kStageWords > kTeCounters ? kStageWords : kTeCounters)];
     uint32_t *s_cnt = s_te + kTeWords;
     STAMP(0);
     STAMP_XCC();
@@ -2825,7 +2897,7 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     int32_t fs = -1;
     if (i < a.n) {
         fs = finish_status(a, p);
-        atomicAdd(&s_cnt[fs & 15], 1u);
+        atomicAdd(&s_cnt[status_counter(a, p, fs)], 1u);
     }
     __syncthreads();
     flush_status_counts(a, s_cnt);
@@ -2989,6 +3061,9 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             store_chunk_quad(a.seg, a.off[p], b, full, d);
 #elif SRTP_COALESCE == 2
             store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
+#elif SRTP_STAGE_STORES
+            if (__builtin_amdgcn_read_exec() == ~0ull) store_chunk_staged(a.seg, (uint32_t)(pkt - a.seg), b, stage_buf(lds), d);
+            else store_chunk_full(pkt, b, d);
 #else
             store_chunk_full(pkt, b, d);
 #endif
@@ -3106,7 +3181,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 
 
 __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
-    __shared__ uint32_t s_te[kTeWords];
+    __shared__ uint32_t s_te[kTeWords + kStageWords];
     STAMP(0);
     STAMP_XCC();
     // the packet's context state and whether it lies deep in a long chain
@@ -3192,7 +3267,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
         const uint32_t sw = a.spec[p0]; // k_unprotect's summary: no context / key-set loads
         const uint32_t cw = a.w_cw[p0], g0 = a.g0[p0];
         const int32_t st = finish_status(a, p0);
-        atomicAdd(&s_cnt[st & 15], 1u);
+        atomicAdd(&s_cnt[status_counter(a, p0, st)], 1u);
         if (slot != kNoSlot) {
             did = (sw & kSpecDid) != 0u;
             const bool rtp = (sw & kSpecRtp) != 0u;

@@ -130,6 +130,7 @@ constexpr uint32_t kDbgForceStall = 1u; // chain-pass tiles 1, 4, 7, ... give up
 // over many addresses; the host sums the copies.
 constexpr int kCountReplicas = 64;
 constexpr int kCtrStatus = 0;        // [0, 16): final status counts (SRTP_STATUS_*)
+constexpr int kStatusHole = 11;      // ... and at SRTP_NUM_STATUS: bundle-former holes (srtp_stats.holes)
 constexpr int kCtrRocRecheck = 16;   // unprotect tags re-checked under a walk ROC != the speculation
 constexpr int kCtrRepaired = 17;     // packets k_unprotect_fix re-ciphered
 constexpr int kCtrOverflow = 18;     // packets refused a new context (table full)

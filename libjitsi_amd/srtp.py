@@ -474,20 +474,24 @@ class SRTPAggregator:
     thread once per packet, in bundle order; packets of one direction (and,
     over a dispatcher, of one shard) complete in the order they were
     accepted.  ``engine`` is an SRTPEngine or an SRTPDispatcher (one lane per
-    shard, srtp_aggregator_create_dispatch).  The engines must have
-    abort_on_error=False: each packet is its own 1-element RawPacket[] as in
-    the reference's RTPConnector streams (RTPConnectorInputStream.java
-    :425-452, RTPConnectorOutputStream.java:268-300,652-830)."""
+    shard, srtp_aggregator_create_dispatch).  Each packet is its own
+    1-element RawPacket[] as in the reference's RTPConnector streams
+    (RTPConnectorInputStream.java:425-452, RTPConnectorOutputStream.java
+    :268-300,652-830), whatever the engine's abort_on_error.  ``callback``
+    None: only synchronous ``transform`` calls.  ``seal_idle``: a lane with no
+    bundle in flight seals at once (SRTP_AGG_SEAL_IDLE)."""
 
     def __init__(self, engine, callback, max_packets: int = 1 << 14,
-                 max_bytes: int = 24 << 20, deadline_us: int = 1000, depth: int = 4):
+                 max_bytes: int = 24 << 20, deadline_us: int = 1000, depth: int = 4,
+                 seal_idle: bool = True):
         self.engine = engine
-        o = N.AggregatorOpts(max_packets, max_bytes, deadline_us, depth)
+        o = N.AggregatorOpts(max_packets, max_bytes, deadline_us, depth,
+                             N.AGG_SEAL_IDLE if seal_idle else 0)
 
         def _cb(user, cookie, status, data, length):
             callback(int(cookie), int(status), C.string_at(data, length) if length else b"")
 
-        self._cb = N.AGG_CB(_cb)  # kept alive with the aggregator
+        self._cb = N.AGG_CB(_cb) if callback is not None else N.AGG_CB()  # kept alive
         h = C.c_void_p()
         if isinstance(engine, SRTPDispatcher):
             rc = N.lib().srtp_aggregator_create_dispatch(engine.h, C.byref(o), self._cb, None,
@@ -507,6 +511,18 @@ class SRTPAggregator:
         if rc == N.EFULL:
             return rc
         return N.check(rc, None, "submit")
+
+    def transform(self, reverse: bool, transformer: "_SRTPBase", data: bytes, flags: int = 0):
+        """Synchronous (srtp_aggregator_transform): (status, bytes) of one
+        packet, sharing bundles with concurrent callers."""
+        data = bytes(data)
+        cap = len(data) if reverse else len(data) + 16
+        out = (C.c_uint8 * max(cap, 1))()
+        st, ol = C.c_int32(), C.c_uint32()
+        N.check(N.lib().srtp_aggregator_transform(self.h, int(reverse), transformer.tid, data, len(data),
+                                                  len(data), cap, flags, out, C.byref(st), C.byref(ol)),
+                None, "srtp_aggregator_transform")
+        return int(st.value), bytes(out[:ol.value])
 
     def flush(self) -> None:
         N.check(N.lib().srtp_aggregator_flush(self.h), None, "flush")
@@ -731,11 +747,60 @@ def _rp_batch(engine) -> C.c_void_p:
 
 
 def _rp_close_all(engine) -> None:
+    agg = engine.__dict__.pop("_pkt_agg", None)
+    if agg is not None:
+        agg.close()
     with _rp_lock:
         for h in engine.__dict__.get("_rp_all", []):
             N.lib().srtp_rawpacket_batch_destroy(h)
         engine.__dict__["_rp_all"] = []
         engine.__dict__.pop("_rp_tls", None)
+
+
+def _packet_aggregator(engine) -> "SRTPAggregator":
+    """The engine's (or dispatcher's: one lane per shard) aggregator for
+    per-packet calls, created on first use -- what the JNI shim keeps one of
+    per process."""
+    with _rp_lock:
+        agg = engine.__dict__.get("_pkt_agg")
+        if agg is None:
+            agg = engine._pkt_agg = SRTPAggregator(engine, None, max_packets=4096, max_bytes=8 << 20,
+                                                   deadline_us=500, depth=4, seal_idle=True)
+    return agg
+
+
+_grow_tls = threading.local()
+_GROW = 65536 + 16
+
+
+def _rawpacket_one(engine, reverse: bool, tid: int, pkt: "RawPacket"):
+    """SinglePacketTransformer.transform / reverseTransform(RawPacket)
+    (SinglePacketTransformer.java:113,169; SRTPTransformer.java:185-219,
+    SRTCPTransformer.java:175-207) through srtp_rawpacket_transform_one: the
+    packet joins the bundles of concurrent callers (srtp_aggregator_transform)
+    and is written back as the reference leaves it.  Returns the packet or
+    None (dropped); raises where the reference throws."""
+    g = getattr(_grow_tls, "buf", None)
+    if g is None:
+        g = _grow_tls.buf = (C.c_uint8 * _GROW)()
+    agg = _packet_aggregator(engine)
+    buf = pkt.buffer if len(pkt.buffer) else bytearray(1)
+    v = (C.c_char * len(buf)).from_buffer(buf)
+    length, st, need = C.c_uint32(pkt.length), C.c_int32(), C.c_uint32()
+    rc = N.lib().srtp_rawpacket_transform_one(
+        agg.h, int(reverse), int(tid), C.addressof(v), len(pkt.buffer), pkt.offset, C.byref(length),
+        pkt.flags & (N.PKT_FLAG_DISCARD | N.PKT_FLAG_SILENCE), C.byref(st), C.byref(need), g, _GROW)
+    del v
+    N.check(rc, None, "srtp_rawpacket_transform_one")
+    if need.value:  # the reference's new byte[] (RawPacket.append / grow): the result at offset 0
+        nb = bytearray(need.value)
+        nb[:length.value] = bytes(g[:length.value])
+        pkt.buffer, pkt.offset = nb, 0
+    pkt.length = int(length.value)
+    s = int(st.value)
+    if s == N.STATUS_ERR_MALFORMED:
+        raise SRTPTransformException("Failed to transform RawPacket! (malformed for SRTP)")
+    return pkt if s == N.STATUS_OK else None
 
 
 def _rawpacket_run(engine, reverse: bool, tids, pkts, predicate=None):
@@ -826,18 +891,37 @@ class _SRTPBase(PacketTransformer):
     def close(self):
         self.engine._transformer_close(self.tid)
 
+    def _count_exception(self, reverse):
+        if reverse:
+            self.exceptionsInReverseTransform += 1
+        else:
+            self.exceptionsInTransform += 1
+
     def _run(self, pkts, reverse):
+        """RawPacket: SinglePacketTransformer's per-packet transform(RawPacket)
+        (coalesced with concurrent callers).  An array of one element: the
+        SinglePacketTransformer array loop over that per-packet call -- the
+        connectors' 1-element arrays.  Longer arrays: one bundle
+        (srtp_rawpacket_transform) with the loop's abort-on-throw."""
         if pkts is None:
             return None
+        if isinstance(pkts, RawPacket):
+            return _rawpacket_one(self.engine, reverse, self.tid, pkts)
         if len(pkts) == 0:
+            return pkts
+        if len(pkts) == 1:
+            p = pkts[0]
+            if p is not None and (self.packetPredicate is None or self.packetPredicate(p)):
+                try:
+                    pkts[0] = _rawpacket_one(self.engine, reverse, self.tid, p)
+                except SRTPTransformException:
+                    self._count_exception(reverse)
+                    raise
             return pkts
         try:
             return _rawpacket_run(self.engine, reverse, self.tid, pkts, self.packetPredicate)
         except SRTPTransformException:
-            if reverse:
-                self.exceptionsInReverseTransform += 1
-            else:
-                self.exceptionsInTransform += 1
+            self._count_exception(reverse)
             raise
 
     def transform(self, pkts):

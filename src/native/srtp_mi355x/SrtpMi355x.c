@@ -13,17 +13,19 @@
  * (the RawPacket[] marshalling is srtp_rawpacket_transform, tested through
  * ctypes in tests/test_rawpacket.py).  Conventions of src/native/openssl:
  * native handles are jlong casts of heap pointers (BlockCipher.c:64-73),
- * arrays are pinned with GetPrimitiveArrayCritical (BlockCipher.c:199-222),
  * errors come back as negative return codes that the Java side turns into a
- * RuntimeException (OpenSSLBlockCipher.java:310-313).
+ * RuntimeException (OpenSSLBlockCipher.java:310-313).  Unlike BlockCipher.c,
+ * whose critical regions span a CPU call, packet bytes are copied in and out
+ * with Get/SetByteArrayRegion: a GPU round trip must not stall the JVM's GC.
  *
  * Java side: org.jitsi.impl.neomedia.transform.srtp.mi355x.SrtpMi355x (the
  * native declarations), GpuSRTPTransformer / GpuSRTCPTransformer (the
- * PacketTransformer drop-ins), GpuSRTPContextFactory.
+ * SinglePacketTransformer drop-ins), GpuSRTPContextFactory.
  */
 #include <jni.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "srtp_mi355x.h"
 
@@ -60,13 +62,16 @@ JNIEXPORT jint JNICALL JFN(factoryCreate)(JNIEnv *env, jclass c, jlong d, jboole
     (*env)->GetIntArrayRegion(env, srtpPol, 0, 6, p1);
     (*env)->GetIntArrayRegion(env, srtcpPol, 0, 6, p2);
     jsize kl = (*env)->GetArrayLength(env, key), sl = (*env)->GetArrayLength(env, salt);
-    jbyte *k = (*env)->GetPrimitiveArrayCritical(env, key, NULL);
-    jbyte *s = (*env)->GetPrimitiveArrayCritical(env, salt, NULL);
+    jbyte k[64], s[64];
+    if (kl > 64 || sl > 64) return SRTP_EINVAL;
+    (*env)->GetByteArrayRegion(env, key, 0, kl, k);
+    (*env)->GetByteArrayRegion(env, salt, 0, sl, s);
+    /* copies the session keys to every GPU: no array is held meanwhile */
     int rc = srtp_dispatch_factory_create((srtp_dispatch *)H(d), sender, (const uint8_t *)k, kl,
                                           (const uint8_t *)s, sl, (const srtp_policy *)p1,
                                           (const srtp_policy *)p2, &id);
-    (*env)->ReleasePrimitiveArrayCritical(env, salt, s, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, key, k, JNI_ABORT);
+    memset(k, 0, sizeof k); /* the master key does not stay on the stack */
+    memset(s, 0, sizeof s);
     return rc == SRTP_OK ? id : rc;
 }
 
@@ -122,7 +127,14 @@ static int raw_packet_ids(JNIEnv *env) {
  * set to null, packets that the reference gives a new buffer
  * (RawPacket.append / grow) get one.  Returns 0, 1 + the index of the first
  * element the reference throws on (the Java side rethrows after this
- * returns: every element is written back), or a negative SRTP_E* code. */
+ * returns: every element is written back), or a negative SRTP_E* code.
+ *
+ * No array stays pinned across the GPU round trip: each element's bytes from
+ * its offset on are copied out with GetByteArrayRegion into one native block,
+ * srtp_rawpacket_transform runs on that block, and the bytes it may have
+ * changed go back with SetByteArrayRegion (BlockCipher.c:194-229 likewise
+ * holds its critical region only around a CPU call).  Two elements sharing one
+ * byte[] stay consistent: each writes back only its own range. */
 JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch, jboolean reverse, jint tid,
                                              jobjectArray pkts, jintArray skip) {
     srtp_rawpacket_batch *b = (srtp_rawpacket_batch *)H(batch);
@@ -133,32 +145,50 @@ JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch,
     jobject *objs = calloc((size_t)n, sizeof *objs);
     jbyteArray *arrs = calloc((size_t)n, sizeof *arrs);
     uint8_t **bufs = calloc((size_t)n, sizeof *bufs);
-    uint32_t *u = calloc((size_t)n * 6, sizeof *u); /* buf_len, offset, length, flags, need_len, (pad) */
+    uint32_t *u = calloc((size_t)n * 6, sizeof *u); /* buf_len, offset, length, flags, need_len, java offset */
     int32_t *status = calloc((size_t)n, sizeof *status);
+    uint8_t *block = NULL;
     jint *sk = skip ? (*env)->GetIntArrayElements(env, skip, NULL) : NULL;
     int rc = SRTP_ENOMEM;
     if (!objs || !arrs || !bufs || !u || !status) goto out;
-    uint32_t *buf_len = u, *offset = u + n, *length = u + 2 * n, *flags = u + 3 * n, *need = u + 4 * n;
-    /* the fields first: no JNI call is allowed between the critical sections */
+    uint32_t *buf_len = u, *offset = u + n, *length = u + 2 * n, *flags = u + 3 * n, *need = u + 4 * n,
+             *joff = u + 5 * n;
+    size_t total = 0;
     for (jsize i = 0; i < n; i++) {
         objs[i] = (*env)->GetObjectArrayElement(env, pkts, i);
         if (!objs[i]) continue;
         arrs[i] = (jbyteArray)(*env)->GetObjectField(env, objs[i], fid_buffer);
-        buf_len[i] = arrs[i] ? (uint32_t)(*env)->GetArrayLength(env, arrs[i]) : 0u;
-        offset[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_offset);
+        const uint32_t al = arrs[i] ? (uint32_t)(*env)->GetArrayLength(env, arrs[i]) : 0u;
+        joff[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_offset);
         length[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_length);
         flags[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_flags) &
                    (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE);
         if (sk && sk[i]) flags[i] |= SRTP_PKT_FLAG_SKIP;
+        /* the native copy holds the buffer from the packet's offset on (what
+         * the reference may read: the packet and the bytes behind it) */
+        buf_len[i] = joff[i] <= al ? al - joff[i] : 0u;
+        offset[i] = 0;
+        total += buf_len[i];
     }
-    for (jsize i = 0; i < n; i++)
-        if (arrs[i]) bufs[i] = (*env)->GetPrimitiveArrayCritical(env, arrs[i], NULL);
+    block = malloc(total ? total : 1);
+    if (!block) goto out;
+    total = 0;
+    for (jsize i = 0; i < n; i++) {
+        if (!arrs[i]) continue;
+        bufs[i] = block + total;
+        (*env)->GetByteArrayRegion(env, arrs[i], (jsize)joff[i], (jsize)buf_len[i], (jbyte *)bufs[i]);
+        total += buf_len[i];
+    }
     int32_t thrown = -1;
+    uint32_t *old_len = calloc((size_t)n, sizeof *old_len);
+    if (!old_len) goto out;
+    for (jsize i = 0; i < n; i++) old_len[i] = length[i];
     rc = srtp_rawpacket_transform(b, reverse ? 1 : 0, NULL, tid, bufs, buf_len, offset, length, flags, status,
                                   need, (uint32_t)n, &thrown);
-    for (jsize i = n; i-- > 0;) /* written in place: mode 0 copies back if the VM copied */
-        if (bufs[i]) (*env)->ReleasePrimitiveArrayCritical(env, arrs[i], bufs[i], 0);
-    if (rc != SRTP_OK) goto out;
+    if (rc != SRTP_OK) {
+        free(old_len);
+        goto out;
+    }
     for (jsize i = 0; i < n; i++) {
         const int32_t st = status[i];
         if (!objs[i] || st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED) continue;
@@ -168,19 +198,26 @@ JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch,
             jbyteArray nb = (*env)->NewByteArray(env, (jsize)need[i]);
             if (!nb || srtp_rawpacket_result(b, (uint32_t)i, &data, &dl) != SRTP_OK) {
                 rc = SRTP_ENOMEM;
+                free(old_len);
                 goto out;
             }
             (*env)->SetByteArrayRegion(env, nb, 0, (jsize)dl, (const jbyte *)data);
             (*env)->SetObjectField(env, objs[i], fid_buffer, nb);
             (*env)->SetIntField(env, objs[i], fid_offset, 0);
+        } else if (arrs[i]) { /* in place: the bytes up to the longer of the two lengths */
+            uint32_t w = old_len[i] > length[i] ? old_len[i] : length[i];
+            if (w > buf_len[i]) w = buf_len[i];
+            (*env)->SetByteArrayRegion(env, arrs[i], (jsize)joff[i], (jsize)w, (const jbyte *)bufs[i]);
         }
         (*env)->SetIntField(env, objs[i], fid_length, (jint)length[i]);
         if (st != SRTP_STATUS_OK && st != SRTP_STATUS_ERR_MALFORMED)
             (*env)->SetObjectArrayElement(env, pkts, i, NULL); /* the reference returned null */
     }
+    free(old_len);
     rc = thrown >= 0 ? thrown + 1 : 0;
 out:
     if (sk) (*env)->ReleaseIntArrayElements(env, skip, sk, JNI_ABORT);
+    free(block);
     free(objs);
     free(arrs);
     free(bufs);
@@ -188,4 +225,72 @@ out:
     free(status);
     (*env)->PopLocalFrame(env, NULL);
     return rc;
+}
+
+/* ---- the per-packet path (SinglePacketTransformer.transform(RawPacket)) ---- */
+
+JNIEXPORT jint JNICALL JFN(deviceCount)(JNIEnv *env, jclass c) {
+    return srtp_device_count();
+}
+
+/* One aggregator per process over the dispatcher: its lanes coalesce the
+ * per-packet calls of every JVM thread into GPU bundles. */
+JNIEXPORT jlong JNICALL JFN(aggregatorCreate)(JNIEnv *env, jclass c, jlong d) {
+    srtp_aggregator_opts o;
+    srtp_aggregator_opts_default(&o); /* SRTP_AGG_SEAL_IDLE */
+    srtp_aggregator *a = NULL;
+    return srtp_aggregator_create_dispatch((srtp_dispatch *)H(d), &o, NULL, NULL, &a) == SRTP_OK
+               ? (jlong)(intptr_t)a : 0;
+}
+
+JNIEXPORT void JNICALL JFN(aggregatorDestroy)(JNIEnv *env, jclass c, jlong a) {
+    srtp_aggregator_destroy((srtp_aggregator *)H(a));
+}
+
+/* Per-thread native copies of one packet: its bytes from the offset on, and
+ * the result where the reference reallocates. */
+#define ONE_BYTES (65535 + 16)
+static __thread uint8_t *tl_pkt, *tl_grow;
+
+/* transform / reverseTransform of one RawPacket (srtp_rawpacket_transform_one):
+ * returns its SRTP_STATUS_* (the Java side returns null for a drop and throws
+ * for SRTP_STATUS_ERR_MALFORMED) or a negative SRTP_E* code.  The call blocks
+ * until the packet's bundle has come back; no Java array is held meanwhile. */
+JNIEXPORT jint JNICALL JFN(transformOne)(JNIEnv *env, jclass c, jlong agg, jboolean reverse, jint tid,
+                                         jobject pkt) {
+    if (!pkt || raw_packet_ids(env) != 0) return SRTP_EINVAL;
+    if (!tl_pkt) {
+        tl_pkt = malloc(ONE_BYTES);
+        tl_grow = malloc(ONE_BYTES);
+        if (!tl_pkt || !tl_grow) return SRTP_ENOMEM;
+    }
+    jbyteArray arr = (jbyteArray)(*env)->GetObjectField(env, pkt, fid_buffer);
+    const uint32_t al = arr ? (uint32_t)(*env)->GetArrayLength(env, arr) : 0u;
+    const uint32_t joff = (uint32_t)(*env)->GetIntField(env, pkt, fid_offset);
+    uint32_t length = (uint32_t)(*env)->GetIntField(env, pkt, fid_length);
+    const uint32_t flags = (uint32_t)(*env)->GetIntField(env, pkt, fid_flags) &
+                           (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE);
+    uint32_t avail = joff <= al ? al - joff : 0u;
+    if (avail > 65535u) avail = 65535u; /* no region is larger */
+    if (arr && avail) (*env)->GetByteArrayRegion(env, arr, (jsize)joff, (jsize)avail, (jbyte *)tl_pkt);
+    const uint32_t old = length;
+    int32_t status = 0;
+    uint32_t need = 0;
+    int rc = srtp_rawpacket_transform_one((srtp_aggregator *)H(agg), reverse ? 1 : 0, tid, arr ? tl_pkt : NULL,
+                                          avail, 0, &length, flags, &status, &need, tl_grow, ONE_BYTES);
+    if (rc != SRTP_OK) return rc;
+    if (status == SRTP_STATUS_SKIPPED) return status;
+    if (need) { /* RawPacket.append / grow: a new byte[] at offset 0 */
+        jbyteArray nb = (*env)->NewByteArray(env, (jsize)need);
+        if (!nb) return SRTP_ENOMEM;
+        (*env)->SetByteArrayRegion(env, nb, 0, (jsize)length, (const jbyte *)tl_grow);
+        (*env)->SetObjectField(env, pkt, fid_buffer, nb);
+        (*env)->SetIntField(env, pkt, fid_offset, 0);
+    } else if (arr) {
+        uint32_t w = old > length ? old : length;
+        if (w > avail) w = avail;
+        (*env)->SetByteArrayRegion(env, arr, (jsize)joff, (jsize)w, (const jbyte *)tl_pkt);
+    }
+    (*env)->SetIntField(env, pkt, fid_length, (jint)length);
+    return status;
 }

@@ -11,6 +11,8 @@ public class GpuSRTPContextFactory
 {
     final int id;
 
+    private boolean closed;
+
     public GpuSRTPContextFactory(boolean sender, byte[] masterKey, byte[] masterSalt,
                                  SRTPPolicy srtpPolicy, SRTPPolicy srtcpPolicy)
     {
@@ -24,9 +26,17 @@ public class GpuSRTPContextFactory
                            p.getAuthTagLength(), p.getSaltKeyLength() };
     }
 
-    /** SRTPContextFactory.close(): zeroes the keys, no new contexts. */
-    public void close()
+    /**
+     * SRTPContextFactory.close() (:74-86): zeroes the keys, no new contexts.
+     * Closing twice is harmless (an SRTCP transformer built from an SRTP
+     * transformer shares its factories, and each closes them).
+     */
+    public synchronized void close()
     {
-        SrtpMi355x.factoryClose(SrtpMi355x.dispatch(), id);
+        if (!closed)
+        {
+            closed = true;
+            SrtpMi355x.factoryClose(SrtpMi355x.dispatch(), id);
+        }
     }
 }

@@ -1,11 +1,15 @@
 /*
  * Native declarations of the JNI shim src/native/srtp_mi355x/SrtpMi355x.c
- * over the MI355X SRTP engine (include/srtp_mi355x.h).  NOT COMPILED IN THIS
- * REPOSITORY (no JDK in the build image); see INTEGRATION.md.
+ * over the MI355X SRTP engine (include/srtp_mi355x.h), and the process-wide
+ * engine state.  NOT COMPILED IN THIS REPOSITORY (no JDK in the build image);
+ * see INTEGRATION.md.
  */
 package org.jitsi.impl.neomedia.transform.srtp.mi355x;
 
 import org.jitsi.impl.neomedia.*;
+import org.jitsi.impl.neomedia.transform.srtp.*;
+import org.jitsi.service.configuration.*;
+import org.jitsi.service.libjitsi.*;
 import org.jitsi.util.*;
 
 public final class SrtpMi355x
@@ -16,8 +20,17 @@ public final class SrtpMi355x
         JNIUtils.loadLibrary("jnsrtp_mi355x", SrtpMi355x.class.getClassLoader());
     }
 
+    /**
+     * The number of GPUs to shard over (default: every device the HIP runtime
+     * reports, srtp_device_count).
+     */
+    public static final String GPUS_PNAME = "org.jitsi.impl.neomedia.transform.srtp.mi355x.GPUS";
+
     /** One dispatcher per process: every GPU of the node, SSRC-sharded. */
     private static long dispatch;
+
+    /** One aggregator per process over it: the per-packet calls' bundles. */
+    private static long aggregator;
 
     private static final ThreadLocal<Long> BATCH = new ThreadLocal<>();
 
@@ -25,15 +38,37 @@ public final class SrtpMi355x
     {
         if (dispatch == 0)
         {
-            int n = Integer.getInteger("org.jitsi.srtp.mi355x.GPUS", 8);
+            // SRTPCryptoContext.readConfigurationServicePropertiesOnce
+            // (SRTPCryptoContext.java:105-121): the same property, the same default
+            boolean checkReplay = true;
+            int n = deviceCount();
+            ConfigurationService cfg = LibJitsi.getConfigurationService();
+            if (cfg != null)
+            {
+                checkReplay = cfg.getBoolean(SRTPCryptoContext.CHECK_REPLAY_PNAME, checkReplay);
+                n = cfg.getInt(GPUS_PNAME, n);
+            }
+            if (n < 1)
+                throw new IllegalStateException("srtp_mi355x: no GPU");
             int[] devices = new int[n];
             for (int i = 0; i < n; i++)
                 devices[i] = i;
-            dispatch = dispatchCreate(devices, true, 0);
+            dispatch = dispatchCreate(devices, checkReplay, 0);
             if (dispatch == 0)
                 throw new IllegalStateException("srtp_mi355x: no engine");
         }
         return dispatch;
+    }
+
+    static synchronized long aggregator()
+    {
+        if (aggregator == 0)
+        {
+            aggregator = aggregatorCreate(dispatch());
+            if (aggregator == 0)
+                throw new IllegalStateException("srtp_mi355x: no aggregator");
+        }
+        return aggregator;
     }
 
     /** The calling thread's RawPacket[] staging (srtp_rawpacket_batch). */
@@ -55,6 +90,7 @@ public final class SrtpMi355x
         return rc;
     }
 
+    static native int deviceCount();
     static native long dispatchCreate(int[] devices, boolean checkReplay, int maxContexts);
     static native void dispatchDestroy(long d);
     static native int factoryCreate(long d, boolean sender, byte[] key, byte[] salt, int[] srtpPolicy,
@@ -68,4 +104,9 @@ public final class SrtpMi355x
     /** 0, 1 + the first throwing element, or a negative error code. */
     static native int transformPackets(long batch, boolean reverse, int transformer, RawPacket[] pkts,
                                        int[] skip);
+    /** srtp_aggregator_create_dispatch with SRTP_AGG_SEAL_IDLE and no callback. */
+    static native long aggregatorCreate(long d);
+    static native void aggregatorDestroy(long a);
+    /** One packet (srtp_rawpacket_transform_one): its SRTP_STATUS_*, or a negative error code. */
+    static native int transformOne(long aggregator, boolean reverse, int transformer, RawPacket pkt);
 }

@@ -190,11 +190,70 @@ def test_backpressure_many_bundles(engine_factory, oracle):
         agg.close()
 
 
-def test_refuses_abort_on_error_engine(engine_factory):
+def test_abort_engine_bundles_run_per_packet(engine_factory, oracle):
+    """An engine with abort_on_error (the RawPacket[] path's) serves the
+    aggregator too: its bundles run without abort-on-throw
+    (srtp_pipeline_submit_ex), so a packet the reference throws on does not
+    stop its transformer's later packets -- each is its own 1-element array."""
     E = engine_factory(abort_on_error=True, max_contexts=1024, max_factories=16,
                        max_transformers=16)
-    with pytest.raises(N.SrtpError):
-        SRTPAggregator(E, lambda *a: None)
+    tw = Twin(E)
+    (k, s), = synth.keys(80, 1)
+    A = tw.transformer(O.KIND_RTP, tw.factory(True, k, s, *P80))
+    b = synth.rtp_bundle(40, 4, (100, 300), seed=81)
+    items = [(A, d, 0) for d in packets(b)]
+    bad = bytearray(items[10][1][:40])
+    bad[0] |= 0x10
+    bad[14:16] = b"\x7f\xff"  # an extension past the end: the reference throws
+    items.insert(10, (A, bytes(bad), 0))
+    col = Collector()
+    agg = SRTPAggregator(E, col, max_packets=64, deadline_us=300, depth=3, seal_idle=False)
+    try:
+        for i, (t, d, fl) in enumerate(items):
+            agg.submit(False, t.e, d, fl, cookie=i)
+        agg.flush()
+        outs = check_against_oracle(col, items, False, 1)
+        assert outs[10][0] == N.STATUS_ERR_MALFORMED
+        assert all(outs[i][0] == N.STATUS_OK for i in range(11, len(items)))
+    finally:
+        agg.close()
+
+
+def test_close_refuses_forwards_and_delivers_accepted(engine_factory, oracle):
+    """Closing while callbacks still forward: every packet the aggregator
+    accepted is delivered to a callback; forwards after the close began are
+    refused (SRTP_EINVAL), none is lost silently."""
+    E = engine_factory(abort_on_error=False, max_contexts=4096, max_factories=16,
+                       max_transformers=16)
+    tw = Twin(E)
+    (k, s), = synth.keys(82, 1)
+    A = tw.transformer(O.KIND_RTP, tw.factory(True, k, s, *P80))
+    B = tw.transformer(O.KIND_RTP, tw.factory(True, k, s, *P80))
+    b = synth.rtp_bundle(400, 20, (100, 300), seed=83)
+    lock = threading.Lock()
+    got, refused = [], [0]
+    holder = {}
+
+    def cb(cookie, status, data):
+        with lock:
+            got.append(cookie)
+        if cookie < 1000:  # forward each packet of A once, as B's
+            try:
+                rc = holder["agg"].submit(False, B.e, bytes(data[:12]) + bytes(50), cookie=cookie + 1000)
+                assert rc == 0
+            except N.SrtpError:
+                with lock:
+                    refused[0] += 1
+
+    agg = SRTPAggregator(E, cb, max_packets=32, max_bytes=1 << 16, deadline_us=200, depth=4)
+    holder["agg"] = agg
+    for i, d in enumerate(packets(b)):
+        agg.submit(False, A.e, d, cookie=i)
+    agg.close()  # no flush first: forwards are still being made
+    firsts = [c for c in got if c < 1000]
+    fwds = [c for c in got if c >= 1000]
+    assert sorted(firsts) == list(range(b.n))
+    assert len(fwds) + refused[0] == b.n  # each forward delivered or refused, never lost
 
 
 def _lane_of(d):

@@ -3,7 +3,7 @@
 # a variant .so, or "default"), alternating, REPS times; prints value and the
 # crypto kernels' per-launch times.  Then a short parity check of each variant.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/${R03_TAG:-r03_ab}
+O=gpurun_out/${AB_TAG:-ab}
 mkdir -p $O
 REPS=${REPS:-2}
 for rep in $(seq $REPS); do

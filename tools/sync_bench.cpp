@@ -1,0 +1,187 @@
+// sync_bench.cpp -- latency and throughput of the per-packet drop-in path:
+// T threads, each calling SinglePacketTransformer.transform(RawPacket) as the
+// reference's callers do (one packet per call: RTPConnectorOutputStream.java
+// :268-300, DtlsPacketTransformer.java:1544-1564), on 50 transformers.
+//
+//   path "one":   srtp_rawpacket_transform_one -- the calls of all threads
+//                 coalesce into shared bundles (srtp_aggregator_transform,
+//                 SRTP_AGG_SEAL_IDLE)
+//   path "array": srtp_rawpacket_transform with a 1-element array on the
+//                 thread's own batch -- one GPU round trip per call (the
+//                 round-3 drop-in)
+//
+// over one engine or a G-shard dispatcher (all shards on device 0 of a one-GPU
+// box).  1200-B RTP packets, AES_CM_128_HMAC_SHA1_80 protect, each thread its
+// own SSRCs.  Prints one JSON line per (path, shards, threads): calls/s and
+// the per-call latency percentiles.
+//
+//   sync_bench [seconds-per-point]
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <thread>
+#include <vector>
+
+#include "../include/srtp_mi355x.h"
+
+namespace {
+using Clock = std::chrono::steady_clock;
+
+int check(int rc, const char *what) {
+    if (rc != SRTP_OK) {
+        fprintf(stderr, "%s failed: %d\n", what, rc);
+        exit(1);
+    }
+    return rc;
+}
+
+void fill_packet(uint8_t *p, uint32_t len, uint64_t &rng) {
+    for (uint32_t i = 12; i < len; i++) {
+        rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+        p[i] = (uint8_t)(rng >> 56);
+    }
+    p[0] = 0x80;
+    p[1] = 96;
+}
+
+double pct(std::vector<uint32_t> &v, double q) {
+    if (v.empty()) return 0.0;
+    const size_t k = std::min(v.size() - 1, (size_t)(q * (double)v.size()));
+    std::nth_element(v.begin(), v.begin() + (long)k, v.end());
+    return v[k] / 1000.0;
+}
+} // namespace
+
+int main(int argc, char **argv) {
+    const double seconds = argc > 1 ? atof(argv[1]) : 2.0;
+    const uint32_t L = 1200, BUF = L + 16; // room behind the packet: the tag is appended in place
+    const int n_tr = 50;
+    srtp_policy pol = {SRTP_AESCM_ENCRYPTION, 16, SRTP_HMACSHA1_AUTHENTICATION, 20, 10, 14};
+    const int shard_counts[] = {0, 8};
+    const int thread_counts[] = {1, 8, 64};
+    for (int path = 0; path < 2; path++) {
+        for (int G : shard_counts) {
+            for (int T : thread_counts) {
+                if (path == 1 && T == 64 && G == 8) continue; // 64 pinned batches x 8 shards: skip
+                srtp_engine_opts o;
+                srtp_engine_opts_default(&o);
+                o.max_contexts = 1u << 16;
+                o.max_factories = 128;
+                o.max_transformers = 128;
+                srtp_engine *e = nullptr;
+                srtp_dispatch *d = nullptr;
+                std::vector<int32_t> tr((size_t)n_tr);
+                if (G == 0) check(srtp_engine_create(&o, &e), "engine");
+                else {
+                    std::vector<int32_t> devs((size_t)G, 0);
+                    check(srtp_dispatch_create(devs.data(), G, &o, &d), "dispatch");
+                }
+                for (int t = 0; t < n_tr; t++) {
+                    uint8_t key[16], salt[14];
+                    for (int i = 0; i < 16; i++) key[i] = (uint8_t)(17 * i + 3 + t);
+                    for (int i = 0; i < 14; i++) salt[i] = (uint8_t)(29 * i + 5 + t);
+                    int32_t f = -1;
+                    check(d ? srtp_dispatch_factory_create(d, 1, key, 16, salt, 14, &pol, &pol, &f)
+                            : srtp_factory_create(e, 1, key, 16, salt, 14, &pol, &pol, &f), "factory");
+                    check(d ? srtp_dispatch_transformer_create(d, SRTP_KIND_RTP, f, f, &tr[(size_t)t])
+                            : srtp_transformer_create(e, SRTP_KIND_RTP, f, f, &tr[(size_t)t]), "transformer");
+                }
+                srtp_aggregator *a = nullptr;
+                if (path == 0) {
+                    srtp_aggregator_opts ao;
+                    srtp_aggregator_opts_default(&ao);
+                    ao.max_packets = 4096;
+                    ao.max_bytes = 8u << 20;
+                    check(d ? srtp_aggregator_create_dispatch(d, &ao, nullptr, nullptr, &a)
+                            : srtp_aggregator_create(e, &ao, nullptr, nullptr, &a), "aggregator");
+                }
+                std::atomic<bool> stop{false};
+                std::atomic<int> started{0};
+                std::vector<std::vector<uint32_t>> lat((size_t)T);
+                std::vector<uint64_t> bad((size_t)T, 0);
+                std::vector<std::thread> th;
+                for (int k = 0; k < T; k++) {
+                    th.emplace_back([&, k] {
+                        srtp_rawpacket_batch *b = nullptr;
+                        if (path == 1)
+                            check(d ? srtp_rawpacket_batch_create_dispatch(d, &b) : srtp_rawpacket_batch_create(e, &b),
+                                  "batch");
+                        std::vector<uint8_t> buf(BUF), grow(65535 + 16);
+                        uint64_t rng = 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1);
+                        fill_packet(buf.data(), L, rng);
+                        const int n_ssrc = 3;
+                        uint16_t seq[n_ssrc];
+                        for (auto &x : seq) x = (uint16_t)(rng >> 40), rng = rng * 6364136223846793005ull + 1;
+                        std::vector<uint32_t> &mine = lat[(size_t)k];
+                        mine.reserve(1u << 20);
+                        started++;
+                        uint64_t n = 0;
+                        while (!stop.load(std::memory_order_relaxed)) {
+                            const int s = (int)(n % n_ssrc);
+                            const uint32_t ssrc = 0x20000000u + (uint32_t)k * 16u + (uint32_t)s;
+                            const int32_t t = tr[(size_t)((k * n_ssrc + s) % n_tr)];
+                            const uint16_t q = seq[s]++;
+                            buf[2] = (uint8_t)(q >> 8); buf[3] = (uint8_t)q;
+                            buf[8] = (uint8_t)(ssrc >> 24); buf[9] = (uint8_t)(ssrc >> 16);
+                            buf[10] = (uint8_t)(ssrc >> 8); buf[11] = (uint8_t)ssrc;
+                            uint32_t len = L, need = 0;
+                            int32_t st = -1;
+                            const auto t0 = Clock::now();
+                            if (path == 0) {
+                                check(srtp_rawpacket_transform_one(a, 0, t, buf.data(), BUF, 0, &len, 0, &st, &need,
+                                                                   grow.data(), (uint32_t)grow.size()), "one");
+                            } else {
+                                uint8_t *bp = buf.data();
+                                uint32_t bl = BUF, off = 0, fl = 0;
+                                int32_t thrown = -1;
+                                check(srtp_rawpacket_transform(b, 0, nullptr, t, &bp, &bl, &off, &len, &fl, &st, &need, 1,
+                                                               &thrown), "array");
+                            }
+                            const auto t1 = Clock::now();
+                            mine.push_back((uint32_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
+                            if (st != SRTP_STATUS_OK || len != L + 10) bad[(size_t)k]++;
+                            n++;
+                        }
+                        if (b) srtp_rawpacket_batch_destroy(b);
+                    });
+                }
+                while (started.load() < T) std::this_thread::yield();
+                const auto t0 = Clock::now();
+                std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+                stop = true;
+                for (auto &x : th) x.join();
+                const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
+                std::vector<uint32_t> all;
+                uint64_t nbad = 0;
+                for (int k = 0; k < T; k++) {
+                    all.insert(all.end(), lat[(size_t)k].begin(), lat[(size_t)k].end());
+                    nbad += bad[(size_t)k];
+                }
+                uint64_t acc = 0, comp = 0, bundles = 0;
+                if (a) {
+                    srtp_aggregator_stats(a, &acc, &comp, &bundles);
+                    srtp_aggregator_destroy(a);
+                }
+                double mean = 0;
+                for (uint32_t x : all) mean += x;
+                mean = all.empty() ? 0 : mean / all.size() / 1000.0;
+                const size_t calls = all.size();
+                printf("{\"path\": \"%s\", \"shards\": %d, \"dispatcher\": %s, \"threads\": %d, \"transformers\": %d, "
+                       "\"pkt_len\": %u, \"calls\": %zu, \"seconds\": %.3f, \"calls_per_s\": %.1f, "
+                       "\"lat_us\": {\"mean\": %.1f, \"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f}, "
+                       "\"bundles\": %llu, \"packets_per_bundle\": %.1f, \"not_ok\": %llu}\n",
+                       path == 0 ? "one" : "array", G ? G : 1, G ? "true" : "false", T, n_tr, L, calls, dt,
+                       calls / dt, mean, pct(all, 0.5), pct(all, 0.9), pct(all, 0.99), pct(all, 0.999),
+                       (unsigned long long)bundles, bundles ? (double)comp / bundles : 0.0,
+                       (unsigned long long)nbad);
+                fflush(stdout);
+                if (d) srtp_dispatch_destroy(d);
+                if (e) srtp_engine_destroy(e);
+            }
+        }
+    }
+    return 0;
+}
