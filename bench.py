@@ -17,10 +17,12 @@ step i = protect(i) then unprotect(i).
 
 Multi-GPU: one process per GPU (torchrun), contexts sharded by SSRC (each rank
 owns its own SSRCs), no collective on the data path ("scaling": "weak").
-Without torchrun, ``--gpus N`` drives N GPUs from this one process (the
-in-process deployment: one engine pair per GPU, each GPU's steps enqueued by a
-host thread of its own; ``SRTP_BENCH_ONE_DEVICE=1`` puts all N on device 0, a
-rehearsal on a one-GPU box).  value = packets protected AND unprotected by all
+Without torchrun, ``--gpus N`` starts the N processes itself (rank r on GPU r,
+rendezvous on 127.0.0.1), before anything touches a GPU, so no GPU's steps
+wait for another's Python; ``SRTP_BENCH_INPROC=1`` drives the N GPUs from this
+one process instead (one host thread each, sharing the GIL: the in-process
+deployment).  ``SRTP_BENCH_ONE_DEVICE=1`` puts all N on device 0, a rehearsal
+on a one-GPU box (with ``--backend gloo`` in process mode).  value = packets protected AND unprotected by all
 GPUs / wall time (max over ranks).  The line also reports the host time spent
 enqueueing a step, per GPU.
 
@@ -55,6 +57,9 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=1 << 18, help="bundle size per GPU")
     ap.add_argument("--ssrcs", type=int, default=10000, help="concurrent SSRCs per GPU")
+    ap.add_argument("--keysets", type=int, default=1,
+                    help="sender/receiver transformer pairs, each with its own master key: SSRC s "
+                         "belongs to pair s %% K (a bridge's many DTLS sessions in one bundle)")
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="SSRC popularity Zipf exponent (0: round-robin, every SSRC equal)")
     ap.add_argument("--len", type=int, default=1200, help="RTP packet length")
@@ -280,15 +285,30 @@ class Side:
         # context table >= 1.6x the SSRCs (load <= 0.31 at 10k); its size sets
         # the sort's key width (2^15 slots + the invalid key: two radix passes)
         max_ctx = 1 << max(12, (int(1.6 * nssrc) - 1).bit_length())
-        mk = dict(device=device, max_contexts=max_ctx, max_factories=64, max_transformers=64,
-                  max_batch=n)
+        K = max(1, args.keysets)
+        mk = dict(device=device, max_contexts=max_ctx, max_factories=max(64, 2 * K + 8),
+                  max_transformers=max(64, 2 * K + 8), max_batch=n)
         self.eng = SRTPEngine(**mk)
         self.eng_r = self.eng if args.serial else SRTPEngine(**mk)
         (k, s), = synth.keys(2 + shard, 1)
         self.keys = (k, s)
         self.snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=self.eng))
         self.rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=self.eng_r))
+        self.tid_s, self.tid_r = self.snd.tid, self.rcv.tid
+        if K > 1:  # K key sets: per-packet transformer ids (srtp_transform_device tids[])
+            ks = synth.keys(1000 + 97 * shard, K - 1)
+            snd, rcv = [self.snd], [self.rcv]
+            for kk, ss in ks:
+                snd.append(SRTPTransformer(SRTPContextFactory(True, kk, ss, *pols, engine=self.eng)))
+                rcv.append(SRTPTransformer(SRTPContextFactory(False, kk, ss, *pols, engine=self.eng_r)))
+            self._tr_keep = (snd, rcv)
+            pair = np.arange(n) % nssrc % K
+            ts_np = np.array([t.tid for t in snd], np.int32)[pair]
+            tr_np = np.array([t.tid for t in rcv], np.int32)[pair]
         with torch.cuda.device(dev):
+            if K > 1:
+                self.tid_s = torch.from_numpy(ts_np).to(dev)
+                self.tid_r = torch.from_numpy(tr_np).to(dev)
             self.off = torch.from_numpy(b.off.view(np.int32)).to(dev)
             self.cap = torch.from_numpy(b.cap.view(np.int32)).to(dev)
             self.st = torch.empty(n, dtype=torch.int32, device=dev)
@@ -336,12 +356,12 @@ class Side:
             stream.wait_event(self.ev_free[j])
             with self.torch.cuda.stream(stream):
                 self.advance_seq(self.segs[j], self.ring)
-        self.eng.transform_device(False, self.snd.tid, self.segs[j], self.off, self.lens[j],
+        self.eng.transform_device(False, self.tid_s, self.segs[j], self.off, self.lens[j],
                                   self.cap, self.st, stream=stream)
 
     def unprotect(self, i, stream):
         j = i % self.ring
-        self.eng_r.transform_device(True, self.rcv.tid, self.segs[j], self.off, self.lens[j],
+        self.eng_r.transform_device(True, self.tid_r, self.segs[j], self.off, self.lens[j],
                                     self.cap, self.st_r, stream=stream)
         self.ev_free[j].record(stream)
 
@@ -450,12 +470,32 @@ def run_steps(torch, sides, g0, warmup, steps, barrier=None):
     return min(r[0] for r in res), max(r[1] for r in res), [r[2] for r in res]
 
 
+def spawn_ranks(n: int) -> int:
+    """--gpus N without torchrun: one child process per GPU, started before
+    this process touches a GPU (it never does), each a torchrun-style rank on
+    127.0.0.1.  Rank 0's stdout (the JSON line) is passed through."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def main():
     args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1 and os.environ.get("SRTP_BENCH_INPROC") != "1":
+        sys.exit(spawn_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # SRTP_BENCH_ONE_DEVICE=1 puts every rank on device 0: a rehearsal of the
@@ -598,18 +638,29 @@ def main():
         if stage not in stages or stages[stage] <= 0:
             return None
         achieved = alg_launch / (stages[stage] / 1e3) / 1e9
+        # traffic: HBM bytes per launch from the committed PMC passes, corrected
+        # as the guide prescribes (FETCH_SIZE x 2 + WRITE_SIZE, gfx950).  The
+        # guide's factor is calibrated for 16-B-per-lane coalesced streams; for
+        # these kernels' per-lane 64-B chunk walk it overstates (profiles/r03/
+        # pmc_calib_factor.json), so the physical bytes lie between the in-place
+        # floor (every payload byte read once, ciphertext + trailer written
+        # once) and this figure: traffic_range.
+        g = (pmc.get("guide_correction_bytes_per_launch") or {}).get(kernel)
+        hdr = 12  # RTP header: read, never rewritten
+        floor = n * (L + (L - hdr + T)) if kernel == "k_protect" else n * ((L + T) + (L - hdr))
         r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-             "traffic": pmc.get(traffic_key), "avg_launch_ms": round(stages[stage], 4),
+             "traffic": g, "avg_launch_ms": round(stages[stage], 4),
              "algorithmic_bytes_per_launch": alg_launch,
              "copy_measured_gbps": copy_gbs}
-        if r["traffic"]:
-            r["traffic_source"] = (f"rocprofv3 FETCH_SIZE/WRITE_SIZE per {kernel} launch, profiles/pmc_traffic.json: "
-                                   + pmc.get("method", ""))
-            r["traffic_over_algorithmic"] = round(r["traffic"] / alg_launch, 3)
-            g = (pmc.get("guide_correction_bytes_per_launch") or {}).get(kernel)
-            if g:  # the guide's stream correction (FETCH x 2), kept for comparison
-                r["traffic_guide_correction"] = g
+        if g:
+            r["traffic_source"] = (f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE per {kernel} launch, "
+                                   f"FETCH x 2 + WRITE (the guide's gfx950 correction), {pmc.get('source', '')}")
+            r["traffic_over_algorithmic"] = round(g / alg_launch, 3)
+            r["traffic_range"] = {"floor": floor, "guide_corrected": g,
+                                  "pattern_calibrated": pmc.get(traffic_key),
+                                  "note": "physical bytes lie in [floor, guide_corrected]; the pattern "
+                                          "calibration (tools/pmc_calib.hip) is quoted, not trusted"}
         if util_key and pmc.get(util_key):
             r["utilisation"] = pmc.get(util_key)
         return r
@@ -702,6 +753,7 @@ def main():
                        "packets_per_gpu_per_step": n, "ssrcs_per_gpu": args.ssrcs, "pkt_len": L,
                        "region_align": args.align,
                        "ssrc_mix": f"zipf({args.zipf})" if args.zipf > 0 else "round-robin",
+                       "keysets": args.keysets,
                        "parallelism": f"ssrc-sharded x{n_gpus} ({'one process per GPU' if mode == 'process' else 'one process, all GPUs'})",
                        "streams": "serial: protect(i), unprotect(i) on one stream" if args.serial else
                                   {"free": "sender + receiver engine, one stream each: unprotect(i) "

@@ -59,9 +59,15 @@
 // reserves its entry and then looks at idle, both sequentially consistent,
 // so at least one of them sees the other and seals.
 //
-// Synchronous calls (srtp_aggregator_transform): the entry carries a waiter
-// instead of a cookie; the lane thread copies the packet's result to the
-// caller's buffer and wakes it (a futex), in bundle order like a callback.
+// Synchronous calls (srtp_aggregator_transform) do not reserve entries: a
+// caller pushes its request (packet pointer, lengths, where the result goes)
+// on its lane's lock-free stack and sleeps on a futex.  The lane thread pops
+// the stack, copies the requests' packets into a free slot itself and submits
+// it -- so a caller preempted between reserving and filling an entry can never
+// hold a bundle back (64 callers on 16 cores made that the common case) -- and
+// when the bundle completes it copies each result back and wakes its caller.
+// While the lane has a bundle in flight the requests pile up on the stack and
+// go out together when it returns: bundles grow with the number of callers.
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -115,6 +121,15 @@ struct Waiter {
     uint8_t *out = nullptr;
 };
 
+// Its request, on the caller's stack until it is woken.
+struct SyncReq {
+    SyncReq *next = nullptr;
+    const uint8_t *pkt = nullptr;
+    uint32_t copy_len = 0, len = 0, cap = 0, flags = 0;
+    int32_t tid = -1, reverse = 0;
+    Waiter w;
+};
+
 void futex_wait(std::atomic<uint32_t> *w, uint32_t v) {
     syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
 }
@@ -162,6 +177,9 @@ struct Lane {
     std::condition_variable cv_work;  // the lane's dispatch thread: something to do
     std::condition_variable cv_space; // producers: a slot of this lane became free
     std::atomic<int> idle{1};         // SRTP_AGG_SEAL_IDLE: nothing sealed or in flight
+    std::atomic<SyncReq *> sync_head{nullptr}; // synchronous requests, newest first
+    std::deque<SyncReq *> sync_pending;        // popped, not yet placed (lane thread, in order)
+    std::atomic<int> sleeping{0};              // the lane thread waits on cv_work
     std::thread thread;
 };
 
@@ -193,6 +211,7 @@ struct srtp_aggregator {
     std::condition_variable cv_idle;  // flush(): everything completed
     std::vector<std::unique_ptr<Lane>> lanes;
     std::atomic<bool> closing{false}; // destroy has begun: submits are refused
+    std::atomic<int> sync_callers{0}; // srtp_aggregator_transform calls inside (destroy waits)
     bool stop = false;
     // transformer kinds, read without a lock (-2: not looked up yet)
     std::unique_ptr<std::atomic<int32_t>[]> kinds;
@@ -386,7 +405,7 @@ uint64_t pending_locked(const srtp_aggregator *a) {
             const Slot &sl = ln->slots[resv_slot1(r) - 1];
             for (uint32_t k = 0; k < resv_n(r); k++) n += blk_used(sl.blocks[k].w.load());
         }
-        n += ln->parked.size();
+        n += ln->parked.size() + ln->sync_pending.size() + (ln->sync_head.load() ? 1 : 0);
     }
     return n;
 }
@@ -418,6 +437,64 @@ void place_parked_locked(srtp_aggregator *a, Lane &ln, uint32_t lane) {
     }
 }
 
+// Synchronous requests may be placed: some are waiting, a slot is free and
+// fewer than two bundles are sealed or in flight.
+bool sync_placeable_locked(const Lane &ln) {
+    if (!ln.sync_head.load() && ln.sync_pending.empty()) return false;
+    if (ln.sealed.size() + ln.inflight.size() >= 2) return false;
+    for (int i = 0; i < ln.n_slots; i++)
+        if (ln.slots[i].state == kFree) return true;
+    return false;
+}
+
+// Copies waiting synchronous requests of one direction (the oldest request's)
+// into a free slot, in arrival order, and seals it.
+void place_sync_locked(srtp_aggregator *a, Lane &ln) {
+    SyncReq *h = ln.sync_head.exchange(nullptr);
+    SyncReq *rev = nullptr; // the stack is newest first
+    while (h) {
+        SyncReq *nx = h->next;
+        h->next = rev;
+        rev = h;
+        h = nx;
+    }
+    for (; rev; rev = rev->next) ln.sync_pending.push_back(rev);
+    int s = -1;
+    for (int i = 0; i < ln.n_slots && s < 0; i++)
+        if (ln.slots[i].state == kFree) s = i;
+    if (s < 0 || ln.sync_pending.empty()) return;
+    Slot &sl = ln.slots[s];
+    const int32_t dir = ln.sync_pending.front()->reverse;
+    uint32_t n = 0;
+    size_t pos = 0;
+    for (auto it = ln.sync_pending.begin(); it != ln.sync_pending.end();) {
+        SyncReq *r = *it;
+        const size_t need = need_of(r->cap);
+        if (r->reverse != dir) { ++it; continue; }
+        if (n == a->opts.max_packets || pos + need > a->opts.max_bytes) break;
+        if (r->copy_len) memcpy(sl.h.seg + pos, r->pkt, r->copy_len);
+        if (need > r->copy_len) memset(sl.h.seg + pos + r->copy_len, 0, need - r->copy_len);
+        sl.h.off[n] = (uint32_t)pos;
+        sl.h.len[n] = r->len;
+        sl.h.cap[n] = r->cap;
+        sl.h.flags[n] = r->flags;
+        sl.h.tids[n] = r->tid;
+        sl.cookies[n] = r->len; // the submitted length (see the completion loop)
+        sl.waiters[n] = &r->w;
+        sl.hole[n] = 0;
+        pos += need;
+        n++;
+        it = ln.sync_pending.erase(it);
+    }
+    sl.state = kSealed;
+    sl.reverse = dir;
+    sl.n = sl.n_real = n;
+    sl.bytes = pos;
+    sl.ready = n; // every entry is complete
+    ln.sealed.push_back(s);
+    ln.idle.store(0);
+}
+
 void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
     std::unique_lock<std::mutex> lk(a->mu);
     // keep up to depth - 2 bundles in flight (one slot per open direction)
@@ -430,12 +507,22 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
             straggler = !slot_ready(ln->slots[ln->sealed.front()]);
             return !straggler;
         };
-        auto go = [&] { return a->stop || can_submit() || !ln->inflight.empty(); };
-        while (!go()) {
+        auto go = [&] {
+            return a->stop || sync_placeable_locked(*ln) || can_submit() || !ln->inflight.empty();
+        };
+        // sleeping is raised before the last look (a synchronous caller pushes,
+        // then looks at it: one of the two sees the other)
+        for (;;) {
+            ln->sleeping.store(1);
+            if (go()) break;
             if (straggler) ln->cv_work.wait_for(lk, std::chrono::microseconds(20)); // copies take ~0.1 us
             else ln->cv_work.wait(lk);
         }
-        if (a->stop && ln->sealed.empty() && ln->inflight.empty() && ln->parked.empty()) return;
+        ln->sleeping.store(0);
+        if (a->stop && ln->sealed.empty() && ln->inflight.empty() && ln->parked.empty() &&
+            !ln->sync_head.load() && ln->sync_pending.empty())
+            return;
+        if (sync_placeable_locked(*ln)) place_sync_locked(a, *ln);
         if (can_submit()) {
             const int s = ln->sealed.front();
             ln->sealed.pop_front();
@@ -674,14 +761,38 @@ int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, 
         cap > 65535u)
         return SRTP_EINVAL;
     if (tl_in_callback == a) return SRTP_EINVAL; // would wait for its own lane
-    Waiter w;
-    w.out = out;
-    // the waiter's entry keeps the submitted length in its cookie word
-    const int rc = submit_entry(a, reverse, tid, pkt, copy_len, len, cap, flags, (uint64_t)len, &w);
-    if (rc != SRTP_OK) return rc;
-    while (w.done.load(std::memory_order_acquire) == 0) futex_wait(&w.done, 0);
-    *status = w.status;
-    *out_len = w.len;
+    if (need_of(cap) > a->opts.max_bytes) return SRTP_EINVAL;
+    struct Inside { // counted before the closing check: destroy waits for every caller inside
+        srtp_aggregator *a;
+        ~Inside() { a->sync_callers.fetch_sub(1); }
+    } inside{a};
+    a->sync_callers.fetch_add(1);
+    if (a->closing.load()) return SRTP_EINVAL;
+    SyncReq r;
+    r.pkt = pkt;
+    r.copy_len = copy_len;
+    r.len = len;
+    r.cap = cap;
+    r.flags = flags;
+    r.tid = tid;
+    r.reverse = reverse ? 1 : 0;
+    r.w.out = out;
+    size_t lane = 0;
+    if (a->d) {
+        const int32_t sh = srtp_dispatch_route(a->d, tid, pkt, copy_len < len ? copy_len : len);
+        lane = sh < 0 ? 0 : (size_t)sh;
+    }
+    Lane &ln = *a->lanes[lane];
+    r.next = ln.sync_head.load();
+    while (!ln.sync_head.compare_exchange_weak(r.next, &r)) {
+    }
+    if (ln.sleeping.load()) {
+        std::lock_guard<std::mutex> lk(a->mu);
+        ln.cv_work.notify_all();
+    }
+    while (r.w.done.load(std::memory_order_acquire) == 0) futex_wait(&r.w.done, 0);
+    *status = r.w.status;
+    *out_len = r.w.len;
     return SRTP_OK;
 }
 
@@ -730,11 +841,11 @@ void srtp_aggregator_destroy(srtp_aggregator *a) {
         // accepted packet: a packet accepted is always delivered
         a->closing.store(true);
         seal_all_locked(a);
-        a->cv_idle.wait(lk, [&] {
-            if (pending_locked(a) == 0) return true;
+        for (;;) {
+            if (pending_locked(a) == 0 && a->sync_callers.load() == 0) break;
             seal_all_locked(a); // parked callback packets placed since, stragglers' slots
-            return false;
-        });
+            a->cv_idle.wait_for(lk, std::chrono::milliseconds(1));
+        }
         a->stop = true;
         a->cv_flush.notify_all();
         for (auto &ln : a->lanes) {

@@ -1194,12 +1194,21 @@ struct srtp_pipeline {
         uint8_t *d_seg = nullptr;   // device copies
         uint32_t *d_off = nullptr, *d_len = nullptr, *d_cap = nullptr, *d_flags = nullptr;
         int32_t *d_tids = nullptr, *d_status = nullptr;
+        // small bundles: the per-packet arrays packed into one block each way
+        // (off | cap | flags | tids | len in, len | status out), so a bundle
+        // of a few packets costs two copies in and two out instead of six and
+        // three -- each copy's fixed cost, not its bytes, is what a small
+        // bundle's round trip pays
+        uint32_t *h_pack = nullptr, *d_pack = nullptr;
+        uint32_t packed_n = 0;      // the bundle in flight used the packed layout (its n), else 0
         hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out = nullptr;
         bool busy = false;
         int rc = SRTP_OK;           // engine return code of the last submit
     };
     std::vector<Slot> slots;
 };
+
+constexpr uint32_t kPackMax = 8192; // bundles up to this many packets use the packed copies
 
 static void pipeline_free(srtp_pipeline *pl) {
     DeviceGuard guard(pl->e->opts.device);
@@ -1208,7 +1217,8 @@ static void pipeline_free(srtp_pipeline *pl) {
         void *hp[] = {sl.h.seg, sl.h.off, sl.h.len, sl.h.cap, sl.h.flags, sl.h.tids, sl.h.status};
         for (void *p : hp)
             if (p) (void)hipHostFree(p);
-        void *dp[] = {sl.d_seg, sl.d_off, sl.d_len, sl.d_cap, sl.d_flags, sl.d_tids, sl.d_status};
+        if (sl.h_pack) (void)hipHostFree(sl.h_pack);
+        void *dp[] = {sl.d_seg, sl.d_off, sl.d_len, sl.d_cap, sl.d_flags, sl.d_tids, sl.d_status, sl.d_pack};
         for (void *p : dp) dfree(p);
         hipEvent_t ev[] = {sl.ev_in, sl.ev_done, sl.ev_out};
         for (auto x : ev)
@@ -1248,6 +1258,8 @@ int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_by
              dalloc(&sl.d_len, n) == hipSuccess && dalloc(&sl.d_cap, n) == hipSuccess &&
              dalloc(&sl.d_flags, n) == hipSuccess && dalloc(&sl.d_tids, n) == hipSuccess &&
              dalloc(&sl.d_status, n) == hipSuccess &&
+             halloc(&sl.h_pack, 6 * std::min<size_t>(n, kPackMax)) == hipSuccess &&
+             dalloc(&sl.d_pack, 6 * std::min<size_t>(n, kPackMax)) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_out, hipEventDisableTiming) == hipSuccess;
@@ -1282,6 +1294,11 @@ static int pipeline_wait_locked(srtp_pipeline *pl, srtp_pipeline::Slot &sl) {
     if (!sl.busy) return SRTP_OK;
     sl.busy = false;
     if (hipEventSynchronize(sl.ev_out) != hipSuccess) return fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
+    if (const uint32_t n = sl.packed_n) { // lengths and statuses to the slot's own arrays
+        memcpy(sl.h.len, sl.h_pack + 4 * (size_t)n, n * 4ull);
+        memcpy(sl.h.status, sl.h_pack + 5 * (size_t)n, n * 4ull);
+        sl.packed_n = 0;
+    }
     return sl.rc;
 }
 
@@ -1308,23 +1325,46 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
     if (!use_tids && (tid < 0 || (size_t)tid >= e->transformers.size()))
         return fail(e, SRTP_EINVAL, "bad transformer id");
     hipStream_t si = pl->s_in, so = pl->s_out, s = e->stream;
+    const int32_t abort = abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0);
     HIPCHK(e, hipMemcpyAsync(sl.d_seg, sl.h.seg, seg_bytes, hipMemcpyHostToDevice, si));
-    HIPCHK(e, hipMemcpyAsync(sl.d_off, sl.h.off, n * 4ull, hipMemcpyHostToDevice, si));
-    HIPCHK(e, hipMemcpyAsync(sl.d_len, sl.h.len, n * 4ull, hipMemcpyHostToDevice, si));
-    HIPCHK(e, hipMemcpyAsync(sl.d_cap, sl.h.cap, n * 4ull, hipMemcpyHostToDevice, si));
-    if (use_flags) HIPCHK(e, hipMemcpyAsync(sl.d_flags, sl.h.flags, n * 4ull, hipMemcpyHostToDevice, si));
-    if (use_tids) HIPCHK(e, hipMemcpyAsync(sl.d_tids, sl.h.tids, n * 4ull, hipMemcpyHostToDevice, si));
-    HIPCHK(e, hipEventRecord(sl.ev_in, si));
-    HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
-    sl.rc = transform_locked(e, reverse, use_tids ? sl.d_tids : nullptr, tid, sl.d_seg, sl.d_off,
-                             sl.d_len, sl.d_cap, use_flags ? sl.d_flags : nullptr, sl.d_status, n, s,
-                             abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0));
-    if (sl.rc != SRTP_OK) return sl.rc;
-    HIPCHK(e, hipEventRecord(sl.ev_done, s));
-    HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
-    HIPCHK(e, hipMemcpyAsync(sl.h.seg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
-    HIPCHK(e, hipMemcpyAsync(sl.h.len, sl.d_len, n * 4ull, hipMemcpyDeviceToHost, so));
-    HIPCHK(e, hipMemcpyAsync(sl.h.status, sl.d_status, n * 4ull, hipMemcpyDeviceToHost, so));
+    if (n <= kPackMax) {
+        uint32_t *hp = sl.h_pack, *dp = sl.d_pack;
+        const size_t n4 = n * 4ull;
+        memcpy(hp, sl.h.off, n4);
+        memcpy(hp + n, sl.h.cap, n4);
+        if (use_flags) memcpy(hp + 2 * (size_t)n, sl.h.flags, n4);
+        if (use_tids) memcpy(hp + 3 * (size_t)n, sl.h.tids, n4);
+        memcpy(hp + 4 * (size_t)n, sl.h.len, n4);
+        HIPCHK(e, hipMemcpyAsync(dp, hp, 5 * n4, hipMemcpyHostToDevice, si));
+        HIPCHK(e, hipEventRecord(sl.ev_in, si));
+        HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+        sl.rc = transform_locked(e, reverse, use_tids ? reinterpret_cast<int32_t *>(dp + 3 * (size_t)n) : nullptr,
+                                 tid, sl.d_seg, dp, dp + 4 * (size_t)n, dp + n,
+                                 use_flags ? dp + 2 * (size_t)n : nullptr,
+                                 reinterpret_cast<int32_t *>(dp + 5 * (size_t)n), n, s, abort);
+        if (sl.rc != SRTP_OK) return sl.rc;
+        HIPCHK(e, hipEventRecord(sl.ev_done, s));
+        HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+        HIPCHK(e, hipMemcpyAsync(sl.h.seg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
+        HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, 2 * n4, hipMemcpyDeviceToHost, so));
+        sl.packed_n = n;
+    } else {
+        HIPCHK(e, hipMemcpyAsync(sl.d_off, sl.h.off, n * 4ull, hipMemcpyHostToDevice, si));
+        HIPCHK(e, hipMemcpyAsync(sl.d_len, sl.h.len, n * 4ull, hipMemcpyHostToDevice, si));
+        HIPCHK(e, hipMemcpyAsync(sl.d_cap, sl.h.cap, n * 4ull, hipMemcpyHostToDevice, si));
+        if (use_flags) HIPCHK(e, hipMemcpyAsync(sl.d_flags, sl.h.flags, n * 4ull, hipMemcpyHostToDevice, si));
+        if (use_tids) HIPCHK(e, hipMemcpyAsync(sl.d_tids, sl.h.tids, n * 4ull, hipMemcpyHostToDevice, si));
+        HIPCHK(e, hipEventRecord(sl.ev_in, si));
+        HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+        sl.rc = transform_locked(e, reverse, use_tids ? sl.d_tids : nullptr, tid, sl.d_seg, sl.d_off,
+                                 sl.d_len, sl.d_cap, use_flags ? sl.d_flags : nullptr, sl.d_status, n, s, abort);
+        if (sl.rc != SRTP_OK) return sl.rc;
+        HIPCHK(e, hipEventRecord(sl.ev_done, s));
+        HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+        HIPCHK(e, hipMemcpyAsync(sl.h.seg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
+        HIPCHK(e, hipMemcpyAsync(sl.h.len, sl.d_len, n * 4ull, hipMemcpyDeviceToHost, so));
+        HIPCHK(e, hipMemcpyAsync(sl.h.status, sl.d_status, n * 4ull, hipMemcpyDeviceToHost, so));
+    }
     HIPCHK(e, hipEventRecord(sl.ev_out, so));
     sl.busy = true;
     return SRTP_OK;

@@ -300,19 +300,20 @@ struct CtrPre {
 };
 
 __device__ __forceinline__ void ctr_precompute(const char *__restrict__ lds, const TeBase &tb,
-                                               const RoundKeys &rk, const uint32_t iv[4],
+                                               const uint32_t *rk, const uint32_t iv[4],
                                                CtrPre &cp) {
-    const uint32_t w0 = iv[0] ^ rk.k[0], w1 = iv[1] ^ rk.k[1], w2 = iv[2] ^ rk.k[2];
-    const uint32_t w3 = iv[3] ^ rk.k[3]; // bytes 14-15 of iv are zero (counter slot)
+    // rk: round keys 0..2 (12 words)
+    const uint32_t w0 = iv[0] ^ rk[0], w1 = iv[1] ^ rk[1], w2 = iv[2] ^ rk[2];
+    const uint32_t w3 = iv[3] ^ rk[3]; // bytes 14-15 of iv are zero (counter slot)
     cp.kb = w3 >> 24;
-    cp.p0 = xor3(TL(w0, 0, 0), TL(w1, 1, 1), TL(w2, 2, 2)) ^ rk.k[4];
-    const uint32_t u1 = xor3(TL(w1, 0, 0), TL(w2, 1, 1), TL(w3, 2, 2)) ^ TL(w0, 3, 3) ^ rk.k[5];
-    const uint32_t u2 = xor3(TL(w2, 0, 0), TL(w3, 1, 1), TL(w0, 2, 2)) ^ TL(w1, 3, 3) ^ rk.k[6];
-    const uint32_t u3 = xor3(TL(w3, 0, 0), TL(w0, 1, 1), TL(w1, 2, 2)) ^ TL(w2, 3, 3) ^ rk.k[7];
-    cp.r[0] = xor3(TL(u1, 1, 1), TL(u2, 2, 2), TL(u3, 3, 3)) ^ rk.k[8];
-    cp.r[1] = xor3(TL(u1, 0, 0), TL(u2, 1, 1), TL(u3, 2, 2)) ^ rk.k[9];
-    cp.r[2] = xor3(TL(u2, 0, 0), TL(u3, 1, 1), TL(u1, 3, 3)) ^ rk.k[10];
-    cp.r[3] = xor3(TL(u3, 0, 0), TL(u1, 2, 2), TL(u2, 3, 3)) ^ rk.k[11];
+    cp.p0 = xor3(TL(w0, 0, 0), TL(w1, 1, 1), TL(w2, 2, 2)) ^ rk[4];
+    const uint32_t u1 = xor3(TL(w1, 0, 0), TL(w2, 1, 1), TL(w3, 2, 2)) ^ TL(w0, 3, 3) ^ rk[5];
+    const uint32_t u2 = xor3(TL(w2, 0, 0), TL(w3, 1, 1), TL(w0, 2, 2)) ^ TL(w1, 3, 3) ^ rk[6];
+    const uint32_t u3 = xor3(TL(w3, 0, 0), TL(w0, 1, 1), TL(w1, 2, 2)) ^ TL(w2, 3, 3) ^ rk[7];
+    cp.r[0] = xor3(TL(u1, 1, 1), TL(u2, 2, 2), TL(u3, 3, 3)) ^ rk[8];
+    cp.r[1] = xor3(TL(u1, 0, 0), TL(u2, 1, 1), TL(u3, 2, 2)) ^ rk[9];
+    cp.r[2] = xor3(TL(u2, 0, 0), TL(u3, 1, 1), TL(u1, 3, 3)) ^ rk[10];
+    cp.r[3] = xor3(TL(u3, 0, 0), TL(u1, 2, 2), TL(u2, 3, 3)) ^ rk[11];
 }
 
 // State after round 2 (round key 2 included) of counter blocks ja and jb
@@ -414,6 +415,161 @@ __device__ __forceinline__ void ks_sha_half(const char *__restrict__ lds, const 
 #pragma unroll
     for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
 }
+
+// ------------------------------------------------ per-lane key schedule
+// A wave whose packets belong to several session-key sets (a bridge's many
+// DTLS sessions in one bundle) runs every lane at once on its own keys rather
+// than one pass per key set (for_each_keyset: k passes for k key sets).  The
+// lane holds round keys 0-2 of its key set (loaded once per packet) and
+// derives rounds 3..10 on the fly (FIPS-197 5.2), four S-box lookups from the
+// LDS T-table image per round key: S(x) is byte 1 of T0[x], so byte j of the
+// rotated word comes from the table whose rotation puts S there.  Per block
+// pair that is 32 lookups and ~90 VALU more than the SGPR path's 266 lookups;
+// a wave of k > 1 key sets costs ~1.15 passes instead of k.
+__device__ __forceinline__ void key_next(const char *__restrict__ lds, const TeBase &tb, uint32_t k[4],
+                                         uint32_t rcon) {
+    const uint32_t w3 = k[3];
+    // SubWord(RotWord(w3)) in little-endian column words: S[a1] | S[a2] << 8 |
+    // S[a3] << 16 | S[a0] << 24, with a_j = byte j of w3
+    const uint32_t t3 = TL(w3, 1, 3), t0 = TL(w3, 2, 0), t1 = TL(w3, 3, 1), t2 = TL(w3, 0, 2);
+    const uint32_t lo = __builtin_amdgcn_perm(t0, t3, 0x0c0c0500u); // S[a1], S[a2]
+    const uint32_t hi = __builtin_amdgcn_perm(t2, t1, 0x07020c0cu); // S[a3], S[a0]
+    k[0] = xor3(k[0], lo | hi, rcon);
+    k[1] ^= k[0];
+    k[2] ^= k[1];
+    k[3] ^= k[2];
+}
+
+constexpr uint32_t kRcon[11] = {0x00, 0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+
+// aes_encrypt2 with the lane's own key schedule from round key 0 (k0).
+__device__ __forceinline__ void aes_encrypt2_v(const char *__restrict__ lds, const TeBase &tb,
+                                               const uint32_t k0[4], uint32_t a[4], uint32_t b[4]) {
+    uint32_t k[4] = {k0[0], k0[1], k0[2], k0[3]};
+#pragma unroll
+    for (int j = 0; j < 4; j++) { a[j] ^= k[j]; b[j] ^= k[j]; }
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        key_next(lds, tb, k, kRcon[r]);
+        aes_round2_asm_v(a, b, tb.b, k);
+    }
+    key_next(lds, tb, k, kRcon[10]);
+    aes_last2_asm_v(a, b, tb.b, k);
+}
+
+// ks_sha_half<P> with the lane's own round keys: k2 = round key 2 (rounds 1-2
+// come from the counter precompute, made with the lane's keys 0-2).
+template <int P>
+__device__ __forceinline__ void ks_sha_half_v(const char *__restrict__ lds, const TeBase &tb,
+                                              const uint32_t k2[4], const CtrPre &cp, int j0,
+                                              uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
+    uint32_t x[4], y[4];
+    constexpr int t = 40 * P;
+    ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
+    sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
+    uint32_t k[4] = {k2[0], k2[1], k2[2], k2[3]};
+    key_next(lds, tb, k, kRcon[3]); aes_round2_sha_v<t + 8>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[4]); aes_round2_sha_v<t + 12>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[5]); aes_round2_sha_v<t + 16>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[6]); aes_round2_sha_v<t + 20>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[7]); aes_round2_sha_v<t + 24>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[8]); aes_round2_sha_v<t + 28>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[9]); aes_round2_sha_v<t + 32>(x, y, tb.b, k, v, w);
+    key_next(lds, tb, k, kRcon[10]); aes_last2_sha_v<t + 36>(x, y, tb.b, k, v, w);
+#pragma unroll
+    for (int q = 0; q < 4; q++) { K8[q] = x[q]; K8[4 + q] = y[q]; }
+}
+
+// The round keys a packet runs with.  LK = false: the wave-uniform key set's
+// 44 words in SGPRs; LK = true: the lane's own round keys 0-2 (the rest are
+// derived per block pair, above).
+template <bool LK> struct PktKeys;
+template <> struct PktKeys<false> {
+    RoundKeys rk;
+};
+template <> struct PktKeys<true> {
+    uint32_t r[12];
+};
+
+__device__ __forceinline__ void ctr_apply(Ctr &cs, int c, const uint32_t K[16], uint32_t d[16]);
+
+__device__ __forceinline__ void ctr_chunk_v(const char *__restrict__ lds, const TeBase &tb,
+                                            const uint32_t k0[4], Ctr &cs, int c, uint32_t d[16]) {
+    const int j0 = 4 * c - (cs.off >> 4);
+    uint32_t K[16];
+#pragma unroll 1
+    for (int pr = 0; pr < 2; pr++) {
+        uint32_t x[4], y[4];
+        ctr_input(cs.iv, j0 + 2 * pr, x);
+        ctr_input(cs.iv, j0 + 2 * pr + 1, y);
+        aes_encrypt2_v(lds, tb, k0, x, y);
+#pragma unroll
+        for (int k = 0; k < 8; k++) K[k] = K[k + 8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) { K[8 + k] = x[k]; K[12 + k] = y[k]; }
+    }
+    ctr_apply(cs, c, K, d);
+}
+
+// The key-set-agnostic forms the packet functions call (pk_load: after
+// load_round_keys_uniform below).
+__device__ __forceinline__ const uint32_t *pk_words(const PktKeys<false> &pk) { return pk.rk.k; }
+__device__ __forceinline__ const uint32_t *pk_words(const PktKeys<true> &pk) { return pk.r; }
+
+template <int P>
+__device__ __forceinline__ void pk_half(const char *__restrict__ lds, const TeBase &tb, const PktKeys<false> &pk,
+                                        const CtrPre &cp, int j0, uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
+    ks_sha_half<P>(lds, tb, pk.rk, cp, j0, K8, v, w);
+}
+template <int P>
+__device__ __forceinline__ void pk_half(const char *__restrict__ lds, const TeBase &tb, const PktKeys<true> &pk,
+                                        const CtrPre &cp, int j0, uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
+    ks_sha_half_v<P>(lds, tb, pk.r + 8, cp, j0, K8, v, w);
+}
+
+__device__ __forceinline__ void pk_chunk(const char *__restrict__ lds, const TeBase &tb, const PktKeys<false> &pk,
+                                         Ctr &cs, int c, uint32_t d[16]) {
+    ctr_chunk(lds, tb, pk.rk, cs, c, d);
+}
+__device__ __forceinline__ void pk_chunk(const char *__restrict__ lds, const TeBase &tb, const PktKeys<true> &pk,
+                                         Ctr &cs, int c, uint32_t d[16]) {
+    ctr_chunk_v(lds, tb, pk.r, cs, c, d);
+}
+
+__device__ __forceinline__ void pk_chunk_pre(const char *__restrict__ lds, const TeBase &tb,
+                                             const PktKeys<false> &pk, const CtrPre &cp, Ctr &cs, int c,
+                                             uint32_t d[16]) {
+    ctr_chunk_pre(lds, tb, pk.rk, cp, cs, c, d);
+}
+__device__ __forceinline__ void pk_chunk_pre(const char *__restrict__ lds, const TeBase &tb,
+                                             const PktKeys<true> &pk, const CtrPre &cp, Ctr &cs, int c,
+                                             uint32_t d[16]) {
+    const int j0 = 4 * c - (cs.off >> 4);
+    if (ctr_pre_exhausted(j0)) {
+        ctr_chunk_v(lds, tb, pk.r, cs, c, d);
+        return;
+    }
+    uint32_t K[16];
+#pragma unroll 1
+    for (int pr = 0; pr < 2; pr++) {
+        uint32_t x[4], y[4];
+        ctr_first2(lds, tb, cp, j0 + 2 * pr, j0 + 2 * pr + 1, x, y);
+        uint32_t k[4] = {pk.r[8], pk.r[9], pk.r[10], pk.r[11]};
+#pragma unroll
+        for (int r = 3; r < 10; r++) {
+            key_next(lds, tb, k, kRcon[r]);
+            aes_round2_asm_v(x, y, tb.b, k);
+        }
+        key_next(lds, tb, k, kRcon[10]);
+        aes_last2_asm_v(x, y, tb.b, k);
+#pragma unroll
+        for (int q = 0; q < 8; q++) K[q] = K[q + 8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) { K[8 + q] = x[q]; K[12 + q] = y[q]; }
+    }
+    ctr_apply(cs, c, K, d);
+}
+
 
 // XOR keystream K (blocks 4c - off/16 .. +3, see ctr_chunk) into the chunk
 // words d[] of chunk c, within [off, end); advances the carry.
@@ -1094,6 +1250,14 @@ __device__ __forceinline__ void for_each_keyset(bool todo, uint32_t ks_id, F &&b
     }
 }
 
+// True when the wave's lanes with `todo` set hold more than one key set.
+__device__ __forceinline__ bool wave_mixes_keysets(bool todo, uint32_t ks_id) {
+    const unsigned long long m = __ballot(todo);
+    if (m == 0ull) return false;
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)ks_id, __ffsll((long long)m) - 1);
+    return __ballot(todo && ks_id != first) != 0ull;
+}
+
 __device__ __forceinline__ uint32_t sgpr(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
 }
@@ -1111,6 +1275,24 @@ __device__ __forceinline__ void load_round_keys_uniform(const KeySet *__restrict
         rk.k[4 * i + 2] = sgpr(v.z); rk.k[4 * i + 3] = sgpr(v.w);
     }
 }
+
+template <bool LK>
+__device__ __forceinline__ void pk_load(const KeySet *__restrict__ ks, PktKeys<LK> &pk);
+template <>
+__device__ __forceinline__ void pk_load<false>(const KeySet *__restrict__ ks, PktKeys<false> &pk) {
+    load_round_keys_uniform(ks, pk.rk);
+}
+template <>
+__device__ __forceinline__ void pk_load<true>(const KeySet *__restrict__ ks, PktKeys<true> &pk) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(ks->rk);
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const uint4 v = q[i];
+        pk.r[4 * i] = v.x; pk.r[4 * i + 1] = v.y; pk.r[4 * i + 2] = v.z; pk.r[4 * i + 3] = v.w;
+    }
+}
+// A key-set field: wave-uniform (SGPR) or the lane's own.
+template <bool LK> __device__ __forceinline__ uint32_t kf(uint32_t x) { return LK ? x : sgpr(x); }
 
 // Re-check one SRTP tag under another ROC from the verify pass's midstate
 // (only the block(s) carrying the ROC are re-hashed).
@@ -2715,14 +2897,15 @@ __device__ __forceinline__ void store_chunk(uint8_t *pkt, int b, const Ctr &cs, 
 // Fused protect, one lane per packet: AES-CM in place (SRTPCipherCTR.process
 // :94-121) + HMAC-SHA1 over the ciphertext (authenticatePacketHMAC :269-278)
 // + trailer (RawPacket.append :203-220).  Packet bytes: one read, one write.
+template <bool LK>
 __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                             const char *__restrict__ lds, const TeBase &tb,
                                             uint32_t p, bool fused) {
     uint8_t *pkt = a.seg + a.off[p];
-    const bool do_enc = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
-    const bool do_mac = sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
-    const bool rtcp = sgpr(ks->kind) == SRTP_KIND_RTCP;
-    const int T = (int)sgpr(ks->tag_len);
+    const bool do_enc = kf<LK>(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
+    const bool do_mac = kf<LK>(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+    const bool rtcp = kf<LK>(ks->kind) == SRTP_KIND_RTCP;
+    const int T = (int)kf<LK>(ks->tag_len);
     const int L = (int)a.w_len[p] - (do_mac ? (T + (rtcp ? 4 : 0)) : 0);
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
     const uint32_t cw = a.w_cw[p];
@@ -2740,11 +2923,11 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     cs.end = L;
 #pragma unroll
     for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
-    RoundKeys rk;
-    load_round_keys_uniform(ks, rk);
+    PktKeys<LK> pk;
+    pk_load<LK>(ks, pk);
     uint32_t h[5];
 #pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
+    for (int k = 0; k < 5; k++) h[k] = kf<LK>(ks->ipad[k]);
     const int nb_data = (L + 63) >> 6;
     const int nb_inner = do_mac ? ((L + 12) >> 6) + 1 : 0;
     const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
@@ -2758,11 +2941,11 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     // stores; bytes outside [off, end) are written back unchanged.)
     const int B = L >> 6;
     CtrPre cp; // AES-CM rounds 1-2 of this packet's counter blocks
-    if (do_enc) ctr_precompute(lds, tb, rk, cs.iv, cp);
+    if (do_enc) ctr_precompute(lds, tb, pk_words(pk), cs.iv, cp);
     if (fused && B >= 2) {
         uint32_t c[16];
         load_chunk(pkt, 0, L, c);
-        ctr_chunk_pre(lds, tb, rk, cp, cs, 0, c);
+        pk_chunk_pre(lds, tb, pk, cp, cs, 0, c);
         store_chunk(pkt, 0, cs, c);
         const int hq = cs.off >> 4;
         const int nbw = SRTP_PRIO ? wave_max_i(B) : 0;
@@ -2774,14 +2957,14 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
             uint32_t K[16], d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
-            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+            pk_half<0>(lds, tb, pk, cp, 4 * b - hq, K, v, c);
 #if SRTP_COALESCE == 1
             const bool full = quad_full();
             load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
 #else
             load_chunk_full(pkt, b, d);
 #endif
-            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
+            pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
 #if SRTP_COALESCE == 1
@@ -2818,7 +3001,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
                 w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
             }
             if (do_enc && 64 * b + 64 > cs.off) {
-                ctr_chunk_pre(lds, tb, rk, cp, cs, b, w);
+                pk_chunk_pre(lds, tb, pk, cp, cs, b, w);
 #pragma unroll
                 for (int m = 0; m < 4; m++)
                     if (64 * b + 16 * m < L && 64 * b + 16 * m + 16 > cs.off)
@@ -2832,7 +3015,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
         if (b < nb_inner) {
             inner_words(w, b, L, suffix);
         } else {
-            outer_words(w, h, ks);
+            outer_words<!LK>(w, h, ks);
         }
         sha1_compress(h, w);
     }
@@ -2902,16 +3085,26 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     __syncthreads();
     flush_status_counts(a, s_cnt);
     if (i >= a.n) return;
-    const bool todo = fs == SRTP_STATUS_OK;
+    bool todo = fs == SRTP_STATUS_OK;
     const uint32_t ks_id = todo ? a.ctx[a.p_slot[p]].ks : 0u;
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
+    if (wave_mixes_keysets(todo, ks_id)) {
+        // several key sets in this wave: the fused AES-CM + HMAC-SHA1 packets
+        // run at once, each lane on its own key schedule; the rest (NULL
+        // cipher or MAC, k_ext's ciphers) per key set below
+        const KeySet *ks = a.keysets + ks_id;
+        const bool lane = todo && ks->ext == 0u && ks->enc_type == SRTP_AESCM_ENCRYPTION &&
+                          ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
+        if (lane) protect_one<true>(a, ks, lds, tb, p, true);
+        todo = todo && !lane;
+    }
     for_each_keyset(todo, ks_id, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
         if (sgpr(ks->ext)) return; // AES-F8 / AES-256-CM: k_ext
-        protect_one(a, ks, lds, tb, p,
-                    sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
-                        sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
+        protect_one<false>(a, ks, lds, tb, p,
+                           sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
+                               sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
     });
     STAMP(2);
 }
@@ -2947,18 +3140,19 @@ __device__ __forceinline__ uint32_t chain_head(const uint32_t *__restrict__ sk, 
 // ROC-carrying block and that block's ciphertext, so the walk can re-check a
 // tag under another ROC cheaply; k_unprotect_fix repairs the rare packets the
 // walk rejects or guesses differently.
+template <bool LK>
 __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                               const char *__restrict__ lds, const TeBase &tb,
                                               uint32_t p, const CtxState &st, bool fused) {
     uint8_t *pkt = a.seg + a.off[p];
     const int L = (int)a.len[p];
-    const int T = (int)sgpr(ks->tag_len);
-    const bool rtp = sgpr(ks->kind) == SRTP_KIND_RTP;
+    const int T = (int)kf<LK>(ks->tag_len);
+    const bool rtp = kf<LK>(ks->kind) == SRTP_KIND_RTP;
     // HMAC-SHA1 here; a Skein-MAC key set's tags are checked by k_skein
     // (its key sets are k_ext's: no speculation, so nothing is done here but g0)
-    const bool do_mac = sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
+    const bool do_mac = kf<LK>(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
     // speculative decryption: AES-128-CM only (k_ext deciphers the rest)
-    const bool aes = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext);
+    const bool aes = kf<LK>(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !kf<LK>(ks->ext);
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
     Ctr cs;
     cs.off = 0;
@@ -3006,11 +3200,11 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     cs.end = spec ? end : 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
-    RoundKeys rk;
-    load_round_keys_uniform(ks, rk);
+    PktKeys<LK> pk;
+    pk_load<LK>(ks, pk);
     uint32_t h[5];
 #pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = sgpr(ks->ipad[k]);
+    for (int k = 0; k < 5; k++) h[k] = kf<LK>(ks->ipad[k]);
     const int nb_full = end >> 6;
     const int nb_data = (end + 63) >> 6;
     const int nb_inner = ((end + 12) >> 6) + 1;
@@ -3023,14 +3217,14 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         // before), so chunk b's load has half a chunk step to land.
         const int hq = cs.off >> 4;
         CtrPre cp;
-        ctr_precompute(lds, tb, rk, cs.iv, cp);
+        ctr_precompute(lds, tb, pk_words(pk), cs.iv, cp);
         uint32_t c[16];
         load_chunk_full(pkt, 0, c);
         {   // chunk 0 holds the header: generic keystream, masked below off
             uint32_t d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) d[k] = c[k];
-            ctr_chunk_pre(lds, tb, rk, cp, cs, 0, d);
+            pk_chunk_pre(lds, tb, pk, cp, cs, 0, d);
             store_chunk(pkt, 0, cs, d); // cs.end = 0 without speculation: no store
         }
         const int nbw = SRTP_PRIO ? wave_max_i(nb_full) : 0;
@@ -3041,14 +3235,14 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             uint32_t K[16], d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
-            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+            pk_half<0>(lds, tb, pk, cp, 4 * b - hq, K, v, c);
 #if SRTP_COALESCE == 1
             const bool full = quad_full();
             load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
 #else
             load_chunk_full(pkt, b, d);
 #endif
-            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
+            pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
 #if SRTP_COALESCE == 1
@@ -3080,9 +3274,9 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             uint32_t K[16], d[16];
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
-            ks_sha_half<0>(lds, tb, rk, cp, 4 * b - hq, K, v, c);
+            pk_half<0>(lds, tb, pk, cp, 4 * b - hq, K, v, c);
             load_chunk(pkt, b, end, d);
-            ks_sha_half<1>(lds, tb, rk, cp, 4 * b - hq, K + 8, v, c);
+            pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
             if (rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
@@ -3109,7 +3303,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 #pragma unroll
                 for (int k = 0; k < 16; k++) w[k] = 0u;
                 if (b < nb_inner) inner_words(w, b, end, suffix);
-                else outer_words(w, h, ks);
+                else outer_words<!LK>(w, h, ks);
                 sha1_compress(h, w);
             }
             a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
@@ -3147,7 +3341,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 }
             }
             if (b < nb_inner) inner_words(d, b, end, suffix);
-            else outer_words(d, h, ks);
+            else outer_words<!LK>(d, h, ks);
             sha1_compress(h, d);
         }
         a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
@@ -3158,8 +3352,8 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         // live across the MAC loop instead (44 VGPRs spilled to scratch)
         const KeySet *ks2 = ks;
         asm volatile("" : "+v"(ks2));
-        RoundKeys rk2;
-        load_round_keys_uniform(ks2, rk2);
+        PktKeys<LK> pk2;
+        pk_load<LK>(ks2, pk2);
         for (int c = b_tail; c < nb_data; c++) {
             if (64 * c + 64 <= cs.off) continue;
             uint32_t d[16];
@@ -3170,7 +3364,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 if (64 * c + 16 * m < end) v = qp[m];
                 d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
             }
-            ctr_chunk(lds, tb, rk2, cs, c, d);
+            pk_chunk(lds, tb, pk2, cs, c, d);
 #pragma unroll
             for (int m = 0; m < 4; m++)
                 if (64 * c + 16 * m < end && 64 * c + 16 * m + 16 > cs.off)
@@ -3225,11 +3419,19 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     }
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s_te);
-    for_each_keyset(todo, st.ks, [&](uint32_t ks_u) {
+    bool rest = todo;
+    if (wave_mixes_keysets(todo, st.ks)) { // see k_protect
+        const KeySet *ks = a.keysets + st.ks;
+        const bool lane = todo && ks->ext == 0u && ks->enc_type == SRTP_AESCM_ENCRYPTION &&
+                          ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
+        if (lane) unprotect_one<true>(a, ks, lds, tb, p, st, true);
+        rest = todo && !lane;
+    }
+    for_each_keyset(rest, st.ks, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
-        unprotect_one(a, ks, lds, tb, p, st,
-                      sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
-                          sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
+        unprotect_one<false>(a, ks, lds, tb, p, st,
+                             sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
+                                 sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
     });
     STAMP(2);
 }

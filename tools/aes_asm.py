@@ -84,8 +84,10 @@ SEL4 = ["0x0c020400u", "0x0c020500u", "0x0c020600u", "0x0c020700u"]
 SEL2 = ["0x0c0c0400u", "0x0c0c0500u", "0x0c0c0600u", "0x0c0c0700u"]
 
 
-def emit(name, blocks, last, tables=4):
-    """A __device__ function running one (middle or last) round on the blocks."""
+def emit(name, blocks, last, tables=4, kv=False):
+    """A __device__ function running one (middle or last) round on the blocks.
+    kv: the round key words are per-lane values (VGPRs: a wave mixing key
+    sets) instead of wave-uniform SGPRs."""
     body = round_body(blocks, last, tables)
     nb = len(blocks)
     args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
@@ -110,7 +112,7 @@ def emit(name, blocks, last, tables=4):
             ins += ['[s6] "s"(0x06010c0cu)']
     if tables == 2 and not last:
         ins += [f'[r{i}] "s"(r16[{i}])' for i in range(4)]
-    ins += [f'[k{i}] "s"(rkr[{i}])' for i in range(4)]
+    ins += [f'[k{i}] "{"v" if kv else "s"}"(rkr[{i}])' for i in range(4)]
     s.append("        : " + ",\n          ".join(outs))
     s.append("        : " + ",\n          ".join(ins))
     s.append('        : "memory");')
@@ -167,9 +169,10 @@ def merge_sha(aes, sha):
     return out
 
 
-def emit_sha(name, blocks, last, t0, tables=4):
+def emit_sha(name, blocks, last, t0, tables=4, kv=False):
     """One AES round on the block pair with SHA-1 rounds t0..t0+3 interleaved;
-    v[5]/w[16] are the hash's working variables and schedule."""
+    v[5]/w[16] are the hash's working variables and schedule.  kv: per-lane
+    round key words (see emit)."""
     body = merge_sha(round_body(blocks, last, tables), sha_rounds(t0))
     nb = len(blocks)
     args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
@@ -189,7 +192,7 @@ def emit_sha(name, blocks, last, t0, tables=4):
     ins += [f'[s{i}] "s"({sels[i]})' for i in range(4)]
     if last:
         ins += ['[s4] "s"(0x0c0c0601u)', '[s5] "s"(0x04000c0cu)']
-    ins += [f'[k{i}] "s"(rkr[{i}])' for i in range(4)]
+    ins += [f'[k{i}] "{"v" if kv else "s"}"(rkr[{i}])' for i in range(4)]
     ins += [f'[sk] "s"({SHA_K[t0 // 20]:#010x}u)']
     s.append("        : " + ",\n          ".join(outs))
     s.append("        : " + ",\n          ".join(ins))

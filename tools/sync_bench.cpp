@@ -15,7 +15,7 @@
 // own SSRCs.  Prints one JSON line per (path, shards, threads): calls/s and
 // the per-call latency percentiles.
 //
-//   sync_bench [seconds-per-point]
+//   sync_bench [seconds-per-point] [path shards threads]   (one point: e.g. "one 0 1")
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -62,10 +62,17 @@ int main(int argc, char **argv) {
     srtp_policy pol = {SRTP_AESCM_ENCRYPTION, 16, SRTP_HMACSHA1_AUTHENTICATION, 20, 10, 14};
     const int shard_counts[] = {0, 8};
     const int thread_counts[] = {1, 8, 64};
+    const bool one_point = argc > 4;
+    const int p_only = one_point ? (strcmp(argv[2], "one") == 0 ? 0 : 1) : -1;
+    const int g_only = one_point ? atoi(argv[3]) : -1, t_only = one_point ? atoi(argv[4]) : -1;
     for (int path = 0; path < 2; path++) {
         for (int G : shard_counts) {
             for (int T : thread_counts) {
-                if (path == 1 && T == 64 && G == 8) continue; // 64 pinned batches x 8 shards: skip
+                if (one_point) {
+                    if (path != p_only || G != g_only || T != t_only) continue;
+                } else if (path == 1 && T == 64 && G == 8) {
+                    continue; // 64 pinned batches x 8 shards: skip
+                }
                 srtp_engine_opts o;
                 srtp_engine_opts_default(&o);
                 o.max_contexts = 1u << 16;
