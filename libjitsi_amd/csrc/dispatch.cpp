@@ -614,18 +614,49 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     if (!tids && (tid < 0 || tid >= nt)) return dfail(d, SRTP_EINVAL, "bad transformer id");
     const size_t ns = d->engines.size();
     std::vector<int32_t> shard(n), mt(n);
-    const int32_t plan = srtp_dispatch_plan((int32_t)ns, d->abort_on_error, reverse, d->kinds.data(), nt,
-                                            d->tag_mask, tids, tid, seg, seg_bytes, off, len, cap, flags,
-                                            n, shard.data(), mt.data());
-    if (plan < 0) return dfail(d, plan, "packet region outside the segment");
+    // The plan (srtp_dispatch_plan: region checks, each packet's shard and
+    // may-throw mark) and the per-shard index lists, split over the copy
+    // helpers: each part plans its range and counts its packets per shard, and
+    // then fills its stretch of each shard's list (bundle order kept).
+    const int parts = (int)std::max<size_t>(1, std::min<size_t>((size_t)d->pool->size() + 1, (n + 16383) / 16384));
+    std::vector<int32_t> plan_p((size_t)parts, 1);
+    std::vector<uint32_t> cnt((size_t)parts * ns, 0u);
+    d->pool->run(parts, [&](int q) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * q / parts), hi = (uint32_t)((uint64_t)n * (q + 1) / parts);
+        plan_p[(size_t)q] = srtp_dispatch_plan((int32_t)ns, d->abort_on_error, reverse, d->kinds.data(), nt,
+                                               d->tag_mask, tids ? tids + lo : nullptr, tid, seg, seg_bytes,
+                                               off + lo, len + lo, cap + lo, flags ? flags + lo : nullptr,
+                                               hi - lo, shard.data() + lo, mt.data() + lo);
+        uint32_t *c = cnt.data() + (size_t)q * ns;
+        for (uint32_t i = lo; i < hi; i++)
+            if (shard[i] >= 0) c[shard[i]]++;
+    });
+    int32_t plan = 1;
+    for (int32_t x : plan_p) {
+        if (x < 0) return dfail(d, x, "packet region outside the segment");
+        plan = std::max(plan, x);
+    }
     d->b_tids = tids; d->b_tid = tid; d->b_seg = seg; d->b_off = off; d->b_len = len;
     d->b_cap = cap; d->b_flags = flags; d->b_status = status;
     auto tid_of = [&](uint32_t i) { return tids ? tids[i] : tid; };
     std::vector<std::vector<uint32_t>> per_shard(ns);
-    for (uint32_t i = 0; i < n; i++) {
-        if (shard[i] < 0) status[i] = SRTP_STATUS_SKIPPED; // SKIP flag or no such transformer
-        else per_shard[(size_t)shard[i]].push_back(i);
+    std::vector<uint32_t> at((size_t)parts * ns);
+    for (size_t s = 0; s < ns; s++) {
+        uint32_t acc = 0;
+        for (int q = 0; q < parts; q++) {
+            at[(size_t)q * ns + s] = acc;
+            acc += cnt[(size_t)q * ns + s];
+        }
+        per_shard[s].resize(acc);
     }
+    d->pool->run(parts, [&](int q) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * q / parts), hi = (uint32_t)((uint64_t)n * (q + 1) / parts);
+        uint32_t *a = at.data() + (size_t)q * ns;
+        for (uint32_t i = lo; i < hi; i++) {
+            if (shard[i] < 0) status[i] = SRTP_STATUS_SKIPPED; // SKIP flag or no such transformer
+            else per_shard[(size_t)shard[i]][a[shard[i]]++] = i;
+        }
+    });
     d->t_plan += now_ns() - t0;
     if (plan == 1) { // nothing can throw: one run
         const int rc = run_phase(d, per_shard, reverse);

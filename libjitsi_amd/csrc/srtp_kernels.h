@@ -73,8 +73,9 @@ struct BundleArgs {
     int32_t *e_min_next;   // the next bundle's e_min, [n_transformers] set to 0x7f7f7f7f by k_parse
     BundleCtl *ctl;
     // radix sort of the walk records (srtp_kernels.hip "radix sort")
-    uint32_t *sort_counts; // [tiles][256] first-digit counts per sort tile, by k_parse
-    int32_t sort_passes;   // 8-bit digits to sort (key width / 8, rounded up)
+    uint32_t *sort_counts; // [tiles][bins] first-digit counts per sort tile, by k_parse
+    int32_t sort_passes;   // digits to sort: key width / 8 rounded up, or 2 wide digits
+    int32_t sort_bits;     // bits of the first digit (8, or 9-11 for a two-pass wide sort)
     uint32_t *sort_zero;   // the last pass's digit counts, re-zeroed by k_walk
     uint32_t sort_zero_words;
 };
@@ -84,8 +85,13 @@ struct SortScratch {
     uint32_t *keys_tmp;
     WalkRec *vals_tmp;
     uint32_t *counts[kSortMaxPass]; // [tiles][256] digit counts per tile and pass (kept zero between uses)
+    // the two-pass wide sort (9-11-bit digits, context tables of 2^16-2^21 slots)
+    uint32_t *wcounts[2];           // [tiles][2^bits] digit counts per pass (pass 0 kept zero between uses)
+    uint32_t *wprefix;              // [tiles][2^bits] per digit, records in earlier tiles
+    uint32_t *wtotal;               // [2^bits] records per digit
     uint32_t max_tiles;
 };
+constexpr int kSortWideMaxBits = 11;
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s);
 size_t sort_temp_bytes(uint32_t n_max);

@@ -916,9 +916,13 @@ constexpr int kSortThreads = 512, kSortItems = SRTP_SORT_ITEMS, kSortTile = kSor
 static_assert(kSortTile % kParseBlock == 0 && kParseBlock >= 256, "k_parse tiles");
 uint32_t sort_tile_records() { return (uint32_t)kSortTile; }
 
+// HB: the first digit's histogram bins (256, or 2^kSortWideMaxBits for the
+// wide sort, which uses 2^a.sort_bits of them).
+template <int HB>
 __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
-    __shared__ uint32_t s_hist[256], s_cls[32];
-    if (threadIdx.x < 256) s_hist[threadIdx.x] = 0u;
+    __shared__ uint32_t s_hist[HB], s_cls[32];
+    const uint32_t bins = HB == 256 ? 256u : 1u << a.sort_bits;
+    for (uint32_t d = threadIdx.x; d < bins; d += kParseBlock) s_hist[d] = 0u;
     if (threadIdx.x < 32) s_cls[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -938,12 +942,12 @@ __global__ __launch_bounds__(kParseBlock) void k_parse(BundleArgs a) {
         const unsigned long long same = __ballot(cls == lc);
         if (cls != lc) atomicAdd(&s_cls[cls], 1u);
         else if ((int)(threadIdx.x & 63u) == leader) atomicAdd(&s_cls[cls], (uint32_t)__popcll(same));
-        atomicAdd(&s_hist[parse_one(a, p) & 255u], 1u);
+        atomicAdd(&s_hist[parse_one(a, p) & (bins - 1u)], 1u);
     }
     __syncthreads();
     const uint32_t tile = (blockIdx.x * blockDim.x) / (uint32_t)kSortTile; // a multiple of kParseBlock
-    if (threadIdx.x < 256 && s_hist[threadIdx.x])
-        atomicAdd(&a.sort_counts[tile * 256 + threadIdx.x], s_hist[threadIdx.x]);
+    for (uint32_t d = threadIdx.x; d < bins; d += kParseBlock)
+        if (s_hist[d]) atomicAdd(&a.sort_counts[tile * bins + d], s_hist[d]);
     if (threadIdx.x < 32) { // per sort tile: at most kSortTile / kParseBlock parse blocks share a word
         const uint32_t c = s_cls[threadIdx.x];
         if (c) atomicAdd(&a.cls_tile[tile * kClsWords + threadIdx.x], c);
@@ -982,8 +986,9 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t sort_temp_bytes(uint32_t n_max) {
     const size_t tiles = (n_max + kSortTile - 1) / kSortTile;
+    const size_t wide = align256(tiles << kSortWideMaxBits << 2);
     return align256((size_t)n_max * 4) + align256((size_t)n_max * sizeof(WalkRec)) +
-           kSortMaxPass * align256(tiles * 256 * 4);
+           kSortMaxPass * align256(tiles * 256 * 4) + 3 * wide + align256((size_t)4 << kSortWideMaxBits);
 }
 
 SortScratch sort_scratch(void *temp, uint32_t n_max) {
@@ -994,6 +999,11 @@ SortScratch sort_scratch(void *temp, uint32_t n_max) {
     ss.keys_tmp = reinterpret_cast<uint32_t *>(p); p += align256((size_t)n_max * 4);
     ss.vals_tmp = reinterpret_cast<WalkRec *>(p); p += align256((size_t)n_max * sizeof(WalkRec));
     for (int q = 0; q < kSortMaxPass; q++) { ss.counts[q] = reinterpret_cast<uint32_t *>(p); p += cb; }
+    const size_t wide = align256((size_t)ss.max_tiles << kSortWideMaxBits << 2);
+    ss.wcounts[0] = reinterpret_cast<uint32_t *>(p); p += wide;
+    ss.wcounts[1] = reinterpret_cast<uint32_t *>(p); p += wide;
+    ss.wprefix = reinterpret_cast<uint32_t *>(p); p += wide;
+    ss.wtotal = reinterpret_cast<uint32_t *>(p);
     return ss;
 }
 
@@ -1199,7 +1209,235 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_count(const uint32_t *key
     if (t < 256) counts[blockIdx.x * 256u + t] = s_h[t];
 }
 
+// ------------------------------------------------- the two-pass wide sort
+// Keys of 17-22 bits (context tables of 2^16-2^21 slots: 40k-1.3M streams)
+// in two passes of 9-11-bit digits instead of three of 8.  A digit's scatter
+// base can no longer come from each tile re-reading the whole count table
+// (2^11 digits x every tile), so a small kernel turns the counts into per-tile
+// prefixes and digit totals once per pass (k_sort_prefix); the scatter scans
+// the totals itself.
+
+// counts [tiles][B] -> prefix[t][d] = records with digit d in tiles < t, and
+// total[d]; counts are zeroed behind (pass 0's table is k_parse's, which
+// accumulates with atomics).  Grid B / 64, 256 threads: 64 digits x 4 groups
+// of tiles.
+__global__ __launch_bounds__(256) void k_sort_prefix(uint32_t *counts, uint32_t tiles, uint32_t B,
+                                                     uint32_t *prefix, uint32_t *total) {
+    __shared__ uint32_t s_sum[4][64];
+    const uint32_t dl = threadIdx.x & 63u, g = threadIdx.x >> 6, d = blockIdx.x * 64u + dl;
+    const uint32_t t0 = tiles * g / 4u, t1 = tiles * (g + 1u) / 4u;
+    uint32_t sum = 0u;
+    for (uint32_t u = t0; u < t1; u++) sum += counts[u * B + d];
+    s_sum[g][dl] = sum;
+    __syncthreads();
+    uint32_t run = 0u;
+    for (uint32_t k = 0; k < g; k++) run += s_sum[k][dl];
+    if (g == 3u) total[d] = run + sum;
+    for (uint32_t u = t0; u < t1; u++) {
+        const uint32_t c = counts[u * B + d];
+        prefix[u * B + d] = run;
+        counts[u * B + d] = 0u;
+        run += c;
+    }
+}
+
+// k_sort_count with B (<= 2^kSortWideMaxBits) bins: every bin stored.
+__global__ __launch_bounds__(kSortThreads) void k_sort_count_wide(const uint32_t *keys, uint32_t n, uint32_t shift,
+                                                                  uint32_t B, uint32_t *counts) {
+    __shared__ uint32_t s_h[1 << kSortWideMaxBits];
+    const uint32_t t = threadIdx.x, base = blockIdx.x * kSortTile;
+    for (uint32_t d = t; d < B; d += kSortThreads) s_h[d] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < n) atomicAdd(&s_h[(keys[i] >> shift) & (B - 1u)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = t; d < B; d += kSortThreads) counts[blockIdx.x * B + d] = s_h[d];
+}
+
+struct SortPassWide {
+    const uint32_t *sk;
+    const WalkRec *sv;
+    uint32_t *dk;
+    WalkRec *dv;
+    uint32_t n, shift, bits, tiles;
+    const uint32_t *prefix, *total;
+    uint32_t *spos;
+    uint32_t walk_max;
+    uint32_t *lord;
+    const uint32_t *len;
+    BundleCtl *ctl;
+    const uint32_t *cls_tile;
+};
+
+// One wide scatter pass: k_sort_scatter's stable tile ranking with B = 2^bits
+// digits (bits ballots per item), bases from k_sort_prefix.
+__global__ __launch_bounds__(kSortThreads) void k_sort_scatter_wide(SortPassWide sp) {
+    constexpr int HB = 1 << kSortWideMaxBits, W = kSortThreads / 64;
+    __shared__ uint32_t s_base[HB], s_run[HB], s_wcnt[W][HB];
+    __shared__ uint32_t s_part[W];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t tile = blockIdx.x, base = tile * kSortTile;
+    const uint32_t B = 1u << sp.bits, per = B / kSortThreads; // 1, 2 or 4 digits per thread
+    {
+        // digit offsets: exclusive scan of the totals (thread t owns digits
+        // [t * per, t * per + per)), plus this tile's prefix
+        uint32_t loc[4], sum = 0u;
+        for (uint32_t k = 0; k < per; k++) {
+            loc[k] = sp.total[t * per + k];
+            sum += loc[k];
+        }
+        uint32_t x = sum; // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_part[w] = x;
+        for (uint32_t d = t; d < B; d += kSortThreads) {
+            s_run[d] = 0u;
+            for (int k = 0; k < W; k++) s_wcnt[k][d] = 0u;
+        }
+        __syncthreads();
+        uint32_t off = x - sum;
+        for (int k = 0; k < w; k++) off += s_part[k];
+        for (uint32_t k = 0; k < per; k++) {
+            const uint32_t d = t * per + k;
+            s_base[d] = off + sp.prefix[tile * B + d];
+            off += loc[k];
+        }
+    }
+    uint32_t key[kSortItems], loc[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < sp.n) key[r] = sp.sk[i];
+    }
+    __syncthreads();
+    // stable local ranks: items in order r-major, t-minor (= index order)
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const bool valid = base + r * kSortThreads + t < sp.n;
+        const uint32_t d = valid ? (key[r] >> sp.shift) & (B - 1u) : 0u;
+        unsigned long long m = __ballot(valid);
+        for (uint32_t bit = 0; bit < sp.bits; bit++) {
+            const unsigned long long b = __ballot((d >> bit) & 1u);
+            m &= ((d >> bit) & 1u) ? b : ~b;
+        }
+        const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        const bool leader = valid && below == 0u;
+        if (leader) s_wcnt[w][d] = cnt;
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = s_run[d];
+            for (int k = 0; k < w; k++) pre += s_wcnt[k][d];
+            loc[r] = pre + below;
+        }
+        __syncthreads();
+        // each wave's leader moves its digit's count into the running totals
+        // and clears its own entry (the next item's ranks read both after the
+        // next barrier)
+        if (leader) {
+            atomicAdd(&s_run[d], cnt);
+            s_wcnt[w][d] = 0u;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < sp.n) {
+            const uint32_t pos = s_base[(key[r] >> sp.shift) & (B - 1u)] + loc[r];
+            sp.dk[pos] = key[r];
+            const WalkRec rec = sp.sv[i];
+            sp.dv[pos] = rec;
+            if (sp.spos && key[r] <= sp.walk_max) sp.spos[rec.p & kRecIdxMask] = pos;
+        }
+    }
+    if (SRTP_LEN_ORDER && sp.lord) { // as k_sort_scatter (first pass only)
+        __syncthreads();
+        uint32_t *s_cb = s_base, *s_cc = s_run, *s_co = s_run + 32, *s_tot = s_run + 64;
+        if (t < 64) {
+            uint32_t m = 0u;
+            for (uint32_t u = (uint32_t)t; u < sp.tiles; u += 64u) m |= sp.cls_tile[u * kClsWords + 32];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+            if (t == 0) {
+                s_run[96] = m;
+                if (tile == 0u) sp.ctl->len_classes = m;
+            }
+        }
+        __syncthreads();
+        if (__popc(s_run[96] & ~1u) <= 1) return;
+        if (t < 32) {
+            uint32_t tot = 0u;
+            for (uint32_t u = 0u; u < sp.tiles; u++) tot += sp.cls_tile[u * kClsWords + t];
+            s_tot[t] = tot;
+            s_cc[t] = 0u;
+        }
+        __syncthreads();
+        if (t == 0) {
+            uint32_t acc = 0u;
+            for (int c = 31; c >= 0; c--) {
+                s_cb[c] = acc;
+                acc += s_tot[c];
+            }
+        }
+        __syncthreads();
+        uint32_t cls[kSortItems], rk[kSortItems];
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            const uint32_t i = base + r * kSortThreads + t;
+            if (i < sp.n) {
+                cls[r] = len_class(sp.len[i]);
+                rk[r] = atomicAdd(&s_cc[cls[r]], 1u);
+            }
+        }
+        __syncthreads();
+        if (t < 32 && s_cc[t]) s_co[t] = atomicAdd(&sp.ctl->cls_cursor[t], s_cc[t]);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            const uint32_t i = base + r * kSortThreads + t;
+            if (i < sp.n) sp.lord[s_cb[cls[r]] + s_co[cls[r]] + rk[r]] = i;
+        }
+    }
+}
+
+hipError_t launch_sort_wide(const BundleArgs &a, const SortScratch &ss, hipStream_t s) {
+    const uint32_t tiles = (a.n + kSortTile - 1) / kSortTile;
+    const uint32_t bits = (uint32_t)a.sort_bits, B = 1u << bits;
+    for (int q = 0; q < 2; q++) {
+        if (q == 1)
+            hipLaunchKernelGGL(k_sort_count_wide, dim3(tiles), dim3(kSortThreads), 0, s, (const uint32_t *)ss.keys_tmp,
+                               a.n, bits, B, ss.wcounts[1]);
+        hipLaunchKernelGGL(k_sort_prefix, dim3(B / 64u), dim3(256), 0, s, q == 0 ? a.sort_counts : ss.wcounts[1],
+                           tiles, B, ss.wprefix, ss.wtotal);
+        SortPassWide sp;
+        sp.sk = q == 0 ? a.sk_in : ss.keys_tmp;
+        sp.sv = q == 0 ? a.sv_in : ss.vals_tmp;
+        sp.dk = q == 0 ? ss.keys_tmp : a.sk_out;
+        sp.dv = q == 0 ? ss.vals_tmp : a.sv_out;
+        sp.n = a.n;
+        sp.shift = bits * (uint32_t)q;
+        sp.bits = bits;
+        sp.tiles = tiles;
+        sp.prefix = ss.wprefix;
+        sp.total = ss.wtotal;
+        sp.spos = q == 1 && a.reverse ? a.spos : nullptr;
+        sp.walk_max = a.ctx_mask;
+        sp.lord = q == 0 ? a.lord : nullptr;
+        sp.len = a.len;
+        sp.ctl = a.ctl;
+        sp.cls_tile = a.cls_tile;
+        hipLaunchKernelGGL(k_sort_scatter_wide, dim3(tiles), dim3(kSortThreads), 0, s, sp);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s) {
+    if (a.sort_bits > 8) return launch_sort_wide(a, ss, s);
     const uint32_t tiles = (a.n + kSortTile - 1) / kSortTile;
     const int P = a.sort_passes;
     for (int q = 0; q < P; q++) {
@@ -4197,7 +4435,11 @@ __global__ void k_rehash_insert(uint64_t *keys, CtxState *ctx, uint32_t mask,
 static inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_parse, dim3((a.n + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, s, a);
+    if (a.sort_bits > 8)
+        hipLaunchKernelGGL(k_parse<1 << kSortWideMaxBits>, dim3((a.n + kParseBlock - 1) / kParseBlock),
+                           dim3(kParseBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_parse<256>, dim3((a.n + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {

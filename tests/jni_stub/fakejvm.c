@@ -1,0 +1,179 @@
+/*
+ * fakejvm.c -- TEST INFRASTRUCTURE: the JNI calls of tests/jni_stub/jni.h over
+ * a toy object model, so that the real JNI shim (src/native/srtp_mi355x/
+ * SrtpMi355x.c, compiled unmodified against the stub header into
+ * tests/jni_stub/libfakejni.so) can be driven from Python through ctypes.
+ *
+ * Objects: byte[], int[], Object[] and org.jitsi.impl.neomedia.RawPacket
+ * (fields buffer, offset, length, flags -- RawPacket.java:53-73).  Arrays are
+ * copied in and out by Get/Set*ArrayRegion exactly as a JVM does; an
+ * out-of-range region is recorded as a pending exception (the checks a JVM's
+ * ArrayIndexOutOfBoundsException would make), which the tests assert is never
+ * raised.  Nothing is garbage-collected: objects live until fj_reset().
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "jni.h"
+
+enum { K_BYTES = 1, K_INTS, K_OBJS, K_PACKET, K_CLASS };
+
+struct fj_obj {
+    int kind;
+    jsize len;        /* arrays */
+    void *data;       /* arrays */
+    jobject buffer;   /* RawPacket */
+    jint offset, length, flags;
+    struct fj_obj *next_alloc;
+};
+
+struct fj_field {
+    int id; /* 0 buffer, 1 offset, 2 length, 3 flags */
+};
+
+static struct fj_field g_fields[4] = {{0}, {1}, {2}, {3}};
+static struct fj_obj g_rawpacket_class = {.kind = K_CLASS};
+static struct fj_obj *g_allocs;
+static int g_exceptions, g_frames;
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER; /* several "JVM threads" at once */
+
+static struct fj_obj *alloc_obj(int kind) {
+    struct fj_obj *o = calloc(1, sizeof *o);
+    o->kind = kind;
+    pthread_mutex_lock(&g_mu);
+    o->next_alloc = g_allocs;
+    g_allocs = o;
+    pthread_mutex_unlock(&g_mu);
+    return o;
+}
+
+static struct fj_obj *new_array(int kind, jsize len, size_t elem) {
+    struct fj_obj *o = alloc_obj(kind);
+    o->len = len;
+    o->data = calloc(len ? (size_t)len : 1, elem);
+    return o;
+}
+
+static int in_range(jarray a, jsize start, jsize len) {
+    if (!a || start < 0 || len < 0 || start > a->len || len > a->len - start) {
+        __atomic_add_fetch(&g_exceptions, 1, __ATOMIC_RELAXED);
+        return 0;
+    }
+    return 1;
+}
+
+static jsize GetArrayLength(JNIEnv *env, jarray a) { return a ? a->len : 0; }
+static void GetIntArrayRegion(JNIEnv *env, jintArray a, jsize s, jsize n, jint *buf) {
+    if (in_range(a, s, n)) memcpy(buf, (jint *)a->data + s, (size_t)n * sizeof(jint));
+}
+static void GetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize s, jsize n, jbyte *buf) {
+    if (in_range(a, s, n)) memcpy(buf, (jbyte *)a->data + s, (size_t)n);
+}
+static void SetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize s, jsize n, const jbyte *buf) {
+    if (in_range(a, s, n)) memcpy((jbyte *)a->data + s, buf, (size_t)n);
+}
+static jclass FindClass(JNIEnv *env, const char *name) {
+    return strcmp(name, "org/jitsi/impl/neomedia/RawPacket") == 0 ? &g_rawpacket_class : NULL;
+}
+static jfieldID GetFieldID(JNIEnv *env, jclass c, const char *name, const char *sig) {
+    if (c != &g_rawpacket_class) return NULL;
+    if (!strcmp(name, "buffer") && !strcmp(sig, "[B")) return &g_fields[0];
+    if (!strcmp(name, "offset") && !strcmp(sig, "I")) return &g_fields[1];
+    if (!strcmp(name, "length") && !strcmp(sig, "I")) return &g_fields[2];
+    if (!strcmp(name, "flags") && !strcmp(sig, "I")) return &g_fields[3];
+    return NULL;
+}
+static jobject GetObjectField(JNIEnv *env, jobject o, jfieldID f) {
+    return o && o->kind == K_PACKET && f->id == 0 ? o->buffer : NULL;
+}
+static jint GetIntField(JNIEnv *env, jobject o, jfieldID f) {
+    if (!o || o->kind != K_PACKET) return 0;
+    return f->id == 1 ? o->offset : f->id == 2 ? o->length : f->id == 3 ? o->flags : 0;
+}
+static void SetIntField(JNIEnv *env, jobject o, jfieldID f, jint v) {
+    if (!o || o->kind != K_PACKET) return;
+    if (f->id == 1) o->offset = v;
+    else if (f->id == 2) o->length = v;
+    else if (f->id == 3) o->flags = v;
+}
+static void SetObjectField(JNIEnv *env, jobject o, jfieldID f, jobject v) {
+    if (o && o->kind == K_PACKET && f->id == 0) o->buffer = v;
+}
+static jobject GetObjectArrayElement(JNIEnv *env, jobjectArray a, jsize i) {
+    return in_range(a, i, 1) ? ((jobject *)a->data)[i] : NULL;
+}
+static void SetObjectArrayElement(JNIEnv *env, jobjectArray a, jsize i, jobject v) {
+    if (in_range(a, i, 1)) ((jobject *)a->data)[i] = v;
+}
+static jint PushLocalFrame(JNIEnv *env, jint cap) {
+    __atomic_add_fetch(&g_frames, 1, __ATOMIC_RELAXED);
+    return JNI_OK;
+}
+static jobject PopLocalFrame(JNIEnv *env, jobject r) {
+    __atomic_sub_fetch(&g_frames, 1, __ATOMIC_RELAXED);
+    return r;
+}
+static jbyteArray NewByteArray(JNIEnv *env, jsize n) { return new_array(K_BYTES, n, 1); }
+static jint *GetIntArrayElements(JNIEnv *env, jintArray a, jboolean *is_copy) {
+    if (is_copy) *is_copy = 0;
+    return a ? (jint *)a->data : NULL;
+}
+static void ReleaseIntArrayElements(JNIEnv *env, jintArray a, jint *e, jint mode) {}
+
+static const struct JNINativeInterface_ g_table = {
+    GetArrayLength, GetIntArrayRegion, GetByteArrayRegion, SetByteArrayRegion, FindClass,
+    GetFieldID, GetObjectField, GetIntField, SetIntField, SetObjectField, GetObjectArrayElement,
+    SetObjectArrayElement, PushLocalFrame, PopLocalFrame, NewByteArray, GetIntArrayElements,
+    ReleaseIntArrayElements,
+};
+static JNIEnv g_env = &g_table;
+
+/* ---- the tests' side (ctypes) ---- */
+
+JNIEXPORT JNIEnv *fj_env(void) { return &g_env; }
+JNIEXPORT jobject fj_rawpacket_class(void) { return &g_rawpacket_class; }
+
+JNIEXPORT jbyteArray fj_new_bytes(const void *data, jsize n) {
+    struct fj_obj *a = new_array(K_BYTES, n, 1);
+    if (data && n) memcpy(a->data, data, (size_t)n);
+    return a;
+}
+JNIEXPORT jintArray fj_new_ints(const jint *data, jsize n) {
+    struct fj_obj *a = new_array(K_INTS, n, sizeof(jint));
+    if (data && n) memcpy(a->data, data, (size_t)n * sizeof(jint));
+    return a;
+}
+JNIEXPORT jobjectArray fj_new_objects(jsize n) { return new_array(K_OBJS, n, sizeof(jobject)); }
+JNIEXPORT void fj_set_element(jobjectArray a, jsize i, jobject v) { ((jobject *)a->data)[i] = v; }
+JNIEXPORT jobject fj_get_element(jobjectArray a, jsize i) { return ((jobject *)a->data)[i]; }
+
+JNIEXPORT jobject fj_new_packet(jbyteArray buffer, jint offset, jint length, jint flags) {
+    struct fj_obj *o = alloc_obj(K_PACKET);
+    o->buffer = buffer;
+    o->offset = offset;
+    o->length = length;
+    o->flags = flags;
+    return o;
+}
+JNIEXPORT jbyteArray fj_packet_buffer(jobject p) { return p->buffer; }
+JNIEXPORT jint fj_packet_offset(jobject p) { return p->offset; }
+JNIEXPORT jint fj_packet_length(jobject p) { return p->length; }
+
+JNIEXPORT jsize fj_bytes_len(jbyteArray a) { return a->len; }
+JNIEXPORT void fj_bytes_read(jbyteArray a, void *out) { memcpy(out, a->data, (size_t)a->len); }
+
+/* pending "exceptions" (out-of-range array regions) and unbalanced local frames */
+JNIEXPORT int fj_exceptions(void) { return g_exceptions; }
+JNIEXPORT int fj_frames(void) { return g_frames; }
+
+JNIEXPORT void fj_reset(void) {
+    while (g_allocs) {
+        struct fj_obj *o = g_allocs;
+        g_allocs = o->next_alloc;
+        free(o->data);
+        free(o);
+    }
+    g_exceptions = 0;
+    g_frames = 0;
+}

@@ -1,0 +1,268 @@
+"""The JNI shim (src/native/srtp_mi355x/SrtpMi355x.c), compiled unmodified
+against a stub JNI header and driven through a toy JVM (tests/jni_stub/).
+
+The image has no JDK, so the Java classes under src/org/ cannot be compiled
+here; the C half of the drop-in can.  tests/jni_stub/libfakejni.so is the shim
+plus fakejvm.c, which implements the JNI calls the shim makes over byte[] /
+int[] / Object[] and RawPacket objects (RawPacket.java:53-73).  The CPU test
+checks that every native method SrtpMi355x.java declares is exported; the GPU
+tests call the exported JNI functions exactly as the Java classes do --
+dispatcher, factories, transformers, transformOne (GpuTransformerBase's
+per-packet path) and transformPackets (its array path) -- and compare every
+RawPacket's bytes, length, buffer replacement and the nulled / thrown elements
+with the oracle.  The toy JVM also checks that no array region is ever out of
+range and that local frames balance.
+"""
+import ctypes as C
+import os
+import re
+import threading
+
+import numpy as np
+import pytest
+
+from libjitsi_amd import profile_policies, synth
+from libjitsi_amd import _native as N
+from oracle import oracle as O
+
+from harness import opol
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "jni_stub", "libfakejni.so")
+JAVA = os.path.join(ROOT, "src", "org", "jitsi", "impl", "neomedia", "transform", "srtp", "mi355x",
+                    "SrtpMi355x.java")
+PREFIX = "Java_org_jitsi_impl_neomedia_transform_srtp_mi355x_SrtpMi355x_"
+P80 = profile_policies("AES_CM_128_HMAC_SHA1_80")
+
+vp, i32, i64, u8 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint8
+
+
+def java_natives():
+    src = open(JAVA).read()
+    return re.findall(r"static native \w+(?:\[\])? (\w+)\(", src)
+
+
+def load():
+    if not os.path.exists(LIB):
+        pytest.skip("tests/jni_stub/libfakejni.so not built (__graft_entry__.build())")
+    L = C.CDLL(LIB)
+    J = lambda n: getattr(L, PREFIX + n)  # noqa: E731
+    L.fj_env.restype = vp
+    L.fj_rawpacket_class.restype = vp
+    for f, a, r in [("fj_new_bytes", [C.c_char_p, i32], vp), ("fj_new_ints", [vp, i32], vp),
+                    ("fj_new_objects", [i32], vp), ("fj_set_element", [vp, i32, vp], None),
+                    ("fj_get_element", [vp, i32], vp), ("fj_new_packet", [vp, i32, i32, i32], vp),
+                    ("fj_packet_buffer", [vp], vp), ("fj_packet_offset", [vp], i32),
+                    ("fj_packet_length", [vp], i32), ("fj_bytes_len", [vp], i32),
+                    ("fj_bytes_read", [vp, vp], None), ("fj_exceptions", [], C.c_int),
+                    ("fj_frames", [], C.c_int), ("fj_reset", [], None)]:
+        getattr(L, f).argtypes, getattr(L, f).restype = a, r
+    sig = {"deviceCount": ([], i32), "dispatchCreate": ([vp, i32, i32], i64), "dispatchDestroy": ([i64], None),
+           "factoryCreate": ([i64, u8, vp, vp, vp, vp], i32), "factoryClose": ([i64, i32], i32),
+           "transformerCreate": ([i64, i32, i32, i32], i32), "transformerSetFactory": ([i64, i32, i32, u8], i32),
+           "transformerClose": ([i64, i32], i32), "batchCreate": ([i64], i64), "batchDestroy": ([i64], None),
+           "transformPackets": ([i64, u8, i32, vp, vp], i32), "aggregatorCreate": ([i64], i64),
+           "aggregatorDestroy": ([i64], None), "transformOne": ([i64, u8, i32, vp], i32)}
+    for n, (a, r) in sig.items():
+        J(n).argtypes, J(n).restype = [vp, vp] + a, r
+    return L, J
+
+
+def test_shim_exports_every_java_native():
+    """Every `static native` method of SrtpMi355x.java has its JNI symbol."""
+    L, J = load()
+    names = java_natives()
+    assert len(names) >= 14
+    for n in names:
+        J(n)  # raises AttributeError when missing
+    # no GPU needed: without one the device count is 0, and Java refuses to start
+    env, cls = L.fj_env(), L.fj_rawpacket_class()
+    assert J("deviceCount")(env, cls) >= 0
+
+
+class Jvm:
+    """The Java side of the shim, as SrtpMi355x / GpuTransformerBase call it."""
+
+    def __init__(self, n_shards=2):
+        self.L, self.J = load()
+        self.env, self.cls = self.L.fj_env(), self.L.fj_rawpacket_class()
+        devs = np.zeros(n_shards, np.int32)
+        self.d = self.J("dispatchCreate")(self.env, self.cls, self.L.fj_new_ints(devs.ctypes.data, n_shards),
+                                          1, 1 << 14)
+        assert self.d
+        self.agg = self.J("aggregatorCreate")(self.env, self.cls, self.d)
+        self.batch = self.J("batchCreate")(self.env, self.cls, self.d)
+        assert self.agg and self.batch
+
+    def close(self):
+        self.J("aggregatorDestroy")(self.env, self.cls, self.agg)
+        self.J("batchDestroy")(self.env, self.cls, self.batch)
+        self.J("dispatchDestroy")(self.env, self.cls, self.d)
+        assert self.L.fj_exceptions() == 0, "the shim read or wrote an array region out of range"
+        assert self.L.fj_frames() == 0, "unbalanced local frames"
+        self.L.fj_reset()
+
+    def ints(self, a):
+        a = np.ascontiguousarray(a, np.int32)
+        return self.L.fj_new_ints(a.ctypes.data, len(a))
+
+    def factory(self, sender, key, salt, pol):
+        p = self.ints([pol.encType, pol.encKeyLength, pol.authType, pol.authKeyLength, pol.authTagLength,
+                       pol.saltKeyLength])
+        f = self.J("factoryCreate")(self.env, self.cls, self.d, int(sender), self.L.fj_new_bytes(key, len(key)),
+                                    self.L.fj_new_bytes(salt, len(salt)), p, p)
+        assert f >= 0
+        return f
+
+    def transformer(self, kind, fwd, rev):
+        t = self.J("transformerCreate")(self.env, self.cls, self.d, kind, fwd, rev)
+        assert t >= 0
+        return t
+
+    def packet(self, data, offset=0, extra=0):
+        buf = b"\xee" * offset + data + b"\x00" * extra
+        return self.L.fj_new_packet(self.L.fj_new_bytes(buf, len(buf)), offset, len(data), 0)
+
+    def packet_bytes(self, p):
+        b = self.L.fj_packet_buffer(p)
+        raw = (C.c_uint8 * self.L.fj_bytes_len(b))()
+        self.L.fj_bytes_read(b, raw)
+        o, n = self.L.fj_packet_offset(p), self.L.fj_packet_length(p)
+        return bytes(raw[o:o + n]), b
+
+    def one(self, reverse, tid, p):
+        return self.J("transformOne")(self.env, self.cls, self.agg, int(reverse), tid, p)
+
+    def array(self, reverse, tid, pkts, skip=None):
+        arr = self.L.fj_new_objects(len(pkts))
+        for i, p in enumerate(pkts):
+            self.L.fj_set_element(arr, i, p)
+        sk = self.ints(skip) if skip is not None else None
+        r = self.J("transformPackets")(self.env, self.cls, self.batch, int(reverse), tid, arr, sk)
+        return r, [self.L.fj_get_element(arr, i) for i in range(len(pkts))]
+
+
+def oracle_one(ot, reverse, data, extra=0):
+    L = len(data)
+    avail = L + extra
+    cap = min(max(avail, L + 16), 65535) if not reverse else avail
+    seg = np.zeros(max((cap + 15) // 16 * 16, 16), np.uint8)
+    seg[:L] = np.frombuffer(data, np.uint8)
+    ln = np.array([L], np.uint32)
+    st = O.process(ot, reverse, seg, np.zeros(1, np.uint32), ln, np.array([cap], np.uint32),
+                   np.zeros(1, np.uint32), True)
+    return int(st[0]), seg[:int(ln[0])].tobytes()
+
+
+def rtp(ssrc, seq, n, rng, bad_ext=False):
+    b = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    b[0], b[1] = 0x80, 96
+    b[2:4] = (seq & 0xFFFF).to_bytes(2, "big")
+    b[8:12] = ssrc.to_bytes(4, "big")
+    if bad_ext:  # an extension length past the packet: the reference throws
+        b[0] |= 0x10
+        b[12:16] = b"\xbe\xde\x7f\xff"
+    return bytes(b)
+
+
+@pytest.mark.gpu
+def test_jni_per_packet_and_array_paths_vs_oracle():
+    jvm = Jvm(n_shards=2)
+    try:
+        (k, s), = synth.keys(31, 1)
+        fs, fr = jvm.factory(True, k, s, P80[0]), jvm.factory(False, k, s, P80[0])
+        ts, tr = jvm.transformer(0, fs, fs), jvm.transformer(0, fr, fr)
+        ofs = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+        ofr = O.Factory(False, k, s, opol(P80[0]), opol(P80[1]))
+        ots, otr = O.Transformer(O.KIND_RTP, ofs, ofs), O.Transformer(O.KIND_RTP, ofr, ofr)
+        rng = np.random.default_rng(7)
+        # per packet (transformOne): a new buffer where append reallocates, in
+        # place where there is room (extra bytes behind the packet, an offset)
+        prot = []
+        for q in range(8):
+            data = rtp(0x1234 + (q & 1), 500 + q, 200 + 40 * q, rng)
+            extra, off = (16, 3) if q % 3 == 0 else (0, 0)
+            p = jvm.packet(data, off, extra)
+            b0 = jvm.L.fj_packet_buffer(p)
+            st = jvm.one(False, ts, p)
+            ost, ob = oracle_one(ots, False, data, extra)
+            got, b = jvm.packet_bytes(p)
+            assert st == ost == N.STATUS_OK and got == ob
+            assert (b == b0) == (extra >= 10)  # the reference's append: in place only with room
+            prot.append(got)
+        # the array path (transformPackets): a replay, a forgery and a throw in
+        # mid-array; later packets of the transformer are not processed
+        bad = bytearray(prot[5])
+        bad[-1] ^= 1
+        inputs = [prot[0], prot[1], prot[0], bytes(bad), prot[2], rtp(0x1234, 9, 40, rng, bad_ext=True),
+                  prot[3], prot[4]]
+        pkts = [jvm.packet(x) for x in inputs]
+        r, out = jvm.array(True, tr, pkts)
+        seg = np.zeros(sum((len(x) + 15) // 16 * 16 for x in inputs), np.uint8)
+        off = np.zeros(len(inputs), np.uint32)
+        pos = 0
+        for i, x in enumerate(inputs):
+            off[i] = pos
+            seg[pos:pos + len(x)] = np.frombuffer(x, np.uint8)
+            pos += (len(x) + 15) // 16 * 16
+        ln = np.array([len(x) for x in inputs], np.uint32)
+        st_o = O.process(otr, True, seg, off, ln, ln.copy(), None, True)
+        thrown = [i for i, s in enumerate(st_o) if s == N.STATUS_ERR_MALFORMED]
+        assert r == (thrown[0] + 1 if thrown else 0)
+        for i in range(len(inputs)):
+            if st_o[i] in (N.STATUS_OK, N.STATUS_ERR_MALFORMED):
+                assert out[i] == pkts[i]
+                got, _ = jvm.packet_bytes(pkts[i])
+                assert got == seg[off[i]:off[i] + ln[i]].tobytes(), i
+            elif st_o[i] == N.STATUS_NOT_PROCESSED:
+                assert out[i] == pkts[i]
+                got, _ = jvm.packet_bytes(pkts[i])
+                assert got == inputs[i]  # untouched
+            else:
+                assert out[i] is None, (i, N.STATUS_NAMES[st_o[i]])  # the reference returned null
+    finally:
+        jvm.close()
+
+
+@pytest.mark.gpu
+def test_jni_per_packet_from_many_threads_vs_oracle():
+    """16 "JVM threads" call transformOne at once, each on its own SSRCs."""
+    jvm = Jvm(n_shards=3)
+    try:
+        keys = synth.keys(41, 4)
+        tids, otids = [], []
+        for k, s in keys:
+            f = jvm.factory(True, k, s, P80[0])
+            tids.append(jvm.transformer(0, f, f))
+            of = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+            otids.append(O.Transformer(O.KIND_RTP, of, of))
+        scripts = []
+        for t in range(16):
+            rng = np.random.default_rng(100 + t)
+            scripts.append([(t % 4, rtp(0x9000 + t, 40 + q, int(rng.integers(60, 1300)), rng)) for q in range(20)])
+        results = [None] * 16
+        errs = []
+
+        def work(t):
+            try:
+                out = []
+                for ti, data in scripts[t]:
+                    p = jvm.packet(data)
+                    st = jvm.one(False, tids[ti], p)
+                    out.append((st, jvm.packet_bytes(p)[0]))
+                results[t] = out
+            except Exception as ex:  # noqa: BLE001
+                errs.append(ex)
+        th = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs
+        for t in range(16):
+            for (ti, data), (st, got) in zip(scripts[t], results[t]):
+                ost, ob = oracle_one(otids[ti], False, data)
+                assert st == ost and got == ob
+    finally:
+        jvm.close()

@@ -1,12 +1,13 @@
 #!/bin/bash
-# Round-3 final evidence of the committed tree: the GPU suite, smoke, the
-# bench line as the driver runs it and at the default step count, every
-# BASELINE config, aggregator throughput, then the profile passes
-# (tools/r03_prof.sh: kernel traces, PMC, calibration, timeline).
+# Round-end evidence of the committed tree: the GPU suite, smoke, the bench
+# line as the driver runs it and at the default step count, every BASELINE
+# config, mixed key sets, the per-packet path (sync_bench) and aggregator
+# throughput, then the profile passes (tools/prof.sh: kernel traces, PMC,
+# calibration, timeline).  TAG names the gpurun_out/ subdirectory.
 # A crash or time limit (exit >= 124) ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/${R03_TAG:-r03z}
+O=gpurun_out/${TAG:-final}
 mkdir -p $O
 t() {
   local name=$1 lim=$2; shift 2
@@ -20,5 +21,9 @@ t smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 t bench20 180 python bench.py --gpus 1 --steps 20 --warmup 5
 t bench100 180 python bench.py
 t configs 300 python -u tools/config_bench.py --out $O/configs.json
+t keysets16 180 python bench.py --steps 20 --keysets 16 --no-cpu --no-e2e --no-dispatch
+t keysets1000 180 python bench.py --steps 20 --keysets 1000 --no-cpu --no-e2e --no-dispatch
+t ssrcs100k 180 python bench.py --steps 20 --ssrcs 100000 --no-cpu --no-e2e --no-dispatch
+t sync_bench 300 ./tools/sync_bench 2
 t agg_bench 120 ./tools/agg_bench 1.5
-R03_TAG=${R03_TAG:-r03z}/prof ./tools/r03_prof.sh
+TAG=${TAG:-final}/prof ./tools/prof.sh

@@ -4,7 +4,7 @@ Usage:
     python tools/pmc_summary.py <prof_dir> [--packets N --len L --out profiles/rNN]
 
 <prof_dir> holds trace/run_kernel_trace.csv and <pass>/run_counter_collection.csv
-for the passes gpu_run.sh `prof` writes (fetch, write, sq, sq2).  Prints, per
+for the passes tools/prof.sh writes (fetch, write, sq, sq2).  Prints, per
 kernel of the SRTP pipeline, the average duration and every counter averaged
 over dispatches, then derived figures for k_protect / k_unprotect:
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 profile evidence of the committed tree: rocprofv3 kernel traces
+# Profile evidence of the committed tree: rocprofv3 kernel traces
 # (serial and default two-stream bench), PMC passes (serial, as the roofline's
 # stage timing), the PMC summary (writes profiles/pmc_traffic.json), and the
 # FETCH_SIZE / WRITE_SIZE calibration of the kernels' access pattern
@@ -7,7 +7,7 @@
 # ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-P=gpurun_out/${R03_TAG:-r03p}
+P=gpurun_out/${TAG:-prof}
 mkdir -p $P
 run() {  # run <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
