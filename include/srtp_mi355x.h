@@ -317,6 +317,30 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
                             int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
                             int32_t abort_on_error);
 
+/* Registered host memory: the zero-copy host path.  srtp_host_register pins
+ * [ptr, ptr + bytes) for DMA by every device of the process (hipHostRegister,
+ * portable) -- a long-lived buffer pool, e.g. the JVM's direct ByteBuffers a
+ * media server receives into, registered once.  Ranges may not overlap;
+ * srtp_host_unregister takes the pointer that was registered, and the caller
+ * must not unregister or free a range while a call uses it.
+ * srtp_host_is_registered tells whether [ptr, ptr + bytes) lies inside one
+ * registered range.  No reference API: the reference's packets are heap
+ * byte[]s copied by every JNI call (src/native/openssl/).
+ *
+ * srtp_pipeline_submit_host is srtp_pipeline_submit_ex with the segment read
+ * from, and written back to, registered caller memory (host_seg, seg_bytes)
+ * instead of the slot's seg: the slot's per-packet arrays still describe the
+ * bundle (off relative to host_seg).  srtp_dispatch_transform_host does this
+ * by itself for every chunk of a shard whose packets lie back to back in a
+ * registered segment, so a one-shard dispatcher moves a registered bundle
+ * with no host copy at all. */
+int srtp_host_register(void *ptr, size_t bytes);
+int srtp_host_unregister(void *ptr);
+int32_t srtp_host_is_registered(const void *ptr, size_t bytes);
+int srtp_pipeline_submit_host(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                              int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                              int32_t abort_on_error, uint8_t *host_seg);
+
 /* Bundle aggregator over the pipeline: per-packet submits
  * from any number of threads become bundles.  Replaces the reference's
  * one-packet-at-a-time calls through the transform chain

@@ -59,6 +59,7 @@ EXPORTED = [
     "srtp_rawpacket_batch_destroy", "srtp_rawpacket_transform", "srtp_rawpacket_result",
     "srtp_dispatch_host_times", "srtp_pipeline_submit_ex", "srtp_aggregator_transform",
     "srtp_aggregator_transformer_info", "srtp_rawpacket_transform_one", "srtp_device_count",
+    "srtp_host_register", "srtp_host_unregister", "srtp_host_is_registered", "srtp_pipeline_submit_host",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -184,6 +185,11 @@ def lib() -> C.CDLL:
     L.srtp_aggregator_transform.argtypes = [vp, i32, i32, vp, u32, u32, u32, u32, vp, pi32, pu32]
     L.srtp_aggregator_transformer_info.argtypes = [vp, i32, pi32, pi32]
     L.srtp_rawpacket_transform_one.argtypes = [vp, i32, i32, vp, u32, u32, pu32, u32, pi32, pu32, vp, u32]
+    L.srtp_host_register.argtypes = [vp, C.c_size_t]
+    L.srtp_host_unregister.argtypes = [vp]
+    L.srtp_host_is_registered.argtypes = [vp, C.c_size_t]
+    L.srtp_host_is_registered.restype = i32
+    L.srtp_pipeline_submit_host.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t, i32, vp]
     L.srtp_device_count.argtypes = []
     L.srtp_device_count.restype = i32
     L.srtp_engine_stats.argtypes = [vp, C.POINTER(Stats)]

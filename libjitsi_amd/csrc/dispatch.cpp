@@ -60,9 +60,9 @@
 namespace {
 
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
-constexpr uint32_t kChunkPackets = 1u << 16;       // packets per pipeline slot
-constexpr size_t kChunkBytes = (size_t)64 << 20;   // segment bytes per pipeline slot
-constexpr int kDepth = 2;                          // pipeline slots per shard
+constexpr uint32_t kChunkPackets = 1u << 15;       // packets per pipeline slot
+constexpr size_t kChunkBytes = (size_t)32 << 20;   // segment bytes per pipeline slot
+constexpr int kDepth = 4;                          // pipeline slots per shard
 
 uint32_t mix32(uint32_t x) { // murmur3 fmix32 (libjitsi_amd/dispatch.py mix32)
     x ^= x >> 16;
@@ -269,6 +269,7 @@ struct srtp_dispatch {
     const uint32_t *b_off = nullptr, *b_cap = nullptr, *b_flags = nullptr;
     uint32_t *b_len = nullptr;
     int32_t *b_status = nullptr;
+    bool b_registered = false; // the segment lies in registered memory (srtp_host_register)
 };
 
 namespace {
@@ -285,6 +286,28 @@ int dfail(srtp_dispatch *d, int code, const std::string &msg) {
 
 size_t region(uint32_t cap) { return ((size_t)cap + 15) & ~(size_t)15; }
 
+// Copies packets [j0, j1) of a chunk between a pipeline slot and the caller's
+// segment, one memcpy per run of packets that lie back to back in both (the
+// slot's are by construction; a one-shard bundle is then a single run): a
+// call per 1.2-KB packet costs as much as its bytes.
+template <bool ToSlot>
+void copy_runs(const srtp_dispatch *d, const srtp_pipeline_slot &sl, const std::vector<uint32_t> &ch, size_t j0,
+               size_t j1) {
+    for (size_t j = j0; j < j1;) {
+        const uint32_t i = ch[j];
+        size_t bytes = region(d->b_cap[i]);
+        size_t e = j + 1;
+        while (e < j1 && d->b_off[ch[e]] == d->b_off[ch[e - 1]] + region(d->b_cap[ch[e - 1]])) {
+            bytes += region(d->b_cap[ch[e]]);
+            e++;
+        }
+        uint8_t *slot = sl.seg + sl.off[j], *user = d->b_seg + d->b_off[i];
+        if (ToSlot) memcpy(slot, user, bytes);
+        else memcpy(user, slot, bytes);
+        j = e;
+    }
+}
+
 // Shard s's share of one phase: chunks through the shard's pipeline slots.
 int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t reverse) {
     srtp_pipeline *pl = d->pipes[(size_t)s];
@@ -295,6 +318,7 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
     }
     std::vector<uint32_t> chunk_of[kDepth]; // global packet indices in each slot
     int busy[kDepth] = {0};
+    bool direct[kDepth] = {false}; // the chunk ran in place in the caller's registered segment
     int rc_all = SRTP_OK;
     auto drain = [&](int k) {
         if (!busy[k]) return;
@@ -312,12 +336,13 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         const size_t nch = ch.size();
         const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
         d->pool->run(parts, [&](int q) {
-            for (size_t j = nch * q / parts; j < nch * (q + 1) / parts; j++) {
+            const size_t j0 = nch * q / parts, j1 = nch * (q + 1) / parts;
+            for (size_t j = j0; j < j1; j++) {
                 const uint32_t i = ch[j];
                 d->b_status[i] = sl[k].status[j];
                 d->b_len[i] = sl[k].len[j];
-                memcpy(d->b_seg + d->b_off[i], sl[k].seg + sl[k].off[j], region(d->b_cap[i]));
             }
+            if (!direct[k]) copy_runs<false>(d, sl[k], ch, j0, j1);
         });
         d->t_scatter += now_ns() - ts;
     };
@@ -329,11 +354,13 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         std::vector<uint32_t> &ch = chunk_of[k];
         ch.clear();
         size_t bytes = 0;
+        bool contig = true; // the chunk's packets lie back to back in the caller's segment
         const uint64_t tp = now_ns();
         while (pos < idx.size() && ch.size() < sl[k].max_packets) { // the chunk's layout
             const uint32_t i = idx[pos];
             const size_t r = region(d->b_cap[i]);
             if (bytes + r > sl[k].seg_cap) break;
+            if (!ch.empty() && d->b_off[i] != d->b_off[ch.back()] + region(d->b_cap[ch.back()])) contig = false;
             const uint32_t j = (uint32_t)ch.size();
             sl[k].off[j] = (uint32_t)bytes;
             sl[k].len[j] = d->b_len[i];
@@ -344,22 +371,23 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             ch.push_back(i);
             pos++;
         }
-        {   // the packet bytes, split over the copy helpers
-            const size_t nch = ch.size();
-            const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
-            d->pool->run(parts, [&](int q) {
-                for (size_t j = nch * q / parts; j < nch * (q + 1) / parts; j++) {
-                    const uint32_t i = ch[j];
-                    memcpy(sl[k].seg + sl[k].off[j], d->b_seg + d->b_off[i], region(d->b_cap[i]));
-                }
-            });
-        }
-        d->t_pack += now_ns() - tp;
         if (ch.empty()) { // a packet larger than a slot (cannot happen: cap <= 65535)
             rc_all = SRTP_EINVAL;
             break;
         }
-        const int rc = srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes);
+        // a registered segment whose chunk is one run: the DMA reads and
+        // writes the caller's bytes in place; else the packet bytes go
+        // through the slot, split over the copy helpers
+        direct[k] = d->b_registered && contig;
+        if (!direct[k]) {
+            const size_t nch = ch.size();
+            const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
+            d->pool->run(parts, [&](int q) { copy_runs<true>(d, sl[k], ch, nch * q / parts, nch * (q + 1) / parts); });
+        }
+        d->t_pack += now_ns() - tp;
+        const int rc = direct[k] ? srtp_pipeline_submit_host(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes, -1,
+                                                             d->b_seg + d->b_off[ch[0]])
+                                 : srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes);
         if (rc != SRTP_OK) {
             rc_all = rc;
             for (uint32_t i : ch) d->b_status[i] = SRTP_STATUS_ERR_INTERNAL;
@@ -638,6 +666,7 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     }
     d->b_tids = tids; d->b_tid = tid; d->b_seg = seg; d->b_off = off; d->b_len = len;
     d->b_cap = cap; d->b_flags = flags; d->b_status = status;
+    d->b_registered = srtp_host_is_registered(seg, seg_bytes) != 0;
     auto tid_of = [&](uint32_t i) { return tids ? tids[i] : tid; };
     std::vector<std::vector<uint32_t>> per_shard(ns);
     std::vector<uint32_t> at((size_t)parts * ns);

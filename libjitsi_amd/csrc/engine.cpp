@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -1190,6 +1191,54 @@ int srtp_block_encrypt(int32_t enc_type, const uint8_t *key, int32_t key_len, co
 
 } // extern "C"
 
+extern "C" {
+
+// ------------------------------------------------- registered host memory
+namespace {
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_reg; // start -> bytes, disjoint
+} // namespace
+
+int srtp_host_register(void *ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return SRTP_EINVAL;
+    const uintptr_t a = (uintptr_t)ptr;
+    if (a + bytes < a) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.upper_bound(a);
+    if (it != g_reg.end() && it->first < a + bytes) return SRTP_EINVAL;
+    if (it != g_reg.begin() && std::prev(it)->first + std::prev(it)->second > a) return SRTP_EINVAL;
+    if (hipHostRegister(ptr, bytes, hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        return SRTP_EDEVICE;
+    }
+    g_reg[a] = bytes;
+    return SRTP_OK;
+}
+
+int srtp_host_unregister(void *ptr) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find((uintptr_t)ptr);
+    if (it == g_reg.end()) return SRTP_EINVAL;
+    g_reg.erase(it);
+    if (hipHostUnregister(ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return SRTP_EDEVICE;
+    }
+    return SRTP_OK;
+}
+
+int32_t srtp_host_is_registered(const void *ptr, size_t bytes) {
+    const uintptr_t a = (uintptr_t)ptr;
+    if (!ptr || a + bytes < a) return 0;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.upper_bound(a);
+    if (it == g_reg.begin()) return 0;
+    --it;
+    return a + bytes <= it->first + it->second ? 1 : 0;
+}
+
+} // extern "C"
+
 // ------------------------------------------------------------ host pipeline
 struct srtp_pipeline {
     srtp_engine *e = nullptr;
@@ -1315,9 +1364,11 @@ int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32
     return srtp_pipeline_submit_ex(pl, slot, reverse, use_tids, tid, use_flags, n, seg_bytes, -1);
 }
 
-int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
-                            int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
-                            int32_t abort_on_error) {
+// hseg: the bundle's host segment -- the slot's pinned seg, or registered
+// caller memory (srtp_pipeline_submit_host)
+static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids, int32_t tid,
+                           int32_t use_flags, uint32_t n, size_t seg_bytes, int32_t abort_on_error,
+                           uint8_t *hseg) {
     if (!pl || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
     std::lock_guard<std::mutex> gp(pl->mu);
     srtp_pipeline::Slot &sl = pl->slots[(size_t)slot];
@@ -1334,7 +1385,8 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
         return fail(e, SRTP_EINVAL, "bad transformer id");
     hipStream_t si = pl->s_in, so = pl->s_out, s = e->stream;
     const int32_t abort = abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0);
-    HIPCHK(e, hipMemcpyAsync(sl.d_seg, sl.h.seg, seg_bytes, hipMemcpyHostToDevice, si));
+    if (!hseg) hseg = sl.h.seg;
+    HIPCHK(e, hipMemcpyAsync(sl.d_seg, hseg, seg_bytes, hipMemcpyHostToDevice, si));
     if (n <= kPackMax) {
         uint32_t *hp = sl.h_pack, *dp = sl.d_pack;
         const size_t n4 = n * 4ull;
@@ -1353,7 +1405,7 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
         if (sl.rc != SRTP_OK) return sl.rc;
         HIPCHK(e, hipEventRecord(sl.ev_done, s));
         HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
-        HIPCHK(e, hipMemcpyAsync(sl.h.seg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
+        HIPCHK(e, hipMemcpyAsync(hseg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
         HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, 2 * n4, hipMemcpyDeviceToHost, so));
         sl.packed_n = n;
     } else {
@@ -1369,13 +1421,28 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
         if (sl.rc != SRTP_OK) return sl.rc;
         HIPCHK(e, hipEventRecord(sl.ev_done, s));
         HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
-        HIPCHK(e, hipMemcpyAsync(sl.h.seg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
+        HIPCHK(e, hipMemcpyAsync(hseg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
         HIPCHK(e, hipMemcpyAsync(sl.h.len, sl.d_len, n * 4ull, hipMemcpyDeviceToHost, so));
         HIPCHK(e, hipMemcpyAsync(sl.h.status, sl.d_status, n * 4ull, hipMemcpyDeviceToHost, so));
     }
     HIPCHK(e, hipEventRecord(sl.ev_out, so));
     sl.busy = true;
     return SRTP_OK;
+}
+
+int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                            int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                            int32_t abort_on_error) {
+    return pipeline_submit(pl, slot, reverse, use_tids, tid, use_flags, n, seg_bytes, abort_on_error, nullptr);
+}
+
+int srtp_pipeline_submit_host(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                              int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                              int32_t abort_on_error, uint8_t *host_seg) {
+    // the D2H writes whole 16-B regions: the registered range must hold them
+    if (!host_seg || (n && !srtp_host_is_registered(host_seg, (seg_bytes + 15) & ~(size_t)15)))
+        return SRTP_EINVAL;
+    return pipeline_submit(pl, slot, reverse, use_tids, tid, use_flags, n, seg_bytes, abort_on_error, host_seg);
 }
 
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot) {

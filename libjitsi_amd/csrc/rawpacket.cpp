@@ -25,11 +25,13 @@
 // element gets need_len[i] = the new buffer's length, its result stays in
 // the batch (srtp_rawpacket_result), and the shim allocates the array, copies
 // the result to offset 0 and sets buffer / offset = 0 / length.  Everything
-// else is written in place while the shim holds the arrays
-// (GetPrimitiveArrayCritical).  The Python mirror (libjitsi_amd/srtp.py
+// else is written in place into the buffers the caller passed (the JNI
+// shim's own copies of the Java arrays, written back with SetByteArrayRegion:
+// no JNI critical region spans a GPU call).  The Python mirror (libjitsi_amd/srtp.py
 // SRTPTransformer.transform) calls these same functions.
 #include <algorithm>
 #include <new>
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 
@@ -41,7 +43,12 @@ struct srtp_rawpacket_batch {
     srtp_pipeline *pl = nullptr;
     uint32_t pl_packets = 0;
     size_t pl_bytes = 0;
-    std::vector<uint8_t> seg;   // dispatch-mode staging
+    // dispatch-mode staging: a segment registered for DMA (srtp_host_register),
+    // so the dispatcher's shards move it in place, with no second copy
+    uint8_t *seg = nullptr;
+    size_t seg_cap = 0;
+    bool seg_registered = false;
+    std::vector<uint32_t> order; // packing order: grouped by shard
     std::vector<uint32_t> off, len, cap, flags;
     std::vector<int32_t> tids, status;
     // the current call's arrays (pipeline slot or the vectors above)
@@ -61,8 +68,16 @@ srtp_engine *engine_of(const srtp_rawpacket_batch *b) {
     return b->e ? b->e : srtp_dispatch_engine(b->d, 0);
 }
 
+void release_seg(srtp_rawpacket_batch *b) {
+    if (b->seg_registered) (void)srtp_host_unregister(b->seg);
+    free(b->seg);
+    b->seg = nullptr;
+    b->seg_cap = 0;
+    b->seg_registered = false;
+}
+
 // Staging for n packets / bytes: the pipeline slot (grown by recreating the
-// pipeline) or the host vectors.
+// pipeline) or the registered host segment and vectors.
 int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
     if (b->e) {
         if (!b->pl || n > b->pl_packets || bytes > b->pl_bytes) {
@@ -81,14 +96,23 @@ int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
         b->s_seg = sl.seg; b->s_off = sl.off; b->s_len = sl.len; b->s_cap = sl.cap;
         b->s_flags = sl.flags; b->s_tids = sl.tids; b->s_status = sl.status;
     } else {
+        if (bytes > b->seg_cap) {
+            release_seg(b);
+            const size_t nb = (std::max<size_t>(std::max<size_t>(bytes, (size_t)1 << 20), 2 * b->seg_cap) + 4095) &
+                              ~(size_t)4095;
+            b->seg = static_cast<uint8_t *>(aligned_alloc(4096, nb));
+            if (!b->seg) return SRTP_ENOMEM;
+            b->seg_cap = nb;
+            // unregistered (no device, a pinning limit) it still works, by copies
+            b->seg_registered = srtp_host_register(b->seg, nb) == SRTP_OK;
+        }
         try {
-            b->seg.resize(std::max<size_t>(bytes, 16));
             b->off.resize(n); b->len.resize(n); b->cap.resize(n); b->flags.resize(n);
             b->tids.resize(n); b->status.resize(n);
         } catch (...) {
             return SRTP_ENOMEM;
         }
-        b->s_seg = b->seg.data(); b->s_off = b->off.data(); b->s_len = b->len.data();
+        b->s_seg = b->seg; b->s_off = b->off.data(); b->s_len = b->len.data();
         b->s_cap = b->cap.data(); b->s_flags = b->flags.data(); b->s_tids = b->tids.data();
         b->s_status = b->status.data();
     }
@@ -162,6 +186,7 @@ int srtp_rawpacket_batch_create_dispatch(srtp_dispatch *d, srtp_rawpacket_batch 
 void srtp_rawpacket_batch_destroy(srtp_rawpacket_batch *b) {
     if (!b) return;
     if (b->pl) srtp_pipeline_destroy(b->pl);
+    release_seg(b);
     delete b;
 }
 
@@ -175,7 +200,7 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
     b->n = 0;
     if (n == 0) return SRTP_OK;
     srtp_engine *eng = engine_of(b);
-    // Packing (the JNI shim's GetPrimitiveArrayCritical view of each buffer):
+    // Packing (the JNI shim's copy of each buffer):
     // region i holds the buffer's bytes from the packet's offset on, so the
     // reference's reads past `length` (getHeaderLength's extension field,
     // readRegionToBuff) see the same bytes; cap is the buffer's length after
@@ -196,8 +221,36 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
     }
     int rc = stage(b, n, bytes);
     if (rc != SRTP_OK) return rc;
+    // Over a dispatcher of several shards, the regions are laid out grouped by
+    // the shard the dispatcher will route each packet to (in array order
+    // within a shard), so each shard's packets lie back to back and its chunks
+    // move by DMA in place.  The routing here only needs to agree with the
+    // dispatcher's for the layout to pay; results never depend on it.
+    const int32_t ns = b->d ? srtp_dispatch_num_shards(b->d) : 1;
+    const uint32_t *ord = nullptr;
+    if (ns > 1) {
+        try {
+            b->order.resize(n);
+        } catch (...) {
+            return SRTP_ENOMEM;
+        }
+        std::vector<uint32_t> at((size_t)ns + 1, 0u);
+        std::vector<int32_t> sh(n);
+        for (uint32_t i = 0; i < n; i++) {
+            const bool skip = !bufs[i] || (flags && (flags[i] & SRTP_PKT_FLAG_SKIP));
+            int32_t s = 0;
+            if (!skip && length[i] <= ccap[i] && length[i] <= avail[i])
+                s = srtp_dispatch_route(b->d, tids ? tids[i] : tid, bufs[i] + offset[i], length[i]);
+            sh[i] = s < 0 ? 0 : s;
+            at[(size_t)sh[i] + 1]++;
+        }
+        for (int32_t s = 0; s < ns; s++) at[(size_t)s + 1] += at[(size_t)s];
+        for (uint32_t i = 0; i < n; i++) b->order[at[(size_t)sh[i]]++] = i;
+        ord = b->order.data();
+    }
     size_t pos = 0;
-    for (uint32_t i = 0; i < n; i++) {
+    for (uint32_t q = 0; q < n; q++) {
+        const uint32_t i = ord ? ord[q] : q;
         const bool skip = !bufs[i] || (flags && (flags[i] & SRTP_PKT_FLAG_SKIP));
         const size_t r = region(ccap[i]);
         b->s_off[i] = (uint32_t)pos;

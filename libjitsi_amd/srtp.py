@@ -347,6 +347,23 @@ class SRTPEngine:
         N.check(rc, self.h, "srtp_transform_device")
 
 
+def host_register(arr: np.ndarray) -> None:
+    """Pins ``arr``'s memory for DMA by every GPU (srtp_host_register): a
+    long-lived buffer pool registered once, which the dispatcher then moves
+    with no host copy (a one-shard bundle, or each shard's packets back to
+    back).  Unregister before the array is freed."""
+    assert arr.flags.c_contiguous and arr.nbytes > 0
+    N.check(N.lib().srtp_host_register(arr.ctypes.data, arr.nbytes), None, "srtp_host_register")
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    N.check(N.lib().srtp_host_unregister(arr.ctypes.data), None, "srtp_host_unregister")
+
+
+def host_is_registered(arr: np.ndarray) -> bool:
+    return bool(N.lib().srtp_host_is_registered(arr.ctypes.data, arr.nbytes))
+
+
 class SRTPDispatcher:
     """In-process multi-GPU engine (srtp_dispatch_*, C ABI): one engine per
     shard on ``devices[i]`` (several shards may share a GPU), each bundle split

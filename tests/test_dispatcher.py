@@ -214,3 +214,57 @@ def test_dispatch_many_throws_bounded_runs(oracle):
         assert d.stats()["bundles"] - n2 <= 2 * shards
     finally:
         d.close()
+
+
+class _Registered:
+    """The dispatcher with each call's segment registered (srtp_host_register),
+    as a caller's long-lived buffer pool would be: a shard's chunk whose packets
+    lie back to back is moved by DMA in place, with no host copy."""
+
+    def __init__(self, d):
+        self._d = d
+
+    def __getattr__(self, k):
+        return getattr(self._d, k)
+
+    def transform_host(self, reverse, tid, seg, *a, **kw):
+        from libjitsi_amd import host_is_registered, host_register, host_unregister
+        host_register(seg)
+        try:
+            assert host_is_registered(seg)
+            return self._d.transform_host(reverse, tid, seg, *a, **kw)
+        finally:
+            host_unregister(seg)
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_dispatch_registered_segment_in_place(oracle, shards):
+    """Registered segments through 1 shard (every chunk one run: no host copy
+    at all) and 3 shards (runs broken by the SSRC split: the copy path), bit
+    for bit against the oracle: several chunks per shard, faults, and
+    malformed packets whose rollback restores the registered bytes."""
+    if _gpus() < 1:
+        pytest.skip("no GPU visible")
+    d = SRTPDispatcher([0] * shards, max_contexts=1 << 15, max_factories=64, max_transformers=64)
+    try:
+        twin = Twin(_Registered(d))
+        (k, s), = synth.keys(81, 1)
+        fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+        snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+        b = synth.rtp_bundle(70000, 500, (60, 400), seed=82)  # > 2 chunks of 2^15 packets
+        seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+        assert (st == N.STATUS_OK).all()
+        seg = seg.copy()
+        o = b.off.astype(np.int64)
+        seg[o[1000] + 20] ^= 1      # forged
+        seg[o[40000] + 30] ^= 0x80  # forged, in a later chunk
+        twin.run(rcv, True, seg, b.off, ln, b.cap)
+        # throws: the rollback restores stashed bytes into the registered segment
+        b2 = synth.rtp_bundle(3000, 40, (40, 700), seed=83)
+        o2 = b2.off.astype(np.int64)
+        for i in (200, 1500):
+            b2.seg[o2[i]] = 0x9F
+        _, _, st2 = twin.run(snd, False, b2.seg, b2.off, b2.length, b2.cap)
+        assert (st2 == N.STATUS_ERR_MALFORMED).any() and (st2 == N.STATUS_NOT_PROCESSED).any()
+    finally:
+        d.close()

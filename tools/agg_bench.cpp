@@ -7,6 +7,7 @@
 // callback counts completions; prints one JSON line per (G, P).
 //
 //   agg_bench [seconds-per-point] [devices: 0 = all shards on device 0]
+//             [shards: only this count, 0 = one engine] [producers: only this count]
 #include <atomic>
 #include <chrono>
 #include <stdio.h>
@@ -54,8 +55,10 @@ int main(int argc, char **argv) {
     const double seconds = argc > 1 ? atof(argv[1]) : 2.0;
     const int distinct_devices = argc > 2 ? atoi(argv[2]) : 0;
     const uint32_t L = 1200;
-    const int shard_counts[] = {0, 1, 4, 8}; // 0: one engine without a dispatcher
-    const int producer_counts[] = {1, 4, 16};
+    std::vector<int> shard_counts = {0, 1, 4, 8}; // 0: one engine without a dispatcher
+    std::vector<int> producer_counts = {1, 4, 16};
+    if (argc > 3) shard_counts = {atoi(argv[3])};
+    if (argc > 4) producer_counts = {atoi(argv[4])};
     srtp_policy pol = {SRTP_AESCM_ENCRYPTION, 16, SRTP_HMACSHA1_AUTHENTICATION, 20, 10, 14};
     uint8_t key[16], salt[14];
     for (int i = 0; i < 16; i++) key[i] = (uint8_t)(17 * i + 3);
