@@ -230,24 +230,32 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
     dispatcher's host time per bundle: plan + split, packing into the shards'
     pinned slots, waiting for the shards (H2D + kernels + D2H), scattering
     back (the last three summed over the shards' worker threads).  Each G runs
-    twice: with the segment registered (srtp_host_register, key "G": a shard's
-    chunk whose packets lie back to back moves by DMA in place, no host copy)
-    and unregistered (key "G_copy": every packet copied into the pinned slots
-    and back)."""
-    from libjitsi_amd import (SRTPContextFactory, SRTPDispatcher, SRTPTransformer, host_register,
-                              host_unregister)
+    with the bundle in the engine's pinned memory (HostBuffer / srtp_host_alloc,
+    key "G": a shard's chunk whose packets lie back to back moves by DMA in
+    place, no host copy) and in plain pageable memory (key "G_copy": every
+    packet copied into the pinned slots and back); G = 1 also with pageable
+    memory registered once (srtp_host_register, key "1_registered")."""
+    from libjitsi_amd import (HostBuffer, SRTPContextFactory, SRTPDispatcher, SRTPTransformer,
+                              host_register, host_unregister)
     out = {}
-    for G, registered in [(G, r) for G in shard_counts for r in (True, False)]:
+    modes = [(G, m) for G in shard_counts for m in ("pinned", "copy")] + [(1, "registered")]
+    for G, mode in modes:
         d = SRTPDispatcher(devices_for(G), check_replay=False, max_contexts=1 << 15,
                            max_factories=8, max_transformers=8)
-        seg = None
+        seg = hb = None
         try:
             k, s = keys
             snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=d))
             rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=d))
-            seg, ln = b.seg.copy(), b.length.copy()
-            if registered:  # a long-lived registered buffer pool: chunks DMA in place
-                host_register(seg)
+            ln = b.length.copy()
+            if mode == "pinned":  # the engine's pinned buffer pool: chunks DMA in place
+                hb = HostBuffer(b.seg.nbytes)
+                seg = hb.array
+                seg[:] = b.seg
+            else:
+                seg = b.seg.copy()
+                if mode == "registered":  # pageable memory registered once
+                    host_register(seg)
             for _ in range(2):  # warm: both directions once
                 d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
                 d.transform_host(True, rcv.tid, seg, b.off, ln, b.cap)
@@ -262,15 +270,18 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
             h1 = d.host_times()
             calls = max(h1["calls"] - h0["calls"], 1)
             per = {k2: round((h1[k2] - h0[k2]) / calls, 3) for k2 in h1 if k2 != "calls"}
-            out[str(G) if registered else f"{G}_copy"] = {
+            out[str(G) if mode == "pinned" else f"{G}_{mode}"] = {
                 "directional_pps": round(2 * bundles * n / dt, 1),
                 "ms_per_bundle": round(dt / (2 * bundles) * 1e3, 3),
                 "host_ms_per_bundle": per, "all_accepted": bool(ok),
-                "devices": sorted(set(devices_for(G))), "registered_segment": registered}
+                "devices": sorted(set(devices_for(G))), "segment": mode}
         finally:
             d.close()
-            if registered and seg is not None:
+            if mode == "registered" and seg is not None:
                 host_unregister(seg)
+            if hb is not None:
+                seg = None
+                hb.close()
     return out
 
 

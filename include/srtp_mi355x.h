@@ -308,6 +308,19 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
 int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                          int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes);
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
+/* srtp_pipeline_create with flags.  SRTP_PIPE_ONE_STREAM puts the copies on
+ * the engine's own stream instead of two copy streams of the pipeline's: a
+ * bundle's H2D, kernels and D2H then run in order with no cross-stream
+ * events.  For engines that share a GPU (several dispatcher shards or
+ * aggregator lanes on one device): every stream maps onto one of the device's
+ * few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and a queue that
+ * holds one engine's kernel waiting on its copy event stalls every other
+ * engine's work behind it.  Without the flag, bundles of up to 1 MB still
+ * copy on the engine's stream (their round trip is fixed costs, and two
+ * cross-stream events are among them); larger ones use the copy streams. */
+#define SRTP_PIPE_ONE_STREAM 0x1u
+int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes, int32_t depth,
+                            uint32_t flags, srtp_pipeline **out);
 /* srtp_pipeline_submit with the bundle's abort-on-throw chosen per bundle:
  * abort_on_error = -1 the engine's option, 1 SinglePacketTransformer's abort of
  * a throwing transformer's later packets (one RawPacket[] call), 0 none (every
@@ -324,7 +337,11 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
  * srtp_host_unregister takes the pointer that was registered, and the caller
  * must not unregister or free a range while a call uses it.
  * srtp_host_is_registered tells whether [ptr, ptr + bytes) lies inside one
- * registered range.  No reference API: the reference's packets are heap
+ * registered range.  srtp_host_alloc allocates such a range as pinned memory
+ * of the engine's own (hipHostMalloc; freed with srtp_host_free): the DMA
+ * engines read it at the full PCIe rate, while registered pageable memory of
+ * 4-KB pages may move slower.  A JVM would wrap it as a direct ByteBuffer
+ * (NewDirectByteBuffer).  No reference API: the reference's packets are heap
  * byte[]s copied by every JNI call (src/native/openssl/).
  *
  * srtp_pipeline_submit_host is srtp_pipeline_submit_ex with the segment read
@@ -336,6 +353,8 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
  * with no host copy at all. */
 int srtp_host_register(void *ptr, size_t bytes);
 int srtp_host_unregister(void *ptr);
+int srtp_host_alloc(size_t bytes, void **out);
+int srtp_host_free(void *ptr);
 int32_t srtp_host_is_registered(const void *ptr, size_t bytes);
 int srtp_pipeline_submit_host(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                               int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,

@@ -9,9 +9,9 @@ hand-written gfx950 kernels behind the C ABI in include/srtp_mi355x.h.
 from .srtp import (PacketTransformer, RawPacket, SRTCPTransformer, SRTPAggregator,  # noqa: F401
                    SRTPContextFactory, SRTPDispatcher,
                    SRTPEngine, SRTPPipeline, SRTPPolicy, SRTPTransformer, SRTPTransformException, pack,
-                   host_is_registered, host_register, host_unregister, profile_policies, transform_bundle)
+                   HostBuffer, host_is_registered, host_register, host_unregister, profile_policies, transform_bundle)
 from . import _native  # noqa: F401
 
 __all__ = ["PacketTransformer", "RawPacket", "SRTCPTransformer", "SRTPAggregator", "SRTPContextFactory", "SRTPDispatcher", "SRTPEngine",
            "SRTPPipeline", "SRTPPolicy", "SRTPTransformer", "SRTPTransformException", "pack", "profile_policies",
-           "transform_bundle", "host_register", "host_unregister", "host_is_registered"]
+           "transform_bundle", "host_register", "host_unregister", "host_is_registered", "HostBuffer"]

@@ -60,6 +60,7 @@ EXPORTED = [
     "srtp_dispatch_host_times", "srtp_pipeline_submit_ex", "srtp_aggregator_transform",
     "srtp_aggregator_transformer_info", "srtp_rawpacket_transform_one", "srtp_device_count",
     "srtp_host_register", "srtp_host_unregister", "srtp_host_is_registered", "srtp_pipeline_submit_host",
+    "srtp_pipeline_create_ex", "srtp_host_alloc", "srtp_host_free",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -185,7 +186,10 @@ def lib() -> C.CDLL:
     L.srtp_aggregator_transform.argtypes = [vp, i32, i32, vp, u32, u32, u32, u32, vp, pi32, pu32]
     L.srtp_aggregator_transformer_info.argtypes = [vp, i32, pi32, pi32]
     L.srtp_rawpacket_transform_one.argtypes = [vp, i32, i32, vp, u32, u32, pu32, u32, pi32, pu32, vp, u32]
+    L.srtp_pipeline_create_ex.argtypes = [vp, u32, C.c_size_t, i32, u32, C.POINTER(vp)]
     L.srtp_host_register.argtypes = [vp, C.c_size_t]
+    L.srtp_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+    L.srtp_host_free.argtypes = [vp]
     L.srtp_host_unregister.argtypes = [vp]
     L.srtp_host_is_registered.argtypes = [vp, C.c_size_t]
     L.srtp_host_is_registered.restype = i32

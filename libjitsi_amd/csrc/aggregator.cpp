@@ -646,11 +646,23 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
         return SRTP_ENOMEM;
     }
     for (uint32_t t = 0; t < a->n_kinds; t++) a->kinds[t].store(-2, std::memory_order_relaxed);
+    // lanes whose engines share a GPU keep each bundle on one stream (see
+    // SRTP_PIPE_ONE_STREAM): spread over the device's few hardware queues, the
+    // copy streams made every lane wait behind the others' copy events.  A lane
+    // alone on its GPU keeps them for large bundles (two in flight overlap);
+    // the pipeline puts small ones on the engine's stream by itself.
+    std::vector<int32_t> dev(n_lanes, -1);
+    for (size_t l = 0; l < n_lanes; l++) {
+        srtp_engine_opts lo;
+        if (srtp_engine_get_opts(engines[l], &lo) == SRTP_OK) dev[l] = lo.device;
+    }
     for (size_t l = 0; l < n_lanes; l++) {
         a->lanes.emplace_back(new Lane());
         Lane &ln = *a->lanes.back();
         ln.e = engines[l];
-        const int rc = srtp_pipeline_create(ln.e, o.max_packets, o.max_bytes, o.depth, &ln.pl);
+        const bool shared = std::count(dev.begin(), dev.end(), dev[l]) > 1;
+        const int rc = srtp_pipeline_create_ex(ln.e, o.max_packets, o.max_bytes, o.depth,
+                                               shared ? SRTP_PIPE_ONE_STREAM : 0u, &ln.pl);
         if (rc != SRTP_OK) {
             destroy_lanes(a);
             delete a;

@@ -60,9 +60,9 @@
 namespace {
 
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
-constexpr uint32_t kChunkPackets = 1u << 15;       // packets per pipeline slot
-constexpr size_t kChunkBytes = (size_t)32 << 20;   // segment bytes per pipeline slot
-constexpr int kDepth = 4;                          // pipeline slots per shard
+constexpr uint32_t kChunkPackets = 1u << 14;       // packets per pipeline slot
+constexpr size_t kChunkBytes = (size_t)24 << 20;   // segment bytes per pipeline slot
+constexpr int kDepth = 6;                          // pipeline slots per shard
 
 uint32_t mix32(uint32_t x) { // murmur3 fmix32 (libjitsi_amd/dispatch.py mix32)
     x ^= x >> 16;
@@ -119,6 +119,7 @@ static int32_t plan_bundle(int32_t n_shards, int32_t abort_on_error, int32_t rev
     for (uint32_t i = 0; i < n; i++) {
         const int32_t t = tids ? tids[i] : tid;
         const uint32_t fl = flags ? flags[i] : 0u;
+        if (i + 16 < n) __builtin_prefetch(seg + off[i + 16]); // the loop is bound by these misses
         may_throw[i] = 0;
         if ((fl & SRTP_PKT_FLAG_SKIP) || t < 0 || t >= n_transformers) {
             shard[i] = -1;
@@ -286,13 +287,13 @@ int dfail(srtp_dispatch *d, int code, const std::string &msg) {
 
 size_t region(uint32_t cap) { return ((size_t)cap + 15) & ~(size_t)15; }
 
-// Copies packets [j0, j1) of a chunk between a pipeline slot and the caller's
-// segment, one memcpy per run of packets that lie back to back in both (the
-// slot's are by construction; a one-shard bundle is then a single run): a
-// call per 1.2-KB packet costs as much as its bytes.
+// Copies packets [j0, j1) of a chunk (ch: their bundle indices) between a
+// pipeline slot and the caller's segment, one memcpy per run of packets that
+// lie back to back in both (the slot's are by construction; a one-shard
+// bundle is then a single run): a call per 1.2-KB packet costs as much as its
+// bytes.
 template <bool ToSlot>
-void copy_runs(const srtp_dispatch *d, const srtp_pipeline_slot &sl, const std::vector<uint32_t> &ch, size_t j0,
-               size_t j1) {
+void copy_runs(const srtp_dispatch *d, const srtp_pipeline_slot &sl, const uint32_t *ch, size_t j0, size_t j1) {
     for (size_t j = j0; j < j1;) {
         const uint32_t i = ch[j];
         size_t bytes = region(d->b_cap[i]);
@@ -316,10 +317,11 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         int rc = srtp_pipeline_slot_get(pl, k, &sl[k]);
         if (rc != SRTP_OK) return rc;
     }
-    std::vector<uint32_t> chunk_of[kDepth]; // global packet indices in each slot
+    size_t chunk_at[kDepth] = {0}, chunk_n[kDepth] = {0}; // each slot's packets: idx[at, at + n)
     int busy[kDepth] = {0};
     bool direct[kDepth] = {false}; // the chunk ran in place in the caller's registered segment
     int rc_all = SRTP_OK;
+    auto parts_for = [&](size_t nch) { return (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024); };
     auto drain = [&](int k) {
         if (!busy[k]) return;
         busy[k] = 0;
@@ -327,14 +329,14 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         const int rc = srtp_pipeline_wait(pl, k);
         const uint64_t ts = now_ns();
         d->t_wait += ts - tw;
-        const std::vector<uint32_t> &ch = chunk_of[k];
+        const uint32_t *ch = idx.data() + chunk_at[k];
+        const size_t nch = chunk_n[k];
         if (rc != SRTP_OK) {
             rc_all = rc;
-            for (uint32_t i : ch) d->b_status[i] = SRTP_STATUS_ERR_INTERNAL;
+            for (size_t j = 0; j < nch; j++) d->b_status[ch[j]] = SRTP_STATUS_ERR_INTERNAL;
             return;
         }
-        const size_t nch = ch.size();
-        const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
+        const int parts = parts_for(nch);
         d->pool->run(parts, [&](int q) {
             const size_t j0 = nch * q / parts, j1 = nch * (q + 1) / parts;
             for (size_t j = j0; j < j1; j++) {
@@ -351,46 +353,53 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
     while (pos < idx.size() && rc_all == SRTP_OK) {
         drain(k);
         if (rc_all != SRTP_OK) break;
-        std::vector<uint32_t> &ch = chunk_of[k];
-        ch.clear();
-        size_t bytes = 0;
-        bool contig = true; // the chunk's packets lie back to back in the caller's segment
         const uint64_t tp = now_ns();
-        while (pos < idx.size() && ch.size() < sl[k].max_packets) { // the chunk's layout
-            const uint32_t i = idx[pos];
+        // the chunk's extent and layout (offsets only: one pass over the caps)
+        const uint32_t *ch = idx.data() + pos;
+        const size_t room = std::min<size_t>(idx.size() - pos, sl[k].max_packets);
+        size_t bytes = 0, nch = 0;
+        bool contig = true; // the chunk's packets lie back to back in the caller's segment
+        for (; nch < room; nch++) {
+            const uint32_t i = ch[nch];
             const size_t r = region(d->b_cap[i]);
             if (bytes + r > sl[k].seg_cap) break;
-            if (!ch.empty() && d->b_off[i] != d->b_off[ch.back()] + region(d->b_cap[ch.back()])) contig = false;
-            const uint32_t j = (uint32_t)ch.size();
-            sl[k].off[j] = (uint32_t)bytes;
-            sl[k].len[j] = d->b_len[i];
-            sl[k].cap[j] = d->b_cap[i];
-            sl[k].flags[j] = d->b_flags ? d->b_flags[i] : 0u;
-            sl[k].tids[j] = d->b_tids ? d->b_tids[i] : d->b_tid;
+            if (nch && d->b_off[i] != d->b_off[ch[nch - 1]] + region(d->b_cap[ch[nch - 1]])) contig = false;
+            sl[k].off[nch] = (uint32_t)bytes;
             bytes += r;
-            ch.push_back(i);
-            pos++;
         }
-        if (ch.empty()) { // a packet larger than a slot (cannot happen: cap <= 65535)
+        if (nch == 0) { // a packet larger than a slot (cannot happen: cap <= 65535)
             rc_all = SRTP_EINVAL;
             break;
         }
+        chunk_at[k] = pos;
+        chunk_n[k] = nch;
+        pos += nch;
         // a registered segment whose chunk is one run: the DMA reads and
         // writes the caller's bytes in place; else the packet bytes go
-        // through the slot, split over the copy helpers
+        // through the slot.  Either way the per-packet arrays, and the copies,
+        // are split over the copy helpers.
         direct[k] = d->b_registered && contig;
-        if (!direct[k]) {
-            const size_t nch = ch.size();
-            const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
-            d->pool->run(parts, [&](int q) { copy_runs<true>(d, sl[k], ch, nch * q / parts, nch * (q + 1) / parts); });
+        {
+            const int parts = parts_for(nch);
+            d->pool->run(parts, [&](int q) {
+                const size_t j0 = nch * q / parts, j1 = nch * (q + 1) / parts;
+                for (size_t j = j0; j < j1; j++) {
+                    const uint32_t i = ch[j];
+                    sl[k].len[j] = d->b_len[i];
+                    sl[k].cap[j] = d->b_cap[i];
+                    sl[k].flags[j] = d->b_flags ? d->b_flags[i] : 0u;
+                    sl[k].tids[j] = d->b_tids ? d->b_tids[i] : d->b_tid;
+                }
+                if (!direct[k]) copy_runs<true>(d, sl[k], ch, j0, j1);
+            });
         }
         d->t_pack += now_ns() - tp;
-        const int rc = direct[k] ? srtp_pipeline_submit_host(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes, -1,
+        const int rc = direct[k] ? srtp_pipeline_submit_host(pl, k, reverse, 1, -1, 1, (uint32_t)nch, bytes, -1,
                                                              d->b_seg + d->b_off[ch[0]])
-                                 : srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)ch.size(), bytes);
+                                 : srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)nch, bytes);
         if (rc != SRTP_OK) {
             rc_all = rc;
-            for (uint32_t i : ch) d->b_status[i] = SRTP_STATUS_ERR_INTERNAL;
+            for (size_t j = 0; j < nch; j++) d->b_status[ch[j]] = SRTP_STATUS_ERR_INTERNAL;
             break;
         }
         busy[k] = 1;
@@ -541,7 +550,10 @@ int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_en
         if (rc != SRTP_OK) break;
         d->engines.push_back(e);
         srtp_pipeline *pl = nullptr;
-        rc = srtp_pipeline_create(e, kChunkPackets, kChunkBytes, kDepth, &pl);
+        // shards sharing a GPU: one stream each (SRTP_PIPE_ONE_STREAM); the
+        // other shards' chunks keep that GPU's copy engines and CUs busy
+        const bool shared = std::count(devices, devices + n_shards, devices[s]) > 1;
+        rc = srtp_pipeline_create_ex(e, kChunkPackets, kChunkBytes, kDepth, shared ? SRTP_PIPE_ONE_STREAM : 0u, &pl);
         if (rc != SRTP_OK) break;
         d->pipes.push_back(pl);
     }
@@ -649,12 +661,29 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     const int parts = (int)std::max<size_t>(1, std::min<size_t>((size_t)d->pool->size() + 1, (n + 16383) / 16384));
     std::vector<int32_t> plan_p((size_t)parts, 1);
     std::vector<uint32_t> cnt((size_t)parts * ns, 0u);
+    // a throw aborts its transformer's later packets across the shard's
+    // chunks only through the plan's rollback; one chunk needs no plan
+    const bool fast1 = ns == 1 && (!d->abort_on_error || (n <= kChunkPackets && seg_bytes <= kChunkBytes));
     d->pool->run(parts, [&](int q) {
         const uint32_t lo = (uint32_t)((uint64_t)n * q / parts), hi = (uint32_t)((uint64_t)n * (q + 1) / parts);
-        plan_p[(size_t)q] = srtp_dispatch_plan((int32_t)ns, d->abort_on_error, reverse, d->kinds.data(), nt,
-                                               d->tag_mask, tids ? tids + lo : nullptr, tid, seg, seg_bytes,
-                                               off + lo, len + lo, cap + lo, flags ? flags + lo : nullptr,
-                                               hi - lo, shard.data() + lo, mt.data() + lo);
+        if (fast1) {
+            // one shard and one chunk (or no abort-on-throw): the engine applies
+            // abort-on-throw itself, so no packet needs reading -- only the
+            // region checks and which packets run
+            int32_t r = 1;
+            for (uint32_t i = lo; i < hi; i++) {
+                if (off[i] % 16 != 0 || cap[i] > 65535u || (uint64_t)off[i] + region(cap[i]) > seg_bytes) r = SRTP_EINVAL;
+                const int32_t t = tids ? tids[i] : tid;
+                shard[i] = ((flags && (flags[i] & SRTP_PKT_FLAG_SKIP)) || t < 0 || t >= nt) ? -1 : 0;
+                mt[i] = 0;
+            }
+            plan_p[(size_t)q] = r;
+        } else {
+            plan_p[(size_t)q] = srtp_dispatch_plan((int32_t)ns, d->abort_on_error, reverse, d->kinds.data(), nt,
+                                                   d->tag_mask, tids ? tids + lo : nullptr, tid, seg, seg_bytes,
+                                                   off + lo, len + lo, cap + lo, flags ? flags + lo : nullptr,
+                                                   hi - lo, shard.data() + lo, mt.data() + lo);
+        }
         uint32_t *c = cnt.data() + (size_t)q * ns;
         for (uint32_t i = lo; i < hi; i++)
             if (shard[i] >= 0) c[shard[i]]++;

@@ -741,7 +741,9 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     e->ctl_cur = c ^ 1;
     {
         StageTimer t(e, s, SRTP_STAGE_SORT);
-        HIPCHK(e, launch_sort(a, ss, s));
+        // a one-tile bundle: one launch (SRTP_SORT_TILE=0: the multi-pass sort, for A/B)
+        static const bool tile_sort = !getenv("SRTP_SORT_TILE") || atoi(getenv("SRTP_SORT_TILE")) != 0;
+        HIPCHK(e, tile_sort && n <= sort_tile_records() ? launch_sort_tile(a, s) : launch_sort(a, ss, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);
@@ -1196,7 +1198,11 @@ extern "C" {
 // ------------------------------------------------- registered host memory
 namespace {
 std::mutex g_reg_mu;
-std::map<uintptr_t, size_t> g_reg; // start -> bytes, disjoint
+struct RegRange {
+    size_t bytes;
+    bool owned; // srtp_host_alloc's (hipHostMalloc) rather than registered caller memory
+};
+std::map<uintptr_t, RegRange> g_reg; // start -> range, disjoint
 } // namespace
 
 int srtp_host_register(void *ptr, size_t bytes) {
@@ -1206,19 +1212,41 @@ int srtp_host_register(void *ptr, size_t bytes) {
     std::lock_guard<std::mutex> g(g_reg_mu);
     auto it = g_reg.upper_bound(a);
     if (it != g_reg.end() && it->first < a + bytes) return SRTP_EINVAL;
-    if (it != g_reg.begin() && std::prev(it)->first + std::prev(it)->second > a) return SRTP_EINVAL;
+    if (it != g_reg.begin() && std::prev(it)->first + std::prev(it)->second.bytes > a) return SRTP_EINVAL;
     if (hipHostRegister(ptr, bytes, hipHostRegisterPortable) != hipSuccess) {
         (void)hipGetLastError();
         return SRTP_EDEVICE;
     }
-    g_reg[a] = bytes;
+    g_reg[a] = RegRange{bytes, false};
     return SRTP_OK;
+}
+
+int srtp_host_alloc(size_t bytes, void **out) {
+    if (!out || bytes == 0) return SRTP_EINVAL;
+    *out = nullptr;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        return SRTP_ENOMEM;
+    }
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    g_reg[(uintptr_t)p] = RegRange{bytes, true};
+    *out = p;
+    return SRTP_OK;
+}
+
+int srtp_host_free(void *ptr) {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_reg.find((uintptr_t)ptr);
+    if (it == g_reg.end() || !it->second.owned) return SRTP_EINVAL;
+    g_reg.erase(it);
+    return hipHostFree(ptr) == hipSuccess ? SRTP_OK : SRTP_EDEVICE;
 }
 
 int srtp_host_unregister(void *ptr) {
     std::lock_guard<std::mutex> g(g_reg_mu);
     auto it = g_reg.find((uintptr_t)ptr);
-    if (it == g_reg.end()) return SRTP_EINVAL;
+    if (it == g_reg.end() || it->second.owned) return SRTP_EINVAL;
     g_reg.erase(it);
     if (hipHostUnregister(ptr) != hipSuccess) {
         (void)hipGetLastError();
@@ -1234,7 +1262,7 @@ int32_t srtp_host_is_registered(const void *ptr, size_t bytes) {
     auto it = g_reg.upper_bound(a);
     if (it == g_reg.begin()) return 0;
     --it;
-    return a + bytes <= it->first + it->second ? 1 : 0;
+    return a + bytes <= it->first + it->second.bytes ? 1 : 0;
 }
 
 } // extern "C"
@@ -1245,6 +1273,7 @@ struct srtp_pipeline {
     uint32_t max_n = 0;
     size_t max_seg = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
+    bool one_stream = false; // SRTP_PIPE_ONE_STREAM: copies on the engine's stream (s_in / s_out not owned)
     std::mutex mu;
     struct Slot {
         srtp_pipeline_slot h{};     // pinned host arrays
@@ -1266,6 +1295,7 @@ struct srtp_pipeline {
 };
 
 constexpr uint32_t kPackMax = 8192; // bundles up to this many packets use the packed copies
+constexpr size_t kOneStreamBytes = (size_t)1 << 20; // bundles up to this size copy on the engine's stream
 
 static void pipeline_free(srtp_pipeline *pl) {
     DeviceGuard guard(pl->e->opts.device);
@@ -1281,8 +1311,8 @@ static void pipeline_free(srtp_pipeline *pl) {
         for (auto x : ev)
             if (x) (void)hipEventDestroy(x);
     }
-    if (pl->s_in) (void)hipStreamDestroy(pl->s_in);
-    if (pl->s_out) (void)hipStreamDestroy(pl->s_out);
+    if (pl->s_in && !pl->one_stream) (void)hipStreamDestroy(pl->s_in);
+    if (pl->s_out && !pl->one_stream) (void)hipStreamDestroy(pl->s_out);
     delete pl;
 }
 
@@ -1292,7 +1322,13 @@ template <class T> static hipError_t halloc(T **p, size_t count) {
 
 int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes,
                          int32_t depth, srtp_pipeline **out) {
-    if (!e || !out || depth < 1 || depth > 16 || max_packets == 0 || max_packets > kRecIdxMask)
+    return srtp_pipeline_create_ex(e, max_packets, max_seg_bytes, depth, 0u, out);
+}
+
+int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes, int32_t depth,
+                            uint32_t flags, srtp_pipeline **out) {
+    if (!e || !out || depth < 1 || depth > 16 || max_packets == 0 || max_packets > kRecIdxMask ||
+        (flags & ~(uint32_t)SRTP_PIPE_ONE_STREAM))
         return SRTP_EINVAL;
     *out = nullptr;
     srtp_pipeline *pl = new (std::nothrow) srtp_pipeline();
@@ -1302,8 +1338,10 @@ int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_by
     pl->max_seg = (max_seg_bytes + 15) & ~(size_t)15;
     pl->slots.resize((size_t)depth);
     DeviceGuard guard(e->opts.device);
-    bool ok = guard.ok && hipStreamCreateWithFlags(&pl->s_in, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&pl->s_out, hipStreamNonBlocking) == hipSuccess;
+    pl->one_stream = (flags & SRTP_PIPE_ONE_STREAM) != 0;
+    if (pl->one_stream) pl->s_in = pl->s_out = e->stream;
+    bool ok = guard.ok && (pl->one_stream || (hipStreamCreateWithFlags(&pl->s_in, hipStreamNonBlocking) == hipSuccess &&
+                                              hipStreamCreateWithFlags(&pl->s_out, hipStreamNonBlocking) == hipSuccess));
     for (auto &sl : pl->slots) {
         if (!ok) break;
         const size_t n = max_packets;
@@ -1383,7 +1421,10 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
     if (rc != SRTP_OK) return rc;
     if (!use_tids && (tid < 0 || (size_t)tid >= e->transformers.size()))
         return fail(e, SRTP_EINVAL, "bad transformer id");
-    hipStream_t si = pl->s_in, so = pl->s_out, s = e->stream;
+    // a small bundle's copies go on the engine's stream: their fixed cost, not
+    // their bytes, is its round trip, and two cross-stream events add to it
+    const bool one = pl->one_stream || seg_bytes <= kOneStreamBytes;
+    hipStream_t s = e->stream, si = one ? s : pl->s_in, so = one ? s : pl->s_out;
     const int32_t abort = abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0);
     if (!hseg) hseg = sl.h.seg;
     HIPCHK(e, hipMemcpyAsync(sl.d_seg, hseg, seg_bytes, hipMemcpyHostToDevice, si));
@@ -1396,15 +1437,19 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
         if (use_tids) memcpy(hp + 3 * (size_t)n, sl.h.tids, n4);
         memcpy(hp + 4 * (size_t)n, sl.h.len, n4);
         HIPCHK(e, hipMemcpyAsync(dp, hp, 5 * n4, hipMemcpyHostToDevice, si));
-        HIPCHK(e, hipEventRecord(sl.ev_in, si));
-        HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+        if (si != s) {
+            HIPCHK(e, hipEventRecord(sl.ev_in, si));
+            HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+        }
         sl.rc = transform_locked(e, reverse, use_tids ? reinterpret_cast<int32_t *>(dp + 3 * (size_t)n) : nullptr,
                                  tid, sl.d_seg, dp, dp + 4 * (size_t)n, dp + n,
                                  use_flags ? dp + 2 * (size_t)n : nullptr,
                                  reinterpret_cast<int32_t *>(dp + 5 * (size_t)n), n, s, abort);
         if (sl.rc != SRTP_OK) return sl.rc;
-        HIPCHK(e, hipEventRecord(sl.ev_done, s));
-        HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+        if (so != s) {
+            HIPCHK(e, hipEventRecord(sl.ev_done, s));
+            HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+        }
         HIPCHK(e, hipMemcpyAsync(hseg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
         HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, 2 * n4, hipMemcpyDeviceToHost, so));
         sl.packed_n = n;
@@ -1414,13 +1459,17 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
         HIPCHK(e, hipMemcpyAsync(sl.d_cap, sl.h.cap, n * 4ull, hipMemcpyHostToDevice, si));
         if (use_flags) HIPCHK(e, hipMemcpyAsync(sl.d_flags, sl.h.flags, n * 4ull, hipMemcpyHostToDevice, si));
         if (use_tids) HIPCHK(e, hipMemcpyAsync(sl.d_tids, sl.h.tids, n * 4ull, hipMemcpyHostToDevice, si));
-        HIPCHK(e, hipEventRecord(sl.ev_in, si));
-        HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+        if (si != s) {
+            HIPCHK(e, hipEventRecord(sl.ev_in, si));
+            HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+        }
         sl.rc = transform_locked(e, reverse, use_tids ? sl.d_tids : nullptr, tid, sl.d_seg, sl.d_off,
                                  sl.d_len, sl.d_cap, use_flags ? sl.d_flags : nullptr, sl.d_status, n, s, abort);
         if (sl.rc != SRTP_OK) return sl.rc;
-        HIPCHK(e, hipEventRecord(sl.ev_done, s));
-        HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+        if (so != s) {
+            HIPCHK(e, hipEventRecord(sl.ev_done, s));
+            HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+        }
         HIPCHK(e, hipMemcpyAsync(hseg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
         HIPCHK(e, hipMemcpyAsync(sl.h.len, sl.d_len, n * 4ull, hipMemcpyDeviceToHost, so));
         HIPCHK(e, hipMemcpyAsync(sl.h.status, sl.d_status, n * 4ull, hipMemcpyDeviceToHost, so));

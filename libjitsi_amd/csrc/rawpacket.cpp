@@ -43,7 +43,7 @@ struct srtp_rawpacket_batch {
     srtp_pipeline *pl = nullptr;
     uint32_t pl_packets = 0;
     size_t pl_bytes = 0;
-    // dispatch-mode staging: a segment registered for DMA (srtp_host_register),
+    // dispatch-mode staging: a segment registered for DMA (srtp_host_alloc),
     // so the dispatcher's shards move it in place, with no second copy
     uint8_t *seg = nullptr;
     size_t seg_cap = 0;
@@ -69,8 +69,8 @@ srtp_engine *engine_of(const srtp_rawpacket_batch *b) {
 }
 
 void release_seg(srtp_rawpacket_batch *b) {
-    if (b->seg_registered) (void)srtp_host_unregister(b->seg);
-    free(b->seg);
+    if (b->seg_registered) (void)srtp_host_free(b->seg);
+    else free(b->seg);
     b->seg = nullptr;
     b->seg_cap = 0;
     b->seg_registered = false;
@@ -85,7 +85,8 @@ int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
             b->pl = nullptr;
             const uint32_t np = std::max<uint32_t>(std::max<uint32_t>(n, 64), b->pl_packets * 2);
             const size_t nb = std::max<size_t>(std::max<size_t>(bytes, (size_t)1 << 16), b->pl_bytes * 2);
-            const int rc = srtp_pipeline_create(b->e, np, nb, 1, &b->pl);
+            // one synchronous bundle at a time: no copy streams to overlap
+            const int rc = srtp_pipeline_create_ex(b->e, np, nb, 1, SRTP_PIPE_ONE_STREAM, &b->pl);
             if (rc != SRTP_OK) return rc;
             b->pl_packets = np;
             b->pl_bytes = nb;
@@ -100,11 +101,13 @@ int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
             release_seg(b);
             const size_t nb = (std::max<size_t>(std::max<size_t>(bytes, (size_t)1 << 20), 2 * b->seg_cap) + 4095) &
                               ~(size_t)4095;
-            b->seg = static_cast<uint8_t *>(aligned_alloc(4096, nb));
+            // pinned memory of the engine's (srtp_host_alloc): the shards' DMA
+            // moves it in place; without it (a pinning limit) copies do
+            void *p = nullptr;
+            b->seg_registered = srtp_host_alloc(nb, &p) == SRTP_OK;
+            b->seg = static_cast<uint8_t *>(b->seg_registered ? p : aligned_alloc(4096, nb));
             if (!b->seg) return SRTP_ENOMEM;
             b->seg_cap = nb;
-            // unregistered (no device, a pinning limit) it still works, by copies
-            b->seg_registered = srtp_host_register(b->seg, nb) == SRTP_OK;
         }
         try {
             b->off.resize(n); b->len.resize(n); b->cap.resize(n); b->flags.resize(n);

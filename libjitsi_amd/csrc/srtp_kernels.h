@@ -100,6 +100,9 @@ SortScratch sort_scratch(void *temp, uint32_t n_max);
 // Stable LSD radix sort of (sk_in, sv_in) by key into (sk_out, sv_out),
 // a.sort_passes passes of 8 bits; zeroes the other parity's histograms.
 hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s);
+// the whole sort of a bundle of at most sort_tile_records() packets in one
+// workgroup (one launch)
+hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s);
 // unprotect: fused tag check + speculative in-place decryption (before the walk)
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
 // Engines with Skein-MAC key sets.  Unprotect: those packets' tag check under

@@ -33,7 +33,10 @@
 // and HMAC midstates are wave-uniform SGPRs; SHA-1 runs per lane with
 // v_alignbit rotates.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 
 #include "../../include/srtp_mi355x.h"
@@ -1026,6 +1029,63 @@ struct SortPass {
     const uint32_t *cls_tile;
 };
 
+// The crypto kernels' lane order (first sort pass): this tile's packets by
+// length class, at the class bases (longest first) plus a reserved range --
+// when the bundle has more than one class (k_parse's per-tile masks).  s_cb
+// (32 words) and s_run (97) are LDS the caller no longer needs.
+__device__ __forceinline__ void write_lord(uint32_t n, uint32_t tiles, uint32_t tile, uint32_t base,
+                                           const uint32_t *len, BundleCtl *ctl, const uint32_t *cls_tile,
+                                           uint32_t *lord, uint32_t *s_cb, uint32_t *s_run) {
+    const int t = threadIdx.x;
+    uint32_t *s_cc = s_run, *s_co = s_run + 32, *s_tot = s_run + 64;
+    if (t < 64) {
+        uint32_t m = 0u;
+        for (uint32_t u = (uint32_t)t; u < tiles; u += 64u) m |= cls_tile[u * kClsWords + 32];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o);
+        if (t == 0) {
+            s_run[96] = m;
+            if (tile == 0u) ctl->len_classes = m; // read by the crypto kernels' lane_packet
+        }
+    }
+    __syncthreads();
+    // one class: lane = packet.  Class 0 (length 0: a bundle former's holes,
+    // null elements) runs no crypto and does not count.
+    if (__popc(s_run[96] & ~1u) <= 1) return;
+    if (t < 32) {
+        uint32_t tot = 0u;
+        for (uint32_t u = 0u; u < tiles; u++) tot += cls_tile[u * kClsWords + t];
+        s_tot[t] = tot;
+        s_cc[t] = 0u;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0u;
+        for (int c = 31; c >= 0; c--) {
+            s_cb[c] = acc;
+            acc += s_tot[c];
+        }
+    }
+    __syncthreads();
+    uint32_t cls[kSortItems], rk[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < n) {
+            cls[r] = len_class(len[i]);
+            rk[r] = atomicAdd(&s_cc[cls[r]], 1u);
+        }
+    }
+    __syncthreads();
+    if (t < 32 && s_cc[t]) s_co[t] = atomicAdd(&ctl->cls_cursor[t], s_cc[t]);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = base + r * kSortThreads + t;
+        if (i < n) lord[s_cb[cls[r]] + s_co[cls[r]] + rk[r]] = i;
+    }
+}
+
 #ifndef SRTP_SORT_COUNT_LOADS
 #define SRTP_SORT_COUNT_LOADS 64
 #endif
@@ -1132,57 +1192,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
         }
     }
     if (SRTP_LEN_ORDER && sp.lord) {
-        // the lane order of the crypto kernels: this tile's packets by length
-        // class, at the class bases (longest first) plus a reserved range --
-        // when the bundle has more than one class (k_parse's per-tile masks)
         __syncthreads(); // s_base / s_run / s_wcnt are free again
-        uint32_t *s_cb = s_base, *s_cc = s_run, *s_co = s_run + 32, *s_tot = s_run + 64;
-        if (t < 64) {
-            uint32_t m = 0u;
-            for (uint32_t u = (uint32_t)t; u < sp.tiles; u += 64u) m |= sp.cls_tile[u * kClsWords + 32];
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o);
-            if (t == 0) {
-                s_run[96] = m;
-                if (tile == 0u) sp.ctl->len_classes = m; // read by the crypto kernels' lane_packet
-            }
-        }
-        __syncthreads();
-        // one class: lane = packet.  Class 0 (length 0: a bundle former's holes,
-        // null elements) runs no crypto and does not count.
-        if (__popc(s_run[96] & ~1u) <= 1) return;
-        if (t < 32) {
-            uint32_t tot = 0u;
-            for (uint32_t u = 0u; u < sp.tiles; u++) tot += sp.cls_tile[u * kClsWords + t];
-            s_tot[t] = tot;
-            s_cc[t] = 0u;
-        }
-        __syncthreads();
-        if (t == 0) {
-            uint32_t acc = 0u;
-            for (int c = 31; c >= 0; c--) {
-                s_cb[c] = acc;
-                acc += s_tot[c];
-            }
-        }
-        __syncthreads();
-        uint32_t cls[kSortItems], rk[kSortItems];
-#pragma unroll
-        for (int r = 0; r < kSortItems; r++) {
-            const uint32_t i = base + r * kSortThreads + t;
-            if (i < sp.n) {
-                cls[r] = len_class(sp.len[i]);
-                rk[r] = atomicAdd(&s_cc[cls[r]], 1u);
-            }
-        }
-        __syncthreads();
-        if (t < 32 && s_cc[t]) s_co[t] = atomicAdd(&sp.ctl->cls_cursor[t], s_cc[t]);
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < kSortItems; r++) {
-            const uint32_t i = base + r * kSortThreads + t;
-            if (i < sp.n) sp.lord[s_cb[cls[r]] + s_co[cls[r]] + rk[r]] = i;
-        }
+        write_lord(sp.n, sp.tiles, tile, base, sp.len, sp.ctl, sp.cls_tile, sp.lord, s_base, s_run);
     }
 }
 
@@ -1357,51 +1368,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter_wide(SortPassWide
     }
     if (SRTP_LEN_ORDER && sp.lord) { // as k_sort_scatter (first pass only)
         __syncthreads();
-        uint32_t *s_cb = s_base, *s_cc = s_run, *s_co = s_run + 32, *s_tot = s_run + 64;
-        if (t < 64) {
-            uint32_t m = 0u;
-            for (uint32_t u = (uint32_t)t; u < sp.tiles; u += 64u) m |= sp.cls_tile[u * kClsWords + 32];
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) m |= (uint32_t)__shfl_xor((int)m, o);
-            if (t == 0) {
-                s_run[96] = m;
-                if (tile == 0u) sp.ctl->len_classes = m;
-            }
-        }
-        __syncthreads();
-        if (__popc(s_run[96] & ~1u) <= 1) return;
-        if (t < 32) {
-            uint32_t tot = 0u;
-            for (uint32_t u = 0u; u < sp.tiles; u++) tot += sp.cls_tile[u * kClsWords + t];
-            s_tot[t] = tot;
-            s_cc[t] = 0u;
-        }
-        __syncthreads();
-        if (t == 0) {
-            uint32_t acc = 0u;
-            for (int c = 31; c >= 0; c--) {
-                s_cb[c] = acc;
-                acc += s_tot[c];
-            }
-        }
-        __syncthreads();
-        uint32_t cls[kSortItems], rk[kSortItems];
-#pragma unroll
-        for (int r = 0; r < kSortItems; r++) {
-            const uint32_t i = base + r * kSortThreads + t;
-            if (i < sp.n) {
-                cls[r] = len_class(sp.len[i]);
-                rk[r] = atomicAdd(&s_cc[cls[r]], 1u);
-            }
-        }
-        __syncthreads();
-        if (t < 32 && s_cc[t]) s_co[t] = atomicAdd(&sp.ctl->cls_cursor[t], s_cc[t]);
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < kSortItems; r++) {
-            const uint32_t i = base + r * kSortThreads + t;
-            if (i < sp.n) sp.lord[s_cb[cls[r]] + s_co[cls[r]] + rk[r]] = i;
-        }
+        write_lord(sp.n, sp.tiles, tile, base, sp.len, sp.ctl, sp.cls_tile, sp.lord, s_base, s_run);
     }
 }
 
@@ -1433,6 +1400,131 @@ hipError_t launch_sort_wide(const BundleArgs &a, const SortScratch &ss, hipStrea
         sp.cls_tile = a.cls_tile;
         hipLaunchKernelGGL(k_sort_scatter_wide, dim3(tiles), dim3(kSortThreads), 0, s, sp);
     }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------ one-tile bundles
+// A bundle of at most one sort tile (the per-packet path's small bundles: a
+// few to a few hundred packets) is sorted by one workgroup in LDS, every
+// 8-bit digit in turn -- one launch, where the multi-pass sort takes a
+// scatter launch per digit plus count / prefix launches (five for the wide
+// sort), each costing more than the sorting at this size.  Same output: the
+// records stable by key, spos as the last pass writes it, lord as the first.
+// It zeroes the tile's first-digit counts that k_parse accumulated (the walk
+// clears the other tables as after a multi-pass sort).
+__global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32_t key_bits, uint32_t bins) {
+    constexpr int W = kSortThreads / 64;
+    __shared__ uint32_t s_key[2][kSortTile];
+    __shared__ uint16_t s_idx[2][kSortTile];
+    __shared__ uint32_t s_base[256], s_run[256], s_wcnt[W][256];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t n = a.n;
+    for (uint32_t d = (uint32_t)t; d < bins; d += kSortThreads) a.sort_counts[d] = 0u;
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = r * kSortThreads + t;
+        if (i < n) {
+            s_key[0][i] = a.sk_in[i];
+            s_idx[0][i] = (uint16_t)i;
+        }
+    }
+    const int passes = (int)((key_bits + 7u) / 8u);
+    for (int q = 0; q < passes; q++) {
+        const int cur = q & 1;
+        const uint32_t shift = 8u * (uint32_t)q;
+        if (t < 256) {
+            s_run[t] = 0u;
+#pragma unroll
+            for (int k = 0; k < W; k++) s_wcnt[k][t] = 0u;
+        }
+        __syncthreads();
+        uint32_t key[kSortItems], loc[kSortItems];
+        uint16_t idx[kSortItems];
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            const uint32_t i = r * kSortThreads + t;
+            key[r] = i < n ? s_key[cur][i] : 0u;
+            idx[r] = i < n ? s_idx[cur][i] : (uint16_t)0;
+        }
+        // stable ranks within each digit, items in index order (k_sort_scatter's)
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            const bool valid = r * kSortThreads + t < (int)n;
+            const uint32_t d = valid ? (key[r] >> shift) & 255u : 0u;
+            unsigned long long m = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; bit++) {
+                const unsigned long long b = __ballot((d >> bit) & 1u);
+                m &= ((d >> bit) & 1u) ? b : ~b;
+            }
+            const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (valid && below == 0u) s_wcnt[w][d] = (uint32_t)__popcll(m);
+            __syncthreads();
+            if (valid) {
+                uint32_t pre = s_run[d];
+                for (int k = 0; k < w; k++) pre += s_wcnt[k][d];
+                loc[r] = pre + below;
+            }
+            __syncthreads();
+            if (t < 256) {
+                uint32_t add = 0u;
+#pragma unroll
+                for (int k = 0; k < W; k++) { add += s_wcnt[k][t]; s_wcnt[k][t] = 0u; }
+                s_run[t] += add;
+            }
+            __syncthreads();
+        }
+        // digit bases: exclusive scan of the digit totals (4 waves x 64 digits)
+        if (t < 256) {
+            const uint32_t c = s_run[t];
+            uint32_t x = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) s_wcnt[0][w] = x;
+            s_base[t] = x - c;
+        }
+        __syncthreads();
+        if (t < 256) {
+            uint32_t off = 0u;
+            for (int k = 0; k < w; k++) off += s_wcnt[0][k];
+            s_base[t] += off;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSortItems; r++) {
+            if (r * kSortThreads + t < (int)n) {
+                const uint32_t np = s_base[(key[r] >> shift) & 255u] + loc[r];
+                s_key[cur ^ 1][np] = key[r];
+                s_idx[cur ^ 1][np] = idx[r];
+            }
+        }
+        __syncthreads();
+    }
+    const int fin = passes & 1;
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t pos = r * kSortThreads + t;
+        if (pos < n) {
+            const uint32_t key = s_key[fin][pos];
+            const WalkRec rec = a.sv_in[s_idx[fin][pos]];
+            a.sk_out[pos] = key;
+            a.sv_out[pos] = rec;
+            if (a.reverse && key <= a.ctx_mask) a.spos[rec.p & kRecIdxMask] = pos;
+        }
+    }
+    if (SRTP_LEN_ORDER) {
+        __syncthreads();
+        write_lord(n, 1u, 0u, 0u, a.len, a.ctl, a.cls_tile, a.lord, s_base, s_run);
+    }
+}
+
+hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s) {
+    const uint32_t wide = a.sort_bits > 8;
+    const uint32_t key_bits = wide ? 2u * (uint32_t)a.sort_bits : 8u * (uint32_t)a.sort_passes;
+    const uint32_t bins = 1u << a.sort_bits;
+    hipLaunchKernelGGL(k_sort_tile, dim3(1), dim3(kSortThreads), 0, s, a, key_bits, bins);
     return hipGetLastError();
 }
 
@@ -4442,9 +4534,32 @@ hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
         hipLaunchKernelGGL(k_parse<256>, dim3((a.n + kParseBlock - 1) / kParseBlock), dim3(kParseBlock), 0, s, a);
     return hipGetLastError();
 }
+// Workgroup size of the AES kernels for a bundle of n packets.  A workgroup
+// holds the 128-KB T-table image, so a CU runs one at a time, and its waves
+// share the CU's four SIMDs: 16 waves per CU give the best throughput on a
+// full bundle, but a small bundle (the per-packet path's, an aggregator lane's)
+// packed 16 waves to a CU finishes in the time of its few busy CUs while the
+// rest idle.  So the waves are spread over every CU, at least 4 per
+// workgroup (one per SIMD: the image is filled by the workgroup's threads)
+// and at most max_block / 64.  A full bundle (2^18 packets = 16 waves per CU)
+// keeps 1024-thread workgroups.  SRTP_AES_SPREAD=0: always max_block (A/B).
+static uint32_t aes_block(uint32_t n, uint32_t max_block) {
+    static const bool spread = !getenv("SRTP_AES_SPREAD") || atoi(getenv("SRTP_AES_SPREAD")) != 0;
+    static int cus[64];
+    int dev = 0;
+    if (!spread || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return max_block;
+    if (cus[dev] <= 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return max_block;
+        cus[dev] = c;
+    }
+    const uint32_t waves = (n + 63u) / 64u, per_cu = (waves + (uint32_t)cus[dev] - 1u) / (uint32_t)cus[dev];
+    return 64u * std::min<uint32_t>(max_block / 64u, std::max<uint32_t>(4u, per_cu));
+}
+
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_unprotect, dim3((a.n + kUnprotectBlock - 1) / kUnprotectBlock),
-                       dim3(kUnprotectBlock), 0, s, a);
+    const uint32_t b = aes_block(a.n, (uint32_t)kUnprotectBlock);
+    hipLaunchKernelGGL(k_unprotect, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_skein(const BundleArgs &a, hipStream_t s) {
@@ -4468,7 +4583,8 @@ hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(k_protect, dim3((a.n + kAesBlock - 1) / kAesBlock), dim3(kAesBlock), 0, s, a);
+    const uint32_t b = aes_block(a.n, (uint32_t)kAesBlock);
+    hipLaunchKernelGGL(k_protect, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {

@@ -360,6 +360,30 @@ def host_unregister(arr: np.ndarray) -> None:
     N.check(N.lib().srtp_host_unregister(arr.ctypes.data), None, "srtp_host_unregister")
 
 
+class HostBuffer:
+    """Pinned host memory of the engine's own (srtp_host_alloc), registered for
+    in-place DMA like host_register's, at the full PCIe rate: ``array`` is a
+    uint8 view of it.  close() frees it; no view may be used afterwards."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        N.check(N.lib().srtp_host_alloc(int(nbytes), C.byref(p)), None, "srtp_host_alloc")
+        self._p = p
+        self.array = np.ctypeslib.as_array((C.c_uint8 * int(nbytes)).from_address(p.value))
+
+    def close(self):
+        if self._p:
+            self.array = None
+            N.check(N.lib().srtp_host_free(self._p), None, "srtp_host_free")
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def host_is_registered(arr: np.ndarray) -> bool:
     return bool(N.lib().srtp_host_is_registered(arr.ctypes.data, arr.nbytes))
 

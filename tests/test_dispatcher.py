@@ -259,10 +259,12 @@ def test_dispatch_registered_segment_in_place(oracle, shards):
         seg[o[1000] + 20] ^= 1      # forged
         seg[o[40000] + 30] ^= 0x80  # forged, in a later chunk
         twin.run(rcv, True, seg, b.off, ln, b.cap)
-        # throws: the rollback restores stashed bytes into the registered segment
-        b2 = synth.rtp_bundle(3000, 40, (40, 700), seed=83)
+        # throws: a throw aborts its transformer's packets in later chunks too
+        # (2^14-packet chunks), and the rollback restores stashed bytes into
+        # the registered segment
+        b2 = synth.rtp_bundle(40000, 40, (40, 300), seed=83)
         o2 = b2.off.astype(np.int64)
-        for i in (200, 1500):
+        for i in (200, 20000):
             b2.seg[o2[i]] = 0x9F
         _, _, st2 = twin.run(snd, False, b2.seg, b2.off, b2.length, b2.cap)
         assert (st2 == N.STATUS_ERR_MALFORMED).any() and (st2 == N.STATUS_NOT_PROCESSED).any()

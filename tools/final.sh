@@ -26,4 +26,7 @@ t keysets1000 180 python bench.py --steps 20 --keysets 1000 --no-cpu --no-e2e --
 t ssrcs100k 180 python bench.py --steps 20 --ssrcs 100000 --no-cpu --no-e2e --no-dispatch
 t sync_bench 300 ./tools/sync_bench 2
 t agg_bench 120 ./tools/agg_bench 1.5
+# --gpus 8 without torchrun: one process per side, all on device 0 here (gloo
+# for the timing reductions); host enqueue per step is in each line
+t rehearsal8 300 env SRTP_BENCH_ONE_DEVICE=1 python bench.py --gpus 8 --backend gloo --steps 20 --no-cpu --no-e2e --no-dispatch
 TAG=${TAG:-final}/prof ./tools/prof.sh
