@@ -60,9 +60,9 @@
 namespace {
 
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
-constexpr uint32_t kChunkPackets = 1u << 14;       // packets per pipeline slot
-constexpr size_t kChunkBytes = (size_t)24 << 20;   // segment bytes per pipeline slot
-constexpr int kDepth = 6;                          // pipeline slots per shard
+constexpr uint32_t kChunkPackets = 1u << 15;       // packets per pipeline slot
+constexpr size_t kChunkBytes = (size_t)48 << 20;   // segment bytes per pipeline slot
+constexpr int kDepth = 4;                          // pipeline slots per shard
 
 uint32_t mix32(uint32_t x) { // murmur3 fmix32 (libjitsi_amd/dispatch.py mix32)
     x ^= x >> 16;

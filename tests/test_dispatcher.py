@@ -260,7 +260,7 @@ def test_dispatch_registered_segment_in_place(oracle, shards):
         seg[o[40000] + 30] ^= 0x80  # forged, in a later chunk
         twin.run(rcv, True, seg, b.off, ln, b.cap)
         # throws: a throw aborts its transformer's packets in later chunks too
-        # (2^14-packet chunks), and the rollback restores stashed bytes into
+        # (2^15-packet chunks), and the rollback restores stashed bytes into
         # the registered segment
         b2 = synth.rtp_bundle(40000, 40, (40, 300), seed=83)
         o2 = b2.off.astype(np.int64)

@@ -29,4 +29,5 @@ t agg_bench 120 ./tools/agg_bench 1.5
 # --gpus 8 without torchrun: one process per side, all on device 0 here (gloo
 # for the timing reductions); host enqueue per step is in each line
 t rehearsal8 300 env SRTP_BENCH_ONE_DEVICE=1 python bench.py --gpus 8 --backend gloo --steps 20 --no-cpu --no-e2e --no-dispatch
-TAG=${TAG:-final}/prof ./tools/prof.sh
+[ -n "$PROF" ] && TAG=${TAG:-final}/prof ./tools/prof.sh
+echo final done
