@@ -5,10 +5,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <stdlib.h>
@@ -1385,10 +1387,28 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
     return SRTP_OK;
 }
 
+// How a pipeline waits for a bundle (SRTP_PIPE_WAIT_US): < 0 (default)
+// hipEventSynchronize; >= 0 polls hipEventQuery, yielding the CPU between
+// polls, and after that many microseconds sleeps 20 us between polls -- so
+// many lane threads waiting at once (an aggregator lane per shard) leave the
+// host's cores to the producers.
+static int wait_event(hipEvent_t ev) {
+    static const long spin_us = getenv("SRTP_PIPE_WAIT_US") ? atol(getenv("SRTP_PIPE_WAIT_US")) : -1;
+    if (spin_us < 0) return hipEventSynchronize(ev) == hipSuccess ? 0 : -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return 0;
+        if (q != hipErrorNotReady) return -1;
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 static int pipeline_wait_locked(srtp_pipeline *pl, srtp_pipeline::Slot &sl) {
     if (!sl.busy) return SRTP_OK;
     sl.busy = false;
-    if (hipEventSynchronize(sl.ev_out) != hipSuccess) return fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
+    if (wait_event(sl.ev_out) != 0) return fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
     if (const uint32_t n = sl.packed_n) { // lengths and statuses to the slot's own arrays
         memcpy(sl.h.len, sl.h_pack + 4 * (size_t)n, n * 4ull);
         memcpy(sl.h.status, sl.h_pack + 5 * (size_t)n, n * 4ull);
