@@ -1230,25 +1230,41 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_count(const uint32_t *key
 
 // counts [tiles][B] -> prefix[t][d] = records with digit d in tiles < t, and
 // total[d]; counts are zeroed behind (pass 0's table is k_parse's, which
-// accumulates with atomics).  Grid B / 64, 256 threads: 64 digits x 4 groups
-// of tiles.
-__global__ __launch_bounds__(256) void k_sort_prefix(uint32_t *counts, uint32_t tiles, uint32_t B,
-                                                     uint32_t *prefix, uint32_t *total) {
-    __shared__ uint32_t s_sum[4][64];
+// accumulates with atomics).  Grid B / 64, 1024 threads: 64 digits x 16
+// groups of tiles, each thread's loads issued 8 at a time (a thread walking
+// its tiles one dependent load after another made this launch the wide
+// sort's longest).
+constexpr int kPrefixGroups = 16, kPrefixUnroll = 8;
+__global__ __launch_bounds__(64 * kPrefixGroups) void k_sort_prefix(uint32_t *counts, uint32_t tiles, uint32_t B,
+                                                                   uint32_t *prefix, uint32_t *total) {
+    __shared__ uint32_t s_sum[kPrefixGroups][64];
     const uint32_t dl = threadIdx.x & 63u, g = threadIdx.x >> 6, d = blockIdx.x * 64u + dl;
-    const uint32_t t0 = tiles * g / 4u, t1 = tiles * (g + 1u) / 4u;
+    const uint32_t t0 = tiles * g / kPrefixGroups, t1 = tiles * (g + 1u) / kPrefixGroups;
     uint32_t sum = 0u;
-    for (uint32_t u = t0; u < t1; u++) sum += counts[u * B + d];
+    for (uint32_t u0 = t0; u0 < t1; u0 += kPrefixUnroll) {
+        uint32_t c[kPrefixUnroll];
+#pragma unroll
+        for (int k = 0; k < kPrefixUnroll; k++) c[k] = u0 + k < t1 ? counts[(u0 + k) * B + d] : 0u;
+#pragma unroll
+        for (int k = 0; k < kPrefixUnroll; k++) sum += c[k];
+    }
     s_sum[g][dl] = sum;
     __syncthreads();
     uint32_t run = 0u;
     for (uint32_t k = 0; k < g; k++) run += s_sum[k][dl];
-    if (g == 3u) total[d] = run + sum;
-    for (uint32_t u = t0; u < t1; u++) {
-        const uint32_t c = counts[u * B + d];
-        prefix[u * B + d] = run;
-        counts[u * B + d] = 0u;
-        run += c;
+    if (g == kPrefixGroups - 1) total[d] = run + sum;
+    for (uint32_t u0 = t0; u0 < t1; u0 += kPrefixUnroll) {
+        uint32_t c[kPrefixUnroll];
+#pragma unroll
+        for (int k = 0; k < kPrefixUnroll; k++) c[k] = u0 + k < t1 ? counts[(u0 + k) * B + d] : 0u;
+#pragma unroll
+        for (int k = 0; k < kPrefixUnroll; k++) {
+            if (u0 + k < t1) {
+                prefix[(u0 + k) * B + d] = run;
+                counts[(u0 + k) * B + d] = 0u;
+                run += c[k];
+            }
+        }
     }
 }
 
@@ -1379,7 +1395,7 @@ hipError_t launch_sort_wide(const BundleArgs &a, const SortScratch &ss, hipStrea
         if (q == 1)
             hipLaunchKernelGGL(k_sort_count_wide, dim3(tiles), dim3(kSortThreads), 0, s, (const uint32_t *)ss.keys_tmp,
                                a.n, bits, B, ss.wcounts[1]);
-        hipLaunchKernelGGL(k_sort_prefix, dim3(B / 64u), dim3(256), 0, s, q == 0 ? a.sort_counts : ss.wcounts[1],
+        hipLaunchKernelGGL(k_sort_prefix, dim3(B / 64u), dim3(64 * kPrefixGroups), 0, s, q == 0 ? a.sort_counts : ss.wcounts[1],
                            tiles, B, ss.wprefix, ss.wtotal);
         SortPassWide sp;
         sp.sk = q == 0 ? a.sk_in : ss.keys_tmp;
