@@ -304,9 +304,10 @@ class Side:
             counts = np.bincount(idx, minlength=nssrc)[idx]
         b = synth.realign(b, args.align)
         self.b = b
-        # context table >= 1.6x the SSRCs (load <= 0.31 at 10k); its size sets
-        # the sort's key width (2^15 slots + the invalid key: two radix passes)
-        max_ctx = 1 << max(12, (int(1.6 * nssrc) - 1).bit_length())
+        # max_contexts = the streams, as a deployment sets it: the engine's table
+        # is next_pow2(2 x max_contexts) slots (2^15 at 10k: load 0.31; 2^18 at
+        # 100k: 0.38), and its size sets the sort's key width (slot bits + 1)
+        max_ctx = max(1 << 12, nssrc)
         K = max(1, args.keysets)
         mk = dict(device=device, max_contexts=max_ctx, max_factories=max(64, 2 * K + 8),
                   max_transformers=max(64, 2 * K + 8), max_batch=n)
@@ -663,10 +664,11 @@ def main():
         # traffic: HBM bytes per launch from the committed PMC passes, corrected
         # as the guide prescribes (FETCH_SIZE x 2 + WRITE_SIZE, gfx950).  The
         # guide's factor is calibrated for 16-B-per-lane coalesced streams; for
-        # these kernels' per-lane 64-B chunk walk it overstates (profiles/r03/
-        # pmc_calib_factor.json), so the physical bytes lie between the in-place
-        # floor (every payload byte read once, ciphertext + trailer written
-        # once) and this figure: traffic_range.
+        # these kernels' per-lane 64-B chunk walk it may overstate, and a
+        # stand-in calibration (tools/pmc_calib.hip) lands below the in-place
+        # floor, so neither is exact: the physical bytes lie between the floor
+        # (every payload byte read once, ciphertext + trailer written once) and
+        # this figure: traffic_range.
         g = (pmc.get("guide_correction_bytes_per_launch") or {}).get(kernel)
         hdr = 12  # RTP header: read, never rewritten
         floor = n * (L + (L - hdr + T)) if kernel == "k_protect" else n * ((L + T) + (L - hdr))

@@ -710,15 +710,23 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     const SortScratch ss = sort_scratch(e->sort_temp, e->scratch_n);
     // keys: slot or ctx_cap (= not walked), ctx_bits + 1 bits: 8-bit digits up
     // to 16 bits, two 9-11-bit digits up to 22 (the wide sort), else 8-bit again
+    // 17-19 bits: an 8-bit pass and one wide pass (hybrid); 20-22: two wide
+    // passes; SRTP_SORT_NARROW / SRTP_SORT_WIDE force 8-bit / two wide passes (A/B)
     const int key_bits = e->ctx_bits + 1;
-    const bool wide = key_bits > 16 && key_bits <= 2 * kSortWideMaxBits && !getenv("SRTP_SORT_NARROW");
-    a.sort_passes = wide ? 2 : (key_bits + 7) / 8;
+    static const bool force_narrow = getenv("SRTP_SORT_NARROW") != nullptr;
+    static const bool force_wide = getenv("SRTP_SORT_WIDE") != nullptr;
+    const bool big = key_bits > 16 && key_bits <= 2 * kSortWideMaxBits && !force_narrow;
+    const bool hybrid = big && key_bits <= 8 + kSortWideMaxBits && !force_wide;
+    const bool wide = big && !hybrid;
+    a.sort_key_bits = key_bits;
+    a.sort_hi_bits = hybrid ? key_bits - 8 : 0;
+    a.sort_passes = big ? 2 : (key_bits + 7) / 8;
     a.sort_bits = wide ? (key_bits + 1) / 2 : 8;
     a.sort_counts = wide ? ss.wcounts[0] : ss.counts[0];
-    // the walk re-zeroes the 8-bit sort's last counts (the wide sort's
-    // k_sort_prefix zeroes its own: the walk then clears a prefix table that is
-    // rewritten before its next use)
-    a.sort_zero = wide ? ss.wprefix : ss.counts[a.sort_passes - 1];
+    // the walk re-zeroes the 8-bit sort's last counts, and the hybrid's first
+    // (k_parse's); the wide sort's k_sort_prefix zeroes its own (the walk then
+    // clears a prefix table that is rewritten before its next use)
+    a.sort_zero = wide ? ss.wprefix : hybrid ? ss.counts[0] : ss.counts[a.sort_passes - 1];
     a.sort_zero_words = ((n + sort_tile_records() - 1u) / sort_tile_records()) * 256u; // tiles of this bundle x 256 digits
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;

@@ -76,6 +76,8 @@ struct BundleArgs {
     uint32_t *sort_counts; // [tiles][bins] first-digit counts per sort tile, by k_parse
     int32_t sort_passes;   // digits to sort: key width / 8 rounded up, or 2 wide digits
     int32_t sort_bits;     // bits of the first digit (8, or 9-11 for a two-pass wide sort)
+    int32_t sort_hi_bits;  // 9-11: an 8-bit first pass, then one wide pass of these bits (0: not)
+    int32_t sort_key_bits; // the key's width (slot bits + 1)
     uint32_t *sort_zero;   // the last pass's digit counts, re-zeroed by k_walk
     uint32_t sort_zero_words;
 };

@@ -1537,14 +1537,63 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32
 }
 
 hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s) {
-    const uint32_t wide = a.sort_bits > 8;
-    const uint32_t key_bits = wide ? 2u * (uint32_t)a.sort_bits : 8u * (uint32_t)a.sort_passes;
-    const uint32_t bins = 1u << a.sort_bits;
+    const uint32_t key_bits = (uint32_t)a.sort_key_bits;
+    const uint32_t bins = 1u << a.sort_bits; // k_parse's first-digit counts
     hipLaunchKernelGGL(k_sort_tile, dim3(1), dim3(kSortThreads), 0, s, a, key_bits, bins);
     return hipGetLastError();
 }
 
+// Keys of 17-19 bits: an 8-bit pass (its bases from k_parse's counts, as the
+// 8-bit sort's first pass: no prefix launch), then one wide pass of the
+// remaining 9-11 bits -- four launches where two wide passes take five.
+hipError_t launch_sort_hybrid(const BundleArgs &a, const SortScratch &ss, hipStream_t s) {
+    const uint32_t tiles = (a.n + kSortTile - 1) / kSortTile;
+    SortPass sp;
+    sp.sk = a.sk_in;
+    sp.sv = a.sv_in;
+    sp.dk = ss.keys_tmp;
+    sp.dv = ss.vals_tmp;
+    sp.n = a.n;
+    sp.shift = 0u;
+    sp.tiles = tiles;
+    sp.counts = a.sort_counts; // k_parse's; the walk re-zeroes them (sort_zero)
+    sp.next_counts = nullptr;
+    sp.zero = nullptr;
+    sp.spos = nullptr;
+    sp.walk_max = a.ctx_mask;
+    sp.lord = a.lord;
+    sp.len = a.len;
+    sp.ctl = a.ctl;
+    sp.cls_tile = a.cls_tile;
+    hipLaunchKernelGGL(k_sort_scatter, dim3(tiles), dim3(kSortThreads), 0, s, sp);
+    const uint32_t bits = (uint32_t)a.sort_hi_bits, B = 1u << bits;
+    hipLaunchKernelGGL(k_sort_count_wide, dim3(tiles), dim3(kSortThreads), 0, s, (const uint32_t *)ss.keys_tmp,
+                       a.n, 8u, B, ss.wcounts[1]);
+    hipLaunchKernelGGL(k_sort_prefix, dim3(B / 64u), dim3(64 * kPrefixGroups), 0, s, ss.wcounts[1], tiles, B,
+                       ss.wprefix, ss.wtotal);
+    SortPassWide sw;
+    sw.sk = ss.keys_tmp;
+    sw.sv = ss.vals_tmp;
+    sw.dk = a.sk_out;
+    sw.dv = a.sv_out;
+    sw.n = a.n;
+    sw.shift = 8u;
+    sw.bits = bits;
+    sw.tiles = tiles;
+    sw.prefix = ss.wprefix;
+    sw.total = ss.wtotal;
+    sw.spos = a.reverse ? a.spos : nullptr;
+    sw.walk_max = a.ctx_mask;
+    sw.lord = nullptr;
+    sw.len = a.len;
+    sw.ctl = a.ctl;
+    sw.cls_tile = a.cls_tile;
+    hipLaunchKernelGGL(k_sort_scatter_wide, dim3(tiles), dim3(kSortThreads), 0, s, sw);
+    return hipGetLastError();
+}
+
 hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s) {
+    if (a.sort_hi_bits) return launch_sort_hybrid(a, ss, s);
     if (a.sort_bits > 8) return launch_sort_wide(a, ss, s);
     const uint32_t tiles = (a.n + kSortTile - 1) / kSortTile;
     const int P = a.sort_passes;

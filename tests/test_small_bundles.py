@@ -27,8 +27,9 @@ P80 = profile_policies("AES_CM_128_HMAC_SHA1_80")
 P32 = profile_policies("AES_CM_128_HMAC_SHA1_32")
 
 # max_contexts -> context table 2 * next_pow2 slots -> sort key ctx_bits + 1:
-# 8 bits (one pass), 14 bits (two 8-bit passes), 20 bits (wide: two 10-bit)
-TABLES = {"key8": 64, "key14": 1 << 12, "key20": 1 << 18}
+# 8 bits (one pass), 14 bits (two 8-bit passes), 18 bits (an 8-bit pass and a
+# 10-bit one), 20 bits (wide: two 10-bit passes)
+TABLES = {"key8": 64, "key14": 1 << 12, "key18": 1 << 16, "key20": 1 << 18}
 
 
 @pytest.fixture(scope="module", params=list(TABLES), ids=list(TABLES))
