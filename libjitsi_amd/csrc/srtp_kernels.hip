@@ -37,6 +37,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 
 
 #include "../../include/srtp_mi355x.h"
@@ -4610,15 +4611,15 @@ hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
 // keeps 1024-thread workgroups.  SRTP_AES_SPREAD=0: always max_block (A/B).
 static uint32_t aes_block(uint32_t n, uint32_t max_block) {
     static const bool spread = !getenv("SRTP_AES_SPREAD") || atoi(getenv("SRTP_AES_SPREAD")) != 0;
-    static int cus[64];
+    static std::atomic<int> cus[64]; // CUs per device, looked up once (any thread)
     int dev = 0;
     if (!spread || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return max_block;
-    if (cus[dev] <= 0) {
-        int c = 0;
+    int c = cus[dev].load(std::memory_order_relaxed);
+    if (c <= 0) {
         if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return max_block;
-        cus[dev] = c;
+        cus[dev].store(c, std::memory_order_relaxed);
     }
-    const uint32_t waves = (n + 63u) / 64u, per_cu = (waves + (uint32_t)cus[dev] - 1u) / (uint32_t)cus[dev];
+    const uint32_t waves = (n + 63u) / 64u, per_cu = (waves + (uint32_t)c - 1u) / (uint32_t)c;
     return 64u * std::min<uint32_t>(max_block / 64u, std::max<uint32_t>(4u, per_cu));
 }
 
