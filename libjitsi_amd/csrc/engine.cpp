@@ -728,6 +728,12 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     // clears a prefix table that is rewritten before its next use)
     a.sort_zero = wide ? ss.wprefix : hybrid ? ss.counts[0] : ss.counts[a.sort_passes - 1];
     a.sort_zero_words = ((n + sort_tile_records() - 1u) / sort_tile_records()) * 256u; // tiles of this bundle x 256 digits
+    // a small bundle's AES-CM keystream by k_ctr_small (a lane per counter-block
+    // pair; the fused kernels only MAC): up to SRTP_SMALL_CTR_MAX packets,
+    // default 8192 (128 waves: under one wave per SIMD), 0 = never
+    static const uint32_t small_max = getenv("SRTP_SMALL_CTR_MAX") ? (uint32_t)atol(getenv("SRTP_SMALL_CTR_MAX"))
+                                                                    : 8192u;
+    a.small_ctr = n <= small_max ? 1 : 0;
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;
     a.ctl = e->ctl + c;
@@ -758,6 +764,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);
         HIPCHK(e, launch_unprotect(a, s));
+        if (a.small_ctr) HIPCHK(e, launch_ctr_small(a, s)); // the speculative decryption
         if (e->n_skein) HIPCHK(e, launch_skein(a, s));
     }
     {
@@ -774,6 +781,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         if (e->n_ext) HIPCHK(e, launch_ext(a, s));
     } else {
         StageTimer t(e, s, SRTP_STAGE_PROTECT);
+        if (a.small_ctr) HIPCHK(e, launch_ctr_small(a, s)); // the keystream, then k_protect MACs
         HIPCHK(e, launch_protect(a, s));
         if (e->n_ext) HIPCHK(e, launch_ext(a, s));
         if (e->n_skein) HIPCHK(e, launch_skein(a, s));

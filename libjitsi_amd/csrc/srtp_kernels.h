@@ -80,6 +80,10 @@ struct BundleArgs {
     int32_t sort_key_bits; // the key's width (slot bits + 1)
     uint32_t *sort_zero;   // the last pass's digit counts, re-zeroed by k_walk
     uint32_t sort_zero_words;
+    // a small bundle: the AES-CM keystream of the AES-CM + HMAC-SHA1 packets is
+    // applied by k_ctr_small (a lane per counter-block pair), the fused
+    // kernels only MAC those packets
+    int32_t small_ctr;
 };
 
 // Layout of the sort's scratch (one allocation of sort_temp_bytes(n_max)).
@@ -113,6 +117,9 @@ hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
 hipError_t launch_skein(const BundleArgs &a, hipStream_t s);
 hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s);
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
+// BundleArgs::small_ctr: the keystream of the AES-CM + HMAC-SHA1 packets, one
+// workgroup per packet -- protect before k_protect, unprotect after k_unprotect
+hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s);
 // unprotect: statuses/lengths out; undo/redo the rare speculation misses (after the walk)
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 // AES-F8 packets after the final statuses: protect (F8 + HMAC + trailer) or

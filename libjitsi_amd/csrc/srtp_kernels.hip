@@ -3293,12 +3293,26 @@ __device__ __forceinline__ void store_chunk(uint8_t *pkt, int b, const Ctr &cs, 
 // Fused protect, one lane per packet: AES-CM in place (SRTPCipherCTR.process
 // :94-121) + HMAC-SHA1 over the ciphertext (authenticatePacketHMAC :269-278)
 // + trailer (RawPacket.append :203-220).  Packet bytes: one read, one write.
+// Block b of a packet for the MAC: the 16-B pieces that start before lim
+// (as the generic loops load them), zeros after.
+__device__ __forceinline__ void load_block16(const uint8_t *pkt, int b, int lim, uint32_t w[16]) {
+    const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (64 * b + 16 * m < lim) v = qp[m];
+        w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+    }
+}
+
 template <bool LK>
 __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                             const char *__restrict__ lds, const TeBase &tb,
-                                            uint32_t p, bool fused) {
+                                            uint32_t p, bool fused, bool mac_only = false) {
     uint8_t *pkt = a.seg + a.off[p];
     const bool do_enc = kf<LK>(ks->enc_type) == SRTP_AESCM_ENCRYPTION;
+    // mac_only: k_ctr_small has ciphered the packet already (small bundles)
+    const bool enc = do_enc && !mac_only;
     const bool do_mac = kf<LK>(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
     const bool rtcp = kf<LK>(ks->kind) == SRTP_KIND_RTCP;
     const int T = (int)kf<LK>(ks->tag_len);
@@ -3337,8 +3351,27 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     // stores; bytes outside [off, end) are written back unchanged.)
     const int B = L >> 6;
     CtrPre cp; // AES-CM rounds 1-2 of this packet's counter blocks
-    if (do_enc) ctr_precompute(lds, tb, pk_words(pk), cs.iv, cp);
-    if (fused && B >= 2) {
+    if (enc) ctr_precompute(lds, tb, pk_words(pk), cs.iv, cp);
+    if (mac_only) {
+        // the MAC over the ciphertext, the next block's load in flight while
+        // a block is hashed (a lone packet's latency is this chain)
+        uint32_t nx[16];
+        load_block16(pkt, 0, L, nx);
+        for (; b < n_blocks; b++) {
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = nx[k];
+            if (b + 1 < nb_data) load_block16(pkt, b + 1, L, nx);
+            else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) nx[k] = 0u;
+            }
+            if (b < nb_inner) inner_words(w, b, L, suffix);
+            else outer_words<!LK>(w, h, ks);
+            sha1_compress(h, w);
+        }
+    }
+    if (fused && !mac_only && B >= 2) {
         uint32_t c[16];
         load_chunk(pkt, 0, L, c);
         pk_chunk_pre(lds, tb, pk, cp, cs, 0, c);
@@ -3396,7 +3429,7 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
                 if (64 * b + 16 * m < L) v = qp[m];
                 w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
             }
-            if (do_enc && 64 * b + 64 > cs.off) {
+            if (enc && 64 * b + 64 > cs.off) {
                 pk_chunk_pre(lds, tb, pk, cp, cs, b, w);
 #pragma unroll
                 for (int m = 0; m < 4; m++)
@@ -3461,6 +3494,10 @@ __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const u
     }
 }
 
+// MacOnly (a small bundle, BundleArgs::small_ctr): k_ctr_small has applied the
+// AES-CM + HMAC-SHA1 packets' keystream; this kernel only MACs them.  A
+// template, so the full-bundle kernel's code is what it was without it.
+template <bool MacOnly>
 __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
     // the status counts sit at the start of wave 0's store buffer, which wave 0
     // first writes after flushing them
@@ -3492,15 +3529,16 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
         const KeySet *ks = a.keysets + ks_id;
         const bool lane = todo && ks->ext == 0u && ks->enc_type == SRTP_AESCM_ENCRYPTION &&
                           ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
-        if (lane) protect_one<true>(a, ks, lds, tb, p, true);
+        if (lane) protect_one<true>(a, ks, lds, tb, p, !MacOnly, MacOnly);
         todo = todo && !lane;
     }
     for_each_keyset(todo, ks_id, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
         if (sgpr(ks->ext)) return; // AES-F8 / AES-256-CM: k_ext
-        protect_one<false>(a, ks, lds, tb, p,
-                           sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
-                               sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
+        const bool fused = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
+                           sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+        const bool mac_only = MacOnly && fused && sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
+        protect_one<false>(a, ks, lds, tb, p, fused && !mac_only, mac_only);
     });
     STAMP(2);
 }
@@ -3539,7 +3577,8 @@ __device__ __forceinline__ uint32_t chain_head(const uint32_t *__restrict__ sk, 
 template <bool LK>
 __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                               const char *__restrict__ lds, const TeBase &tb,
-                                              uint32_t p, const CtxState &st, bool fused) {
+                                              uint32_t p, const CtxState &st, bool fused,
+                                              bool mac_only = false) {
     uint8_t *pkt = a.seg + a.off[p];
     const int L = (int)a.len[p];
     const int T = (int)kf<LK>(ks->tag_len);
@@ -3593,7 +3632,8 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     a.spec[p] = (spec ? kSpecDid : 0u) | (aes ? kSpecAes : 0u) | (rtp ? kSpecRtp : 0u) |
                 (rtp && a.flags && (a.flags[p] & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ? kSpecSkip : 0u);
     if (!do_mac && !spec) return;
-    cs.end = spec ? end : 0;
+    // mac_only: k_ctr_small decrypts the packets marked kSpecDid (small bundles)
+    cs.end = spec && !mac_only ? end : 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) cs.carry[k] = 0u;
     PktKeys<LK> pk;
@@ -3606,7 +3646,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     const int nb_inner = ((end + 12) >> 6) + 1;
     const int n_blocks = do_mac ? nb_inner + 1 : nb_data;
     int b = 0;
-    if (fused && nb_full >= 2) {
+    if (fused && !mac_only && nb_full >= 2) {
         // AES-CM + HMAC, wave-uniform, over the full blocks before the
         // ROC-carrying one.  As in protect, iteration b computes the keystream
         // of chunk b beside the hash of block b-1 (loaded the iteration
@@ -3742,7 +3782,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         }
         a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
     }
-    if (spec) {
+    if (spec && !mac_only) {
         // reload the round keys through an opaque copy of the key-set pointer:
         // with the plain pointer the compiler keeps the first load's VGPR copies
         // live across the MAC loop instead (44 VGPRs spilled to scratch)
@@ -3770,6 +3810,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 }
 
 
+template <bool MacOnly> // as k_protect's: k_ctr_small decrypts afterwards
 __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords + kStageWords];
     STAMP(0);
@@ -3820,14 +3861,15 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
         const KeySet *ks = a.keysets + st.ks;
         const bool lane = todo && ks->ext == 0u && ks->enc_type == SRTP_AESCM_ENCRYPTION &&
                           ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
-        if (lane) unprotect_one<true>(a, ks, lds, tb, p, st, true);
+        if (lane) unprotect_one<true>(a, ks, lds, tb, p, st, !MacOnly, MacOnly);
         rest = todo && !lane;
     }
     for_each_keyset(rest, st.ks, [&](uint32_t ks_u) {
         const KeySet *ks = a.keysets + ks_u;
-        unprotect_one<false>(a, ks, lds, tb, p, st,
-                             sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
-                                 sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION);
+        const bool fused = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
+                           sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
+        const bool mac_only = MacOnly && fused && sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
+        unprotect_one<false>(a, ks, lds, tb, p, st, fused && !mac_only, mac_only);
     });
     STAMP(2);
 }
@@ -4625,7 +4667,8 @@ static uint32_t aes_block(uint32_t n, uint32_t max_block) {
 
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
     const uint32_t b = aes_block(a.n, (uint32_t)kUnprotectBlock);
-    hipLaunchKernelGGL(k_unprotect, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    if (a.small_ctr) hipLaunchKernelGGL(k_unprotect<true>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    else hipLaunchKernelGGL(k_unprotect<false>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_skein(const BundleArgs &a, hipStream_t s) {
@@ -4648,9 +4691,120 @@ hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
     }
     return hipGetLastError();
 }
+// ------------------------------------------------ small bundles' AES-CM
+// In a bundle of a few waves the fused kernels are one lane walking each
+// packet's chunks with every LDS latency exposed (~100 us for a lone 1200-B
+// packet: most of a per-packet call's round trip).  With BundleArgs::small_ctr
+// this kernel applies the keystream of the AES-CM + HMAC-SHA1 packets instead,
+// one wave per packet and a lane per pair of counter blocks, and the
+// fused kernels only MAC them: protect runs it before k_protect (which MACs
+// the ciphertext and appends the trailer), unprotect after k_unprotect (which
+// MACs the ciphertext, checks the tag, saves the walk's re-check state and
+// marks the packets it speculates on, kSpecDid) and before the walk -- the
+// same bytes, in the same order, as the fused kernels leave.
+constexpr int kCtrSmallBlock = 256;
+
+__device__ __forceinline__ bool small_ctr_ks(const KeySet *ks) {
+    return ks->ext == 0 && ks->enc_type == SRTP_AESCM_ENCRYPTION && ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
+}
+
+// finish_status without its stores (k_protect makes them)
+__device__ __forceinline__ int32_t peek_status(const BundleArgs &a, uint32_t p) {
+    int32_t st = a.w_status[p];
+    if (st == kStPending) st = SRTP_STATUS_ERR_INTERNAL;
+    if (st != SRTP_STATUS_SKIPPED && a.abort_on_error && a.ctl->any_throw &&
+        (int32_t)p > a.e_min[packet_tid(a, p)])
+        st = SRTP_STATUS_NOT_PROCESSED;
+    return st;
+}
+
+// packet p's keystream job: [start, end) under iv with key set ks, or false
+__device__ __forceinline__ bool ctr_small_job(const BundleArgs &a, uint32_t p, int &start, int &end,
+                                              uint32_t iv[4], const KeySet *&ks) {
+    const uint32_t slot = a.p_slot[p];
+    if (slot == kNoSlot) return false;
+    if (!a.reverse && peek_status(a, p) != SRTP_STATUS_OK) return false;
+    ks = a.keysets + a.ctx[slot].ks;
+    if (!small_ctr_ks(ks)) return false;
+    if (a.reverse && !(a.spec[p] & kSpecDid)) return false; // k_unprotect did not speculate
+    const uint8_t *pkt = a.seg + a.off[p];
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const bool rtcp = ks->kind == SRTP_KIND_RTCP;
+    const int T = ks->tag_len;
+    if (!a.reverse) { // protect_one's region and IV
+        end = (int)a.w_len[p] - T - (rtcp ? 4 : 0);
+        if (rtcp) {
+            start = 8;
+            make_iv_rtcp(ks, hdr, a.w_cw[p], iv);
+        } else {
+            start = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+            make_iv_rtp(ks, hdr, a.w_cw[p], iv);
+        }
+    } else { // unprotect_one's speculative decryption
+        const int L = (int)a.len[p];
+        if (rtcp) {
+            const int io = L - 4 - T;
+            start = 8;
+            end = io;
+            make_iv_rtcp(ks, hdr, ld_be32(pkt + io) & 0x7FFFFFFFu, iv);
+        } else {
+            start = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
+            end = L - T;
+            make_iv_rtp(ks, hdr, a.g0[p], iv);
+        }
+    }
+    return end > start;
+}
+
+// XOR keystream block x over up to 16 bytes (lim) at dst
+__device__ __forceinline__ void xor_ks16(uint8_t *dst, int lim, const uint32_t x[4]) {
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        if (i < lim) dst[i] ^= (uint8_t)(x[i >> 2] >> (8 * (i & 3)));
+}
+
+__global__ __launch_bounds__(kCtrSmallBlock) void k_ctr_small(BundleArgs a) {
+    __shared__ uint32_t s_te[kTeWords];
+    fill_te4(s_te); // ends with a barrier
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s_te);
+    // a wave per packet: every lane works out the packet's job (the same loads
+    // across the wave), then the lanes take its counter-block pairs
+    const uint32_t waves = gridDim.x * (kCtrSmallBlock / 64);
+    const int lane = (int)(threadIdx.x & 63u);
+    for (uint32_t p = blockIdx.x * (kCtrSmallBlock / 64) + (threadIdx.x >> 6); p < a.n; p += waves) {
+        int start = 0, end = 0;
+        uint32_t iv[4];
+        const KeySet *ks = nullptr;
+        if (!ctr_small_job(a, p, start, end, iv, ks)) continue;
+        uint32_t k0[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) k0[k] = ks->rk[k];
+        uint8_t *pkt = a.seg + a.off[p];
+        const int nblk = (end - start + 15) >> 4;
+        for (int j = 2 * lane; j < nblk; j += 128) {
+            uint32_t x[4], y[4];
+            ctr_input(iv, j, x);
+            ctr_input(iv, j + 1, y);
+            aes_encrypt2_v(lds, tb, k0, x, y);
+            xor_ks16(pkt + start + 16 * j, end - (start + 16 * j), x);
+            if (j + 1 < nblk) xor_ks16(pkt + start + 16 * (j + 1), end - (start + 16 * (j + 1)), y);
+        }
+    }
+}
+
+hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    // one workgroup per CU at most (each fills the 128-KB T-table image)
+    const uint32_t wgs = (a.n + kCtrSmallBlock / 64 - 1) / (kCtrSmallBlock / 64);
+    hipLaunchKernelGGL(k_ctr_small, dim3(wgs < 256u ? wgs : 256u), dim3(kCtrSmallBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
     const uint32_t b = aes_block(a.n, (uint32_t)kAesBlock);
-    hipLaunchKernelGGL(k_protect, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    if (a.small_ctr) hipLaunchKernelGGL(k_protect<true>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    else hipLaunchKernelGGL(k_protect<false>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {

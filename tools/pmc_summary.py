@@ -41,7 +41,8 @@ def short(name: str) -> str:
         return "rocprim::" + ("onesweep" if "onesweep_iteration" in name else
                               "histogram" if "histogram" in name else "other")
     n = name.split("(")[0].replace("srtp::", "").replace("void ", "")
-    return n
+    # the full-bundle instances of the crypto kernels keep their plain names
+    return n.replace("k_protect<false>", "k_protect").replace("k_unprotect<false>", "k_unprotect")
 
 
 def load_trace(path):
