@@ -3755,7 +3755,41 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     // (round keys, counter, keystream carry) is live across SHA-1 and nothing
     // spills to scratch; the round keys are reloaded for the second loop.
     const int b_tail = b;
-    if (do_mac) {
+    if (do_mac && mac_only) {
+        // as below, the next block's load in flight while a block is hashed
+        // (a lone packet's latency is this chain)
+        uint32_t nx[16];
+        if (b < nb_data) load_block16(pkt, b, end, nx);
+        else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) nx[k] = 0u;
+        }
+        for (; b < n_blocks; b++) {
+            uint32_t d[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) d[k] = nx[k];
+            if (b + 1 < nb_data) load_block16(pkt, b + 1, end, nx);
+            else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) nx[k] = 0u;
+            }
+            if (b == nb_full && rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
+                uint32_t *mp = a.mid + 5 * (size_t)p;
+#pragma unroll
+                for (int k = 0; k < 5; k++) mp[k] = h[k];
+                if (spec) {
+                    uint4 *tp = reinterpret_cast<uint4 *>(a.tailc + 16 * (size_t)p);
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+                        tp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
+                }
+            }
+            if (b < nb_inner) inner_words(d, b, end, suffix);
+            else outer_words<!LK>(d, h, ks);
+            sha1_compress(h, d);
+        }
+        a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+    } else if (do_mac) {
         for (; b < n_blocks; b++) {
             uint32_t d[16];
             const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
