@@ -772,8 +772,10 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         HIPCHK(e, launch_walk(a, 0, s));
         // second pass: abort-on-throw's limit pass when a packet may throw,
         // else the wave-parallel walk of context chains longer than the
-        // first pass's window (returns at once when there are none)
-        HIPCHK(e, launch_walk(a, 1, s));
+        // first pass's window (returns at once when there are none) -- which a
+        // bundle of fewer than kLongMin packets cannot hold: a small bundle
+        // without abort-on-throw saves the launch
+        if (a.abort_on_error || n >= kLongMin || a.debug || a.dbg) HIPCHK(e, launch_walk(a, 1, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
@@ -1305,6 +1307,10 @@ struct srtp_pipeline {
         // bundle's round trip pays
         uint32_t *h_pack = nullptr, *d_pack = nullptr;
         uint32_t packed_n = 0;      // the bundle in flight used the packed layout (its n), else 0
+        // tiny bundles (kTinySeg bytes): the segment rides in the packed block
+        // too -- one copy each way -- and is copied back to tiny_dst on wait
+        uint8_t *tiny_dst = nullptr;
+        size_t tiny_off = 0, tiny_bytes = 0;
         hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out = nullptr;
         bool busy = false;
         int rc = SRTP_OK;           // engine return code of the last submit
@@ -1314,6 +1320,7 @@ struct srtp_pipeline {
 
 constexpr uint32_t kPackMax = 8192; // bundles up to this many packets use the packed copies
 constexpr size_t kOneStreamBytes = (size_t)1 << 20; // bundles up to this size copy on the engine's stream
+constexpr size_t kTinySeg = (size_t)64 << 10;       // bundles up to this size: one copy each way
 
 static void pipeline_free(srtp_pipeline *pl) {
     DeviceGuard guard(pl->e->opts.device);
@@ -1371,8 +1378,8 @@ int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg
              dalloc(&sl.d_len, n) == hipSuccess && dalloc(&sl.d_cap, n) == hipSuccess &&
              dalloc(&sl.d_flags, n) == hipSuccess && dalloc(&sl.d_tids, n) == hipSuccess &&
              dalloc(&sl.d_status, n) == hipSuccess &&
-             halloc(&sl.h_pack, 6 * std::min<size_t>(n, kPackMax)) == hipSuccess &&
-             dalloc(&sl.d_pack, 6 * std::min<size_t>(n, kPackMax)) == hipSuccess &&
+             halloc(&sl.h_pack, 6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) == hipSuccess &&
+             dalloc(&sl.d_pack, 6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_out, hipEventDisableTiming) == hipSuccess;
@@ -1430,6 +1437,10 @@ static int pipeline_wait_locked(srtp_pipeline *pl, srtp_pipeline::Slot &sl) {
         memcpy(sl.h.status, sl.h_pack + 5 * (size_t)n, n * 4ull);
         sl.packed_n = 0;
     }
+    if (sl.tiny_dst) { // a tiny bundle's segment, back where the caller reads it
+        memcpy(sl.tiny_dst, reinterpret_cast<const uint8_t *>(sl.h_pack) + sl.tiny_off, sl.tiny_bytes);
+        sl.tiny_dst = nullptr;
+    }
     return sl.rc;
 }
 
@@ -1463,7 +1474,11 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
     hipStream_t s = e->stream, si = one ? s : pl->s_in, so = one ? s : pl->s_out;
     const int32_t abort = abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0);
     if (!hseg) hseg = sl.h.seg;
-    HIPCHK(e, hipMemcpyAsync(sl.d_seg, hseg, seg_bytes, hipMemcpyHostToDevice, si));
+    // tiny: [off | cap | flags | tids | len | status | segment] in one block
+    const bool tiny = n <= kPackMax && seg_bytes <= kTinySeg;
+    const size_t tiny_off = (24ull * n + 15) & ~(size_t)15;
+    uint8_t *d_seg = tiny ? reinterpret_cast<uint8_t *>(sl.d_pack) + tiny_off : sl.d_seg;
+    if (!tiny) HIPCHK(e, hipMemcpyAsync(sl.d_seg, hseg, seg_bytes, hipMemcpyHostToDevice, si));
     if (n <= kPackMax) {
         uint32_t *hp = sl.h_pack, *dp = sl.d_pack;
         const size_t n4 = n * 4ull;
@@ -1472,13 +1487,18 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
         if (use_flags) memcpy(hp + 2 * (size_t)n, sl.h.flags, n4);
         if (use_tids) memcpy(hp + 3 * (size_t)n, sl.h.tids, n4);
         memcpy(hp + 4 * (size_t)n, sl.h.len, n4);
-        HIPCHK(e, hipMemcpyAsync(dp, hp, 5 * n4, hipMemcpyHostToDevice, si));
+        if (tiny) {
+            memcpy(reinterpret_cast<uint8_t *>(hp) + tiny_off, hseg, seg_bytes);
+            HIPCHK(e, hipMemcpyAsync(dp, hp, tiny_off + seg_bytes, hipMemcpyHostToDevice, si));
+        } else {
+            HIPCHK(e, hipMemcpyAsync(dp, hp, 5 * n4, hipMemcpyHostToDevice, si));
+        }
         if (si != s) {
             HIPCHK(e, hipEventRecord(sl.ev_in, si));
             HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
         }
         sl.rc = transform_locked(e, reverse, use_tids ? reinterpret_cast<int32_t *>(dp + 3 * (size_t)n) : nullptr,
-                                 tid, sl.d_seg, dp, dp + 4 * (size_t)n, dp + n,
+                                 tid, d_seg, dp, dp + 4 * (size_t)n, dp + n,
                                  use_flags ? dp + 2 * (size_t)n : nullptr,
                                  reinterpret_cast<int32_t *>(dp + 5 * (size_t)n), n, s, abort);
         if (sl.rc != SRTP_OK) return sl.rc;
@@ -1486,8 +1506,16 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
             HIPCHK(e, hipEventRecord(sl.ev_done, s));
             HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
         }
-        HIPCHK(e, hipMemcpyAsync(hseg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
-        HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, 2 * n4, hipMemcpyDeviceToHost, so));
+        if (tiny) { // len | status | segment back in one copy
+            HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, tiny_off - 16 * (size_t)n + seg_bytes,
+                                     hipMemcpyDeviceToHost, so));
+            sl.tiny_dst = hseg;
+            sl.tiny_off = tiny_off;
+            sl.tiny_bytes = seg_bytes;
+        } else {
+            HIPCHK(e, hipMemcpyAsync(hseg, sl.d_seg, seg_bytes, hipMemcpyDeviceToHost, so));
+            HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, 2 * n4, hipMemcpyDeviceToHost, so));
+        }
         sl.packed_n = n;
     } else {
         HIPCHK(e, hipMemcpyAsync(sl.d_off, sl.h.off, n * 4ull, hipMemcpyHostToDevice, si));

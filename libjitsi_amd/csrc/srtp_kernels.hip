@@ -89,10 +89,22 @@ constexpr int kAesBlock = 1024;  // threads per workgroup of the AES kernels (1 
 constexpr int kUnprotectBlock = SRTP_UNPROTECT_BLOCK; // k_unprotect's workgroup size
 
 __device__ __forceinline__ void fill_te4(uint32_t *s_te) {
-    for (int i = threadIdx.x; i < kTeWords; i += blockDim.x) {
-        const int t = ((i >> 14) << 1) | ((i >> 5) & 1);
-        const uint32_t v = d_te0[(i >> 6) & 255];
-        s_te[i] = t ? rotl(v, 8u * (uint32_t)t) : v;
+    // 8 table loads in flight per thread, then their stores (a workgroup of a
+    // few waves, as small bundles run, otherwise waits out one load per word)
+    constexpr int U = 8;
+    for (int i0 = threadIdx.x; i0 < kTeWords; i0 += U * blockDim.x) {
+        uint32_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * (int)blockDim.x;
+            v[u] = i < kTeWords ? d_te0[(i >> 6) & 255] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * (int)blockDim.x;
+            const int t = ((i >> 14) << 1) | ((i >> 5) & 1);
+            if (i < kTeWords) s_te[i] = t ? rotl(v[u], 8u * (uint32_t)t) : v[u];
+        }
     }
     __syncthreads();
     // The table is read only by inline asm (aes_rounds_asm.inc): let the
@@ -1463,9 +1475,11 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32
             key[r] = i < n ? s_key[cur][i] : 0u;
             idx[r] = i < n ? s_idx[cur][i] : (uint16_t)0;
         }
-        // stable ranks within each digit, items in index order (k_sort_scatter's)
+        // stable ranks within each digit, items in index order (k_sort_scatter's);
+        // rows past the last record are skipped (block-uniform)
 #pragma unroll
         for (int r = 0; r < kSortItems; r++) {
+            if (r * kSortThreads >= (int)n) break;
             const bool valid = r * kSortThreads + t < (int)n;
             const uint32_t d = valid ? (key[r] >> shift) & 255u : 0u;
             unsigned long long m = __ballot(valid);
