@@ -11,6 +11,8 @@ last = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 ev = []
 for r in rows:
     name = r["Kernel_Name"].split("(")[0].replace("srtp::", "")
+    # the full-bundle instances of the crypto kernels by their plain names
+    name = name.replace("void k_protect<false>", "k_protect").replace("void k_unprotect<false>", "k_unprotect")
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r.get("Stream_Id", r.get("Queue_Id", "?"))))
 ev.sort()
 # one step = one k_protect launch; take the span of the last `last` steps
