@@ -124,3 +124,29 @@ def test_spread_workgroup_boundaries(engine_factory, oracle):
         pb.seg, pb.length = seg, ln
         fb = G.inject_faults(pb, rng)
         twin.run(rcv, True, fb.seg, fb.off, fb.length, fb.cap, check_state=False)
+
+
+def test_maximum_size_packets(engine_factory, oracle):
+    """Packets up to the 64-KB region limit, RTP and RTCP, in a small bundle
+    (k_ctr_small's lanes loop over thousands of counter blocks per packet; the
+    MAC-only kernels hash a thousand blocks) and in a large one (the fused
+    kernels' counter precompute runs out past block 256 and the generic loop
+    finishes), each against the oracle with a forged packet on the way back."""
+    e = engine_factory(max_contexts=1 << 12, max_factories=16, max_transformers=16)
+    twin = Twin(e)
+    (k, s), = synth.keys(4000, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+    csnd, crcv = twin.transformer(O.KIND_RTCP, fs), twin.transformer(O.KIND_RTCP, fr)
+    for n, lens in ((6, (40000, 65000)), (9000, (3000, 9000))):
+        b = synth.rtp_bundle(n, 3, lens, seed=4100 + n)
+        seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap, check_state=n < 100)
+        assert (st == N.STATUS_OK).all()
+        seg = seg.copy()
+        seg[int(b.off[n - 1]) + 1000] ^= 2
+        _, _, st2 = twin.run(rcv, True, seg, b.off, ln, b.cap, check_state=n < 100)
+        assert (st2 == N.STATUS_DROP_AUTH).sum() == 1
+    cb = synth.rtcp_bundle(5, 2, len_range=(30000, 60000), seed=4200)
+    cseg, cln, cst = twin.run(csnd, False, cb.seg, cb.off, cb.length, cb.cap)
+    assert (cst == N.STATUS_OK).all()
+    twin.run(crcv, True, cseg, cb.off, cln, cb.cap)
