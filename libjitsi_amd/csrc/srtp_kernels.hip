@@ -83,6 +83,7 @@ __device__ __forceinline__ int64_t java_lshl(int64_t v, int64_t n) {
 constexpr int kTeWords = 32768;  // 128 KB
 constexpr int kTeCounters = 16;  // per-workgroup status counts, after the image (which stays at LDS 0)
 constexpr int kAesBlock = 1024;  // threads per workgroup of the AES kernels (1 WG per CU)
+constexpr int kMacBlock = 256;   // at most, the MacOnly instances' (small bundles)
 #ifndef SRTP_UNPROTECT_BLOCK
 #define SRTP_UNPROTECT_BLOCK 1024
 #endif
@@ -3319,6 +3320,37 @@ __device__ __forceinline__ void load_block16(const uint8_t *pkt, int b, int lim,
     }
 }
 
+// load_block16 for blocks below nb, zeros for the rest (the MAC's padding blocks)
+__device__ __forceinline__ void load_or_zero16(const uint8_t *pkt, int b, int nb, int lim, uint32_t w[16]) {
+    if (b < nb) {
+        load_block16(pkt, b, lim, w);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = 0u;
+    }
+}
+
+// The MAC-only loops' look-ahead: the next kMacAhead blocks of a packet held
+// in registers, the oldest handed out and the one after the newest loaded.
+constexpr int kMacAhead = 4;
+struct MacRing {
+    uint32_t q[kMacAhead][16];
+    __device__ __forceinline__ void fill(const uint8_t *pkt, int b0, int nb, int lim) {
+#pragma unroll
+        for (int k = 0; k < kMacAhead; k++) load_or_zero16(pkt, b0 + k, nb, lim, q[k]);
+    }
+    // block b (the oldest) into w; block b + kMacAhead loaded behind it
+    __device__ __forceinline__ void next(const uint8_t *pkt, int b, int nb, int lim, uint32_t w[16]) {
+#pragma unroll
+        for (int m = 0; m < 16; m++) w[m] = q[0][m];
+#pragma unroll
+        for (int k = 0; k + 1 < kMacAhead; k++)
+#pragma unroll
+            for (int m = 0; m < 16; m++) q[k][m] = q[k + 1][m];
+        load_or_zero16(pkt, b + kMacAhead, nb, lim, q[kMacAhead - 1]);
+    }
+};
+
 template <bool LK>
 __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                             const char *__restrict__ lds, const TeBase &tb,
@@ -3367,19 +3399,14 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
     CtrPre cp; // AES-CM rounds 1-2 of this packet's counter blocks
     if (enc) ctr_precompute(lds, tb, pk_words(pk), cs.iv, cp);
     if (mac_only) {
-        // the MAC over the ciphertext, the next block's load in flight while
-        // a block is hashed (a lone packet's latency is this chain)
-        uint32_t nx[16];
-        load_block16(pkt, 0, L, nx);
+        // the MAC over the ciphertext with kMacAhead blocks' loads in flight
+        // while one is hashed: a lone packet's latency is this chain, and one
+        // block of look-ahead left it waiting on memory
+        MacRing q;
+        q.fill(pkt, 0, nb_data, L);
         for (; b < n_blocks; b++) {
             uint32_t w[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) w[k] = nx[k];
-            if (b + 1 < nb_data) load_block16(pkt, b + 1, L, nx);
-            else {
-#pragma unroll
-                for (int k = 0; k < 16; k++) nx[k] = 0u;
-            }
+            q.next(pkt, b, nb_data, L, w);
             if (b < nb_inner) inner_words(w, b, L, suffix);
             else outer_words<!LK>(w, h, ks);
             sha1_compress(h, w);
@@ -3511,8 +3538,10 @@ __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const u
 // MacOnly (a small bundle, BundleArgs::small_ctr): k_ctr_small has applied the
 // AES-CM + HMAC-SHA1 packets' keystream; this kernel only MACs them.  A
 // template, so the full-bundle kernel's code is what it was without it.
+// (MacOnly instances run small bundles in workgroups of at most kMacBlock
+// threads: registers for the MAC's look-ahead)
 template <bool MacOnly>
-__global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
+__global__ __launch_bounds__(MacOnly ? kMacBlock : kAesBlock) void k_protect(BundleArgs a) {
     // the status counts sit at the start of wave 0's store buffer, which wave 0
     // first writes after flushing them
     __shared__ uint32_t s_te[kTeWords + (kStageWords > kTeCounters ? kStageWords : kTeCounters)];
@@ -3552,7 +3581,8 @@ __global__ __launch_bounds__(kAesBlock) void k_protect(BundleArgs a) {
         const bool fused = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION &&
                            sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
         const bool mac_only = MacOnly && fused && sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
-        protect_one<false>(a, ks, lds, tb, p, fused && !mac_only, mac_only);
+        // (a MacOnly instance never runs the fused loop: compiled out)
+        protect_one<false>(a, ks, lds, tb, p, !MacOnly && fused, mac_only);
     });
     STAMP(2);
 }
@@ -3770,27 +3800,17 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
     // spills to scratch; the round keys are reloaded for the second loop.
     const int b_tail = b;
     if (do_mac && mac_only) {
-        // as below, the next block's load in flight while a block is hashed
+        // as below, with kMacAhead blocks' loads in flight while one is hashed
         // (a lone packet's latency is this chain)
-        uint32_t nx[16];
-        if (b < nb_data) load_block16(pkt, b, end, nx);
-        else {
-#pragma unroll
-            for (int k = 0; k < 16; k++) nx[k] = 0u;
-        }
+        MacRing q;
+        q.fill(pkt, b, nb_data, end);
         for (; b < n_blocks; b++) {
             uint32_t d[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) d[k] = nx[k];
-            if (b + 1 < nb_data) load_block16(pkt, b + 1, end, nx);
-            else {
-#pragma unroll
-                for (int k = 0; k < 16; k++) nx[k] = 0u;
-            }
+            q.next(pkt, b, nb_data, end, d);
             if (b == nb_full && rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
-                for (int k = 0; k < 5; k++) mp[k] = h[k];
+                for (int m = 0; m < 5; m++) mp[m] = h[m];
                 if (spec) {
                     uint4 *tp = reinterpret_cast<uint4 *>(a.tailc + 16 * (size_t)p);
 #pragma unroll
@@ -3859,7 +3879,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 
 
 template <bool MacOnly> // as k_protect's: k_ctr_small decrypts afterwards
-__global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
+__global__ __launch_bounds__(MacOnly ? kMacBlock : kUnprotectBlock) void k_unprotect(BundleArgs a) {
     __shared__ uint32_t s_te[kTeWords + kStageWords];
     STAMP(0);
     STAMP_XCC();
@@ -3917,7 +3937,7 @@ __global__ __launch_bounds__(kUnprotectBlock) void k_unprotect(BundleArgs a) {
         const bool fused = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
                            sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
         const bool mac_only = MacOnly && fused && sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
-        unprotect_one<false>(a, ks, lds, tb, p, st, fused && !mac_only, mac_only);
+        unprotect_one<false>(a, ks, lds, tb, p, st, !MacOnly && fused, mac_only);
     });
     STAMP(2);
 }
@@ -4715,8 +4735,12 @@ static uint32_t aes_block(uint32_t n, uint32_t max_block) {
 
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s) {
     const uint32_t b = aes_block(a.n, (uint32_t)kUnprotectBlock);
-    if (a.small_ctr) hipLaunchKernelGGL(k_unprotect<true>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
-    else hipLaunchKernelGGL(k_unprotect<false>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    if (a.small_ctr) {
+        const uint32_t bm = std::min<uint32_t>(b, (uint32_t)kMacBlock);
+        hipLaunchKernelGGL(k_unprotect<true>, dim3((a.n + bm - 1) / bm), dim3(bm), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_unprotect<false>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    }
     return hipGetLastError();
 }
 hipError_t launch_skein(const BundleArgs &a, hipStream_t s) {
@@ -4851,8 +4875,12 @@ hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s) {
 
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
     const uint32_t b = aes_block(a.n, (uint32_t)kAesBlock);
-    if (a.small_ctr) hipLaunchKernelGGL(k_protect<true>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
-    else hipLaunchKernelGGL(k_protect<false>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    if (a.small_ctr) {
+        const uint32_t bm = std::min<uint32_t>(b, (uint32_t)kMacBlock);
+        hipLaunchKernelGGL(k_protect<true>, dim3((a.n + bm - 1) / bm), dim3(bm), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_protect<false>, dim3((a.n + b - 1) / b), dim3(b), 0, s, a);
+    }
     return hipGetLastError();
 }
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s) {
