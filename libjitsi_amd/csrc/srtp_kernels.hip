@@ -90,21 +90,24 @@ constexpr int kMacBlock = 256;   // at most, the MacOnly instances' (small bundl
 constexpr int kUnprotectBlock = SRTP_UNPROTECT_BLOCK; // k_unprotect's workgroup size
 
 __device__ __forceinline__ void fill_te4(uint32_t *s_te) {
-    // 8 table loads in flight per thread, then their stores (a workgroup of a
-    // few waves, as small bundles run, otherwise waits out one load per word)
-    constexpr int U = 8;
-    for (int i0 = threadIdx.x; i0 < kTeWords; i0 += U * blockDim.x) {
-        uint32_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int i = i0 + u * (int)blockDim.x;
-            v[u] = i < kTeWords ? d_te0[(i >> 6) & 255] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int i = i0 + u * (int)blockDim.x;
-            const int t = ((i >> 14) << 1) | ((i >> 5) & 1);
-            if (i < kTeWords) s_te[i] = t ? rotl(v[u], 8u * (uint32_t)t) : v[u];
+    // Entry e of te0 fills words (h << 14) | (e << 6) | l (h = 0, 1; l =
+    // 0..63) of table t = 2h + (l >> 5), rotated left by 8t.  Wave w of W
+    // takes entries w, w + W, ...: one te0 load per lane for up to 64 of
+    // them, then per entry a broadcast (readlane) and two stores per lane to
+    // consecutive words (no bank conflicts) -- one memory round trip per
+    // workgroup instead of one per 8 words per thread.  blockDim.x is a
+    // multiple of 64.
+    const int W = (int)(blockDim.x >> 6), w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+    const uint32_t r = (uint32_t)(lane >> 5) << 3;
+    for (int j0 = 0; w + j0 * W < 256; j0 += 64) {
+        const int ej = w + (j0 + lane) * W;
+        const uint32_t mine = ej < 256 ? d_te0[ej] : 0u;
+        for (int k = 0; k < 64; k++) {
+            const int e = w + (j0 + k) * W;
+            if (e >= 256) break;
+            const uint32_t v = __builtin_amdgcn_readlane(mine, k);
+            s_te[(e << 6) | lane] = rotl(v, r);
+            s_te[(1 << 14) | (e << 6) | lane] = rotl(v, r + 16u);
         }
     }
     __syncthreads();
@@ -3304,6 +3307,17 @@ __device__ __forceinline__ void store_chunk(uint8_t *pkt, int b, const Ctr &cs, 
             qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
 }
 
+// A MacOnly instance (a small bundle: k_ctr_small ciphers the AES-CM +
+// HMAC-SHA1 packets) needs the T-tables only for the other AES-CM packets of
+// its workgroup (a NULL or Skein MAC): a workgroup of AES-CM + HMAC-SHA1
+// packets alone skips the 128-KB fill.  Conservative: any other key set fills.
+__device__ __forceinline__ bool mac_only_needs_te(const BundleArgs &a, uint32_t slot) {
+    if (slot == kNoSlot) return false;
+    const KeySet *ks = a.keysets + a.ctx[slot].ks;
+    const int32_t ext = ks->ext, enc = ks->enc_type, auth = ks->auth_type;
+    return !((ext == 0) & (enc == SRTP_AESCM_ENCRYPTION) & (auth == SRTP_HMACSHA1_AUTHENTICATION));
+}
+
 // ============================================================== k_protect
 // Fused protect, one lane per packet: AES-CM in place (SRTPCipherCTR.process
 // :94-121) + HMAC-SHA1 over the ciphertext (authenticatePacketHMAC :269-278)
@@ -3551,7 +3565,8 @@ __global__ __launch_bounds__(MacOnly ? kMacBlock : kAesBlock) void k_protect(Bun
     if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t p = i < a.n ? lane_packet(a, i) : i;
-    fill_te4(s_te); // ends with a barrier
+    if (!MacOnly || __syncthreads_or(i < a.n && mac_only_needs_te(a, a.p_slot[p])))
+        fill_te4(s_te); // ends with a barrier
     STAMP(1);
     int32_t fs = -1;
     if (i < a.n) {
@@ -3901,7 +3916,7 @@ __global__ __launch_bounds__(MacOnly ? kMacBlock : kUnprotectBlock) void k_unpro
         st = a.ctx[slot];
         lng = pos >= kLongRank && a.sk_out[pos - kLongRank] == slot;
     }
-    fill_te4(s_te);
+    if (!MacOnly || __syncthreads_or(todo && mac_only_needs_te(a, slot))) fill_te4(s_te);
     STAMP(1);
     if (!live) return;
     // The ROC speculated on is the walk's guess were the packet its context's
@@ -4777,7 +4792,9 @@ hipError_t launch_walk(const BundleArgs &a, int limit_pass, hipStream_t s) {
 constexpr int kCtrSmallBlock = 256;
 
 __device__ __forceinline__ bool small_ctr_ks(const KeySet *ks) {
-    return ks->ext == 0 && ks->enc_type == SRTP_AESCM_ENCRYPTION && ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
+    // the three fields loaded together (no short-circuit chain of loads)
+    const int32_t ext = ks->ext, enc = ks->enc_type, auth = ks->auth_type;
+    return (ext == 0) & (enc == SRTP_AESCM_ENCRYPTION) & (auth == SRTP_HMACSHA1_AUTHENTICATION);
 }
 
 // finish_status without its stores (k_protect makes them)
@@ -4790,39 +4807,44 @@ __device__ __forceinline__ int32_t peek_status(const BundleArgs &a, uint32_t p) 
     return st;
 }
 
-// packet p's keystream job: [start, end) under iv with key set ks, or false
+// packet p's keystream job: [start, end) under iv with key set ks, or false.
+// The per-packet words are loaded together up front (one memory round trip,
+// not one per test), then the context's key set and the packet header.
 __device__ __forceinline__ bool ctr_small_job(const BundleArgs &a, uint32_t p, int &start, int &end,
                                               uint32_t iv[4], const KeySet *&ks) {
     const uint32_t slot = a.p_slot[p];
+    const uint32_t o = a.off[p], cap = a.cap[p];
+    const uint32_t L = a.reverse ? a.len[p] : a.w_len[p];
+    const uint32_t cw = a.reverse ? a.g0[p] : a.w_cw[p];
+    const uint32_t sp = a.reverse ? a.spec[p] : 0u;
     if (slot == kNoSlot) return false;
+    if (a.reverse && !(sp & kSpecDid)) return false; // k_unprotect did not speculate
     if (!a.reverse && peek_status(a, p) != SRTP_STATUS_OK) return false;
     ks = a.keysets + a.ctx[slot].ks;
-    if (!small_ctr_ks(ks)) return false;
-    if (a.reverse && !(a.spec[p] & kSpecDid)) return false; // k_unprotect did not speculate
-    const uint8_t *pkt = a.seg + a.off[p];
+    const uint8_t *pkt = a.seg + o;
     const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    if (!small_ctr_ks(ks)) return false;
     const bool rtcp = ks->kind == SRTP_KIND_RTCP;
     const int T = ks->tag_len;
     if (!a.reverse) { // protect_one's region and IV
-        end = (int)a.w_len[p] - T - (rtcp ? 4 : 0);
+        end = (int)L - T - (rtcp ? 4 : 0);
         if (rtcp) {
             start = 8;
-            make_iv_rtcp(ks, hdr, a.w_cw[p], iv);
+            make_iv_rtcp(ks, hdr, cw, iv);
         } else {
-            start = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-            make_iv_rtp(ks, hdr, a.w_cw[p], iv);
+            start = rtp_header_len(pkt, hdr.x & 0xffu, (int)cap);
+            make_iv_rtp(ks, hdr, cw, iv);
         }
     } else { // unprotect_one's speculative decryption
-        const int L = (int)a.len[p];
         if (rtcp) {
-            const int io = L - 4 - T;
+            const int io = (int)L - 4 - T;
             start = 8;
             end = io;
             make_iv_rtcp(ks, hdr, ld_be32(pkt + io) & 0x7FFFFFFFu, iv);
         } else {
-            start = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
-            end = L - T;
-            make_iv_rtp(ks, hdr, a.g0[p], iv);
+            start = rtp_header_len(pkt, hdr.x & 0xffu, (int)cap);
+            end = (int)L - T;
+            make_iv_rtp(ks, hdr, cw, iv);
         }
     }
     return end > start;
@@ -4833,6 +4855,32 @@ __device__ __forceinline__ void xor_ks16(uint8_t *dst, int lim, const uint32_t x
 #pragma unroll
     for (int i = 0; i < 16; i++)
         if (i < lim) dst[i] ^= (uint8_t)(x[i >> 2] >> (8 * (i & 3)));
+}
+
+// XOR keystream blocks x, y over the 32 bytes at pkt + o, up to end: o is a
+// multiple of 4 (a 16-B aligned packet, a header of whole words), so the two
+// blocks are eight words -- all eight loaded before any store, the bytes of
+// the last word past end XORed with zero (only this lane touches that word
+// in this kernel)
+__device__ __forceinline__ void xor_ks32(uint8_t *pkt, int o, int end, const uint32_t x[4], const uint32_t y[4]) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(pkt + o);
+    uint32_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = o + 4 * i < end ? w[i] : 0u;
+    // every result before the first store: one wait for the eight loads, not
+    // one per (conditional) store
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int r = end - (o + 4 * i);
+        const uint32_t k = i < 4 ? x[i] : y[i - 4];
+        v[i] ^= r >= 4 ? k : (r > 0 ? k & ((1u << (8 * r)) - 1u) : 0u);
+    }
+    // the compiler sinks the XORs into the conditional stores and then waits
+    // for memory before each one: wait once (vmcnt 0) here instead
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (o + 4 * i < end) w[i] = v[i];
 }
 
 __global__ __launch_bounds__(kCtrSmallBlock) void k_ctr_small(BundleArgs a) {
@@ -4859,8 +4907,12 @@ __global__ __launch_bounds__(kCtrSmallBlock) void k_ctr_small(BundleArgs a) {
             ctr_input(iv, j, x);
             ctr_input(iv, j + 1, y);
             aes_encrypt2_v(lds, tb, k0, x, y);
-            xor_ks16(pkt + start + 16 * j, end - (start + 16 * j), x);
-            if (j + 1 < nblk) xor_ks16(pkt + start + 16 * (j + 1), end - (start + 16 * (j + 1)), y);
+            if ((start & 3) == 0) {
+                xor_ks32(pkt, start + 16 * j, end, x, y);
+            } else { // not a header of whole words: byte by byte
+                xor_ks16(pkt + start + 16 * j, end - (start + 16 * j), x);
+                if (j + 1 < nblk) xor_ks16(pkt + start + 16 * (j + 1), end - (start + 16 * (j + 1)), y);
+            }
         }
     }
 }

@@ -13,9 +13,13 @@
 // over one engine or a G-shard dispatcher (all shards on device 0 of a one-GPU
 // box).  1200-B RTP packets, AES_CM_128_HMAC_SHA1_80 protect, each thread its
 // own SSRCs.  Prints one JSON line per (path, shards, threads): calls/s and
-// the per-call latency percentiles.
+// the per-call latency percentiles.  With "rt" each protected packet is then
+// unprotected by a receiving transformer of the same keys (the
+// reverseTransform call of the receive side), timed on its own: calls count
+// both calls, "lat_us" the protect calls and "lat_unprotect_us" the unprotect
+// calls.
 //
-//   sync_bench [seconds-per-point] [path shards threads]   (one point: e.g. "one 0 1")
+//   sync_bench [seconds-per-point] [path shards threads [rt]]   (one point: e.g. "one 0 1")
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -57,7 +61,9 @@ double pct(std::vector<uint32_t> &v, double q) {
 
 int main(int argc, char **argv) {
     const double seconds = argc > 1 ? atof(argv[1]) : 2.0;
-    const uint32_t L = 1200, BUF = L + 16; // room behind the packet: the tag is appended in place
+    // packet length: 1200 B, or SYNC_LEN (the per-block cost of the MAC chain)
+    const uint32_t L = getenv("SYNC_LEN") ? (uint32_t)atoi(getenv("SYNC_LEN")) : 1200u;
+    const uint32_t BUF = L + 16; // room behind the packet: the tag is appended in place
     const int n_tr = 50;
     srtp_policy pol = {SRTP_AESCM_ENCRYPTION, 16, SRTP_HMACSHA1_AUTHENTICATION, 20, 10, 14};
     const int shard_counts[] = {0, 8};
@@ -65,6 +71,7 @@ int main(int argc, char **argv) {
     const bool one_point = argc > 4;
     const int p_only = one_point ? (strcmp(argv[2], "one") == 0 ? 0 : 1) : -1;
     const int g_only = one_point ? atoi(argv[3]) : -1, t_only = one_point ? atoi(argv[4]) : -1;
+    const bool rt = argc > 5 && strcmp(argv[5], "rt") == 0;
     for (int path = 0; path < 2; path++) {
         for (int G : shard_counts) {
             for (int T : thread_counts) {
@@ -80,7 +87,7 @@ int main(int argc, char **argv) {
                 o.max_transformers = 128;
                 srtp_engine *e = nullptr;
                 srtp_dispatch *d = nullptr;
-                std::vector<int32_t> tr((size_t)n_tr);
+                std::vector<int32_t> tr((size_t)n_tr), trr((size_t)n_tr);
                 if (G == 0) check(srtp_engine_create(&o, &e), "engine");
                 else {
                     std::vector<int32_t> devs((size_t)G, 0);
@@ -95,6 +102,12 @@ int main(int argc, char **argv) {
                             : srtp_factory_create(e, 1, key, 16, salt, 14, &pol, &pol, &f), "factory");
                     check(d ? srtp_dispatch_transformer_create(d, SRTP_KIND_RTP, f, f, &tr[(size_t)t])
                             : srtp_transformer_create(e, SRTP_KIND_RTP, f, f, &tr[(size_t)t]), "transformer");
+                    if (!rt) continue;
+                    int32_t fr = -1;
+                    check(d ? srtp_dispatch_factory_create(d, 0, key, 16, salt, 14, &pol, &pol, &fr)
+                            : srtp_factory_create(e, 0, key, 16, salt, 14, &pol, &pol, &fr), "factory");
+                    check(d ? srtp_dispatch_transformer_create(d, SRTP_KIND_RTP, fr, fr, &trr[(size_t)t])
+                            : srtp_transformer_create(e, SRTP_KIND_RTP, fr, fr, &trr[(size_t)t]), "transformer");
                 }
                 srtp_aggregator *a = nullptr;
                 if (path == 0) {
@@ -107,7 +120,7 @@ int main(int argc, char **argv) {
                 }
                 std::atomic<bool> stop{false};
                 std::atomic<int> started{0};
-                std::vector<std::vector<uint32_t>> lat((size_t)T);
+                std::vector<std::vector<uint32_t>> lat((size_t)T), latu((size_t)T);
                 std::vector<uint64_t> bad((size_t)T, 0);
                 std::vector<std::thread> th;
                 for (int k = 0; k < T; k++) {
@@ -122,14 +135,16 @@ int main(int argc, char **argv) {
                         const int n_ssrc = 3;
                         uint16_t seq[n_ssrc];
                         for (auto &x : seq) x = (uint16_t)(rng >> 40), rng = rng * 6364136223846793005ull + 1;
-                        std::vector<uint32_t> &mine = lat[(size_t)k];
+                        std::vector<uint32_t> &mine = lat[(size_t)k], &mineu = latu[(size_t)k];
                         mine.reserve(1u << 20);
+                        if (rt) mineu.reserve(1u << 20);
                         started++;
                         uint64_t n = 0;
                         while (!stop.load(std::memory_order_relaxed)) {
                             const int s = (int)(n % n_ssrc);
                             const uint32_t ssrc = 0x20000000u + (uint32_t)k * 16u + (uint32_t)s;
-                            const int32_t t = tr[(size_t)((k * n_ssrc + s) % n_tr)];
+                            const int ti = (k * n_ssrc + s) % n_tr;
+                            const int32_t t = tr[(size_t)ti];
                             const uint16_t q = seq[s]++;
                             buf[2] = (uint8_t)(q >> 8); buf[3] = (uint8_t)q;
                             buf[8] = (uint8_t)(ssrc >> 24); buf[9] = (uint8_t)(ssrc >> 16);
@@ -151,6 +166,24 @@ int main(int argc, char **argv) {
                             mine.push_back((uint32_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
                             if (st != SRTP_STATUS_OK || len != L + 10) bad[(size_t)k]++;
                             n++;
+                            if (!rt) continue;
+                            // the receive side: reverseTransform of the packet just protected
+                            const int32_t tu = trr[(size_t)ti];
+                            const uint32_t plen = len;
+                            const auto u0 = Clock::now();
+                            if (path == 0) {
+                                check(srtp_rawpacket_transform_one(a, 1, tu, buf.data(), BUF, 0, &len, 0, &st, &need,
+                                                                   grow.data(), (uint32_t)grow.size()), "one");
+                            } else {
+                                uint8_t *bp = buf.data();
+                                uint32_t bl = BUF, off = 0, fl = 0;
+                                int32_t thrown = -1;
+                                check(srtp_rawpacket_transform(b, 1, nullptr, tu, &bp, &bl, &off, &len, &fl, &st, &need, 1,
+                                                               &thrown), "array");
+                            }
+                            const auto u1 = Clock::now();
+                            mineu.push_back((uint32_t)std::chrono::duration_cast<std::chrono::nanoseconds>(u1 - u0).count());
+                            if (st != SRTP_STATUS_OK || len != plen - 10) bad[(size_t)k]++;
                         }
                         if (b) srtp_rawpacket_batch_destroy(b);
                     });
@@ -161,10 +194,11 @@ int main(int argc, char **argv) {
                 stop = true;
                 for (auto &x : th) x.join();
                 const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
-                std::vector<uint32_t> all;
+                std::vector<uint32_t> all, allu;
                 uint64_t nbad = 0;
                 for (int k = 0; k < T; k++) {
                     all.insert(all.end(), lat[(size_t)k].begin(), lat[(size_t)k].end());
+                    allu.insert(allu.end(), latu[(size_t)k].begin(), latu[(size_t)k].end());
                     nbad += bad[(size_t)k];
                 }
                 uint64_t acc = 0, comp = 0, bundles = 0;
@@ -175,13 +209,17 @@ int main(int argc, char **argv) {
                 double mean = 0;
                 for (uint32_t x : all) mean += x;
                 mean = all.empty() ? 0 : mean / all.size() / 1000.0;
-                const size_t calls = all.size();
+                const size_t calls = all.size() + allu.size();
+                char ul[160] = "";
+                if (rt)
+                    snprintf(ul, sizeof ul, "\"lat_unprotect_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f}, ",
+                             pct(allu, 0.5), pct(allu, 0.9), pct(allu, 0.99), pct(allu, 0.999));
                 printf("{\"path\": \"%s\", \"shards\": %d, \"dispatcher\": %s, \"threads\": %d, \"transformers\": %d, "
                        "\"pkt_len\": %u, \"calls\": %zu, \"seconds\": %.3f, \"calls_per_s\": %.1f, "
                        "\"lat_us\": {\"mean\": %.1f, \"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f}, "
-                       "\"bundles\": %llu, \"packets_per_bundle\": %.1f, \"not_ok\": %llu}\n",
+                       "%s\"bundles\": %llu, \"packets_per_bundle\": %.1f, \"not_ok\": %llu}\n",
                        path == 0 ? "one" : "array", G ? G : 1, G ? "true" : "false", T, n_tr, L, calls, dt,
-                       calls / dt, mean, pct(all, 0.5), pct(all, 0.9), pct(all, 0.99), pct(all, 0.999),
+                       calls / dt, mean, pct(all, 0.5), pct(all, 0.9), pct(all, 0.99), pct(all, 0.999), ul,
                        (unsigned long long)bundles, bundles ? (double)comp / bundles : 0.0,
                        (unsigned long long)nbad);
                 fflush(stdout);
