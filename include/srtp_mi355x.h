@@ -319,6 +319,13 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
  * copy on the engine's stream (their round trip is fixed costs, and two
  * cross-stream events are among them); larger ones use the copy streams. */
 #define SRTP_PIPE_ONE_STREAM 0x1u
+/* SRTP_PIPE_POLL_CROWDED: a wait on this pipeline polls the bundle's event
+ * (sleeping between polls) instead of spinning in hipEventSynchronize while
+ * more than SRTP_PIPE_SPIN_WAITERS (env, default 4) threads of the process
+ * wait on such pipelines -- for one pipeline per caller thread (the 1-packet
+ * RawPacket path): 64 spinning callers took the host's cores from the threads
+ * enqueueing the next bundles.  Few waiters keep the spin's quicker wake-up. */
+#define SRTP_PIPE_POLL_CROWDED 0x2u
 int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes, int32_t depth,
                             uint32_t flags, srtp_pipeline **out);
 /* srtp_pipeline_submit with the bundle's abort-on-throw chosen per bundle:

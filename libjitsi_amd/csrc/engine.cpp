@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -1294,6 +1295,7 @@ struct srtp_pipeline {
     size_t max_seg = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     bool one_stream = false; // SRTP_PIPE_ONE_STREAM: copies on the engine's stream (s_in / s_out not owned)
+    bool poll_crowded = false; // SRTP_PIPE_POLL_CROWDED
     std::mutex mu;
     struct Slot {
         srtp_pipeline_slot h{};     // pinned host arrays
@@ -1353,7 +1355,7 @@ int srtp_pipeline_create(srtp_engine *e, uint32_t max_packets, size_t max_seg_by
 int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg_bytes, int32_t depth,
                             uint32_t flags, srtp_pipeline **out) {
     if (!e || !out || depth < 1 || depth > 16 || max_packets == 0 || max_packets > kRecIdxMask ||
-        (flags & ~(uint32_t)SRTP_PIPE_ONE_STREAM))
+        (flags & ~(uint32_t)(SRTP_PIPE_ONE_STREAM | SRTP_PIPE_POLL_CROWDED)))
         return SRTP_EINVAL;
     *out = nullptr;
     srtp_pipeline *pl = new (std::nothrow) srtp_pipeline();
@@ -1364,6 +1366,7 @@ int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg
     pl->slots.resize((size_t)depth);
     DeviceGuard guard(e->opts.device);
     pl->one_stream = (flags & SRTP_PIPE_ONE_STREAM) != 0;
+    pl->poll_crowded = (flags & SRTP_PIPE_POLL_CROWDED) != 0;
     if (pl->one_stream) pl->s_in = pl->s_out = e->stream;
     bool ok = guard.ok && (pl->one_stream || (hipStreamCreateWithFlags(&pl->s_in, hipStreamNonBlocking) == hipSuccess &&
                                               hipStreamCreateWithFlags(&pl->s_out, hipStreamNonBlocking) == hipSuccess));
@@ -1411,12 +1414,29 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
 }
 
 // How a pipeline waits for a bundle (SRTP_PIPE_WAIT_US): < 0 (default)
-// hipEventSynchronize; >= 0 polls hipEventQuery, yielding the CPU between
-// polls, and after that many microseconds sleeps 20 us between polls -- so
-// many lane threads waiting at once (an aggregator lane per shard) leave the
-// host's cores to the producers.
-static int wait_event(hipEvent_t ev) {
-    static const long spin_us = getenv("SRTP_PIPE_WAIT_US") ? atol(getenv("SRTP_PIPE_WAIT_US")) : -1;
+// hipEventSynchronize, which spins on a core; >= 0 polls hipEventQuery,
+// yielding the CPU between polls, and after that many microseconds sleeps
+// 20 us between polls.  A SRTP_PIPE_POLL_CROWDED pipeline's wait also polls
+// (at once) when more than SRTP_PIPE_SPIN_WAITERS (4) threads are waiting on
+// such pipelines: 64 callers each spinning on its own 1-packet bundle took the
+// host's cores from the threads enqueueing the next bundles (4.7k calls/s,
+// p99 82 ms; polling 12.9k, 4.7 ms).  Other pipelines (aggregator lanes,
+// dispatcher shards: a few waiters) always keep the spin's wake-up.
+static std::atomic<int> g_crowd{0};
+
+static int wait_event(hipEvent_t ev, bool crowd) {
+    static const long env_us = getenv("SRTP_PIPE_WAIT_US") ? atol(getenv("SRTP_PIPE_WAIT_US")) : -1;
+    static const int spin_waiters =
+        getenv("SRTP_PIPE_SPIN_WAITERS") ? atoi(getenv("SRTP_PIPE_SPIN_WAITERS")) : 4;
+    struct Crowd {
+        bool on;
+        int n;
+        explicit Crowd(bool c) : on(c), n(c ? g_crowd.fetch_add(1, std::memory_order_relaxed) + 1 : 0) {}
+        ~Crowd() {
+            if (on) g_crowd.fetch_sub(1, std::memory_order_relaxed);
+        }
+    } cr(crowd);
+    const long spin_us = env_us < 0 && cr.n > spin_waiters ? 0 : env_us;
     if (spin_us < 0) return hipEventSynchronize(ev) == hipSuccess ? 0 : -1;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
@@ -1431,7 +1451,7 @@ static int wait_event(hipEvent_t ev) {
 static int pipeline_wait_locked(srtp_pipeline *pl, srtp_pipeline::Slot &sl) {
     if (!sl.busy) return SRTP_OK;
     sl.busy = false;
-    if (wait_event(sl.ev_out) != 0) return fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
+    if (wait_event(sl.ev_out, pl->poll_crowded) != 0) return fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
     if (const uint32_t n = sl.packed_n) { // lengths and statuses to the slot's own arrays
         memcpy(sl.h.len, sl.h_pack + 4 * (size_t)n, n * 4ull);
         memcpy(sl.h.status, sl.h_pack + 5 * (size_t)n, n * 4ull);

@@ -86,7 +86,7 @@ int stage(srtp_rawpacket_batch *b, uint32_t n, size_t bytes) {
             const uint32_t np = std::max<uint32_t>(std::max<uint32_t>(n, 64), b->pl_packets * 2);
             const size_t nb = std::max<size_t>(std::max<size_t>(bytes, (size_t)1 << 16), b->pl_bytes * 2);
             // one synchronous bundle at a time: no copy streams to overlap
-            const int rc = srtp_pipeline_create_ex(b->e, np, nb, 1, SRTP_PIPE_ONE_STREAM, &b->pl);
+            const int rc = srtp_pipeline_create_ex(b->e, np, nb, 1, SRTP_PIPE_ONE_STREAM | SRTP_PIPE_POLL_CROWDED, &b->pl);
             if (rc != SRTP_OK) return rc;
             b->pl_packets = np;
             b->pl_bytes = nb;

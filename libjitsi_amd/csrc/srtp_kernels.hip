@@ -199,6 +199,14 @@ __device__ __forceinline__ void ctr_chunk(const char *__restrict__ lds, const Te
 }
 
 // ----------------------------------------------------------------- SHA-1
+// (xor3 is defined with the AES helpers below)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c);
+
+// One block.  Each step in single gfx950 instructions: the schedule word
+// xor3 + xor + rotate, f one v_bitop3 (Ch 0xCA, parity 0x96, Maj 0xE8),
+// e + k + w and rotl(a, 5) + f + (e + k + w) one v_add3 each -- five VALU
+// per round, where the plain expressions took about eight (a lone packet's
+// MAC is this chain: the per-packet path's latency).
 __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
 #pragma unroll
@@ -207,15 +215,16 @@ __device__ __forceinline__ void sha1_compress(uint32_t h[5], uint32_t w[16]) {
         if (t < 16) {
             wt = w[t];
         } else {
-            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
             w[t & 15] = wt;
         }
         uint32_t f, k;
-        if (t < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
-        else if (t < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
-        else if (t < 60) { f = (b & c) | (d & (b | c)); k = 0x8F1BBCDCu; }
-        else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
-        uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+        if (t < 20) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA); k = 0x5A827999u; }
+        else if (t < 40) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0x6ED9EBA1u; }
+        else if (t < 60) { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8); k = 0x8F1BBCDCu; }
+        else { f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96); k = 0xCA62C1D6u; }
+        const uint32_t ekw = e + k + wt;
+        const uint32_t tmp = rotl(a, 5) + f + ekw;
         e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
@@ -3325,28 +3334,29 @@ __device__ __forceinline__ bool mac_only_needs_te(const BundleArgs &a, uint32_t 
 // Block b of a packet for the MAC: the 16-B pieces that start before lim
 // (as the generic loops load them), zeros after.
 __device__ __forceinline__ void load_block16(const uint8_t *pkt, int b, int lim, uint32_t w[16]) {
-    const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
+    // Branch-free: every piece is loaded -- one at or past lim from the
+    // packet's first 16 bytes (inside its region), then zeroed -- so that the
+    // compiler counts the loads in flight exactly: conditional loads made it
+    // wait for all of them (vmcnt 0), the look-ahead's included, each block.
+    const uint4 *qp = reinterpret_cast<const uint4 *>(pkt);
 #pragma unroll
     for (int m = 0; m < 4; m++) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (64 * b + 16 * m < lim) v = qp[m];
-        w[4 * m] = v.x; w[4 * m + 1] = v.y; w[4 * m + 2] = v.z; w[4 * m + 3] = v.w;
+        const int o = 64 * b + 16 * m;
+        const bool ok = o < lim;
+        const uint4 v = qp[ok ? (o >> 4) : 0];
+        w[4 * m] = ok ? v.x : 0u; w[4 * m + 1] = ok ? v.y : 0u;
+        w[4 * m + 2] = ok ? v.z : 0u; w[4 * m + 3] = ok ? v.w : 0u;
     }
 }
 
 // load_block16 for blocks below nb, zeros for the rest (the MAC's padding blocks)
 __device__ __forceinline__ void load_or_zero16(const uint8_t *pkt, int b, int nb, int lim, uint32_t w[16]) {
-    if (b < nb) {
-        load_block16(pkt, b, lim, w);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; k++) w[k] = 0u;
-    }
+    load_block16(pkt, b, b < nb ? lim : 0, w);
 }
 
 // The MAC-only loops' look-ahead: the next kMacAhead blocks of a packet held
 // in registers, the oldest handed out and the one after the newest loaded.
-constexpr int kMacAhead = 4;
+constexpr int kMacAhead = 2; // ~3 us of loads in flight at ~1.5 us per block; each more costs 16 moves per block
 struct MacRing {
     uint32_t q[kMacAhead][16];
     __device__ __forceinline__ void fill(const uint8_t *pkt, int b0, int nb, int lim) {
@@ -3362,6 +3372,10 @@ struct MacRing {
 #pragma unroll
             for (int m = 0; m < 16; m++) q[k][m] = q[k + 1][m];
         load_or_zero16(pkt, b + kMacAhead, nb, lim, q[kMacAhead - 1]);
+        // a compiler-only barrier: without it the loop carries no loaded
+        // values -- memory being unchanged, the compiler re-loads each block
+        // where it is hashed, and the look-ahead is gone
+        asm volatile("" ::: "memory");
     }
 };
 
