@@ -749,18 +749,22 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (a.abort_on_error) e->emin_filled[c] = 0u;
     if (need_ctl) HIPCHK(e, hipMemsetAsync(a.ctl, 0, sizeof(BundleCtl), s));
     if (need_emin) HIPCHK(e, hipMemsetAsync(a.e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
+    // a one-tile bundle is sorted by one workgroup in one launch
+    // (SRTP_SORT_TILE=0: the multi-pass sort); SRTP_SORT_TILE=2: parsed by the
+    // same workgroup in the same launch (k_parse_sort_tile)
+    static const int tile_sort = getenv("SRTP_SORT_TILE") ? atoi(getenv("SRTP_SORT_TILE")) : 1;
+    const bool one_tile = tile_sort && n <= sort_tile_records();
     {
         StageTimer t(e, s, SRTP_STAGE_PARSE);
-        HIPCHK(e, launch_parse(a, s)); // also resets control block c ^ 1
+        // also resets control block c ^ 1
+        HIPCHK(e, one_tile && tile_sort == 2 ? launch_parse_sort_tile(a, s) : launch_parse(a, s));
     }
     e->ctl_clean[c ^ 1] = true;
     if (a.abort_on_error) e->emin_filled[c ^ 1] = a.n_transformers;
     e->ctl_cur = c ^ 1;
-    {
+    if (!(one_tile && tile_sort == 2)) {
         StageTimer t(e, s, SRTP_STAGE_SORT);
-        // a one-tile bundle: one launch (SRTP_SORT_TILE=0: the multi-pass sort, for A/B)
-        static const bool tile_sort = !getenv("SRTP_SORT_TILE") || atoi(getenv("SRTP_SORT_TILE")) != 0;
-        HIPCHK(e, tile_sort && n <= sort_tile_records() ? launch_sort_tile(a, s) : launch_sort(a, ss, s));
+        HIPCHK(e, one_tile ? launch_sort_tile(a, s) : launch_sort(a, ss, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);

@@ -109,6 +109,9 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
 // the whole sort of a bundle of at most sort_tile_records() packets in one
 // workgroup (one launch)
 hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s);
+// k_parse + the one-tile sort in one launch (a bundle of at most
+// sort_tile_records() packets)
+hipError_t launch_parse_sort_tile(const BundleArgs &a, hipStream_t s);
 // unprotect: fused tag check + speculative in-place decryption (before the walk)
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
 // Engines with Skein-MAC key sets.  Unprotect: those packets' tag check under

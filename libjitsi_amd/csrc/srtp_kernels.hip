@@ -1454,19 +1454,22 @@ hipError_t launch_sort_wide(const BundleArgs &a, const SortScratch &ss, hipStrea
 // records stable by key, spos as the last pass writes it, lord as the first.
 // It zeroes the tile's first-digit counts that k_parse accumulated (the walk
 // clears the other tables as after a multi-pass sort).
-__global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32_t key_bits, uint32_t bins) {
+// The one-tile sort of the records whose keys key_in[r] (record r *
+// kSortThreads + threadIdx.x) the calling workgroup holds: k_sort_tile loads
+// them, k_parse_sort_tile has just parsed them.
+__device__ __forceinline__ void sort_tile_body(const BundleArgs &a, uint32_t key_bits,
+                                               const uint32_t key_in[kSortItems]) {
     constexpr int W = kSortThreads / 64;
     __shared__ uint32_t s_key[2][kSortTile];
     __shared__ uint16_t s_idx[2][kSortTile];
     __shared__ uint32_t s_base[256], s_run[256], s_wcnt[W][256];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const uint32_t n = a.n;
-    for (uint32_t d = (uint32_t)t; d < bins; d += kSortThreads) a.sort_counts[d] = 0u;
 #pragma unroll
     for (int r = 0; r < kSortItems; r++) {
         const uint32_t i = r * kSortThreads + t;
         if (i < n) {
-            s_key[0][i] = a.sk_in[i];
+            s_key[0][i] = key_in[r];
             s_idx[0][i] = (uint16_t)i;
         }
     }
@@ -1564,10 +1567,65 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32
     }
 }
 
+__global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32_t key_bits, uint32_t bins) {
+    const int t = threadIdx.x;
+    for (uint32_t d = (uint32_t)t; d < bins; d += kSortThreads) a.sort_counts[d] = 0u;
+    uint32_t key[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = r * kSortThreads + t;
+        key[r] = i < a.n ? a.sk_in[i] : 0u;
+    }
+    sort_tile_body(a, key_bits, key);
+}
+
+// k_parse and k_sort_tile in one launch for a one-tile bundle (the per-packet
+// path's): the workgroup parses every packet (as k_parse: the records, the
+// class counts of the tile, the next bundle's control block), keeps the keys
+// in registers and sorts them.  No first-digit counts (the multi-pass sort's
+// input) are made, so none need zeroing.
+__global__ __launch_bounds__(kSortThreads) void k_parse_sort_tile(BundleArgs a, uint32_t key_bits) {
+    __shared__ uint32_t s_cls[32];
+    const int t = threadIdx.x;
+    if (t < 32) s_cls[t] = 0u;
+    __syncthreads();
+    if (t == 0) *a.ctl_next = BundleCtl{};
+    if (a.abort_on_error)
+        for (uint32_t i = (uint32_t)t; i < a.n_transformers; i += kSortThreads) a.e_min_next[i] = 0x7f7f7f7f;
+    uint32_t key[kSortItems];
+#pragma unroll
+    for (int r = 0; r < kSortItems; r++) {
+        const uint32_t i = r * kSortThreads + t;
+        key[r] = 0u;
+        if (i < a.n) {
+            atomicAdd(&s_cls[len_class(a.len[i])], 1u);
+            key[r] = parse_one(a, i);
+        }
+    }
+    __syncthreads();
+    if (t < 32) {
+        const uint32_t c = s_cls[t];
+        if (c) atomicAdd(&a.cls_tile[t], c);
+        const unsigned long long m = __ballot(c != 0u);
+        if (t == 0 && (uint32_t)m) atomicOr(&a.cls_tile[32], (uint32_t)m);
+    }
+    // the records (sv_in, read back by index) and the class counts (write_lord)
+    // before the sort reads them
+    __threadfence();
+    __syncthreads();
+    sort_tile_body(a, key_bits, key);
+}
+
 hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s) {
     const uint32_t key_bits = (uint32_t)a.sort_key_bits;
     const uint32_t bins = 1u << a.sort_bits; // k_parse's first-digit counts
     hipLaunchKernelGGL(k_sort_tile, dim3(1), dim3(kSortThreads), 0, s, a, key_bits, bins);
+    return hipGetLastError();
+}
+
+hipError_t launch_parse_sort_tile(const BundleArgs &a, hipStream_t s) {
+    if (a.n > (uint32_t)kSortTile) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_parse_sort_tile, dim3(1), dim3(kSortThreads), 0, s, a, (uint32_t)a.sort_key_bits);
     return hipGetLastError();
 }
 
