@@ -107,6 +107,8 @@ extern "C" {
 #define SRTP_EFULL -3   /* context / factory / transformer table full */
 #define SRTP_EDEVICE -4 /* HIP runtime error */
 #define SRTP_EPOLICY -5 /* policy outside the implemented ciphers x MACs (see srtp_factory_create) */
+#define SRTP_EAGAIN -6  /* srtp_queue_submit: the queue is full, or no slot is free while it holds
+                           completed packets -- reap, then submit again */
 
 typedef struct srtp_engine srtp_engine;
 
@@ -449,6 +451,59 @@ int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, 
 int srtp_aggregator_transformer_info(srtp_aggregator *a, int32_t t, int32_t *kind,
                                      int32_t *fwd_rtcp_tag_len);
 
+/* Completion queues: the asynchronous per-packet call.  The
+ * reference's connectors already queue: RTPConnectorOutputStream.write hands
+ * packets to a send thread that drains them (RTPConnectorOutputStream.java
+ * :652-830, runInSendThread :775), and the receive thread hands on every
+ * datagram (RTPConnectorInputStream.java:425-452,780-806).  Such a thread owns
+ * a queue, submits every packet it has and reaps the results, so it keeps
+ * many packets in flight instead of one.
+ *
+ * srtp_queue_submit: one packet as srtp_aggregator_transform takes it
+ * (copy_len bytes of pkt, length len, room cap >= copy_len) joins its lane's
+ * open bundle (the aggregator's sealing rules apply); cookie is the caller's.
+ * A packet with SRTP_PKT_FLAG_SKIP, or with len > cap (RawPacket.isInvalid),
+ * completes at once with SRTP_STATUS_SKIPPED / SRTP_STATUS_DROP_INVALID and
+ * no bytes.  Returns SRTP_EAGAIN when max_inflight packets are outstanding,
+ * or when no slot is free while the queue holds submitted or reaped
+ * packets: the caller reaps and submits again (only a queue with nothing
+ * outstanding waits for a slot).
+ *
+ * srtp_queue_reap: up to max completions, in SUBMISSION order (so per
+ * transformer and SSRC the reference's order), into out; with wait != 0 it
+ * blocks until at least one is there when any packet is outstanding.
+ * Returns the count.  out[i].data points at the packet's processed bytes in
+ * the aggregator's pinned slot (max(len, in_len) bytes, within cap; NULL for
+ * packets completed at submit) and stays valid until the next reap or
+ * destroy of this queue: reaping releases the previous reap's packets, and a
+ * slot is reused only when every packet of it has been released.
+ *
+ * A queue belongs to one thread at a time (submit and reap are not
+ * thread-safe on one queue); queues of one aggregator are independent.
+ * Packets of one direction and lane still run in the order the aggregator
+ * accepted them across all its producers.  srtp_queue_destroy waits for the
+ * queue's outstanding packets; every queue must be destroyed before its
+ * aggregator (srtp_aggregator_destroy waits for that).  Not from an
+ * aggregator callback (SRTP_EINVAL). */
+typedef struct srtp_queue srtp_queue;
+typedef struct {
+    uint64_t cookie;     /* as submitted */
+    int32_t status;      /* SRTP_STATUS_* (-1: the bundle could not be submitted) */
+    uint32_t len;        /* the packet's length after the call */
+    uint32_t in_len;     /* its length at submit */
+    int32_t reverse;     /* as submitted */
+    int32_t tid;         /* as submitted */
+    const uint8_t *data; /* processed bytes (see above) */
+} srtp_completion;
+int srtp_queue_create(srtp_aggregator *a, uint32_t max_inflight, srtp_queue **out);
+int srtp_queue_submit(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t *pkt, uint32_t copy_len,
+                      uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie);
+int srtp_queue_reap(srtp_queue *q, srtp_completion *out, uint32_t max, int32_t wait);
+/* packets submitted and not yet reaped */
+int32_t srtp_queue_outstanding(srtp_queue *q);
+srtp_aggregator *srtp_queue_aggregator(srtp_queue *q);
+void srtp_queue_destroy(srtp_queue *q);
+
 /* In-process multi-GPU dispatcher (SURVEY.md 8b engine_create(devices, opts),
  * 8e): one engine per shard, shard i on device devices[i] (a device may host
  * several shards).  A host bundle is split by shard = srtp_shard_of(SSRC)
@@ -510,6 +565,16 @@ int srtp_dispatch_host_times(srtp_dispatch *d, uint64_t ns[6]);
  * routes it: its SSRC's shard, shard 0 for a packet shorter than 12 bytes);
  * -1 for an unknown transformer.  Does not wait for bundles in flight. */
 int32_t srtp_dispatch_route(srtp_dispatch *d, int32_t tid, const uint8_t *pkt, uint32_t len);
+/* 1 when the reference could throw on this packet of a transformer of `kind`
+ * (SRTP_KIND_*) -- the per-packet test of srtp_dispatch_plan, a superset of the
+ * engine's SRTP_STATUS_ERR_MALFORMED: RawPacket.getHeaderLength,
+ * SRTPCipherCTR.process / SRTPCipherF8.process bounds, RawPacket.getSRTCPIndex
+ * -- for policies whose tag lengths are in tag_mask (bit T: tag length T, bit
+ * 0: NULL authentication); pkt holds cap bytes (a smaller cap only widens the
+ * superset: the header may then seem to end past it).  0 for a
+ * packet that is skipped or invalid (len < 12 or len > cap).  Host only. */
+int32_t srtp_packet_may_throw(int32_t kind, int32_t reverse, const uint8_t *pkt, uint32_t len, uint32_t cap,
+                              uint32_t flags, uint32_t tag_mask);
 /* The aggregator over a dispatcher: one lane per shard (its own pinned slots
  * and dispatch thread); each packet goes to the lane of its shard, so
  * per-packet submits from one process reach every GPU.  Callbacks of
@@ -549,6 +614,14 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
                              uint32_t *length, const uint32_t *flags, int32_t *status,
                              uint32_t *need_len, uint32_t n, int32_t *thrown);
 int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **data, uint32_t *len);
+/* Arrays of up to 8192 packets none of which can throw (srtp_packet_may_throw)
+ * then go through a completion queue of the batch on aggregator a -- whose
+ * lanes must be over the batch's engine or dispatcher -- instead of a bundle
+ * of their own: concurrent callers' arrays share bundles, and no caller waits
+ * behind another's GPU round trip.  The results are the same (no packet can
+ * throw, so abort-on-throw has nothing to stop); other arrays keep the batch's
+ * own bundle.  a = NULL turns this off. */
+int srtp_rawpacket_batch_set_aggregator(srtp_rawpacket_batch *b, srtp_aggregator *a);
 /* One RawPacket through SinglePacketTransformer.transform / reverseTransform
  * (RawPacket) (SinglePacketTransformer.java:113,169; every
  * RTPConnector*Stream call and DtlsPacketTransformer.transformSrtp,
@@ -566,6 +639,23 @@ int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **d
 int srtp_rawpacket_transform_one(srtp_aggregator *a, int32_t reverse, int32_t tid, uint8_t *buf,
                                  uint32_t buf_len, uint32_t offset, uint32_t *length, uint32_t flags,
                                  int32_t *status, uint32_t *need_len, uint8_t *grow, uint32_t grow_cap);
+/* The per-packet call, asynchronous (a connector's send thread
+ * or receive loop keeping many packets in flight): one RawPacket element as
+ * srtp_rawpacket_transform_one takes it (buf NULL or flags with
+ * SRTP_PKT_FLAG_SKIP: SKIPPED; *length past the buffer: DROP_INVALID, both
+ * completed at once) submitted to queue q (srtp_queue_submit; SRTP_EAGAIN:
+ * reap first).  Each completion reaped from q then goes back into its
+ * RawPacket by srtp_rawpacket_complete, given the buffer's bytes after the
+ * packet's offset (avail): *need_len == 0: *copy_len bytes of c->data go back
+ * in place at the offset; else the reference allocates a new buffer of
+ * *need_len bytes (RawPacket.append / grow) at offset 0 that receives
+ * *copy_len bytes of c->data.  Either way the RawPacket's length becomes
+ * c->len; SRTP_STATUS_ERR_MALFORMED is the reference's throw (the packet keeps
+ * its partial mutation), other non-OK statuses its null. */
+int srtp_rawpacket_submit(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t *buf, uint32_t buf_len,
+                          uint32_t offset, uint32_t length, uint32_t flags, uint64_t cookie);
+int srtp_rawpacket_complete(srtp_queue *q, const srtp_completion *c, uint32_t avail, uint32_t *copy_len,
+                            uint32_t *need_len);
 /* Devices the engine can use (hipGetDeviceCount; 0 without a GPU): what the
  * Java drop-in sizes its dispatcher with. */
 int32_t srtp_device_count(void);

@@ -30,8 +30,9 @@ ABI_VERSION = 3
 AGG_SEAL_IDLE = 0x1
 PKT_FLAG_DISCARD, PKT_FLAG_SILENCE, PKT_FLAG_SKIP = 0x2, 0x4, 0x80000000
 RC = {0: "SRTP_OK", -1: "SRTP_EINVAL", -2: "SRTP_ENOMEM", -3: "SRTP_EFULL", -4: "SRTP_EDEVICE",
-      -5: "SRTP_EPOLICY"}
+      -5: "SRTP_EPOLICY", -6: "SRTP_EAGAIN"}
 EFULL = -3
+EAGAIN = -6
 
 EXPORTED = [
     "srtp_engine_opts_default", "srtp_engine_create", "srtp_engine_destroy",
@@ -61,6 +62,9 @@ EXPORTED = [
     "srtp_aggregator_transformer_info", "srtp_rawpacket_transform_one", "srtp_device_count",
     "srtp_host_register", "srtp_host_unregister", "srtp_host_is_registered", "srtp_pipeline_submit_host",
     "srtp_pipeline_create_ex", "srtp_host_alloc", "srtp_host_free",
+    "srtp_queue_create", "srtp_queue_submit", "srtp_queue_reap", "srtp_queue_outstanding",
+    "srtp_queue_aggregator", "srtp_queue_destroy", "srtp_packet_may_throw",
+    "srtp_rawpacket_batch_set_aggregator", "srtp_rawpacket_submit", "srtp_rawpacket_complete",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -113,6 +117,13 @@ class DtlsKeys(C.Structure):
 class AggregatorOpts(C.Structure):
     _fields_ = [("max_packets", C.c_uint32), ("max_bytes", C.c_size_t), ("deadline_us", C.c_uint32),
                 ("depth", C.c_int32), ("flags", C.c_uint32)]
+
+
+class Completion(C.Structure):
+    """srtp_completion (include/srtp_mi355x.h)"""
+    _fields_ = [("cookie", C.c_uint64), ("status", C.c_int32), ("len", C.c_uint32),
+                ("in_len", C.c_uint32), ("reverse", C.c_int32), ("tid", C.c_int32),
+                ("data", C.POINTER(C.c_uint8))]
 
 
 AGG_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(C.c_uint8), C.c_uint32)
@@ -242,6 +253,20 @@ def lib() -> C.CDLL:
     L.srtp_dispatch_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_dispatch_stats.argtypes = [vp, C.POINTER(Stats)]
     L.srtp_dispatch_host_times.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.srtp_queue_create.argtypes = [vp, u32, C.POINTER(vp)]
+    L.srtp_queue_submit.argtypes = [vp, i32, i32, vp, u32, u32, u32, u32, C.c_uint64]
+    L.srtp_queue_reap.argtypes = [vp, C.POINTER(Completion), u32, i32]
+    L.srtp_queue_outstanding.argtypes = [vp]
+    L.srtp_queue_outstanding.restype = i32
+    L.srtp_queue_aggregator.argtypes = [vp]
+    L.srtp_queue_aggregator.restype = vp
+    L.srtp_queue_destroy.argtypes = [vp]
+    L.srtp_queue_destroy.restype = None
+    L.srtp_packet_may_throw.argtypes = [i32, i32, C.c_char_p, u32, u32, u32, u32]
+    L.srtp_packet_may_throw.restype = i32
+    L.srtp_rawpacket_batch_set_aggregator.argtypes = [vp, vp]
+    L.srtp_rawpacket_submit.argtypes = [vp, i32, i32, vp, u32, u32, u32, u32, C.c_uint64]
+    L.srtp_rawpacket_complete.argtypes = [vp, C.POINTER(Completion), u32, pu32, pu32]
     _lib = L
     return L
 

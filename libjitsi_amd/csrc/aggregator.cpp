@@ -68,6 +68,24 @@
 // when the bundle completes it copies each result back and wakes its caller.
 // While the lane has a bundle in flight the requests pile up on the stack and
 // go out together when it returns: bundles grow with the number of callers.
+// Before it places them the lane seals its open bundle of that direction, so a
+// thread's earlier submits run before its later synchronous call.
+//
+// Completion queues (srtp_queue_*): the asynchronous form of the per-packet
+// call for a thread that keeps many packets in flight (a connector's send
+// thread draining its queue, a receive loop).  A queue submit reserves and
+// fills an entry exactly like srtp_aggregator_submit, but the entry carries a
+// pointer to the queue's ring entry instead of a callback cookie.  When the
+// bundle completes, the lane thread only publishes each such entry's status,
+// length and a pointer to its bytes in the pinned slot (a few stores, no copy
+// and no upcall) and wakes the queue's owner if it sleeps; the owner reaps the
+// entries in submission order and copies the bytes out itself.  The slot stays
+// held (kHeld) until every reaped entry of it has been released -- at the
+// owner's next reap -- so a completed packet's bytes never move.  A submit
+// that finds no free slot while its queue still holds entries returns
+// SRTP_EAGAIN instead of waiting (the owner reaps, which releases slots):
+// only a queue with nothing outstanding may wait for a slot, so a thread never
+// waits on slots that only it can free.
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -76,6 +94,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string.h>
 #include <string>
 #include <thread>
@@ -90,7 +109,7 @@
 namespace {
 using Clock = std::chrono::steady_clock;
 
-enum SlotState { kFree, kOpen, kSealed, kInflight };
+enum SlotState { kFree, kOpen, kSealed, kInflight, kHeld };
 constexpr uint32_t kNoLen = 0xffffffffu; // h.len[i] until packet i's copy has finished
 constexpr uint32_t kBlock = 16;          // entries per producer block (a cache line of u32s)
 
@@ -130,6 +149,18 @@ struct SyncReq {
     Waiter w;
 };
 
+struct Slot;
+struct Lane;
+
+// A queue's ring entry (srtp_queue_submit .. srtp_queue_reap).
+struct QEntry {
+    std::atomic<uint32_t> ready{0}; // published by the lane thread (release)
+    srtp_completion c{};            // cookie / in_len / avail / reverse / tid at submit, the rest at completion
+    srtp_queue *q = nullptr;
+    Slot *slot = nullptr;           // held until released (nullptr: completed at submit)
+    Lane *lane = nullptr;
+};
+
 void futex_wait(std::atomic<uint32_t> *w, uint32_t v) {
     syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
 }
@@ -144,6 +175,8 @@ struct alignas(64) Block {
 
 struct Slot {
     SlotState state = kFree;                 // under the aggregator's lock
+    int idx = 0;
+    std::atomic<uint32_t> holds{0};          // kHeld: reaped-or-not queue entries + the lane's own
     std::atomic<uint32_t> gen{0};            // opened how often (producers' cached blocks)
     int32_t reverse = 0;
     uint32_t n = 0;                          // entries (with holes), final once sealed
@@ -155,6 +188,7 @@ struct Slot {
     std::vector<uint8_t> hole;
     std::vector<uint64_t> cookies;
     std::vector<Waiter *> waiters;           // non-null: a synchronous caller's entry
+    std::vector<QEntry *> qents;             // non-null: a completion queue's entry
     srtp_pipeline_slot h{};
 };
 
@@ -167,6 +201,7 @@ struct Parked {
 };
 
 struct Lane {
+    uint32_t idx = 0;
     srtp_engine *e = nullptr;
     srtp_pipeline *pl = nullptr;
     std::unique_ptr<Slot[]> slots;
@@ -212,6 +247,7 @@ struct srtp_aggregator {
     std::vector<std::unique_ptr<Lane>> lanes;
     std::atomic<bool> closing{false}; // destroy has begun: submits are refused
     std::atomic<int> sync_callers{0}; // srtp_aggregator_transform calls inside (destroy waits)
+    std::atomic<int> queues{0};       // live srtp_queue objects (destroy waits)
     bool stop = false;
     // transformer kinds, read without a lock (-2: not looked up yet)
     std::unique_ptr<std::atomic<int32_t>[]> kinds;
@@ -220,6 +256,18 @@ struct srtp_aggregator {
     int error = SRTP_OK;
     std::string last_error;
     std::thread flusher;
+};
+
+// A completion queue: one owner thread (or externally serialised callers).
+struct srtp_queue {
+    srtp_aggregator *a = nullptr;
+    uint32_t cap = 0;                  // ring entries: packets submitted and not yet reaped
+    std::unique_ptr<QEntry[]> ring;
+    uint64_t head = 0, tail = 0;       // next to reap, next to submit
+    uint64_t rel_from = 0, rel_to = 0; // the last reap's entries, released at the next
+    std::atomic<uint32_t> wake{0};     // futex word: bumped by a lane that saw `waiting`
+    std::atomic<uint32_t> waiting{0};  // the owner sleeps (or is about to) in srtp_queue_reap
+    std::atomic<uint32_t> lane_refs{0}; // lane threads between publishing entries and their wake-up
 };
 
 namespace {
@@ -432,9 +480,28 @@ void place_parked_locked(srtp_aggregator *a, Lane &ln, uint32_t lane) {
             if (!try_reserve(a, ln, lane, dir, need, s, i, off)) return; // cannot happen: need <= max_bytes
         }
         ln.slots[s].waiters[i] = nullptr;
+        ln.slots[s].qents[i] = nullptr;
         fill(ln, s, i, off, pk.tid, pk.pkt.data(), len, cap, need, pk.flags, pk.cookie, len);
         ln.parked.pop_front();
     }
+}
+
+// A completed slot none of whose queue entries is still held goes back to the
+// free list (under the lock): parked callback packets are placed first, then
+// an idle lane's open bundle is sealed.
+void slot_free_locked(srtp_aggregator *a, Lane &ln, Slot &sl) {
+    for (uint32_t i = 0; i < sl.n; i++) {
+        sl.h.len[i] = kNoLen;
+        sl.hole[i] = 0;
+    }
+    sl.state = kFree;
+    sl.n = sl.n_real = 0;
+    sl.bytes = 0;
+    place_parked_locked(a, ln, ln.idx);
+    seal_if_idle_locked(a, ln);
+    ln.cv_space.notify_all();
+    ln.cv_work.notify_all(); // synchronous requests may wait for a free slot
+    a->cv_idle.notify_all();
 }
 
 // Synchronous requests may be placed: some are waiting, a slot is free and
@@ -465,6 +532,8 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
     if (s < 0 || ln.sync_pending.empty()) return;
     Slot &sl = ln.slots[s];
     const int32_t dir = ln.sync_pending.front()->reverse;
+    // packets a caller submitted before its synchronous call go first
+    seal_locked(a, ln, dir);
     uint32_t n = 0;
     size_t pos = 0;
     for (auto it = ln.sync_pending.begin(); it != ln.sync_pending.end();) {
@@ -481,6 +550,7 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
         sl.h.tids[n] = r->tid;
         sl.cookies[n] = r->len; // the submitted length (see the completion loop)
         sl.waiters[n] = &r->w;
+        sl.qents[n] = nullptr;
         sl.hole[n] = 0;
         pos += need;
         n++;
@@ -496,6 +566,8 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
 }
 
 void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
+    (void)lane;
+    std::vector<srtp_queue *> touched; // queues with entries in the completed bundle
     std::unique_lock<std::mutex> lk(a->mu);
     // keep up to depth - 2 bundles in flight (one slot per open direction)
     const size_t max_inflight = ln->n_slots > 2 ? (size_t)ln->n_slots - 2 : 1;
@@ -547,17 +619,39 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
         Slot &sl = ln->slots[s];
         lk.unlock();
         (void)srtp_pipeline_wait(ln->pl, s);
+        // queue entries hold the slot until their owners release them; the
+        // lane holds it too until this loop is done
+        uint32_t nq = 0;
+        for (uint32_t i = 0; i < sl.n; i++) nq += !sl.hole[i] && sl.qents[i];
+        if (nq) sl.holds.store(nq + 1u, std::memory_order_relaxed);
+        touched.clear();
         // callbacks outside the lock, in bundle order; synchronous callers get
-        // their packet's bytes (as much as it occupied before or after) and wake
+        // their packet's bytes (as much as it occupied before or after, within
+        // its room) and wake; queue entries get their results published
         tl_in_callback = a;
         for (uint32_t i = 0; i < sl.n; i++) {
             if (sl.hole[i]) continue;
             const int32_t st = sl.h.status[i];
+            if (QEntry *qe = sl.qents[i]) {
+                sl.qents[i] = nullptr;
+                qe->c.status = st;
+                qe->c.len = sl.h.len[i];
+                qe->c.data = sl.h.seg + sl.h.off[i];
+                qe->slot = &sl;
+                qe->lane = ln;
+                srtp_queue *q = qe->q;
+                if (std::find(touched.begin(), touched.end(), q) == touched.end()) {
+                    q->lane_refs.fetch_add(1, std::memory_order_relaxed); // ordered by the release below
+                    touched.push_back(q);
+                }
+                qe->ready.store(1, std::memory_order_release);
+                continue;
+            }
             if (Waiter *w = sl.waiters[i]) {
                 sl.waiters[i] = nullptr;
                 const uint32_t nl = sl.h.len[i];
                 const uint32_t ol = (uint32_t)(uintptr_t)sl.cookies[i]; // the length submitted
-                memcpy(w->out, sl.h.seg + sl.h.off[i], std::max(nl, ol));
+                memcpy(w->out, sl.h.seg + sl.h.off[i], std::min(std::max(nl, ol), sl.h.cap[i]));
                 w->status = st;
                 w->len = nl;
                 w->done.store(1, std::memory_order_release);
@@ -567,21 +661,29 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
             if (a->cb) a->cb(a->user, sl.cookies[i], st, sl.h.seg + sl.h.off[i], sl.h.len[i]);
         }
         tl_in_callback = nullptr;
+        if (!touched.empty()) {
+            // ready (release) before waiting (seq_cst), against the owner's
+            // waiting before ready: one of the two sees the other
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            for (srtp_queue *q : touched) {
+                if (q->waiting.load()) {
+                    q->wake.fetch_add(1);
+                    futex_wake(&q->wake);
+                }
+                q->lane_refs.fetch_sub(1, std::memory_order_release); // destroy may free q now
+            }
+        }
         lk.lock();
         ln->inflight.pop_front();
         a->completed += sl.n_real;
         a->bundles++;
-        for (uint32_t i = 0; i < sl.n; i++) {
-            sl.h.len[i] = kNoLen;
-            sl.hole[i] = 0;
+        if (nq == 0 || sl.holds.fetch_sub(1) == 1) {
+            slot_free_locked(a, *ln, sl);
+        } else {
+            sl.state = kHeld; // freed by the last release (queue_release)
+            seal_if_idle_locked(a, *ln);
+            a->cv_idle.notify_all();
         }
-        sl.state = kFree;
-        sl.n = sl.n_real = 0;
-        sl.bytes = 0;
-        place_parked_locked(a, *ln, lane);
-        seal_if_idle_locked(a, *ln);
-        ln->cv_space.notify_all();
-        a->cv_idle.notify_all();
     }
 }
 
@@ -659,6 +761,7 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
     for (size_t l = 0; l < n_lanes; l++) {
         a->lanes.emplace_back(new Lane());
         Lane &ln = *a->lanes.back();
+        ln.idx = (uint32_t)l;
         ln.e = engines[l];
         const bool shared = std::count(dev.begin(), dev.end(), dev[l]) > 1;
         const int rc = srtp_pipeline_create_ex(ln.e, o.max_packets, o.max_bytes, o.depth,
@@ -672,9 +775,11 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
         ln.slots.reset(new Slot[(size_t)o.depth]);
         for (int i = 0; i < o.depth; i++) {
             Slot &sl = ln.slots[i];
+            sl.idx = i;
             srtp_pipeline_slot_get(ln.pl, i, &sl.h);
             sl.cookies.resize(o.max_packets);
             sl.waiters.assign(o.max_packets, nullptr);
+            sl.qents.assign(o.max_packets, nullptr);
             sl.hole.assign(o.max_packets, 0);
             sl.blocks.reset(new Block[a->n_blk]);
             for (uint32_t k = 0; k < o.max_packets; k++) sl.h.len[k] = kNoLen;
@@ -690,7 +795,8 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
 // copy_len bytes of pkt, length len, room cap; w != nullptr: a synchronous
 // caller's entry.
 int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt, uint32_t copy_len,
-                 uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie, Waiter *w) {
+                 uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie, Waiter *w, QEntry *qe = nullptr,
+                 bool may_wait = true) {
     if (a->closing.load()) return SRTP_EINVAL; // destroy has begun
     const int dir = reverse ? 1 : 0;
     const size_t need = need_of(cap);
@@ -720,13 +826,58 @@ int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t
                 ln.parked.push_back(Parked{dir, tid, flags, cookie, std::vector<uint8_t>(pkt, pkt + len)});
                 return SRTP_OK;
             }
-            ln.cv_space.wait(lk); // backpressure: every slot is sealed or in flight
+            if (!may_wait) return SRTP_EAGAIN; // a queue holding slots: its owner reaps first
+            ln.cv_space.wait(lk); // backpressure: every slot is sealed, in flight or held
         }
     }
     ln.slots[s].waiters[i] = w;
+    ln.slots[s].qents[i] = qe;
     fill(ln, s, i, off, tid, pkt, len, cap, need, flags, cookie, copy_len);
     producer_seal_if_idle(a, ln, dir);
     return SRTP_OK;
+}
+
+// Releases the entries [from, to) of a queue's ring: each slot's holds drop by
+// its entries' count, and the release that reaches zero frees the slot.
+void queue_release(srtp_queue *q, uint64_t from, uint64_t to) {
+    Slot *cur = nullptr;
+    Lane *cur_lane = nullptr;
+    uint32_t k = 0;
+    auto drop = [&] {
+        if (cur && cur->holds.fetch_sub(k) == k) {
+            std::lock_guard<std::mutex> lk(q->a->mu);
+            slot_free_locked(q->a, *cur_lane, *cur);
+        }
+    };
+    for (uint64_t x = from; x < to; x++) {
+        QEntry &e = q->ring[x % q->cap];
+        if (!e.slot) continue;
+        if (e.slot != cur) {
+            drop();
+            cur = e.slot;
+            cur_lane = e.lane;
+            k = 0;
+        }
+        k++;
+        e.slot = nullptr;
+    }
+    drop();
+}
+
+// The owner waits for entry e of its queue: a short spin, then the futex.
+void queue_wait(srtp_queue *q, QEntry &e) {
+    for (int i = 0; i < 256; i++) {
+        if (e.ready.load(std::memory_order_acquire)) return;
+        __builtin_ia32_pause();
+    }
+    for (;;) {
+        const uint32_t w0 = q->wake.load(std::memory_order_acquire);
+        q->waiting.store(1);
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        if (e.ready.load(std::memory_order_acquire)) break;
+        futex_wait(&q->wake, w0);
+    }
+    q->waiting.store(0, std::memory_order_relaxed);
 }
 
 } // namespace
@@ -774,6 +925,11 @@ int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, 
         return SRTP_EINVAL;
     if (tl_in_callback == a) return SRTP_EINVAL; // would wait for its own lane
     if (need_of(cap) > a->opts.max_bytes) return SRTP_EINVAL;
+    if (len > cap) { // RawPacket.isInvalid: what k_parse reports, without a round trip
+        *status = SRTP_STATUS_DROP_INVALID;
+        *out_len = len;
+        return SRTP_OK;
+    }
     struct Inside { // counted before the closing check: destroy waits for every caller inside
         srtp_aggregator *a;
         ~Inside() { a->sync_callers.fetch_sub(1); }
@@ -854,7 +1010,9 @@ void srtp_aggregator_destroy(srtp_aggregator *a) {
         a->closing.store(true);
         seal_all_locked(a);
         for (;;) {
-            if (pending_locked(a) == 0 && a->sync_callers.load() == 0) break;
+            // queues hold slots whose bytes their owners still read: every
+            // queue must be destroyed first (see the header)
+            if (pending_locked(a) == 0 && a->sync_callers.load() == 0 && a->queues.load() == 0) break;
             seal_all_locked(a); // parked callback packets placed since, stragglers' slots
             a->cv_idle.wait_for(lk, std::chrono::milliseconds(1));
         }
@@ -869,6 +1027,100 @@ void srtp_aggregator_destroy(srtp_aggregator *a) {
     a->flusher.join();
     destroy_lanes(a);
     delete a;
+}
+
+int srtp_queue_create(srtp_aggregator *a, uint32_t max_inflight, srtp_queue **out) {
+    if (!a || !out || max_inflight == 0 || max_inflight > (1u << 20)) return SRTP_EINVAL;
+    *out = nullptr;
+    if (a->closing.load()) return SRTP_EINVAL;
+    srtp_queue *q = new (std::nothrow) srtp_queue();
+    if (!q) return SRTP_ENOMEM;
+    q->ring.reset(new (std::nothrow) QEntry[max_inflight]);
+    if (!q->ring) {
+        delete q;
+        return SRTP_ENOMEM;
+    }
+    q->a = a;
+    q->cap = max_inflight;
+    for (uint32_t i = 0; i < max_inflight; i++) q->ring[i].q = q;
+    a->queues.fetch_add(1);
+    *out = q;
+    return SRTP_OK;
+}
+
+int srtp_queue_submit(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t *pkt, uint32_t copy_len,
+                      uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie) {
+    if (!q || (!pkt && copy_len) || copy_len > cap || cap > 65535u || len > 65535u) return SRTP_EINVAL;
+    srtp_aggregator *a = q->a;
+    if (tl_in_callback == a) return SRTP_EINVAL; // a lane's own thread must not wait on its lanes
+    if (need_of(cap) > a->opts.max_bytes) return SRTP_EINVAL;
+    if (q->tail - q->head >= q->cap) return SRTP_EAGAIN; // reap first
+    QEntry &e = q->ring[q->tail % q->cap];
+    e.slot = nullptr;
+    e.lane = nullptr;
+    e.c = srtp_completion{};
+    e.c.cookie = cookie;
+    e.c.in_len = len;
+    e.c.len = len;
+    e.c.reverse = reverse ? 1 : 0;
+    e.c.tid = tid;
+    if ((flags & SRTP_PKT_FLAG_SKIP) || len > cap) {
+        // untouched, as the engine would report it: a null element or one the
+        // predicate rejected (SKIPPED), RawPacket.isInvalid (DROP_INVALID)
+        e.c.status = (flags & SRTP_PKT_FLAG_SKIP) ? SRTP_STATUS_SKIPPED : SRTP_STATUS_DROP_INVALID;
+        e.ready.store(1, std::memory_order_relaxed);
+        q->tail++;
+        return SRTP_OK;
+    }
+    e.ready.store(0, std::memory_order_relaxed);
+    // only a queue with nothing outstanding may wait for a slot (file comment)
+    const bool may_wait = q->tail == q->head && q->rel_from == q->rel_to;
+    const int rc = submit_entry(a, reverse, tid, pkt, copy_len, len, cap,
+                                flags & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE), cookie, nullptr, &e,
+                                may_wait);
+    if (rc != SRTP_OK) return rc;
+    q->tail++;
+    return SRTP_OK;
+}
+
+int srtp_queue_reap(srtp_queue *q, srtp_completion *out, uint32_t max, int32_t wait) {
+    if (!q || (!out && max) || max > (uint32_t)INT_MAX) return SRTP_EINVAL;
+    queue_release(q, q->rel_from, q->rel_to);
+    q->rel_from = q->rel_to = q->head;
+    uint32_t n = 0;
+    while (n < max && q->head < q->tail) {
+        QEntry &e = q->ring[q->head % q->cap];
+        if (!e.ready.load(std::memory_order_acquire)) {
+            if (n > 0 || !wait) break;
+            queue_wait(q, e);
+        }
+        out[n++] = e.c;
+        q->head++;
+    }
+    q->rel_to = q->head;
+    return (int)n;
+}
+
+srtp_aggregator *srtp_queue_aggregator(srtp_queue *q) { return q ? q->a : nullptr; }
+
+int32_t srtp_queue_outstanding(srtp_queue *q) { return q ? (int32_t)(q->tail - q->head) : 0; }
+
+void srtp_queue_destroy(srtp_queue *q) {
+    if (!q) return;
+    // every submitted packet completes, then every slot it holds is released
+    queue_release(q, q->rel_from, q->rel_to);
+    while (q->head < q->tail) {
+        QEntry &e = q->ring[q->head % q->cap];
+        if (!e.ready.load(std::memory_order_acquire)) queue_wait(q, e);
+        queue_release(q, q->head, q->head + 1);
+        q->head++;
+    }
+    while (q->lane_refs.load(std::memory_order_acquire)) std::this_thread::yield();
+    srtp_aggregator *a = q->a;
+    delete q;
+    std::lock_guard<std::mutex> lk(a->mu);
+    a->queues.fetch_sub(1);
+    a->cv_idle.notify_all();
 }
 
 } // extern "C"

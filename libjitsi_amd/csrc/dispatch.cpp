@@ -100,6 +100,29 @@ bool cipher_may_throw(int32_t h, int32_t plen) {
     return plen > 0 && h < 0;
 }
 
+// Whether the reference could throw on a valid packet (12 <= L <= C): a
+// superset of its throws (RawPacket.getHeaderLength, SRTPCipherCTR.process /
+// SRTPCipherF8.process bounds, RawPacket.getSRTCPIndex).  t_max: the largest
+// tag length in tag_mask.
+bool may_throw_one(bool rtp, int32_t reverse, const uint8_t *pkt, uint32_t L, uint32_t C, uint32_t fl,
+                   uint32_t tag_mask, int t_max) {
+    if (rtp) {
+        const int32_t h = rtp_header_len(pkt, C);
+        if (!reverse) return cipher_may_throw(h, (int32_t)L - (h == kHdrThrow ? 0 : h));
+        if (!(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) || h == kHdrThrow) {
+            for (int T = 0; T < 32; T++) {
+                if (!(tag_mask & (1u << T))) continue;
+                const int32_t newL = (int32_t)L - T > 0 ? (int32_t)L - T : 0;
+                if (cipher_may_throw(h, newL - (h == kHdrThrow ? 0 : h))) return true;
+            }
+        }
+        return false;
+    }
+    // getSRTCPIndex at length - 4 - tag, decryption from byte 8
+    // (SRTCPCryptoContext.reverseTransformPacket :315-374)
+    return reverse && (int32_t)L < 12 + t_max;
+}
+
 } // namespace
 
 // Plan of one bundle: the shard of each packet and whether it could throw
@@ -131,26 +154,7 @@ static int32_t plan_bundle(int32_t n_shards, int32_t abort_on_error, int32_t rev
         const bool rtp = kinds[t] == SRTP_KIND_RTP;
         shard[i] = invalid ? 0
                            : (int32_t)(mix32(be32(pkt + (rtp ? 8 : 4))) % (uint32_t)n_shards);
-        bool mt = false;
-        if (abort_on_error && !invalid) {
-            if (rtp) {
-                const int32_t h = rtp_header_len(pkt, C);
-                if (!reverse) {
-                    mt = cipher_may_throw(h, (int32_t)L - (h == kHdrThrow ? 0 : h));
-                } else if (!(fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ||
-                           h == kHdrThrow) {
-                    for (int T = 0; T < 32 && !mt; T++) {
-                        if (!(tag_mask & (1u << T))) continue;
-                        const int32_t newL = (int32_t)L - T > 0 ? (int32_t)L - T : 0;
-                        mt = cipher_may_throw(h, newL - (h == kHdrThrow ? 0 : h));
-                    }
-                }
-            } else if (reverse) {
-                // getSRTCPIndex at length - 4 - tag, decryption from byte 8
-                // (SRTCPCryptoContext.reverseTransformPacket :315-374)
-                mt = (int32_t)L < 12 + t_max;
-            }
-        }
+        const bool mt = abort_on_error && !invalid && may_throw_one(rtp, reverse, pkt, L, C, fl, tag_mask, t_max);
         may_throw[i] = mt ? 1 : 0;
         any |= may_throw[i];
     }
@@ -502,6 +506,15 @@ int32_t srtp_dispatch_plan(int32_t n_shards, int32_t abort_on_error, int32_t rev
             return SRTP_EINVAL;
     return plan_bundle(n_shards, abort_on_error, reverse, kinds, n_transformers, tag_mask, tids, tid,
                        seg, off, len, cap, flags, n, shard, may_throw);
+}
+
+int32_t srtp_packet_may_throw(int32_t kind, int32_t reverse, const uint8_t *pkt, uint32_t len, uint32_t cap,
+                              uint32_t flags, uint32_t tag_mask) {
+    if (!pkt || (flags & SRTP_PKT_FLAG_SKIP) || len < 12 || len > cap || cap > 65535u) return 0;
+    int t_max = 0;
+    for (int T = 0; T < 32; T++)
+        if (tag_mask & (1u << T)) t_max = T;
+    return may_throw_one(kind == SRTP_KIND_RTP, reverse, pkt, len, cap, flags, tag_mask, t_max) ? 1 : 0;
 }
 
 void srtp_dispatch_destroy(srtp_dispatch *d) {

@@ -40,6 +40,15 @@
 struct srtp_rawpacket_batch {
     srtp_engine *e = nullptr;   // engine mode: a pinned pipeline slot is the staging
     srtp_dispatch *d = nullptr; // dispatch mode: host staging (the dispatcher pins per shard)
+    // srtp_rawpacket_batch_set_aggregator: small arrays that cannot throw go
+    // through this queue on the aggregator's lanes (shared bundles)
+    srtp_aggregator *agg = nullptr;
+    srtp_queue *q = nullptr;
+    std::vector<srtp_completion> comps;
+    bool via_queue = false;               // the last call took the queue
+    std::vector<const uint8_t *> res_ptr; // its results (srtp_rawpacket_result)
+    std::vector<uint32_t> res_len;
+    std::vector<uint8_t> grown;           // bytes of its results that need a new buffer
     srtp_pipeline *pl = nullptr;
     uint32_t pl_packets = 0;
     size_t pl_bytes = 0;
@@ -131,14 +140,21 @@ uint32_t element_cap(int32_t reverse, uint32_t avail, uint32_t length) {
     return (uint32_t)std::min<uint64_t>(c, 65535u);
 }
 
-// Write-back of one processed element (SinglePacketTransformer + RawPacket.append
-// / grow / shrink): res / nl = the engine's bytes and length of the packet,
-// dst = buffer + offset with avail bytes.  Returns need_len (0: written in
-// place) or a negative SRTP_E*.  info(kind, rtcp_tag) gives the transformer's
-// kind and, when rtcp_tag != nullptr, its forward factory's SRTCP tag length.
+// Write-back plan of one processed element (SinglePacketTransformer +
+// RawPacket.append / grow / shrink): st / nl = the engine's status and length
+// of the packet, old = its length before, avail = the buffer's bytes after
+// the offset.  *need = 0: *copy bytes of the result go back in place at the
+// offset; else the reference allocates a new buffer of *need bytes at offset 0,
+// which receives *copy bytes of the result.  Returns SRTP_OK or a negative
+// SRTP_E*.  info(kind, rtcp_tag) gives the transformer's kind and, when
+// rtcp_tag != nullptr, its forward factory's SRTCP tag length.
 template <class Info>
-int64_t write_back(int32_t reverse, int32_t st, uint8_t *dst, uint32_t avail, uint32_t old, const uint8_t *res,
-                   uint32_t nl, Info &&info) {
+int plan_back(int32_t reverse, int32_t st, uint32_t avail, uint32_t old, uint32_t nl, Info &&info, uint32_t *copy,
+              uint32_t *need) {
+    *need = 0;
+    *copy = 0;
+    if (st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED || st < 0) return SRTP_OK;
+    if (old > avail) return SRTP_OK; // RawPacket.isInvalid: untouched (DROP_INVALID)
     if (!reverse && st == SRTP_STATUS_OK) {
         int32_t kind = SRTP_KIND_RTP, rtcp_tag = 0;
         int rc = info(&kind, nullptr);
@@ -149,19 +165,149 @@ int64_t write_back(int32_t reverse, int32_t st, uint8_t *dst, uint32_t avail, ui
             // buffer is length + 4 + the policy's tag length (the forward
             // factory's SRTCP policy: a context kept across an SDES rekey with a
             // different tag length is the one case this does not cover)
-            if (nl != old) return nl;
+            *copy = nl;
+            if (nl != old) {
+                *need = nl;
+                return SRTP_OK;
+            }
             rc = info(&kind, &rtcp_tag);
             if (rc != SRTP_OK) return rc;
-            return (int64_t)old + 4 + rtcp_tag;
+            *need = old + 4u + (uint32_t)rtcp_tag;
+            return SRTP_OK;
         }
         if (nl != old) {
-            if (nl > avail) return nl; // append reallocates: exactly length + tag
-            memcpy(dst, res, nl);
-            return 0;
+            *copy = nl;
+            if (nl > avail) *need = nl; // append reallocates: exactly length + tag
+            return SRTP_OK;
         }
     }
-    memcpy(dst, res, std::min(old, avail));
+    *copy = std::min(old, avail);
+    return SRTP_OK;
+}
+
+// The same, applied: in place into dst (buffer + offset), or returns need_len
+// (the result stays at res for the caller's new buffer), or a negative SRTP_E*.
+template <class Info>
+int64_t write_back(int32_t reverse, int32_t st, uint8_t *dst, uint32_t avail, uint32_t old, const uint8_t *res,
+                   uint32_t nl, Info &&info) {
+    uint32_t copy = 0, need = 0;
+    const int rc = plan_back(reverse, st, avail, old, nl, info, &copy, &need);
+    if (rc != SRTP_OK) return rc;
+    if (need) return need;
+    if (copy) memcpy(dst, res, copy);
     return 0;
+}
+
+constexpr uint32_t kQueueArray = 8192; // arrays up to this size may take the batch's queue
+constexpr uint32_t kTagsAny = 0x1fffu; // tag lengths 0..12: every policy the engine takes
+
+// The caller's element i as a queue submit (srtp_rawpacket_submit's rules).
+int submit_element(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t *buf, uint32_t buf_len,
+                   uint32_t offset, uint32_t length, uint32_t flags, uint64_t cookie) {
+    if (!buf || (flags & SRTP_PKT_FLAG_SKIP))
+        return srtp_queue_submit(q, reverse, tid, nullptr, 0, 0, 0, SRTP_PKT_FLAG_SKIP, cookie);
+    const uint32_t avail = offset <= buf_len ? buf_len - offset : 0u;
+    if (length > avail || length > 65535u) // RawPacket.isInvalid: completes untouched
+        return srtp_queue_submit(q, reverse, tid, nullptr, 0, std::min<uint32_t>(length, 65535u), 0, 0, cookie);
+    const uint32_t cap = element_cap(reverse, avail, length);
+    return srtp_queue_submit(q, reverse, tid, buf + offset, std::min(avail, cap), length, cap,
+                             flags & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE), cookie);
+}
+
+// srtp_rawpacket_transform through the batch's queue: every element submitted,
+// every completion written back as it is reaped.  Only for arrays no packet of
+// which can throw (so the aggregator's run without abort-on-throw is the
+// reference's result).  Returns 1 when the array is not eligible.
+int transform_via_queue(srtp_rawpacket_batch *b, int32_t reverse, const int32_t *tids, int32_t tid,
+                        uint8_t *const *bufs, const uint32_t *buf_len, const uint32_t *offset, uint32_t *length,
+                        const uint32_t *flags, int32_t *status, uint32_t *need_len, uint32_t n, int32_t *thrown) {
+    if (!b->agg || n > kQueueArray) return 1;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t fl = flags ? flags[i] : 0u;
+        if (!bufs[i] || (fl & SRTP_PKT_FLAG_SKIP)) continue;
+        const uint32_t avail = offset[i] <= buf_len[i] ? buf_len[i] - offset[i] : 0u;
+        if (length[i] > avail) continue; // untouched
+        int32_t kind = SRTP_KIND_RTP;
+        if (srtp_aggregator_transformer_info(b->agg, tids ? tids[i] : tid, &kind, nullptr) != SRTP_OK) return 1;
+        const uint32_t cap = std::min(avail, element_cap(reverse, avail, length[i]));
+        if (srtp_packet_may_throw(kind, reverse, bufs[i] + offset[i], length[i], cap, fl, kTagsAny)) return 1;
+    }
+    if (!b->q) {
+        const int rc = srtp_queue_create(b->agg, kQueueArray, &b->q);
+        if (rc != SRTP_OK) return rc;
+    }
+    try {
+        b->comps.resize(kQueueArray);
+        b->res_ptr.assign(n, nullptr);
+        b->res_len.assign(n, 0u);
+    } catch (...) {
+        return SRTP_ENOMEM;
+    }
+    b->grown.clear();
+    std::vector<size_t> grown_at;
+    uint32_t done = 0;
+    int err = SRTP_OK;
+    auto reap = [&](int32_t wait) {
+        const int k = srtp_queue_reap(b->q, b->comps.data(), kQueueArray, wait);
+        if (k < 0) return k;
+        for (int j = 0; j < k; j++) {
+            const srtp_completion &c = b->comps[(size_t)j];
+            const uint32_t i = (uint32_t)c.cookie;
+            const int32_t st = c.status < 0 ? SRTP_STATUS_ERR_INTERNAL : c.status;
+            status[i] = st;
+            need_len[i] = 0;
+            done++;
+            if (!bufs[i] || st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED) continue;
+            const uint32_t avail = offset[i] <= buf_len[i] ? buf_len[i] - offset[i] : 0u;
+            uint32_t copy = 0, need = 0;
+            const int rc = plan_back(reverse, st, avail, c.in_len, c.len, [&](int32_t *kind, int32_t *tag) {
+                return srtp_aggregator_transformer_info(b->agg, c.tid, kind, tag);
+            }, &copy, &need);
+            if (rc != SRTP_OK) {
+                err = rc;
+                continue;
+            }
+            if (need) { // kept for srtp_rawpacket_result
+                grown_at.resize(n, SIZE_MAX);
+                grown_at[i] = b->grown.size();
+                b->grown.insert(b->grown.end(), c.data, c.data + copy);
+                need_len[i] = need;
+                b->res_len[i] = copy;
+            } else {
+                if (copy) memcpy(bufs[i] + offset[i], c.data, copy);
+                b->res_ptr[i] = bufs[i] + offset[i];
+                b->res_len[i] = c.len;
+            }
+            if (c.data) length[i] = c.len;
+            if (st == SRTP_STATUS_ERR_MALFORMED && (*thrown < 0 || (int32_t)i < *thrown)) *thrown = (int32_t)i;
+        }
+        return SRTP_OK;
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        for (;;) {
+            int rc2;
+            const int rc = submit_element(b->q, reverse, tids ? tids[i] : tid, bufs[i], buf_len[i], offset[i],
+                                          length[i], flags ? flags[i] : 0u, i);
+            if (rc == SRTP_OK) break;
+            if (rc == SRTP_EAGAIN) rc2 = reap(1);
+            else rc2 = rc; // nothing of this element was queued
+            if (rc2 != SRTP_OK) {
+                // what was queued completes (written back) before the error returns
+                while (srtp_queue_outstanding(b->q) > 0 && reap(1) == SRTP_OK) {
+                }
+                return rc2;
+            }
+        }
+    }
+    while (done < n) {
+        const int rc = reap(1);
+        if (rc != SRTP_OK) return rc;
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if (need_len[i]) b->res_ptr[i] = b->grown.data() + grown_at[i];
+    b->via_queue = true;
+    b->n = n;
+    return err;
 }
 
 } // namespace
@@ -188,6 +334,7 @@ int srtp_rawpacket_batch_create_dispatch(srtp_dispatch *d, srtp_rawpacket_batch 
 
 void srtp_rawpacket_batch_destroy(srtp_rawpacket_batch *b) {
     if (!b) return;
+    if (b->q) srtp_queue_destroy(b->q);
     if (b->pl) srtp_pipeline_destroy(b->pl);
     release_seg(b);
     delete b;
@@ -201,7 +348,13 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
         return SRTP_EINVAL;
     *thrown = -1;
     b->n = 0;
+    b->via_queue = false;
     if (n == 0) return SRTP_OK;
+    {
+        const int rc = transform_via_queue(b, reverse, tids, tid, bufs, buf_len, offset, length, flags, status,
+                                           need_len, n, thrown);
+        if (rc != 1) return rc;
+    }
     srtp_engine *eng = engine_of(b);
     // Packing (the JNI shim's copy of each buffer):
     // region i holds the buffer's bytes from the packet's offset on, so the
@@ -312,9 +465,42 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
 
 int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **data, uint32_t *len) {
     if (!b || !data || !len || i >= b->n) return SRTP_EINVAL;
+    if (b->via_queue) {
+        if (!b->res_ptr[i]) return SRTP_EINVAL; // untouched element
+        *data = b->res_ptr[i];
+        *len = b->res_len[i];
+        return SRTP_OK;
+    }
     *data = b->s_seg + b->s_off[i];
     *len = b->s_len[i];
     return SRTP_OK;
+}
+
+int srtp_rawpacket_batch_set_aggregator(srtp_rawpacket_batch *b, srtp_aggregator *a) {
+    if (!b) return SRTP_EINVAL;
+    if (b->q) {
+        srtp_queue_destroy(b->q);
+        b->q = nullptr;
+    }
+    b->agg = a;
+    return SRTP_OK;
+}
+
+int srtp_rawpacket_submit(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t *buf, uint32_t buf_len,
+                          uint32_t offset, uint32_t length, uint32_t flags, uint64_t cookie) {
+    if (!q) return SRTP_EINVAL;
+    return submit_element(q, reverse, tid, buf, buf_len, offset, length, flags, cookie);
+}
+
+int srtp_rawpacket_complete(srtp_queue *q, const srtp_completion *c, uint32_t avail, uint32_t *copy_len,
+                            uint32_t *need_len) {
+    if (!q || !c || !copy_len || !need_len) return SRTP_EINVAL;
+    srtp_aggregator *a = srtp_queue_aggregator(q);
+    const int rc = plan_back(c->reverse, c->status, avail, c->in_len, c->len, [&](int32_t *kind, int32_t *tag) {
+        return srtp_aggregator_transformer_info(a, c->tid, kind, tag);
+    }, copy_len, need_len);
+    if (rc == SRTP_OK && !c->data) *copy_len = 0; // completed at submit: untouched
+    return rc;
 }
 
 int srtp_rawpacket_transform_one(srtp_aggregator *a, int32_t reverse, int32_t tid, uint8_t *buf,
@@ -328,7 +514,7 @@ int srtp_rawpacket_transform_one(srtp_aggregator *a, int32_t reverse, int32_t ti
     }
     const uint32_t avail = offset <= buf_len ? buf_len - offset : 0u;
     const uint32_t old = *length;
-    if (old > 65535u) { // longer than any region: RawPacket.isInvalid, as the array path reports it
+    if (old > 65535u || old > avail) { // RawPacket.isInvalid, as the array path reports it: untouched
         *status = SRTP_STATUS_DROP_INVALID;
         return SRTP_OK;
     }

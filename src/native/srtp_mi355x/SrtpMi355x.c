@@ -2,12 +2,13 @@
  * SrtpMi355x.c -- JNI shim between libjitsi's Java transformers and the
  * MI355X SRTP engine (include/srtp_mi355x.h, libsrtp_mi355x.so).
  *
- * NOT COMPILED IN THIS REPOSITORY: the image has no JDK and no jni.h.  It is
- * the file a maintainer adds next to src/native/openssl/ and builds like
- * libjnopenssl:
+ * Built like libjnopenssl next to src/native/openssl/ (INTEGRATION.md 2):
  *
  *   gcc -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
  *       src/native/srtp_mi355x/SrtpMi355x.c -Llibjitsi_amd -lsrtp_mi355x -o libjnsrtp_mi355x.so
+ *
+ * The image has no JDK, so here it is compiled unmodified against a stub JNI
+ * header and driven through a toy JVM (tests/jni_stub/, tests/test_jni_shim.py).
  *
  * Everything below the JNI calls is srtp_* C ABI that the GPU tests exercise
  * (the RawPacket[] marshalling is srtp_rawpacket_transform, tested through
@@ -23,6 +24,7 @@
  * SinglePacketTransformer drop-ins), GpuSRTPContextFactory.
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -97,14 +99,44 @@ JNIEXPORT jint JNICALL JFN(transformerClose)(JNIEnv *env, jclass c, jlong d, jin
 
 /* ---- RawPacket[] (PacketTransformer.transform / reverseTransform) ---- */
 
-/* One srtp_rawpacket_batch per Java thread (a ThreadLocal<Long> on the Java side). */
-JNIEXPORT jlong JNICALL JFN(batchCreate)(JNIEnv *env, jclass c, jlong d) {
-    srtp_rawpacket_batch *b = NULL;
-    return srtp_rawpacket_batch_create_dispatch((srtp_dispatch *)H(d), &b) == SRTP_OK ? (jlong)(intptr_t)b : 0;
-}
+/* One srtp_rawpacket_batch per Java thread, owned here: created on the
+ * thread's first array call and destroyed when the thread exits (a pthread key
+ * destructor), so a media thread that dies does not leak its pinned staging.
+ * Arrays that cannot throw go through the aggregator's lanes
+ * (srtp_rawpacket_batch_set_aggregator); the others run as one bundle. */
+struct tl_batch {
+    srtp_rawpacket_batch *b;
+    jlong d, agg;
+};
+static pthread_key_t batch_key;
+static pthread_once_t batch_once = PTHREAD_ONCE_INIT;
 
-JNIEXPORT void JNICALL JFN(batchDestroy)(JNIEnv *env, jclass c, jlong b) {
-    srtp_rawpacket_batch_destroy((srtp_rawpacket_batch *)H(b));
+static void batch_free(void *p) {
+    struct tl_batch *t = p;
+    srtp_rawpacket_batch_destroy(t->b);
+    free(t);
+}
+static void batch_key_init(void) { pthread_key_create(&batch_key, batch_free); }
+
+static srtp_rawpacket_batch *thread_batch(jlong d, jlong agg) {
+    pthread_once(&batch_once, batch_key_init);
+    struct tl_batch *t = pthread_getspecific(batch_key);
+    if (t && t->d == d && t->agg == agg) return t->b;
+    if (t) { /* another dispatcher (a test's second JVM): start over */
+        pthread_setspecific(batch_key, NULL);
+        batch_free(t);
+    }
+    t = calloc(1, sizeof *t);
+    if (!t) return NULL;
+    if (srtp_rawpacket_batch_create_dispatch((srtp_dispatch *)H(d), &t->b) != SRTP_OK) {
+        free(t);
+        return NULL;
+    }
+    srtp_rawpacket_batch_set_aggregator(t->b, (srtp_aggregator *)H(agg));
+    t->d = d;
+    t->agg = agg;
+    pthread_setspecific(batch_key, t);
+    return t->b;
 }
 
 static jfieldID fid_buffer, fid_offset, fid_length, fid_flags;
@@ -135,10 +167,11 @@ static int raw_packet_ids(JNIEnv *env) {
  * changed go back with SetByteArrayRegion (BlockCipher.c:194-229 likewise
  * holds its critical region only around a CPU call).  Two elements sharing one
  * byte[] stay consistent: each writes back only its own range. */
-JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch, jboolean reverse, jint tid,
-                                             jobjectArray pkts, jintArray skip) {
-    srtp_rawpacket_batch *b = (srtp_rawpacket_batch *)H(batch);
-    if (!b || !pkts || raw_packet_ids(env) != 0) return SRTP_EINVAL;
+JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong d, jlong agg, jboolean reverse,
+                                             jint tid, jobjectArray pkts, jintArray skip) {
+    if (!pkts || raw_packet_ids(env) != 0) return SRTP_EINVAL;
+    srtp_rawpacket_batch *b = thread_batch(d, agg);
+    if (!b) return SRTP_ENOMEM;
     const jsize n = (*env)->GetArrayLength(env, pkts);
     if (n == 0) return 0;
     if ((*env)->PushLocalFrame(env, 2 * n + 16) != 0) return SRTP_ENOMEM;
@@ -159,7 +192,8 @@ JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch,
         if (!objs[i]) continue;
         arrs[i] = (jbyteArray)(*env)->GetObjectField(env, objs[i], fid_buffer);
         const uint32_t al = arrs[i] ? (uint32_t)(*env)->GetArrayLength(env, arrs[i]) : 0u;
-        joff[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_offset);
+        const jint jo = (*env)->GetIntField(env, objs[i], fid_offset);
+        joff[i] = jo < 0 ? UINT32_MAX : (uint32_t)jo; /* a negative offset holds nothing */
         length[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_length);
         flags[i] = (uint32_t)(*env)->GetIntField(env, objs[i], fid_flags) &
                    (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE);
@@ -176,7 +210,9 @@ JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch,
     for (jsize i = 0; i < n; i++) {
         if (!arrs[i]) continue;
         bufs[i] = block + total;
-        (*env)->GetByteArrayRegion(env, arrs[i], (jsize)joff[i], (jsize)buf_len[i], (jbyte *)bufs[i]);
+        /* an offset outside the buffer holds nothing: no region call (it would
+         * throw), the engine reports the packet invalid */
+        if (buf_len[i]) (*env)->GetByteArrayRegion(env, arrs[i], (jsize)joff[i], (jsize)buf_len[i], (jbyte *)bufs[i]);
         total += buf_len[i];
     }
     int32_t thrown = -1;
@@ -207,7 +243,7 @@ JNIEXPORT jint JNICALL JFN(transformPackets)(JNIEnv *env, jclass c, jlong batch,
         } else if (arrs[i]) { /* in place: the bytes up to the longer of the two lengths */
             uint32_t w = old_len[i] > length[i] ? old_len[i] : length[i];
             if (w > buf_len[i]) w = buf_len[i];
-            (*env)->SetByteArrayRegion(env, arrs[i], (jsize)joff[i], (jsize)w, (const jbyte *)bufs[i]);
+            if (w) (*env)->SetByteArrayRegion(env, arrs[i], (jsize)joff[i], (jsize)w, (const jbyte *)bufs[i]);
         }
         (*env)->SetIntField(env, objs[i], fid_length, (jint)length[i]);
         if (st != SRTP_STATUS_OK && st != SRTP_STATUS_ERR_MALFORMED)
@@ -234,10 +270,14 @@ JNIEXPORT jint JNICALL JFN(deviceCount)(JNIEnv *env, jclass c) {
 }
 
 /* One aggregator per process over the dispatcher: its lanes coalesce the
- * per-packet calls of every JVM thread into GPU bundles. */
+ * per-packet calls of every JVM thread into GPU bundles.  Bundles of at most
+ * 4096 packets / 8 MB per lane (what a round trip's worth of per-packet calls
+ * fills), four pinned slots per lane. */
 JNIEXPORT jlong JNICALL JFN(aggregatorCreate)(JNIEnv *env, jclass c, jlong d) {
     srtp_aggregator_opts o;
     srtp_aggregator_opts_default(&o); /* SRTP_AGG_SEAL_IDLE */
+    o.max_packets = 4096;
+    o.max_bytes = (size_t)8 << 20;
     srtp_aggregator *a = NULL;
     return srtp_aggregator_create_dispatch((srtp_dispatch *)H(d), &o, NULL, NULL, &a) == SRTP_OK
                ? (jlong)(intptr_t)a : 0;
@@ -252,6 +292,28 @@ JNIEXPORT void JNICALL JFN(aggregatorDestroy)(JNIEnv *env, jclass c, jlong a) {
 #define ONE_BYTES (65535 + 16)
 static __thread uint8_t *tl_pkt, *tl_grow;
 
+/* Reads a RawPacket's fields and copies its bytes from the offset on (at
+ * most 65535: no region is larger) into the calling thread's buffer; *arr
+ * NULL for a packet without a buffer. */
+static int read_packet(JNIEnv *env, jobject pkt, jbyteArray *arr, uint32_t *joff, uint32_t *avail,
+                       uint32_t *length, uint32_t *flags) {
+    if (!tl_pkt) {
+        tl_pkt = malloc(ONE_BYTES);
+        tl_grow = malloc(ONE_BYTES);
+        if (!tl_pkt || !tl_grow) return SRTP_ENOMEM;
+    }
+    *arr = (jbyteArray)(*env)->GetObjectField(env, pkt, fid_buffer);
+    const uint32_t al = *arr ? (uint32_t)(*env)->GetArrayLength(env, *arr) : 0u;
+    const jint jo = (*env)->GetIntField(env, pkt, fid_offset);
+    *joff = jo < 0 ? UINT32_MAX : (uint32_t)jo;
+    *length = (uint32_t)(*env)->GetIntField(env, pkt, fid_length);
+    *flags = (uint32_t)(*env)->GetIntField(env, pkt, fid_flags) & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE);
+    *avail = *joff <= al ? al - *joff : 0u;
+    if (*avail > 65535u) *avail = 65535u;
+    if (*arr && *avail) (*env)->GetByteArrayRegion(env, *arr, (jsize)*joff, (jsize)*avail, (jbyte *)tl_pkt);
+    return SRTP_OK;
+}
+
 /* transform / reverseTransform of one RawPacket (srtp_rawpacket_transform_one):
  * returns its SRTP_STATUS_* (the Java side returns null for a drop and throws
  * for SRTP_STATUS_ERR_MALFORMED) or a negative SRTP_E* code.  The call blocks
@@ -259,27 +321,17 @@ static __thread uint8_t *tl_pkt, *tl_grow;
 JNIEXPORT jint JNICALL JFN(transformOne)(JNIEnv *env, jclass c, jlong agg, jboolean reverse, jint tid,
                                          jobject pkt) {
     if (!pkt || raw_packet_ids(env) != 0) return SRTP_EINVAL;
-    if (!tl_pkt) {
-        tl_pkt = malloc(ONE_BYTES);
-        tl_grow = malloc(ONE_BYTES);
-        if (!tl_pkt || !tl_grow) return SRTP_ENOMEM;
-    }
-    jbyteArray arr = (jbyteArray)(*env)->GetObjectField(env, pkt, fid_buffer);
-    const uint32_t al = arr ? (uint32_t)(*env)->GetArrayLength(env, arr) : 0u;
-    const uint32_t joff = (uint32_t)(*env)->GetIntField(env, pkt, fid_offset);
-    uint32_t length = (uint32_t)(*env)->GetIntField(env, pkt, fid_length);
-    const uint32_t flags = (uint32_t)(*env)->GetIntField(env, pkt, fid_flags) &
-                           (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE);
-    uint32_t avail = joff <= al ? al - joff : 0u;
-    if (avail > 65535u) avail = 65535u; /* no region is larger */
-    if (arr && avail) (*env)->GetByteArrayRegion(env, arr, (jsize)joff, (jsize)avail, (jbyte *)tl_pkt);
+    jbyteArray arr;
+    uint32_t joff, avail, length, flags;
+    int rc = read_packet(env, pkt, &arr, &joff, &avail, &length, &flags);
+    if (rc != SRTP_OK) return rc;
     const uint32_t old = length;
     int32_t status = 0;
     uint32_t need = 0;
-    int rc = srtp_rawpacket_transform_one((srtp_aggregator *)H(agg), reverse ? 1 : 0, tid, arr ? tl_pkt : NULL,
-                                          avail, 0, &length, flags, &status, &need, tl_grow, ONE_BYTES);
+    rc = srtp_rawpacket_transform_one((srtp_aggregator *)H(agg), reverse ? 1 : 0, tid, arr ? tl_pkt : NULL,
+                                      avail, 0, &length, flags, &status, &need, tl_grow, ONE_BYTES);
     if (rc != SRTP_OK) return rc;
-    if (status == SRTP_STATUS_SKIPPED) return status;
+    if (status == SRTP_STATUS_SKIPPED || (status == SRTP_STATUS_DROP_INVALID && old > avail)) return status;
     if (need) { /* RawPacket.append / grow: a new byte[] at offset 0 */
         jbyteArray nb = (*env)->NewByteArray(env, (jsize)need);
         if (!nb) return SRTP_ENOMEM;
@@ -289,8 +341,106 @@ JNIEXPORT jint JNICALL JFN(transformOne)(JNIEnv *env, jclass c, jlong agg, jbool
     } else if (arr) {
         uint32_t w = old > length ? old : length;
         if (w > avail) w = avail;
-        (*env)->SetByteArrayRegion(env, arr, (jsize)joff, (jsize)w, (const jbyte *)tl_pkt);
+        if (w) (*env)->SetByteArrayRegion(env, arr, (jsize)joff, (jsize)w, (const jbyte *)tl_pkt);
     }
     (*env)->SetIntField(env, pkt, fid_length, (jint)length);
     return status;
+}
+
+/* ---- the asynchronous per-packet path (GpuPacketQueue) ---- */
+
+/* A completion queue on the process's aggregator for one Java thread (a
+ * connector's send thread, a receive loop): up to maxInFlight packets
+ * submitted and not yet reaped. */
+JNIEXPORT jlong JNICALL JFN(queueCreate)(JNIEnv *env, jclass c, jlong agg, jint maxInFlight) {
+    srtp_queue *q = NULL;
+    if (maxInFlight < 1) return 0;
+    return srtp_queue_create((srtp_aggregator *)H(agg), (uint32_t)maxInFlight, &q) == SRTP_OK
+               ? (jlong)(intptr_t)q : 0;
+}
+
+JNIEXPORT void JNICALL JFN(queueDestroy)(JNIEnv *env, jclass c, jlong q) {
+    srtp_queue_destroy((srtp_queue *)H(q));
+}
+
+/* Submits one RawPacket (srtp_rawpacket_submit): 0, SRTP_EAGAIN (reap first)
+ * or another negative SRTP_E* code.  The packet's bytes are copied now; the
+ * RawPacket must not change until its completion is reaped, which writes the
+ * result back.  skip: the transformer's packet predicate rejected it (it
+ * completes untouched, in order). */
+JNIEXPORT jint JNICALL JFN(queueSubmit)(JNIEnv *env, jclass c, jlong q, jboolean reverse, jint tid, jobject pkt,
+                                        jboolean skip, jlong cookie) {
+    if (!pkt || raw_packet_ids(env) != 0) return SRTP_EINVAL;
+    if (skip)
+        return srtp_rawpacket_submit((srtp_queue *)H(q), reverse ? 1 : 0, tid, NULL, 0, 0, 0, SRTP_PKT_FLAG_SKIP,
+                                     (uint64_t)cookie);
+    jbyteArray arr;
+    uint32_t joff, avail, length, flags;
+    const int rc = read_packet(env, pkt, &arr, &joff, &avail, &length, &flags);
+    if (rc != SRTP_OK) return rc;
+    return srtp_rawpacket_submit((srtp_queue *)H(q), reverse ? 1 : 0, tid, arr ? tl_pkt : NULL, avail, 0, length,
+                                 flags, (uint64_t)cookie);
+}
+
+static __thread srtp_completion *tl_comps;
+static __thread jint *tl_status;
+static __thread uint32_t tl_comps_n;
+
+/* Reaps up to status.length completions in submission order and writes each
+ * back into its RawPacket -- ring[cookie % ring.length], the Java side's ring
+ * of packets in flight -- as SinglePacketTransformer leaves it (in place, or a
+ * new buffer where RawPacket.append / grow reallocate; length updated).
+ * status[i] receives completion i's SRTP_STATUS_*.  wait: block until at least
+ * one is there.  Returns the count or a negative SRTP_E* code. */
+JNIEXPORT jint JNICALL JFN(queueReap)(JNIEnv *env, jclass c, jlong qh, jobjectArray ring, jintArray status,
+                                      jboolean wait) {
+    srtp_queue *q = (srtp_queue *)H(qh);
+    if (!q || !ring || !status || raw_packet_ids(env) != 0) return SRTP_EINVAL;
+    const jsize max = (*env)->GetArrayLength(env, status), rl = (*env)->GetArrayLength(env, ring);
+    if (max < 1 || rl < 1) return SRTP_EINVAL;
+    if (tl_comps_n < (uint32_t)max) {
+        free(tl_comps);
+        free(tl_status);
+        tl_comps = malloc((size_t)max * sizeof *tl_comps);
+        tl_status = malloc((size_t)max * sizeof *tl_status);
+        tl_comps_n = tl_comps && tl_status ? (uint32_t)max : 0u;
+        if (!tl_comps_n) return SRTP_ENOMEM;
+    }
+    const int n = srtp_queue_reap(q, tl_comps, (uint32_t)max, wait ? 1 : 0);
+    if (n <= 0) return n;
+    if ((*env)->PushLocalFrame(env, 2 * n + 16) != 0) return SRTP_ENOMEM;
+    int rc = n;
+    for (int i = 0; i < n; i++) {
+        const srtp_completion *cp = &tl_comps[i];
+        tl_status[i] = cp->status;
+        jobject pkt = (*env)->GetObjectArrayElement(env, ring, (jsize)(cp->cookie % (uint64_t)rl));
+        if (!pkt) continue;
+        jbyteArray arr = (jbyteArray)(*env)->GetObjectField(env, pkt, fid_buffer);
+        const uint32_t al = arr ? (uint32_t)(*env)->GetArrayLength(env, arr) : 0u;
+        const jint jo = (*env)->GetIntField(env, pkt, fid_offset);
+        const uint32_t joff = jo < 0 ? UINT32_MAX : (uint32_t)jo;
+        uint32_t avail = joff <= al ? al - joff : 0u;
+        if (avail > 65535u) avail = 65535u;
+        uint32_t copy = 0, need = 0;
+        if (srtp_rawpacket_complete(q, cp, avail, &copy, &need) != SRTP_OK) {
+            rc = SRTP_EINVAL;
+            continue;
+        }
+        if (need) { /* RawPacket.append / grow: a new byte[] at offset 0 */
+            jbyteArray nb = (*env)->NewByteArray(env, (jsize)need);
+            if (!nb) {
+                rc = SRTP_ENOMEM;
+                continue;
+            }
+            (*env)->SetByteArrayRegion(env, nb, 0, (jsize)copy, (const jbyte *)cp->data);
+            (*env)->SetObjectField(env, pkt, fid_buffer, nb);
+            (*env)->SetIntField(env, pkt, fid_offset, 0);
+        } else if (copy && arr) {
+            (*env)->SetByteArrayRegion(env, arr, (jsize)joff, (jsize)copy, (const jbyte *)cp->data);
+        }
+        if (cp->data) (*env)->SetIntField(env, pkt, fid_length, (jint)cp->len);
+    }
+    (*env)->SetIntArrayRegion(env, status, 0, n, tl_status);
+    (*env)->PopLocalFrame(env, NULL);
+    return rc;
 }

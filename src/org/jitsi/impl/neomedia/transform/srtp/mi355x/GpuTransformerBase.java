@@ -2,17 +2,20 @@
  * What GpuSRTPTransformer and GpuSRTCPTransformer share: a SinglePacketTransformer
  * (transform/SinglePacketTransformer.java:33-217) whose per-packet
  * transform(RawPacket) / reverseTransform(RawPacket) run on the MI355X engine.
- * NOT COMPILED IN THIS REPOSITORY (no JDK); see INTEGRATION.md.
+ * Not compiled in this repository (no JDK); see INTEGRATION.md.
  *
  * Per packet (what every reference caller does: the connectors' 1-element
  * arrays, RTPConnectorInputStream.java:425-452 / RTPConnectorOutputStream.java
  * :268-300, and DtlsPacketTransformer.transformSrtp, :1544-1564): one
  * srtp_rawpacket_transform_one through the process's aggregator, which puts the
  * packets of all concurrently calling threads into shared GPU bundles and
- * returns each caller its own packet.  Arrays of more than one packet go to the
- * GPU as one bundle (srtp_rawpacket_transform) with SinglePacketTransformer's
- * abort-on-throw; an array of one takes the inherited loop over the per-packet
- * call.
+ * returns each caller its own packet.  Arrays of more than one packet go
+ * through srtp_rawpacket_transform with SinglePacketTransformer's
+ * abort-on-throw: up to 8192 packets none of which can throw share the
+ * aggregator's bundles with every other thread's packets, other arrays run as
+ * one bundle of their own; an array of one takes the inherited loop over the
+ * per-packet call.  Threads that keep many packets in flight use
+ * GpuPacketQueue instead.
  */
 package org.jitsi.impl.neomedia.transform.srtp.mi355x;
 
@@ -33,7 +36,7 @@ abstract class GpuTransformerBase
 
     final int tid;
 
-    private final Predicate<RawPacket> packetPredicate;
+    final Predicate<RawPacket> packetPredicate;
 
     private long exceptionsInBatchTransform, exceptionsInBatchReverseTransform;
 
@@ -122,7 +125,8 @@ abstract class GpuTransformerBase
                 if (pkts[i] != null && !packetPredicate.test(pkts[i]))
                     skip[i] = 1;
         }
-        int r = SrtpMi355x.check(SrtpMi355x.transformPackets(SrtpMi355x.batch(), reverse, tid, pkts, skip));
+        int r = SrtpMi355x.check(SrtpMi355x.transformPackets(SrtpMi355x.dispatch(), SrtpMi355x.aggregator(),
+                                                             reverse, tid, pkts, skip));
         if (r > 0)
         {
             if (reverse)

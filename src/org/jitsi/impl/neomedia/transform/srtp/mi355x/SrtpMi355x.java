@@ -1,8 +1,8 @@
 /*
  * Native declarations of the JNI shim src/native/srtp_mi355x/SrtpMi355x.c
  * over the MI355X SRTP engine (include/srtp_mi355x.h), and the process-wide
- * engine state.  NOT COMPILED IN THIS REPOSITORY (no JDK in the build image);
- * see INTEGRATION.md.
+ * engine state.  The Java classes are not compiled in this repository (no JDK
+ * in the build image); the shim is (tests/jni_stub/), see INTEGRATION.md.
  */
 package org.jitsi.impl.neomedia.transform.srtp.mi355x;
 
@@ -29,10 +29,12 @@ public final class SrtpMi355x
     /** One dispatcher per process: every GPU of the node, SSRC-sharded. */
     private static long dispatch;
 
-    /** One aggregator per process over it: the per-packet calls' bundles. */
-    private static long aggregator;
-
-    private static final ThreadLocal<Long> BATCH = new ThreadLocal<>();
+    /**
+     * One aggregator per process over it: the per-packet calls' bundles.
+     * Read on every per-packet call, so it is published once (volatile) and
+     * read without a lock.
+     */
+    private static volatile long aggregator;
 
     public static synchronized long dispatch()
     {
@@ -60,27 +62,22 @@ public final class SrtpMi355x
         return dispatch;
     }
 
-    static synchronized long aggregator()
+    static long aggregator()
     {
-        if (aggregator == 0)
+        long a = aggregator;
+        if (a != 0)
+            return a;
+        synchronized (SrtpMi355x.class)
         {
-            aggregator = aggregatorCreate(dispatch());
             if (aggregator == 0)
-                throw new IllegalStateException("srtp_mi355x: no aggregator");
+            {
+                a = aggregatorCreate(dispatch());
+                if (a == 0)
+                    throw new IllegalStateException("srtp_mi355x: no aggregator");
+                aggregator = a;
+            }
+            return aggregator;
         }
-        return aggregator;
-    }
-
-    /** The calling thread's RawPacket[] staging (srtp_rawpacket_batch). */
-    static long batch()
-    {
-        Long b = BATCH.get();
-        if (b == null)
-        {
-            b = batchCreate(dispatch());
-            BATCH.set(b);
-        }
-        return b;
     }
 
     static int check(int rc)
@@ -99,14 +96,29 @@ public final class SrtpMi355x
     static native int transformerCreate(long d, int kind, int fwd, int rev);
     static native int transformerSetFactory(long d, int transformer, int factory, boolean forward);
     static native int transformerClose(long d, int transformer);
-    static native long batchCreate(long d);
-    static native void batchDestroy(long b);
-    /** 0, 1 + the first throwing element, or a negative error code. */
-    static native int transformPackets(long batch, boolean reverse, int transformer, RawPacket[] pkts,
-                                       int[] skip);
+    /**
+     * 0, 1 + the first throwing element, or a negative error code.  The
+     * calling thread's staging is kept natively and freed when the thread
+     * exits; arrays that cannot throw share the aggregator's bundles.
+     */
+    static native int transformPackets(long d, long aggregator, boolean reverse, int transformer,
+                                       RawPacket[] pkts, int[] skip);
     /** srtp_aggregator_create_dispatch with SRTP_AGG_SEAL_IDLE and no callback. */
     static native long aggregatorCreate(long d);
     static native void aggregatorDestroy(long a);
     /** One packet (srtp_rawpacket_transform_one): its SRTP_STATUS_*, or a negative error code. */
     static native int transformOne(long aggregator, boolean reverse, int transformer, RawPacket pkt);
+
+    /* GpuPacketQueue: srtp_queue_* / srtp_rawpacket_submit / srtp_rawpacket_complete */
+    static final int EAGAIN = -6;
+    static native long queueCreate(long aggregator, int maxInFlight);
+    static native void queueDestroy(long q);
+    /** 0, EAGAIN (reap first) or a negative error code. */
+    static native int queueSubmit(long q, boolean reverse, int transformer, RawPacket pkt, boolean skip,
+                                  long cookie);
+    /**
+     * Completions in submission order, written back into ring[cookie % ring.length];
+     * their statuses in status; the count or a negative error code.
+     */
+    static native int queueReap(long q, RawPacket[] ring, int[] status, boolean wait);
 }

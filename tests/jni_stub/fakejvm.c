@@ -120,12 +120,15 @@ static jint *GetIntArrayElements(JNIEnv *env, jintArray a, jboolean *is_copy) {
     return a ? (jint *)a->data : NULL;
 }
 static void ReleaseIntArrayElements(JNIEnv *env, jintArray a, jint *e, jint mode) {}
+static void SetIntArrayRegion(JNIEnv *env, jintArray a, jsize s, jsize n, const jint *buf) {
+    if (in_range(a, s, n)) memcpy((jint *)a->data + s, buf, (size_t)n * sizeof(jint));
+}
 
 static const struct JNINativeInterface_ g_table = {
     GetArrayLength, GetIntArrayRegion, GetByteArrayRegion, SetByteArrayRegion, FindClass,
     GetFieldID, GetObjectField, GetIntField, SetIntField, SetObjectField, GetObjectArrayElement,
     SetObjectArrayElement, PushLocalFrame, PopLocalFrame, NewByteArray, GetIntArrayElements,
-    ReleaseIntArrayElements,
+    ReleaseIntArrayElements, SetIntArrayRegion,
 };
 static JNIEnv g_env = &g_table;
 
@@ -146,6 +149,7 @@ JNIEXPORT jintArray fj_new_ints(const jint *data, jsize n) {
 }
 JNIEXPORT jobjectArray fj_new_objects(jsize n) { return new_array(K_OBJS, n, sizeof(jobject)); }
 JNIEXPORT void fj_set_element(jobjectArray a, jsize i, jobject v) { ((jobject *)a->data)[i] = v; }
+JNIEXPORT void fj_ints_read(jintArray a, jint *out) { memcpy(out, a->data, (size_t)a->len * sizeof(jint)); }
 JNIEXPORT jobject fj_get_element(jobjectArray a, jsize i) { return ((jobject *)a->data)[i]; }
 
 JNIEXPORT jobject fj_new_packet(jbyteArray buffer, jint offset, jint length, jint flags) {

@@ -55,6 +55,7 @@ struct JNINativeInterface_ {
     jbyteArray (*NewByteArray)(JNIEnv *env, jsize len);
     jint *(*GetIntArrayElements)(JNIEnv *env, jintArray a, jboolean *is_copy);
     void (*ReleaseIntArrayElements)(JNIEnv *env, jintArray a, jint *elems, jint mode);
+    void (*SetIntArrayRegion)(JNIEnv *env, jintArray a, jsize start, jsize len, const jint *buf);
 };
 
 #endif

@@ -56,14 +56,16 @@ def load():
                     ("fj_packet_buffer", [vp], vp), ("fj_packet_offset", [vp], i32),
                     ("fj_packet_length", [vp], i32), ("fj_bytes_len", [vp], i32),
                     ("fj_bytes_read", [vp, vp], None), ("fj_exceptions", [], C.c_int),
-                    ("fj_frames", [], C.c_int), ("fj_reset", [], None)]:
+                    ("fj_frames", [], C.c_int), ("fj_reset", [], None), ("fj_ints_read", [vp, vp], None)]:
         getattr(L, f).argtypes, getattr(L, f).restype = a, r
     sig = {"deviceCount": ([], i32), "dispatchCreate": ([vp, i32, i32], i64), "dispatchDestroy": ([i64], None),
            "factoryCreate": ([i64, u8, vp, vp, vp, vp], i32), "factoryClose": ([i64, i32], i32),
            "transformerCreate": ([i64, i32, i32, i32], i32), "transformerSetFactory": ([i64, i32, i32, u8], i32),
-           "transformerClose": ([i64, i32], i32), "batchCreate": ([i64], i64), "batchDestroy": ([i64], None),
-           "transformPackets": ([i64, u8, i32, vp, vp], i32), "aggregatorCreate": ([i64], i64),
-           "aggregatorDestroy": ([i64], None), "transformOne": ([i64, u8, i32, vp], i32)}
+           "transformerClose": ([i64, i32], i32),
+           "transformPackets": ([i64, i64, u8, i32, vp, vp], i32), "aggregatorCreate": ([i64], i64),
+           "aggregatorDestroy": ([i64], None), "transformOne": ([i64, u8, i32, vp], i32),
+           "queueCreate": ([i64, i32], i64), "queueDestroy": ([i64], None),
+           "queueSubmit": ([i64, u8, i32, vp, u8, i64], i32), "queueReap": ([i64, vp, vp, u8], i32)}
     for n, (a, r) in sig.items():
         J(n).argtypes, J(n).restype = [vp, vp] + a, r
     return L, J
@@ -92,12 +94,10 @@ class Jvm:
                                           1, 1 << 14)
         assert self.d
         self.agg = self.J("aggregatorCreate")(self.env, self.cls, self.d)
-        self.batch = self.J("batchCreate")(self.env, self.cls, self.d)
-        assert self.agg and self.batch
+        assert self.agg
 
     def close(self):
         self.J("aggregatorDestroy")(self.env, self.cls, self.agg)
-        self.J("batchDestroy")(self.env, self.cls, self.batch)
         self.J("dispatchDestroy")(self.env, self.cls, self.d)
         assert self.L.fj_exceptions() == 0, "the shim read or wrote an array region out of range"
         assert self.L.fj_frames() == 0, "unbalanced local frames"
@@ -139,8 +139,57 @@ class Jvm:
         for i, p in enumerate(pkts):
             self.L.fj_set_element(arr, i, p)
         sk = self.ints(skip) if skip is not None else None
-        r = self.J("transformPackets")(self.env, self.cls, self.batch, int(reverse), tid, arr, sk)
+        r = self.J("transformPackets")(self.env, self.cls, self.d, self.agg, int(reverse), tid, arr, sk)
         return r, [self.L.fj_get_element(arr, i) for i in range(len(pkts))]
+
+
+class PacketQueue:
+    """GpuPacketQueue.java over the shim's queue entries: a ring of the
+    RawPackets in flight by submission number, reaped in submission order."""
+
+    def __init__(self, jvm, max_in_flight):
+        self.jvm, self.J, self.env, self.cls = jvm, jvm.J, jvm.env, jvm.cls
+        self.q = self.J("queueCreate")(self.env, self.cls, jvm.agg, max_in_flight)
+        assert self.q
+        self.n = max_in_flight
+        self.ring = jvm.L.fj_new_objects(max_in_flight)
+        self.status = jvm.ints(np.zeros(min(max_in_flight, 1024), np.int32))
+        self.nst = min(max_in_flight, 1024)
+        self.pkts = [None] * max_in_flight
+        self.submitted = self.reaped = 0
+
+    def submit(self, reverse, tid, p, skip=False):
+        """False when the queue is full (GpuPacketQueue.submit)."""
+        if self.submitted - self.reaped == self.n:
+            return False
+        i = self.submitted % self.n
+        self.jvm.L.fj_set_element(self.ring, i, p)
+        rc = self.J("queueSubmit")(self.env, self.cls, self.q, int(reverse), tid, p, int(skip), self.submitted)
+        if rc == N.EAGAIN:
+            return False
+        assert rc == 0, rc
+        self.pkts[i] = p
+        self.submitted += 1
+        return True
+
+    def reap(self, wait=True):
+        """[(packet, status)] in submission order (GpuPacketQueue.reap)."""
+        if self.submitted == self.reaped:
+            return []
+        n = self.J("queueReap")(self.env, self.cls, self.q, self.ring, self.status, int(wait))
+        assert n >= 0, n
+        st = np.zeros(self.nst, np.int32)
+        self.jvm.L.fj_ints_read(self.status, st.ctypes.data)
+        out = []
+        for k in range(n):
+            i = self.reaped % self.n
+            out.append((self.pkts[i], int(st[k])))
+            self.pkts[i] = None
+            self.reaped += 1
+        return out
+
+    def close(self):
+        self.J("queueDestroy")(self.env, self.cls, self.q)
 
 
 def oracle_one(ot, reverse, data, extra=0):
@@ -264,5 +313,195 @@ def test_jni_per_packet_from_many_threads_vs_oracle():
             for (ti, data), (st, got) in zip(scripts[t], results[t]):
                 ost, ob = oracle_one(otids[ti], False, data)
                 assert st == ost and got == ob
+    finally:
+        jvm.close()
+
+
+def rtp_of(k, s, q, n, rng, bad_ext=False):
+    return rtp(0x50000000 + 8 * k + s, 1000 + 97 * k + q, n, rng, bad_ext)
+
+
+@pytest.mark.gpu
+def test_jni_queue_64_threads_in_flight_vs_oracle():
+    """GpuPacketQueue: 64 "JVM threads" (a connector send thread each), 50
+    sender and 50 receiver transformers, each thread keeping >= 32 packets in
+    flight through queueSubmit / queueReap.  Protect with a throw (an
+    extension header past the packet) in mid-stream, then unprotect of the
+    results with replays and forgeries; every RawPacket -- status, bytes,
+    length, and the new buffer where RawPacket.append reallocates -- against
+    the oracle replaying each thread's packets as 1-element arrays in its
+    submission order (each thread owns its SSRCs, so that is each context's
+    order)."""
+    T, NT, PER = 64, 50, 48
+    jvm = Jvm(n_shards=2)
+    try:
+        keys = synth.keys(77, NT)
+        ts, tr, ots, otr = [], [], [], []
+        for k, s in keys:
+            fs, fr = jvm.factory(True, k, s, P80[0]), jvm.factory(False, k, s, P80[0])
+            ts.append(jvm.transformer(0, fs, fs))
+            tr.append(jvm.transformer(0, fr, fr))
+            ofs = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+            ofr = O.Factory(False, k, s, opol(P80[0]), opol(P80[1]))
+            ots.append(O.Transformer(O.KIND_RTP, ofs, ofs))
+            otr.append(O.Transformer(O.KIND_RTP, ofr, ofr))
+        # per thread: (transformer index, data, buffer extra, offset)
+        scripts = []
+        for k in range(T):
+            rng = np.random.default_rng(500 + k)
+            sc = []
+            for q in range(PER):
+                s = q % 3
+                bad = q == 20 and k % 4 == 0
+                data = rtp_of(k, s, q // 3, int(rng.integers(60, 1300)), rng, bad_ext=bad)
+                extra, off = [(0, 0), (16, 5), (3, 0)][q % 3]
+                sc.append(((3 * k + s) % NT, data, extra, off))
+            scripts.append(sc)
+        depth = 64
+        results = [None] * T
+        in_flight = [0] * T
+        errs = []
+
+        def run(k, reverse, items):
+            qu = PacketQueue(jvm, depth)
+            out, pk = [], []
+            try:
+                for ti, data, extra, off in items:
+                    p = jvm.packet(data, off, extra)
+                    pk.append((p, jvm.L.fj_packet_buffer(p)))
+                    while not qu.submit(reverse, (tr if reverse else ts)[ti], p):
+                        out += qu.reap(True)
+                    in_flight[k] = max(in_flight[k], qu.submitted - qu.reaped)
+                while qu.submitted != qu.reaped:
+                    out += qu.reap(True)
+            finally:
+                qu.close()
+            assert [p for p, _ in out] == [p for p, _ in pk]  # submission order
+            return [(st, jvm.packet_bytes(p)[0], jvm.L.fj_packet_buffer(p) == b0)
+                    for (p, st), (_, b0) in zip(out, pk)]
+
+        def work(k, reverse, items):
+            try:
+                results[k] = run(k, reverse, items)
+            except Exception as ex:  # noqa: BLE001
+                errs.append(ex)
+
+        def run_all(reverse, all_items):
+            th = [threading.Thread(target=work, args=(k, reverse, all_items[k])) for k in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errs, errs[:3]
+
+        run_all(False, scripts)
+        assert min(in_flight) >= 32
+        seen = set()
+        protected = []
+        for k in range(T):
+            pr = []
+            for (ti, data, extra, off), (st, got, same_buf) in zip(scripts[k], results[k]):
+                ost, ob = oracle_one(ots[ti], False, data, extra)
+                assert st == ost and got == ob, (k, N.STATUS_NAMES[st], N.STATUS_NAMES[ost])
+                if ost == N.STATUS_OK:
+                    assert same_buf == (extra >= 10)  # append: in place only with room
+                    pr.append((ti, got))
+                seen.add(st)
+            protected.append(pr)
+        assert N.STATUS_ERR_MALFORMED in seen
+        # unprotect: the thread's protected packets with a replay and a forgery
+        un = []
+        for k in range(T):
+            items = [(ti, d, 0, 0) for ti, d in protected[k]]
+            bad = bytearray(items[7][1])
+            bad[-3] ^= 0x40
+            items.insert(9, (items[7][0], bytes(bad), 0, 0))   # forged copy of an earlier packet
+            items.insert(15, items[4])                           # exact replay
+            un.append(items)
+        run_all(True, un)
+        seen = set()
+        for k in range(T):
+            for (ti, data, extra, off), (st, got, _) in zip(un[k], results[k]):
+                ost, ob = oracle_one(otr[ti], True, data, extra)
+                assert st == ost and got == ob, (k, N.STATUS_NAMES[st], N.STATUS_NAMES[ost])
+                seen.add(st)
+        assert {N.STATUS_OK, N.STATUS_DROP_REPLAY, N.STATUS_DROP_AUTH} <= seen
+    finally:
+        jvm.close()
+
+
+@pytest.mark.gpu
+def test_jni_small_arrays_share_bundles_vs_oracle():
+    """transformPackets of arrays that cannot throw (replays, forgeries, a
+    predicate-skipped element and a packet longer than its buffer, but no
+    malformed header) from 16 threads at once: they run through the thread's
+    queue on the aggregator's lanes; every element against the oracle."""
+    T, NT = 16, 8
+    jvm = Jvm(n_shards=2)
+    try:
+        keys = synth.keys(88, NT)
+        ts, tr, ots, otr = [], [], [], []
+        for k, s in keys:
+            fs, fr = jvm.factory(True, k, s, P80[0]), jvm.factory(False, k, s, P80[0])
+            ts.append(jvm.transformer(0, fs, fs))
+            tr.append(jvm.transformer(0, fr, fr))
+            ofs = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+            ofr = O.Factory(False, k, s, opol(P80[0]), opol(P80[1]))
+            ots.append(O.Transformer(O.KIND_RTP, ofs, ofs))
+            otr.append(O.Transformer(O.KIND_RTP, ofr, ofr))
+        res = [None] * T
+        errs = []
+
+        def work(k):
+            try:
+                rng = np.random.default_rng(900 + k)
+                ti = k % NT
+                out = []
+                for rnd in range(6):
+                    datas = [rtp_of(k, q % 2, 8 * rnd + q, int(rng.integers(60, 1300)), rng) for q in range(8)]
+                    pk = [jvm.packet(d, 0, 16 if q % 2 else 0) for q, d in enumerate(datas)]
+                    r, o = jvm.array(False, ts[ti], pk)
+                    prot = [(r, [(x is not None, jvm.packet_bytes(p)[0]) for x, p in zip(o, pk)])]
+                    got = [g for _, g in prot[0][1]]
+                    ins = list(got)
+                    ins[3] = ins[1]                      # replay
+                    f = bytearray(ins[5])
+                    f[20] ^= 1
+                    ins[5] = bytes(f)                    # forgery
+                    pk2 = [jvm.packet(d) for d in ins]
+                    skip = np.zeros(8, np.int32)
+                    skip[6] = 1                          # the packet predicate said no
+                    long_p = jvm.L.fj_new_packet(jvm.L.fj_new_bytes(ins[7], len(ins[7])), 0, len(ins[7]) + 5, 0)
+                    pk2[7] = long_p                      # length past its buffer: RawPacket.isInvalid
+                    r2, o2 = jvm.array(True, tr[ti], pk2, skip)
+                    out.append((datas, r, prot, ins, r2, [(x is not None, jvm.packet_bytes(p)[0]
+                                                           if q != 7 else None) for q, (x, p) in enumerate(zip(o2, pk2))]))
+                res[k] = out
+            except Exception as ex:  # noqa: BLE001
+                errs.append(ex)
+
+        th = [threading.Thread(target=work, args=(k,)) for k in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs, errs[:3]
+        for k in range(T):
+            ti = k % NT
+            for datas, r, prot, ins, r2, un in res[k]:
+                assert r == 0
+                for q, (d, (kept, got)) in enumerate(zip(datas, prot[0][1])):
+                    ost, ob = oracle_one(ots[ti], False, d, 16 if q % 2 else 0)
+                    assert kept == (ost == N.STATUS_OK) and got == ob
+                assert r2 == 0
+                for q, (d, (kept, got)) in enumerate(zip(ins, un)):
+                    if q == 6:
+                        assert kept and got == d        # skipped: untouched
+                        continue
+                    if q == 7:
+                        assert not kept                 # DROP_INVALID: null
+                        continue
+                    ost, ob = oracle_one(otr[ti], True, d)
+                    assert kept == (ost == N.STATUS_OK) and got == ob, (q, N.STATUS_NAMES[ost])
     finally:
         jvm.close()

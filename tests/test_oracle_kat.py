@@ -134,7 +134,7 @@ def test_abi_exports_every_declared_symbol():
     import ctypes
     import re
     from libjitsi_amd import _native
-    decl = re.findall(r"^\s*(?:int|void|void \*|int32_t|int64_t|const char \*|srtp_engine \*)\s*\*?(srtp_\w+)\(",
+    decl = re.findall(r"^\s*(?:int|void|void \*|int32_t|int64_t|const char \*|srtp_\w+ \*)\s*\*?(srtp_\w+)\(",
                       open(_native.HEADER_PATH).read(), re.M)
     assert set(decl) == set(_native.EXPORTED)
     lib = ctypes.CDLL(_native.LIB_PATH)

@@ -9,6 +9,16 @@
 //   path "array": srtp_rawpacket_transform with a 1-element array on the
 //                 thread's own batch -- one GPU round trip per call (the
 //                 round-3 drop-in)
+//   path "arrayq": as "array", the batch routed through the aggregator
+//                 (srtp_rawpacket_batch_set_aggregator: what the JNI shim's
+//                 transformPackets does for arrays that cannot throw)
+//   path "queue": the asynchronous call (GpuPacketQueue): each thread owns a
+//                 completion queue and keeps SYNC_DEPTH (default 64) packets in
+//                 flight -- srtp_rawpacket_submit, srtp_queue_reap, and
+//                 srtp_rawpacket_complete + a copy of each result back into its
+//                 buffer (the shim's SetByteArrayRegion); with "rt" each
+//                 protected packet is then submitted for unprotect before its
+//                 buffer takes the next packet
 //
 // over one engine or a G-shard dispatcher (all shards on device 0 of a one-GPU
 // box).  1200-B RTP packets, AES_CM_128_HMAC_SHA1_80 protect, each thread its
@@ -20,9 +30,12 @@
 // calls.
 //
 //   sync_bench [seconds-per-point] [path shards threads [rt]]   (one point: e.g. "one 0 1")
+//
+// The latency of a queued call runs from its submit to its reap.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <deque>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -51,6 +64,94 @@ void fill_packet(uint8_t *p, uint32_t len, uint64_t &rng) {
     p[1] = 96;
 }
 
+uint32_t ns_since(Clock::time_point t0) {
+    return (uint32_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+}
+
+// One thread of the "queue" path (see the file comment).
+struct QueueWorker {
+    srtp_aggregator *a;
+    const std::vector<int32_t> &tr, &trr;
+    int k, n_tr;
+    uint32_t L, BUF, depth;
+    bool rt;
+    std::atomic<bool> &stop;
+    std::vector<uint32_t> &lat, &latu;
+    uint64_t &bad;
+
+    struct Buf {
+        std::vector<uint8_t> b;
+        uint32_t len = 0;
+        int s = 0;
+        Clock::time_point t0;
+    };
+
+    void run() {
+        srtp_queue *q = nullptr;
+        check(srtp_queue_create(a, depth, &q), "queue");
+        std::vector<Buf> bufs(depth);
+        std::vector<srtp_completion> comps(depth);
+        std::deque<std::pair<uint32_t, int32_t>> pend; // (buffer, reverse) to submit, in order
+        uint64_t rng = 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1);
+        const int n_ssrc = 3;
+        uint16_t seq[n_ssrc];
+        for (auto &x : seq) x = (uint16_t)(rng >> 40), rng = rng * 6364136223846793005ull + 1;
+        uint64_t n = 0;
+        auto next_packet = [&](uint32_t i) {
+            Buf &bf = bufs[i];
+            const int s = (int)(n++ % n_ssrc);
+            const uint32_t ssrc = 0x20000000u + (uint32_t)k * 16u + (uint32_t)s;
+            const uint16_t sq = seq[s]++;
+            uint8_t *p = bf.b.data();
+            p[2] = (uint8_t)(sq >> 8); p[3] = (uint8_t)sq;
+            p[8] = (uint8_t)(ssrc >> 24); p[9] = (uint8_t)(ssrc >> 16); p[10] = (uint8_t)(ssrc >> 8); p[11] = (uint8_t)ssrc;
+            bf.len = L;
+            bf.s = s;
+            pend.emplace_back(i, 0);
+        };
+        for (uint32_t i = 0; i < depth; i++) {
+            bufs[i].b.resize(BUF);
+            fill_packet(bufs[i].b.data(), L, rng);
+            next_packet(i);
+        }
+        for (;;) {
+            const bool stopping = stop.load(std::memory_order_relaxed);
+            while (!stopping && !pend.empty()) {
+                const auto [i, rev] = pend.front();
+                Buf &bf = bufs[i];
+                const int ti = (k * n_ssrc + bf.s) % n_tr;
+                const int rc = srtp_rawpacket_submit(q, rev, rev ? trr[(size_t)ti] : tr[(size_t)ti], bf.b.data(), BUF, 0,
+                                                     bf.len, 0, ((uint64_t)rev << 32) | i);
+                if (rc == SRTP_EAGAIN) break;
+                check(rc, "submit");
+                bf.t0 = Clock::now();
+                pend.pop_front();
+            }
+            if (srtp_queue_outstanding(q) == 0) {
+                if (stopping) break;
+                continue;
+            }
+            const int m = srtp_queue_reap(q, comps.data(), depth, 1);
+            if (m < 0) check(m, "reap");
+            for (int j = 0; j < m; j++) {
+                const srtp_completion &c = comps[(size_t)j];
+                const uint32_t i = (uint32_t)c.cookie;
+                Buf &bf = bufs[i];
+                (c.reverse ? latu : lat).push_back(ns_since(bf.t0));
+                uint32_t copy = 0, need = 0;
+                check(srtp_rawpacket_complete(q, &c, BUF, &copy, &need), "complete");
+                if (need || c.status != SRTP_STATUS_OK || c.len != (c.reverse ? L : L + 10)) bad++;
+                if (!need && copy) memcpy(bf.b.data(), c.data, copy); // SetByteArrayRegion
+                bf.len = c.len;
+                if (stopping) continue;
+                if (!c.reverse && rt) pend.emplace_back(i, 1);
+                else next_packet(i);
+            }
+        }
+        srtp_queue_destroy(q);
+    }
+};
+
 double pct(std::vector<uint32_t> &v, double q) {
     if (v.empty()) return 0.0;
     const size_t k = std::min(v.size() - 1, (size_t)(q * (double)v.size()));
@@ -69,15 +170,17 @@ int main(int argc, char **argv) {
     const int shard_counts[] = {0, 8};
     const int thread_counts[] = {1, 8, 64};
     const bool one_point = argc > 4;
-    const int p_only = one_point ? (strcmp(argv[2], "one") == 0 ? 0 : 1) : -1;
+    const int p_only = one_point ? (strcmp(argv[2], "one") == 0 ? 0 : strcmp(argv[2], "array") == 0 ? 1
+                                    : strcmp(argv[2], "queue") == 0 ? 2 : 3) : -1;
+    const uint32_t depth = getenv("SYNC_DEPTH") ? (uint32_t)atoi(getenv("SYNC_DEPTH")) : 64u;
     const int g_only = one_point ? atoi(argv[3]) : -1, t_only = one_point ? atoi(argv[4]) : -1;
     const bool rt = argc > 5 && strcmp(argv[5], "rt") == 0;
-    for (int path = 0; path < 2; path++) {
+    for (int path = 0; path < 4; path++) {
         for (int G : shard_counts) {
             for (int T : thread_counts) {
                 if (one_point) {
                     if (path != p_only || G != g_only || T != t_only) continue;
-                } else if (path == 1 && T == 64 && G == 8) {
+                } else if (((path == 1 || path == 3) && T == 64 && G == 8) || (path == 2 && T == 1)) {
                     continue; // 64 pinned batches x 8 shards: skip
                 }
                 srtp_engine_opts o;
@@ -110,7 +213,7 @@ int main(int argc, char **argv) {
                             : srtp_transformer_create(e, SRTP_KIND_RTP, fr, fr, &trr[(size_t)t]), "transformer");
                 }
                 srtp_aggregator *a = nullptr;
-                if (path == 0) {
+                if (path != 1) {
                     srtp_aggregator_opts ao;
                     srtp_aggregator_opts_default(&ao);
                     ao.max_packets = 4096;
@@ -125,10 +228,17 @@ int main(int argc, char **argv) {
                 std::vector<std::thread> th;
                 for (int k = 0; k < T; k++) {
                     th.emplace_back([&, k] {
+                        if (path == 2) {
+                            started++;
+                            QueueWorker{a, tr, trr, k, n_tr, L, BUF, depth, rt, stop, lat[(size_t)k], latu[(size_t)k],
+                                        bad[(size_t)k]}.run();
+                            return;
+                        }
                         srtp_rawpacket_batch *b = nullptr;
-                        if (path == 1)
+                        if (path == 1 || path == 3)
                             check(d ? srtp_rawpacket_batch_create_dispatch(d, &b) : srtp_rawpacket_batch_create(e, &b),
                                   "batch");
+                        if (path == 3) check(srtp_rawpacket_batch_set_aggregator(b, a), "batch agg");
                         std::vector<uint8_t> buf(BUF), grow(65535 + 16);
                         uint64_t rng = 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1);
                         fill_packet(buf.data(), L, rng);
@@ -218,7 +328,7 @@ int main(int argc, char **argv) {
                        "\"pkt_len\": %u, \"calls\": %zu, \"seconds\": %.3f, \"calls_per_s\": %.1f, "
                        "\"lat_us\": {\"mean\": %.1f, \"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f}, "
                        "%s\"bundles\": %llu, \"packets_per_bundle\": %.1f, \"not_ok\": %llu}\n",
-                       path == 0 ? "one" : "array", G ? G : 1, G ? "true" : "false", T, n_tr, L, calls, dt,
+                       path == 0 ? "one" : path == 1 ? "array" : path == 2 ? "queue" : "arrayq", G ? G : 1, G ? "true" : "false", T, n_tr, L, calls, dt,
                        calls / dt, mean, pct(all, 0.5), pct(all, 0.9), pct(all, 0.99), pct(all, 0.999), ul,
                        (unsigned long long)bundles, bundles ? (double)comp / bundles : 0.0,
                        (unsigned long long)nbad);
