@@ -323,7 +323,7 @@ int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
 #define SRTP_PIPE_ONE_STREAM 0x1u
 /* SRTP_PIPE_POLL_CROWDED: a wait on this pipeline polls the bundle's event
  * (sleeping between polls) instead of spinning in hipEventSynchronize while
- * more than SRTP_PIPE_SPIN_WAITERS (env, default 4) threads of the process
+ * more than 4 threads of the process
  * wait on such pipelines -- for one pipeline per caller thread (the 1-packet
  * RawPacket path): 64 spinning callers took the host's cores from the threads
  * enqueueing the next bundles.  Few waiters keep the spin's quicker wake-up. */

@@ -226,10 +226,9 @@ class CopyPool {
     bool stop_ = false;
 };
 
-// copy helpers: SRTP_DISPATCH_COPY_THREADS, else the CPUs this process may
-// run on beyond one per shard worker, at most 8
+// copy helpers: the CPUs this process may run on beyond one per shard
+// worker, at most 8
 int copy_threads(int n_shards) {
-    if (const char *e = getenv("SRTP_DISPATCH_COPY_THREADS")) return std::max(0, atoi(e));
     cpu_set_t cs;
     int ncpu = 4;
     if (sched_getaffinity(0, sizeof cs, &cs) == 0) ncpu = CPU_COUNT(&cs);

@@ -99,6 +99,7 @@ struct srtp_engine {
 };
 
 namespace {
+constexpr uint32_t kSmallCtrMax = 8192u; // k_ctr_small takes bundles up to this size
 
 int fail(srtp_engine *e, int code, const std::string &msg) {
     if (e) e->last_error = msg;
@@ -690,8 +691,6 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.check_replay = e->opts.check_replay;
     a.abort_on_error = abort < 0 ? e->opts.abort_on_error : (abort ? 1 : 0);
     a.serial = e->serial++;
-    static const int debug_mode = getenv("SRTP_DEBUG") ? atoi(getenv("SRTP_DEBUG")) : 0;
-    a.debug = debug_mode;
     a.dbg = e->dbg;
     a.counters = e->d_counters;
 #ifdef SRTP_STAMPS
@@ -712,12 +711,10 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     // keys: slot or ctx_cap (= not walked), ctx_bits + 1 bits: 8-bit digits up
     // to 16 bits, two 9-11-bit digits up to 22 (the wide sort), else 8-bit again
     // 17-19 bits: an 8-bit pass and one wide pass (hybrid); 20-22: two wide
-    // passes; SRTP_SORT_NARROW / SRTP_SORT_WIDE force 8-bit / two wide passes (A/B)
+    // passes (profiles/r04/kernel_experiments.md 8)
     const int key_bits = e->ctx_bits + 1;
-    static const bool force_narrow = getenv("SRTP_SORT_NARROW") != nullptr;
-    static const bool force_wide = getenv("SRTP_SORT_WIDE") != nullptr;
-    const bool big = key_bits > 16 && key_bits <= 2 * kSortWideMaxBits && !force_narrow;
-    const bool hybrid = big && key_bits <= 8 + kSortWideMaxBits && !force_wide;
+    const bool big = key_bits > 16 && key_bits <= 2 * kSortWideMaxBits;
+    const bool hybrid = big && key_bits <= 8 + kSortWideMaxBits;
     const bool wide = big && !hybrid;
     a.sort_key_bits = key_bits;
     a.sort_hi_bits = hybrid ? key_bits - 8 : 0;
@@ -730,11 +727,9 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.sort_zero = wide ? ss.wprefix : hybrid ? ss.counts[0] : ss.counts[a.sort_passes - 1];
     a.sort_zero_words = ((n + sort_tile_records() - 1u) / sort_tile_records()) * 256u; // tiles of this bundle x 256 digits
     // a small bundle's AES-CM keystream by k_ctr_small (a lane per counter-block
-    // pair; the fused kernels only MAC): up to SRTP_SMALL_CTR_MAX packets,
-    // default 8192 (128 waves: under one wave per SIMD), 0 = never
-    static const uint32_t small_max = getenv("SRTP_SMALL_CTR_MAX") ? (uint32_t)atol(getenv("SRTP_SMALL_CTR_MAX"))
-                                                                    : 8192u;
-    a.small_ctr = n <= small_max ? 1 : 0;
+    // pair; the fused kernels only MAC): up to 8192 packets (128 waves: under
+    // one wave per SIMD; profiles/r04/kernel_experiments.md 9)
+    a.small_ctr = n <= kSmallCtrMax ? 1 : 0;
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;
     a.ctl = e->ctl + c;
@@ -750,19 +745,16 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (need_ctl) HIPCHK(e, hipMemsetAsync(a.ctl, 0, sizeof(BundleCtl), s));
     if (need_emin) HIPCHK(e, hipMemsetAsync(a.e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
     // a one-tile bundle is sorted by one workgroup in one launch
-    // (SRTP_SORT_TILE=0: the multi-pass sort); SRTP_SORT_TILE=2: parsed by the
-    // same workgroup in the same launch (k_parse_sort_tile)
-    static const int tile_sort = getenv("SRTP_SORT_TILE") ? atoi(getenv("SRTP_SORT_TILE")) : 1;
-    const bool one_tile = tile_sort && n <= sort_tile_records();
+    const bool one_tile = n <= sort_tile_records();
     {
         StageTimer t(e, s, SRTP_STAGE_PARSE);
         // also resets control block c ^ 1
-        HIPCHK(e, one_tile && tile_sort == 2 ? launch_parse_sort_tile(a, s) : launch_parse(a, s));
+        HIPCHK(e, launch_parse(a, s));
     }
     e->ctl_clean[c ^ 1] = true;
     if (a.abort_on_error) e->emin_filled[c ^ 1] = a.n_transformers;
     e->ctl_cur = c ^ 1;
-    if (!(one_tile && tile_sort == 2)) {
+    {
         StageTimer t(e, s, SRTP_STAGE_SORT);
         HIPCHK(e, one_tile ? launch_sort_tile(a, s) : launch_sort(a, ss, s));
     }
@@ -780,7 +772,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         // first pass's window (returns at once when there are none) -- which a
         // bundle of fewer than kLongMin packets cannot hold: a small bundle
         // without abort-on-throw saves the launch
-        if (a.abort_on_error || n >= kLongMin || a.debug || a.dbg) HIPCHK(e, launch_walk(a, 1, s));
+        if (a.abort_on_error || n >= kLongMin || a.dbg) HIPCHK(e, launch_walk(a, 1, s));
     }
     if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
@@ -1417,21 +1409,19 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
     return SRTP_OK;
 }
 
-// How a pipeline waits for a bundle (SRTP_PIPE_WAIT_US): < 0 (default)
-// hipEventSynchronize, which spins on a core; >= 0 polls hipEventQuery,
-// yielding the CPU between polls, and after that many microseconds sleeps
-// 20 us between polls.  A SRTP_PIPE_POLL_CROWDED pipeline's wait also polls
-// (at once) when more than SRTP_PIPE_SPIN_WAITERS (4) threads are waiting on
-// such pipelines: 64 callers each spinning on its own 1-packet bundle took the
+// How a pipeline waits for a bundle: hipEventSynchronize, which spins on a
+// core -- except that a SRTP_PIPE_POLL_CROWDED pipeline polls hipEventQuery,
+// yielding the CPU between polls (sleeping 20 us between polls after the
+// first), while more than kSpinWaiters threads are waiting on such
+// pipelines: 64 callers each spinning on its own 1-packet bundle took the
 // host's cores from the threads enqueueing the next bundles (4.7k calls/s,
-// p99 82 ms; polling 12.9k, 4.7 ms).  Other pipelines (aggregator lanes,
-// dispatcher shards: a few waiters) always keep the spin's wake-up.
+// p99 82 ms; polling 12.9k, 4.7 ms; profiles/r04/kernel_experiments.md 7 and
+// 10).  Other pipelines (aggregator lanes, dispatcher shards: a few waiters)
+// always keep the spin's wake-up.
 static std::atomic<int> g_crowd{0};
+constexpr int kSpinWaiters = 4;
 
 static int wait_event(hipEvent_t ev, bool crowd) {
-    static const long env_us = getenv("SRTP_PIPE_WAIT_US") ? atol(getenv("SRTP_PIPE_WAIT_US")) : -1;
-    static const int spin_waiters =
-        getenv("SRTP_PIPE_SPIN_WAITERS") ? atoi(getenv("SRTP_PIPE_SPIN_WAITERS")) : 4;
     struct Crowd {
         bool on;
         int n;
@@ -1440,15 +1430,15 @@ static int wait_event(hipEvent_t ev, bool crowd) {
             if (on) g_crowd.fetch_sub(1, std::memory_order_relaxed);
         }
     } cr(crowd);
-    const long spin_us = env_us < 0 && cr.n > spin_waiters ? 0 : env_us;
-    if (spin_us < 0) return hipEventSynchronize(ev) == hipSuccess ? 0 : -1;
-    const auto t0 = std::chrono::steady_clock::now();
+    if (cr.n <= kSpinWaiters) return hipEventSynchronize(ev) == hipSuccess ? 0 : -1;
+    bool first = true;
     for (;;) {
         const hipError_t q = hipEventQuery(ev);
         if (q == hipSuccess) return 0;
         if (q != hipErrorNotReady) return -1;
-        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us)) std::this_thread::yield();
+        if (first) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(20));
+        first = false;
     }
 }
 

@@ -43,7 +43,6 @@ struct BundleArgs {
     int32_t check_replay;
     int32_t abort_on_error;
     uint32_t serial;       // bundle serial (context birth stamp)
-    int32_t debug;         // diagnostics only (SRTP_DEBUG env): 0 in production
     uint32_t dbg;          // kDbg* test hooks (srtp_engine_set_debug): 0 in production
     int32_t has_skein;     // the engine has Skein-MAC key sets (the walk's Skein re-check)
     unsigned long long *counters; // [kCountReplicas][kCtrStride] cumulative event counters
@@ -111,7 +110,6 @@ hipError_t launch_sort(const BundleArgs &a, const SortScratch &ss, hipStream_t s
 hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s);
 // k_parse + the one-tile sort in one launch (a bundle of at most
 // sort_tile_records() packets)
-hipError_t launch_parse_sort_tile(const BundleArgs &a, hipStream_t s);
 // unprotect: fused tag check + speculative in-place decryption (before the walk)
 hipError_t launch_unprotect(const BundleArgs &a, hipStream_t s);
 // Engines with Skein-MAC key sets.  Unprotect: those packets' tag check under

@@ -404,31 +404,6 @@ __device__ __forceinline__ void ks_sha_half(const char *__restrict__ lds, const 
                                             uint32_t K8[8], uint32_t v[5], uint32_t w[16]) {
     uint32_t x[4], y[4];
     constexpr int t = 40 * P;
-#if defined(SRTP_EXP_NOSHA) && defined(SRTP_EXP_NOAES) // diagnostic: neither
-#pragma unroll
-    for (int k = 0; k < 4; k++) { K8[k] = cp.r[k] ^ (uint32_t)j0; K8[4 + k] = cp.r[k] + (uint32_t)j0; }
-    (void)x; (void)y; (void)v; (void)w;
-    return;
-#elif defined(SRTP_EXP_NOSHA) // diagnostic builds: AES only / SHA-1 only (results wrong)
-    ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
-#pragma unroll
-    for (int r = 3; r < 10; r++) aes_round2(lds, tb, rk.k + 4 * r, x, y);
-    aes_last2(lds, tb, rk.k + 40, x, y);
-#pragma unroll
-    for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
-    return;
-#elif defined(SRTP_EXP_NOAES)
-#pragma unroll
-    for (int k = 0; k < 4; k++) { x[k] = cp.r[k] ^ (uint32_t)j0; y[k] = cp.r[k] + (uint32_t)j0; }
-    sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
-    sha1_rounds4<t + 8>(v, w); sha1_rounds4<t + 12>(v, w);
-    sha1_rounds4<t + 16>(v, w); sha1_rounds4<t + 20>(v, w);
-    sha1_rounds4<t + 24>(v, w); sha1_rounds4<t + 28>(v, w);
-    sha1_rounds4<t + 32>(v, w); sha1_rounds4<t + 36>(v, w);
-#pragma unroll
-    for (int k = 0; k < 4; k++) { K8[k] = x[k]; K8[4 + k] = y[k]; }
-    return;
-#endif
     ctr_first2(lds, tb, cp, j0 + 2 * P, j0 + 2 * P + 1, x, y);
     sha1_rounds4<t + 0>(v, w); sha1_rounds4<t + 4>(v, w);
     // rounds 3..10: SHA-1 rounds t+8 .. t+39 inside the round asm, at its LDS
@@ -1211,10 +1186,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_scatter(SortPass sp) {
             // record of a skipped / invalid packet unwritten (stale scratch,
             // whose index may lie anywhere)
             if (sp.spos && key[r] <= sp.walk_max) sp.spos[rec.p & kRecIdxMask] = pos;
-#ifndef SRTP_DIAG_NOATOM // diagnostic build: without the next pass's counts (results wrong)
             if (sp.next_counts)
                 atomicAdd(&sp.next_counts[(pos / kSortTile) * 256 + ((key[r] >> (sp.shift + 8)) & 255u)], 1u);
-#endif
         }
     }
     if (SRTP_LEN_ORDER && sp.lord) {
@@ -1455,8 +1428,8 @@ hipError_t launch_sort_wide(const BundleArgs &a, const SortScratch &ss, hipStrea
 // It zeroes the tile's first-digit counts that k_parse accumulated (the walk
 // clears the other tables as after a multi-pass sort).
 // The one-tile sort of the records whose keys key_in[r] (record r *
-// kSortThreads + threadIdx.x) the calling workgroup holds: k_sort_tile loads
-// them, k_parse_sort_tile has just parsed them.
+// kSortThreads + threadIdx.x) the calling workgroup holds (k_sort_tile loads
+// them).
 __device__ __forceinline__ void sort_tile_body(const BundleArgs &a, uint32_t key_bits,
                                                const uint32_t key_in[kSortItems]) {
     constexpr int W = kSortThreads / 64;
@@ -1579,53 +1552,10 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_tile(BundleArgs a, uint32
     sort_tile_body(a, key_bits, key);
 }
 
-// k_parse and k_sort_tile in one launch for a one-tile bundle (the per-packet
-// path's): the workgroup parses every packet (as k_parse: the records, the
-// class counts of the tile, the next bundle's control block), keeps the keys
-// in registers and sorts them.  No first-digit counts (the multi-pass sort's
-// input) are made, so none need zeroing.
-__global__ __launch_bounds__(kSortThreads) void k_parse_sort_tile(BundleArgs a, uint32_t key_bits) {
-    __shared__ uint32_t s_cls[32];
-    const int t = threadIdx.x;
-    if (t < 32) s_cls[t] = 0u;
-    __syncthreads();
-    if (t == 0) *a.ctl_next = BundleCtl{};
-    if (a.abort_on_error)
-        for (uint32_t i = (uint32_t)t; i < a.n_transformers; i += kSortThreads) a.e_min_next[i] = 0x7f7f7f7f;
-    uint32_t key[kSortItems];
-#pragma unroll
-    for (int r = 0; r < kSortItems; r++) {
-        const uint32_t i = r * kSortThreads + t;
-        key[r] = 0u;
-        if (i < a.n) {
-            atomicAdd(&s_cls[len_class(a.len[i])], 1u);
-            key[r] = parse_one(a, i);
-        }
-    }
-    __syncthreads();
-    if (t < 32) {
-        const uint32_t c = s_cls[t];
-        if (c) atomicAdd(&a.cls_tile[t], c);
-        const unsigned long long m = __ballot(c != 0u);
-        if (t == 0 && (uint32_t)m) atomicOr(&a.cls_tile[32], (uint32_t)m);
-    }
-    // the records (sv_in, read back by index) and the class counts (write_lord)
-    // before the sort reads them
-    __threadfence();
-    __syncthreads();
-    sort_tile_body(a, key_bits, key);
-}
-
 hipError_t launch_sort_tile(const BundleArgs &a, hipStream_t s) {
     const uint32_t key_bits = (uint32_t)a.sort_key_bits;
     const uint32_t bins = 1u << a.sort_bits; // k_parse's first-digit counts
     hipLaunchKernelGGL(k_sort_tile, dim3(1), dim3(kSortThreads), 0, s, a, key_bits, bins);
-    return hipGetLastError();
-}
-
-hipError_t launch_parse_sort_tile(const BundleArgs &a, hipStream_t s) {
-    if (a.n > (uint32_t)kSortTile) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_parse_sort_tile, dim3(1), dim3(kSortThreads), 0, s, a, (uint32_t)a.sort_key_bits);
     return hipGetLastError();
 }
 
@@ -2841,7 +2771,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     // Long chains (kWalkSpan records or more) are walked by the tiles they
     // cross (chain_part) in the second launch, unless abort-on-throw needs the
     // serial two-pass walk; the first pass only flags that there are some.
-    const bool chains = !two_pass && a.debug == 0;
+    const bool chains = !two_pass;
     const bool chain_pass = limit_pass && !two_pass;
     if (chain_pass && a.ctl->n_long == 0u) return; // no long chain in this bundle
     if (!limit_pass) { // the sort's last digit counts and k_parse's class counts, zero again for the next bundle
@@ -2891,7 +2821,6 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
         }
     }
     __syncthreads();
-    if (a.debug == 1) return;
     const uint32_t prev_key = base ? a.sk_out[base - 1] : ~0u;
     // A chain of kWalkSpan records or more (it reaches the end of the tile it
     // starts in): record j's chain, starting at j, is that long iff the record
@@ -3036,7 +2965,6 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
         // One record of the chain; false ends it.
         auto step = [&](const WalkRec &r, uint32_t g0, uint32_t ok) -> bool {
             if (limit_pass && (int32_t)(r.p & kRecIdxMask) > E) return false;
-            if (a.debug == 2) { st.window += r.p ^ g0 ^ ok; return true; }
             return walk_one<SK>(a, ks, c, st, r, g0, ok, dry, tid);
         };
         // The staged window, from LDS only: no global load in this loop, so
@@ -3052,7 +2980,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
         // of walk_long's speculation).  Such records cost a few instructions
         // here instead of walk_one's branches; the first record that leaves
         // the path, and every record after it, goes through walk_one.
-        if (!two_pass && c.kind == SRTP_KIND_RTP && (st.flags & 1u) && a.debug == 0) {
+        if (!two_pass && c.kind == SRTP_KIND_RTP && (st.flags & 1u)) {
             const bool mac = c.auth != SRTP_NULL_AUTHENTICATION;
             for (; jj < win; jj++) {
                 if (s_key[jj] != key) break;
@@ -3193,11 +3121,6 @@ __device__ __forceinline__ void load_chunk(const uint8_t *pkt, int b, int lim, u
 
 // Whole 64-B chunk b (inside the packet: no bounds checks, no branches).
 __device__ __forceinline__ void load_chunk_full(const uint8_t *pkt, int b, uint32_t d[16]) {
-#ifdef SRTP_EXP_NOMEM // diagnostic build: no packet loads in the fused loops (results wrong)
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = (uint32_t)(uintptr_t)pkt * (uint32_t)(k + 1) + (uint32_t)b;
-    return;
-#endif
     const uint4 *qp = reinterpret_cast<const uint4 *>(pkt + 64 * b);
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -3207,26 +3130,11 @@ __device__ __forceinline__ void load_chunk_full(const uint8_t *pkt, int b, uint3
 }
 
 __device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint32_t d[16]) {
-#ifdef SRTP_EXP_NOMEM
-    if (d[0] != 0x9e3779b9u) return;
-#endif
     uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
 #pragma unroll
     for (int m = 0; m < 4; m++) qp[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
 }
 
-// ---------------------------------------------- quad-cooperative chunk access
-// One lane per packet reads its 64-B chunk as four 16-B pieces, each wave
-// instruction touching 64 lines.  With SRTP_COALESCE the four lanes of a quad
-// read each other's chunks instead -- lane m of the quad takes piece m of every
-// quad packet, so one instruction covers 16 whole 64-B chunks -- and a 4x4
-// transpose across the quad (DPP quad_perm, VALU only) hands every lane its
-// own packet's chunk.  Stores go the same way back.  Only lanes active in the
-// calling loop iteration (at the same chunk b) take part; a piece whose quad
-// lane is inactive is read / written by the packet's own lane.
-#ifndef SRTP_COALESCE
-#define SRTP_COALESCE 0
-#endif
 // SRTP_TAIL_STEP: k_unprotect's fused loop takes the packet's ROC-carrying
 // chunk in one more fused step (0.301 -> 0.296 ms per bundle).  The same for
 // k_protect's last partial chunk was measured slower either way -- as a step
@@ -3236,136 +3144,6 @@ __device__ __forceinline__ void store_chunk_full(uint8_t *pkt, int b, const uint
 #ifndef SRTP_TAIL_STEP
 #define SRTP_TAIL_STEP 1
 #endif
-template <int CTRL>
-__device__ __forceinline__ uint32_t qdpp(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ uint32_t qbcast(uint32_t x) { return qdpp<CTRL>(x); }
-
-// transpose of r[reg][lane-in-quad] over the quad, one stage per lane-index bit
-template <int S>
-__device__ __forceinline__ void quad_tstage(uint32_t r[4], bool hi) {
-    constexpr int CTRL = S == 1 ? 0xB1 : 0x4E; // quad_perm [1,0,3,2] / [2,3,0,1]
-#pragma unroll
-    for (int a = 0; a < 4; a++) {
-        if (a & S) continue;
-        const int bb = a | S;
-        const uint32_t xa = qdpp<CTRL>(r[a]), xb = qdpp<CTRL>(r[bb]);
-        const uint32_t na = hi ? xb : r[a];
-        const uint32_t nb = hi ? r[bb] : xa;
-        r[a] = na;
-        r[bb] = nb;
-    }
-}
-__device__ __forceinline__ void quad_transpose(uint32_t d[16]) {
-    const uint32_t lane = __lane_id();
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-        uint32_t r[4] = {d[e], d[4 + e], d[8 + e], d[12 + e]};
-        quad_tstage<1>(r, (lane & 1u) != 0u);
-        quad_tstage<2>(r, (lane & 2u) != 0u);
-        d[e] = r[0]; d[4 + e] = r[1]; d[8 + e] = r[2]; d[12 + e] = r[3];
-    }
-}
-__device__ __forceinline__ uint32_t quad_peer_off(uint32_t own, int i) {
-    return i == 0 ? qbcast<0x00>(own) : i == 1 ? qbcast<0x55>(own) : i == 2 ? qbcast<0xAA>(own)
-                                                                            : qbcast<0xFF>(own);
-}
-// True when all four lanes of this lane's quad are active in the calling loop
-// iteration: only then do they share their chunks (else each lane reads and
-// writes its own, as load_chunk_full / store_chunk_full).
-__device__ __forceinline__ bool quad_full() {
-    const uint32_t qb = __lane_id() & ~3u;
-    return ((__ballot(1) >> qb) & 0xFull) == 0xFull;
-}
-// Issue the loads of chunk b: in a full quad lane m reads piece m of every
-// quad packet (d[4i..4i+3] = piece m of packet i), else its own pieces.
-// load_chunk_quad_finish (after the loads have had time to land) transposes.
-__device__ __forceinline__ void load_chunk_quad_issue(const uint8_t *seg, uint32_t off, int b,
-                                                      bool full, uint32_t d[16]) {
-    const uint32_t m = __lane_id() & 3u;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t po = full ? quad_peer_off(off, i) + 16u * m : off + 16u * (uint32_t)i;
-        const uint4 v = *reinterpret_cast<const uint4 *>(seg + po + 64u * (uint32_t)b);
-        d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
-    }
-}
-__device__ __forceinline__ void load_chunk_quad_finish(bool full, uint32_t d[16]) {
-    if (full) quad_transpose(d);
-}
-// Store chunk b (d is clobbered).
-__device__ __forceinline__ void store_chunk_quad(uint8_t *seg, uint32_t off, int b, bool full,
-                                                 uint32_t d[16]) {
-    if (full) quad_transpose(d);
-    const uint32_t m = __lane_id() & 3u;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t po = full ? quad_peer_off(off, i) + 16u * m : off + 16u * (uint32_t)i;
-        *reinterpret_cast<uint4 *>(seg + po + 64u * (uint32_t)b) =
-            make_uint4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
-    }
-}
-
-// ------------------------------------------- stores staged through LDS
-// SRTP_STAGE_STORES: the fused loops' 64-B chunk stores leave the wave
-// quad-coalesced -- four lanes write the four 16-B pieces of one packet's
-// chunk, so a store instruction covers 16 whole chunks instead of touching 64
-// lines -- after a transpose through a 2-KB wave buffer in LDS behind the
-// T-table image (16 waves x 2 KB: the image and the buffers fill the 160 KB).
-// Two passes of 32 lanes: the pass's lanes write their chunks (4 x
-// ds_write_b128), then every lane reads one 16-B piece (2 x ds_read_b128) and
-// stores it.  The LDS, not the VALU, pays for the transpose (the DPP form of
-// round 3 cost 48 VALU per chunk).  Only when every lane of the wave is at the
-// same chunk; otherwise each lane stores its own chunk.
-#ifndef SRTP_STAGE_STORES
-#define SRTP_STAGE_STORES 0
-#endif
-constexpr int kStageWordsPerWave = SRTP_STAGE_STORES ? 512 : 0; // 2 KB
-constexpr int kStageWords = kStageWordsPerWave * (kAesBlock / 64);
-
-// the calling wave's store buffer, behind the T-table image at LDS 0
-__device__ __forceinline__ uint4 *stage_buf(const char *lds) {
-    return reinterpret_cast<uint4 *>(const_cast<char *>(lds) + 4 * kTeWords) +
-           (threadIdx.x >> 6) * (kStageWordsPerWave / 4);
-}
-
-// Chunk b of every lane's packet (d[16]; own_off = the lane's packet offset in
-// seg) to HBM, quad-coalesced, through the wave's buffer wb.  Every lane of the
-// wave must be active.  Peer offsets are fetched per store (ds_bpermute) rather
-// than held across the loop: the fused loops have no VGPRs to spare.
-__device__ __forceinline__ void store_chunk_staged(uint8_t *seg, uint32_t own_off, int b, uint4 *wb,
-                                                   const uint32_t d[16]) {
-    const uint32_t lane = __lane_id();
-    const int q = (int)(lane >> 2);
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        if ((lane >> 5) == (uint32_t)h) {
-            uint4 *dst = wb + 4 * (lane & 31u);
-#pragma unroll
-            for (int m = 0; m < 4; m++) dst[m] = make_uint4(d[4 * m], d[4 * m + 1], d[4 * m + 2], d[4 * m + 3]);
-        }
-        // the LDS runs one wave's instructions in order: only the compiler
-        // must not move the other lanes' writes and reads across (no s_waitcnt)
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_wave_barrier();
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const uint32_t po = (uint32_t)__shfl((int)own_off, 32 * h + 16 * r + q);
-            const uint4 v = wb[64 * r + lane];
-            *reinterpret_cast<uint4 *>(seg + po + 64u * (uint32_t)b + 16u * (lane & 3u)) = v;
-        }
-        // the LDS runs one wave's instructions in order: only the compiler
-        // must not move the other lanes' writes and reads across (no s_waitcnt)
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_wave_barrier();
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
-}
-
-// Store the 16-B pieces of chunk b that overlap the ciphered range [off, end).
 __device__ __forceinline__ void store_chunk(uint8_t *pkt, int b, const Ctr &cs, const uint32_t d[16]) {
     uint4 *qp = reinterpret_cast<uint4 *>(pkt + 64 * b);
 #pragma unroll
@@ -3514,31 +3292,14 @@ __device__ __forceinline__ void protect_one(const BundleArgs &a, const KeySet *_
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
             pk_half<0>(lds, tb, pk, cp, 4 * b - hq, K, v, c);
-#if SRTP_COALESCE == 1
-            const bool full = quad_full();
-            load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
-#else
             load_chunk_full(pkt, b, d);
-#endif
             pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-#if SRTP_COALESCE == 1
-            load_chunk_quad_finish(full, d);
-#endif
             ctr_apply_wave(cs, b, K, d);
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k];
-#if SRTP_COALESCE == 1
-            store_chunk_quad(a.seg, a.off[p], b, full, d);
-#elif SRTP_COALESCE == 2
-            store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
-#elif SRTP_STAGE_STORES
-            if (__builtin_amdgcn_read_exec() == ~0ull) store_chunk_staged(a.seg, (uint32_t)(pkt - a.seg), b, stage_buf(lds), d);
-            else store_chunk_full(pkt, b, d);
-#else
             store_chunk_full(pkt, b, d);
-#endif
         }
 
         inner_words(c, b - 1, L, suffix); // block b-1 (B-1 may carry the suffix)
@@ -3628,9 +3389,8 @@ __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const u
 // threads: registers for the MAC's look-ahead)
 template <bool MacOnly>
 __global__ __launch_bounds__(MacOnly ? kMacBlock : kAesBlock) void k_protect(BundleArgs a) {
-    // the status counts sit at the start of wave 0's store buffer, which wave 0
-    // first writes after flushing them
-    __shared__ uint32_t s_te[kTeWords + (kStageWords > kTeCounters ? kStageWords : kTeCounters)];
+    // the status counts sit behind the T-table image
+    __shared__ uint32_t s_te[kTeWords + kTeCounters];
     uint32_t *s_cnt = s_te + kTeWords;
     STAMP(0);
     STAMP_XCC();
@@ -3757,7 +3517,6 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             spec = true;
         }
     }
-    if (a.debug == 5) spec = false; // diagnostics: MAC only (results wrong by design)
     // for k_unprotect_fix: decrypted here, AES-CM packet of the fused path,
     // RTP, DISCARD/SILENCE (so it needs no key-set lookup to decide a repair)
     a.spec[p] = (spec ? kSpecDid : 0u) | (aes ? kSpecAes : 0u) | (rtp ? kSpecRtp : 0u) |
@@ -3803,31 +3562,14 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = bswap(c[k]);
             pk_half<0>(lds, tb, pk, cp, 4 * b - hq, K, v, c);
-#if SRTP_COALESCE == 1
-            const bool full = quad_full();
-            load_chunk_quad_issue(a.seg, a.off[p], b, full, d);
-#else
             load_chunk_full(pkt, b, d);
-#endif
             pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-#if SRTP_COALESCE == 1
-            load_chunk_quad_finish(full, d);
-#endif
 #pragma unroll
             for (int k = 0; k < 16; k++) c[k] = d[k]; // ciphertext of chunk b, hashed next
             ctr_apply_wave(cs, b, K, d); // cs.end = 0 without speculation: d unchanged
-#if SRTP_COALESCE == 1
-            store_chunk_quad(a.seg, a.off[p], b, full, d);
-#elif SRTP_COALESCE == 2
-            store_chunk_quad(a.seg, a.off[p], b, quad_full(), d);
-#elif SRTP_STAGE_STORES
-            if (__builtin_amdgcn_read_exec() == ~0ull) store_chunk_staged(a.seg, (uint32_t)(pkt - a.seg), b, stage_buf(lds), d);
-            else store_chunk_full(pkt, b, d);
-#else
             store_chunk_full(pkt, b, d);
-#endif
         }
         // The ROC-carrying chunk nb_full (MAC'd bytes up to end) in one more
         // fused step: its keystream beside the hash of block nb_full-1, the
@@ -3846,7 +3588,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-            if (rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
+            if (rtp) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
@@ -3894,7 +3636,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         for (; b < n_blocks; b++) {
             uint32_t d[16];
             q.next(pkt, b, nb_data, end, d);
-            if (b == nb_full && rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
+            if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int m = 0; m < 5; m++) mp[m] = h[m];
@@ -3920,7 +3662,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 if (b < nb_data && 64 * b + 16 * m < end) v = qp[m];
                 d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
             }
-            if (b == nb_full && rtp && a.debug != 3) { // midstate + ciphertext of the ROC-carrying block
+            if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
@@ -3967,7 +3709,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
 
 template <bool MacOnly> // as k_protect's: k_ctr_small decrypts afterwards
 __global__ __launch_bounds__(MacOnly ? kMacBlock : kUnprotectBlock) void k_unprotect(BundleArgs a) {
-    __shared__ uint32_t s_te[kTeWords + kStageWords];
+    __shared__ uint32_t s_te[kTeWords];
     STAMP(0);
     STAMP_XCC();
     // the packet's context state and whether it lies deep in a long chain
@@ -4805,12 +4547,11 @@ hipError_t launch_parse(const BundleArgs &a, hipStream_t s) {
 // rest idle.  So the waves are spread over every CU, at least 4 per
 // workgroup (one per SIMD: the image is filled by the workgroup's threads)
 // and at most max_block / 64.  A full bundle (2^18 packets = 16 waves per CU)
-// keeps 1024-thread workgroups.  SRTP_AES_SPREAD=0: always max_block (A/B).
+// keeps 1024-thread workgroups (profiles/r04/kernel_experiments.md 5).
 static uint32_t aes_block(uint32_t n, uint32_t max_block) {
-    static const bool spread = !getenv("SRTP_AES_SPREAD") || atoi(getenv("SRTP_AES_SPREAD")) != 0;
     static std::atomic<int> cus[64]; // CUs per device, looked up once (any thread)
     int dev = 0;
-    if (!spread || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return max_block;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return max_block;
     int c = cus[dev].load(std::memory_order_relaxed);
     if (c <= 0) {
         if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return max_block;
