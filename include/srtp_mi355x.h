@@ -475,8 +475,10 @@ int srtp_aggregator_transformer_info(srtp_aggregator *a, int32_t t, int32_t *kin
  * Returns the count.  out[i].data points at the packet's processed bytes in
  * the aggregator's pinned slot (max(len, in_len) bytes, within cap; NULL for
  * packets completed at submit) and stays valid until the next reap or
- * destroy of this queue: reaping releases the previous reap's packets, and a
- * slot is reused only when every packet of it has been released.
+ * destroy of this queue (or srtp_queue_release): reaping releases the
+ * previous reap's packets, and a slot is reused only when every packet of it
+ * has been released -- so a caller done with its completions releases them
+ * (srtp_queue_release) rather than holding slots until its next reap.
  *
  * A queue belongs to one thread at a time (submit and reap are not
  * thread-safe on one queue); queues of one aggregator are independent.
@@ -499,6 +501,8 @@ int srtp_queue_create(srtp_aggregator *a, uint32_t max_inflight, srtp_queue **ou
 int srtp_queue_submit(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t *pkt, uint32_t copy_len,
                       uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie);
 int srtp_queue_reap(srtp_queue *q, srtp_completion *out, uint32_t max, int32_t wait);
+/* Releases the last reap's completions (their data pointers become invalid). */
+void srtp_queue_release(srtp_queue *q);
 /* packets submitted and not yet reaped */
 int32_t srtp_queue_outstanding(srtp_queue *q);
 srtp_aggregator *srtp_queue_aggregator(srtp_queue *q);

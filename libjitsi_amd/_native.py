@@ -63,7 +63,7 @@ EXPORTED = [
     "srtp_host_register", "srtp_host_unregister", "srtp_host_is_registered", "srtp_pipeline_submit_host",
     "srtp_pipeline_create_ex", "srtp_host_alloc", "srtp_host_free",
     "srtp_queue_create", "srtp_queue_submit", "srtp_queue_reap", "srtp_queue_outstanding",
-    "srtp_queue_aggregator", "srtp_queue_destroy", "srtp_packet_may_throw",
+    "srtp_queue_aggregator", "srtp_queue_destroy", "srtp_queue_release", "srtp_packet_may_throw",
     "srtp_rawpacket_batch_set_aggregator", "srtp_rawpacket_submit", "srtp_rawpacket_complete",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
@@ -260,6 +260,8 @@ def lib() -> C.CDLL:
     L.srtp_queue_outstanding.restype = i32
     L.srtp_queue_aggregator.argtypes = [vp]
     L.srtp_queue_aggregator.restype = vp
+    L.srtp_queue_release.argtypes = [vp]
+    L.srtp_queue_release.restype = None
     L.srtp_queue_destroy.argtypes = [vp]
     L.srtp_queue_destroy.restype = None
     L.srtp_packet_may_throw.argtypes = [i32, i32, C.c_char_p, u32, u32, u32, u32]

@@ -1101,6 +1101,12 @@ int srtp_queue_reap(srtp_queue *q, srtp_completion *out, uint32_t max, int32_t w
     return (int)n;
 }
 
+void srtp_queue_release(srtp_queue *q) {
+    if (!q) return;
+    queue_release(q, q->rel_from, q->rel_to);
+    q->rel_from = q->rel_to = q->head;
+}
+
 srtp_aggregator *srtp_queue_aggregator(srtp_queue *q) { return q ? q->a : nullptr; }
 
 int32_t srtp_queue_outstanding(srtp_queue *q) { return q ? (int32_t)(q->tail - q->head) : 0; }

@@ -281,6 +281,7 @@ int transform_via_queue(srtp_rawpacket_batch *b, int32_t reverse, const int32_t 
             if (c.data) length[i] = c.len;
             if (st == SRTP_STATUS_ERR_MALFORMED && (*thrown < 0 || (int32_t)i < *thrown)) *thrown = (int32_t)i;
         }
+        srtp_queue_release(b->q); // written back: the slots go back at once
         return SRTP_OK;
     };
     for (uint32_t i = 0; i < n; i++) {

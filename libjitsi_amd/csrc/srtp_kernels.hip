@@ -287,7 +287,11 @@ __device__ __forceinline__ void sha1_rounds4(uint32_t v[5], uint32_t w[16]) {
 // hand-scheduled asm (aes_rounds_asm.inc, generated by tools/gen_aes_asm.py),
 // which needs the T-table image at LDS address 0 -- s_te is the only LDS
 // object of the AES kernels.
-#include "aes_rounds_asm.inc"
+// (tools/build_variant.sh may compile a candidate schedule in its place)
+#ifndef SRTP_AES_ROUNDS
+#define SRTP_AES_ROUNDS "aes_rounds_asm.inc"
+#endif
+#include SRTP_AES_ROUNDS
 
 __device__ __forceinline__ void aes_round2(const char *__restrict__ lds, const TeBase &tb,
                                            const uint32_t *rkr, uint32_t a[4], uint32_t b[4]) {

@@ -440,6 +440,8 @@ JNIEXPORT jint JNICALL JFN(queueReap)(JNIEnv *env, jclass c, jlong qh, jobjectAr
         }
         if (cp->data) (*env)->SetIntField(env, pkt, fid_length, (jint)cp->len);
     }
+    /* every result is in its Java array: the pinned slots go back at once */
+    srtp_queue_release(q);
     (*env)->SetIntArrayRegion(env, status, 0, n, tl_status);
     (*env)->PopLocalFrame(env, NULL);
     return rc;

@@ -80,6 +80,83 @@ def round_body(blocks, last, tables=4):
     return L
 
 
+def round_body_lean(blocks, last, tables=4, R=16):
+    """round_body with R lookup registers instead of 16 per block: lookup i
+    (block-major, column-major) lives in register i mod R, so the perms of a
+    later lookup wait until the column that used its register has been
+    folded.  A column is folded only once every perm of its block has read
+    the block's state.  Keeps up to 15 reads in flight where registers allow."""
+    assert R >= 16, "a block's 16 perms must all read its state before any of its folds"
+    per = [lookups(z, 16 * i, tables) for i, z in enumerate(blocks)]
+    lk = [x for p in per for x in p]
+    n = len(lk)
+    ncols = n // 4
+    reg = lambda i: f"%[t{i % R}]"  # noqa: E731
+    L = []
+    st = {"issued": 0, "landed": -1, "folded": 0, "permed": 0}
+
+    def fold_ready():
+        while (st["folded"] < ncols and 4 * st["folded"] + 3 <= st["landed"]
+               and st["permed"] >= 16 * (st["folded"] // 4 + 1)):
+            c = st["folded"]
+            blk, j = divmod(c, 4)
+            z = blocks[blk]
+            a, b, cc, d = (reg(4 * c + t) for t in range(4))
+            if last:
+                if tables == 4:
+                    L.extend([f"v_perm_b32 {a}, {b}, {a}, %[s4]", f"v_perm_b32 {cc}, {d}, {cc}, %[s5]",
+                              f"v_bitop3_b32 %[{z}{j}], {a}, {cc}, %[k{j}] bitop3:0x96"])
+                else:
+                    L.extend([f"v_perm_b32 {a}, {b}, {a}, %[s4]", f"v_perm_b32 {cc}, {d}, {cc}, %[s6]",
+                              f"v_bitop3_b32 %[{z}{j}], {a}, {cc}, %[k{j}] bitop3:0x96"])
+            elif tables == 4:
+                L.extend([f"v_bitop3_b32 {a}, {a}, {b}, {cc} bitop3:0x96",
+                          f"v_bitop3_b32 %[{z}{j}], {a}, {d}, %[k{j}] bitop3:0x96"])
+            else:
+                L.extend([f"v_bitop3_b32 {cc}, {cc}, {d}, %[r{j}] bitop3:0x96",
+                          f"v_alignbit_b32 {cc}, {cc}, {cc}, 16",
+                          f"v_bitop3_b32 %[{z}{j}], {a}, {b}, {cc} bitop3:0x96"])
+            st["folded"] += 1
+
+    def wait_until(idx):
+        cnt = st["issued"] - 1 - idx
+        L.append(f"s_waitcnt lgkmcnt({min(cnt, MAX_LGKM)})")
+        st["landed"] = max(st["landed"], idx)
+        fold_ready()
+
+    while st["issued"] < n:
+        while st["permed"] < n and (st["permed"] < R or (st["permed"] - R) // 4 < st["folded"]):
+            i = st["permed"]
+            _, src, t, k = lk[i]
+            L.append(f"v_perm_b32 {reg(i)}, {src}, %[b{t}], %[s{k}]")
+            st["permed"] += 1
+        fold_ready()
+        while st["issued"] < st["permed"] and st["issued"] - (st["landed"] + 1) < MAX_LGKM:
+            L.append(f"ds_read_b32 {reg(st['issued'])}, {reg(st['issued'])}")
+            st["issued"] += 1
+        if st["issued"] < n:
+            if st["issued"] - (st["landed"] + 1) >= MAX_LGKM:
+                wait_until(st["issued"] - MAX_LGKM)
+            else:  # a register must free: the column that held it
+                wait_until(4 * ((st["permed"] - R) // 4) + 3)
+    L.append("s_waitcnt lgkmcnt(0)")
+    st["landed"] = n - 1
+    fold_ready()
+    assert st["folded"] == ncols
+    return L
+
+
+LEAN_R = 0  # > 0: emit rounds with LEAN_R lookup registers (round_body_lean)
+
+
+def body_for(blocks, last, tables):
+    return round_body_lean(blocks, last, tables, LEAN_R) if LEAN_R else round_body(blocks, last, tables)
+
+
+def nregs(nb):
+    return LEAN_R if LEAN_R else 16 * nb
+
+
 SEL4 = ["0x0c020400u", "0x0c020500u", "0x0c020600u", "0x0c020700u"]
 SEL2 = ["0x0c0c0400u", "0x0c0c0500u", "0x0c0c0600u", "0x0c0c0700u"]
 
@@ -88,12 +165,12 @@ def emit(name, blocks, last, tables=4, kv=False):
     """A __device__ function running one (middle or last) round on the blocks.
     kv: the round key words are per-lane values (VGPRs: a wave mixing key
     sets) instead of wave-uniform SGPRs."""
-    body = round_body(blocks, last, tables)
+    body = body_for(blocks, last, tables)
     nb = len(blocks)
     args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
     s = [f"__device__ __forceinline__ void {name}({args}, const uint32_t bs[4],",
          "                                       const uint32_t *__restrict__ rkr) {",
-         f"    uint32_t t[{16 * nb}];"]
+         f"    uint32_t t[{nregs(nb)}];"]
     if tables == 2 and not last:
         s.append("    uint32_t r16[4];")
         s.append("#pragma unroll")
@@ -102,7 +179,7 @@ def emit(name, blocks, last, tables=4, kv=False):
     for ln in body:
         s.append(f'        "{ln}\\n"')
     outs = [f'[{z}{i}] "+v"({z}[{i}])' for z in blocks for i in range(4)]
-    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(16 * nb)]
+    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(nregs(nb))]
     ins = [f'[b{i}] "v"(bs[{i}])' for i in range(4)]
     sels = SEL4 if tables == 4 else SEL2
     ins += [f'[s{i}] "s"({sels[i]})' for i in range(4)]
@@ -173,17 +250,17 @@ def emit_sha(name, blocks, last, t0, tables=4, kv=False):
     """One AES round on the block pair with SHA-1 rounds t0..t0+3 interleaved;
     v[5]/w[16] are the hash's working variables and schedule.  kv: per-lane
     round key words (see emit)."""
-    body = merge_sha(round_body(blocks, last, tables), sha_rounds(t0))
+    body = merge_sha(body_for(blocks, last, tables), sha_rounds(t0))
     nb = len(blocks)
     args = ", ".join(f"uint32_t {z}[4]" for z in blocks)
     s = [f"template <> __device__ __forceinline__ void {name}<{t0}>({args}, const uint32_t bs[4],",
          "        const uint32_t *__restrict__ rkr, uint32_t v[5], uint32_t w[16]) {",
-         f"    uint32_t t[{16 * nb}], sf, sr, sx;"]
+         f"    uint32_t t[{nregs(nb)}], sf, sr, sx;"]
     s.append("    asm volatile(")
     for ln in body:
         s.append(f'        "{ln}\\n"')
     outs = [f'[{z}{i}] "+v"({z}[{i}])' for z in blocks for i in range(4)]
-    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(16 * nb)]
+    outs += [f'[t{i}] "=&v"(t[{i}])' for i in range(nregs(nb))]
     outs += [f'[h{r}] "+v"(v[{i}])' for i, r in enumerate("abcde")]
     outs += [f'[w{i}] "+v"(w[{i}])' for i in range(16)]
     outs += ['[sf] "=&v"(sf)', '[sr] "=&v"(sr)', '[sx] "=&v"(sx)']

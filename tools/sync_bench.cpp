@@ -147,6 +147,8 @@ struct QueueWorker {
                 if (!c.reverse && rt) pend.emplace_back(i, 1);
                 else next_packet(i);
             }
+            srtp_queue_release(q); // written back
+
         }
         srtp_queue_destroy(q);
     }
