@@ -464,10 +464,11 @@ int srtp_aggregator_transformer_info(srtp_aggregator *a, int32_t t, int32_t *kin
  * open bundle (the aggregator's sealing rules apply); cookie is the caller's.
  * A packet with SRTP_PKT_FLAG_SKIP, or with len > cap (RawPacket.isInvalid),
  * completes at once with SRTP_STATUS_SKIPPED / SRTP_STATUS_DROP_INVALID and
- * no bytes.  Returns SRTP_EAGAIN when max_inflight packets are outstanding,
- * or when no slot is free while the queue holds submitted or reaped
- * packets: the caller reaps and submits again (only a queue with nothing
- * outstanding waits for a slot).
+ * no bytes.  Returns SRTP_EAGAIN when max_inflight packets are outstanding;
+ * when no slot is free it waits for one, but only until the queue's oldest
+ * outstanding packet has completed (then SRTP_EAGAIN: the caller reaps and
+ * submits again), or at once when the last reap's completions are still
+ * held (not released).
  *
  * srtp_queue_reap: up to max completions, in SUBMISSION order (so per
  * transformer and SSRC the reference's order), into out; with wait != 0 it

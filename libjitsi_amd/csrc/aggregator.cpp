@@ -80,12 +80,11 @@
 // length and a pointer to its bytes in the pinned slot (a few stores, no copy
 // and no upcall) and wakes the queue's owner if it sleeps; the owner reaps the
 // entries in submission order and copies the bytes out itself.  The slot stays
-// held (kHeld) until every reaped entry of it has been released -- at the
-// owner's next reap -- so a completed packet's bytes never move.  A submit
-// that finds no free slot while its queue still holds entries returns
-// SRTP_EAGAIN instead of waiting (the owner reaps, which releases slots):
-// only a queue with nothing outstanding may wait for a slot, so a thread never
-// waits on slots that only it can free.
+// held (kHeld) until every reaped entry of it has been released (by
+// srtp_queue_release or the owner's next reap), so a completed packet's bytes
+// never move.  A submit that finds no free slot waits for one only until its
+// queue's oldest packet completes, then returns SRTP_EAGAIN (the owner reaps,
+// which releases slots): a thread never waits on slots that only it can free.
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -682,6 +681,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
         } else {
             sl.state = kHeld; // freed by the last release (queue_release)
             seal_if_idle_locked(a, *ln);
+            ln->cv_space.notify_all(); // queue submitters waiting for a slot look at their entries
             a->cv_idle.notify_all();
         }
     }
@@ -794,9 +794,14 @@ int create(srtp_dispatch *d, srtp_engine *const *engines, size_t n_lanes, const 
 // A packet into its lane's open bundle (srtp_aggregator_submit / _transform):
 // copy_len bytes of pkt, length len, room cap; w != nullptr: a synchronous
 // caller's entry.
+// qe: a completion queue's entry; its queue's oldest outstanding entry
+// (q_head, or nullptr when the queue has none) bounds a wait for a slot: the
+// submit returns SRTP_EAGAIN once that entry has completed (the caller then
+// reaps, which frees slots), so a thread never waits on slots that only its
+// own reaping can free.
 int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t *pkt, uint32_t copy_len,
                  uint32_t len, uint32_t cap, uint32_t flags, uint64_t cookie, Waiter *w, QEntry *qe = nullptr,
-                 bool may_wait = true) {
+                 const QEntry *q_head = nullptr) {
     if (a->closing.load()) return SRTP_EINVAL; // destroy has begun
     const int dir = reverse ? 1 : 0;
     const size_t need = need_of(cap);
@@ -826,7 +831,12 @@ int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t
                 ln.parked.push_back(Parked{dir, tid, flags, cookie, std::vector<uint8_t>(pkt, pkt + len)});
                 return SRTP_OK;
             }
-            if (!may_wait) return SRTP_EAGAIN; // a queue holding slots: its owner reaps first
+            if (q_head) {
+                if (q_head->ready.load(std::memory_order_acquire)) return SRTP_EAGAIN; // reap first
+                // (its completion may come from another lane: poll)
+                ln.cv_space.wait_for(lk, std::chrono::microseconds(200));
+                continue;
+            }
             ln.cv_space.wait(lk); // backpressure: every slot is sealed, in flight or held
         }
     }
@@ -1073,11 +1083,20 @@ int srtp_queue_submit(srtp_queue *q, int32_t reverse, int32_t tid, const uint8_t
         return SRTP_OK;
     }
     e.ready.store(0, std::memory_order_relaxed);
-    // only a queue with nothing outstanding may wait for a slot (file comment)
-    const bool may_wait = q->tail == q->head && q->rel_from == q->rel_to;
+    // completions still held: the caller must release (reap) before it may
+    // wait for a slot that they could be holding
+    if (q->rel_from != q->rel_to) {
+        std::lock_guard<std::mutex> lk(a->mu); // (cheap check first: any free slot at all?)
+        bool any = false;
+        for (auto &ln : a->lanes)
+            for (int i = 0; i < ln->n_slots && !any; i++) any = ln->slots[i].state == kFree;
+        if (!any) return SRTP_EAGAIN;
+    }
+    // a wait for a slot ends when the queue's oldest packet completes (file comment)
+    const QEntry *q_head = q->tail > q->head ? &q->ring[q->head % q->cap] : nullptr;
     const int rc = submit_entry(a, reverse, tid, pkt, copy_len, len, cap,
                                 flags & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE), cookie, nullptr, &e,
-                                may_wait);
+                                q_head);
     if (rc != SRTP_OK) return rc;
     q->tail++;
     return SRTP_OK;

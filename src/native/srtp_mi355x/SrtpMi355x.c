@@ -272,12 +272,15 @@ JNIEXPORT jint JNICALL JFN(deviceCount)(JNIEnv *env, jclass c) {
 /* One aggregator per process over the dispatcher: its lanes coalesce the
  * per-packet calls of every JVM thread into GPU bundles.  Bundles of at most
  * 4096 packets / 8 MB per lane (what a round trip's worth of per-packet calls
- * fills), four pinned slots per lane. */
+ * fills); six pinned slots per lane (48 MB), so that queued callers
+ * (GpuPacketQueue) keep bundles filling while others are in flight or held
+ * for their write-back. */
 JNIEXPORT jlong JNICALL JFN(aggregatorCreate)(JNIEnv *env, jclass c, jlong d) {
     srtp_aggregator_opts o;
     srtp_aggregator_opts_default(&o); /* SRTP_AGG_SEAL_IDLE */
     o.max_packets = 4096;
     o.max_bytes = (size_t)8 << 20;
+    o.depth = 6;
     srtp_aggregator *a = NULL;
     return srtp_aggregator_create_dispatch((srtp_dispatch *)H(d), &o, NULL, NULL, &a) == SRTP_OK
                ? (jlong)(intptr_t)a : 0;

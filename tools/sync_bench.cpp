@@ -220,6 +220,7 @@ int main(int argc, char **argv) {
                     srtp_aggregator_opts_default(&ao);
                     ao.max_packets = 4096;
                     ao.max_bytes = 8u << 20;
+                    if (path != 0) ao.depth = 6; // as the JNI shim's aggregator
                     check(d ? srtp_aggregator_create_dispatch(d, &ao, nullptr, nullptr, &a)
                             : srtp_aggregator_create(e, &ao, nullptr, nullptr, &a), "aggregator");
                 }
