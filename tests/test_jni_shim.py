@@ -395,6 +395,7 @@ def test_jni_queue_64_threads_in_flight_vs_oracle():
             assert not errs, errs[:3]
 
         run_all(False, scripts)
+        print("max packets in flight per thread:", sorted(in_flight))
         assert min(in_flight) >= 32
         seen = set()
         protected = []

@@ -221,6 +221,15 @@ int main(int argc, char **argv) {
                     ao.max_packets = 4096;
                     ao.max_bytes = 8u << 20;
                     if (path != 0) ao.depth = 6; // as the JNI shim's aggregator
+                    // SYNC_AGG="packets,MB,depth": other bundle sizes / slot counts
+                    if (const char *g = getenv("SYNC_AGG")) {
+                        unsigned pk = 0, mb = 0, dp = 0;
+                        if (sscanf(g, "%u,%u,%u", &pk, &mb, &dp) == 3) {
+                            ao.max_packets = pk;
+                            ao.max_bytes = (size_t)mb << 20;
+                            ao.depth = (int32_t)dp;
+                        }
+                    }
                     check(d ? srtp_aggregator_create_dispatch(d, &ao, nullptr, nullptr, &a)
                             : srtp_aggregator_create(e, &ao, nullptr, nullptr, &a), "aggregator");
                 }
