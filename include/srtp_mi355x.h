@@ -310,6 +310,9 @@ int srtp_pipeline_slot_get(srtp_pipeline *pl, int32_t slot, srtp_pipeline_slot *
 int srtp_pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                          int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes);
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot);
+/* 1 when slot's bundle has come back (srtp_pipeline_wait then returns without
+ * blocking) or none is in flight, 0 while it is still running, < 0 on error. */
+int srtp_pipeline_query(srtp_pipeline *pl, int32_t slot);
 /* srtp_pipeline_create with flags.  SRTP_PIPE_ONE_STREAM puts the copies on
  * the engine's own stream instead of two copy streams of the pipeline's: a
  * bundle's H2D, kernels and D2H then run in order with no cross-stream

@@ -65,6 +65,7 @@ EXPORTED = [
     "srtp_queue_create", "srtp_queue_submit", "srtp_queue_reap", "srtp_queue_outstanding",
     "srtp_queue_aggregator", "srtp_queue_destroy", "srtp_queue_release", "srtp_packet_may_throw",
     "srtp_rawpacket_batch_set_aggregator", "srtp_rawpacket_submit", "srtp_rawpacket_complete",
+    "srtp_pipeline_query",
 ]
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
@@ -193,6 +194,7 @@ def lib() -> C.CDLL:
     L.srtp_pipeline_slot_get.argtypes = [vp, i32, C.POINTER(PipelineSlot)]
     L.srtp_pipeline_submit.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t]
     L.srtp_pipeline_wait.argtypes = [vp, i32]
+    L.srtp_pipeline_query.argtypes = [vp, i32]
     L.srtp_pipeline_submit_ex.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t, i32]
     L.srtp_aggregator_transform.argtypes = [vp, i32, i32, vp, u32, u32, u32, u32, vp, pi32, pu32]
     L.srtp_aggregator_transformer_info.argtypes = [vp, i32, pi32, pi32]

@@ -54,7 +54,12 @@
 // flight the next one fills, and is sealed when the one in flight completes.
 // So a lone packet waits one GPU round trip, not the deadline, and under load
 // bundles grow to what arrives during a round trip -- the group commit of a
-// database log.  The lane thread and the producers meet through `idle`:
+// database log.  Pipelined (round 5): with one bundle in flight, the lane
+// thread does not block on it at once; half an average round trip after its
+// submit it seals what has arrived meanwhile and submits that too, so two
+// bundles are in flight and one's copies run beside the other's kernels (a
+// lone bundle's GPU round trip is mostly copies and latency-bound kernels; the
+// GPU idled a third of the time between bundles).  The lane thread and the producers meet through `idle`:
 // the lane stores idle = 1 and then looks at its open slot, a producer
 // reserves its entry and then looks at idle, both sequentially consistent,
 // so at least one of them sees the other and seals.
@@ -564,12 +569,17 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
     ln.idle.store(0);
 }
 
+constexpr size_t kPipe = 2; // bundles a lane keeps in flight under load (SRTP_AGG_SEAL_IDLE)
+
 void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
     (void)lane;
     std::vector<srtp_queue *> touched; // queues with entries in the completed bundle
     std::unique_lock<std::mutex> lk(a->mu);
     // keep up to depth - 2 bundles in flight (one slot per open direction)
     const size_t max_inflight = ln->n_slots > 2 ? (size_t)ln->n_slots - 2 : 1;
+    // submit time per slot and the average round trip (EWMA, us)
+    std::vector<Clock::time_point> t_sub((size_t)ln->n_slots);
+    double rt_us = 200.0;
     for (;;) {
         bool straggler = false; // a sealed slot still being copied into
         auto can_submit = [&] {
@@ -604,6 +614,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
             const size_t bytes = sl.bytes;
             const int32_t rev = sl.reverse;
             lk.unlock(); // the slot is ours: producers only touch open slots
+            t_sub[(size_t)s] = Clock::now();
             const int rc = srtp_pipeline_submit_ex(ln->pl, s, rev, 1, -1, 1, n, bytes, 0);
             lk.lock();
             if (rc != SRTP_OK) {
@@ -616,8 +627,38 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
         if (ln->inflight.empty()) continue; // stop requested with sealed slots still being written
         const int s = ln->inflight.front();
         Slot &sl = ln->slots[s];
+        // Pipelining (file comment): one bundle in flight, room for another
+        // and a free slot -- wait for it only until half a round trip after
+        // its submit, then seal what has arrived and go submit that as well.
+        if ((a->opts.flags & SRTP_AGG_SEAL_IDLE) && ln->inflight.size() + ln->sealed.size() < kPipe &&
+            ln->inflight.size() < max_inflight && !a->stop) {
+            const auto t_seal = t_sub[(size_t)s] + std::chrono::microseconds((long)(rt_us / 2));
+            bool done = false, sealed_more = false;
+            for (;;) {
+                lk.unlock();
+                done = srtp_pipeline_query(ln->pl, s) != 0;
+                lk.lock();
+                if (done || a->stop || !ln->sealed.empty()) break;
+                if (Clock::now() >= t_seal) {
+                    for (int d = 0; d < 2; d++)
+                        if (resv_n(ln->resv[d].load()) > 0) {
+                            seal_locked(a, *ln, d);
+                            sealed_more = true;
+                        }
+                    if (sealed_more || sync_placeable_locked(*ln)) break;
+                }
+                const auto now = Clock::now();
+                ln->cv_work.wait_for(lk, now < t_seal ? std::min<Clock::duration>(t_seal - now, std::chrono::microseconds(20))
+                                                       : Clock::duration(std::chrono::microseconds(20)));
+            }
+            if (!done) continue; // submit what was sealed (or placed), then come back
+        }
         lk.unlock();
         (void)srtp_pipeline_wait(ln->pl, s);
+        {
+            const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_sub[(size_t)s]).count();
+            rt_us = 0.875 * rt_us + 0.125 * us;
+        }
         // queue entries hold the slot until their owners release them; the
         // lane holds it too until this loop is done
         uint32_t nq = 0;

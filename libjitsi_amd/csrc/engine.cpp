@@ -1572,6 +1572,16 @@ int srtp_pipeline_submit_host(srtp_pipeline *pl, int32_t slot, int32_t reverse, 
     return pipeline_submit(pl, slot, reverse, use_tids, tid, use_flags, n, seg_bytes, abort_on_error, host_seg);
 }
 
+int srtp_pipeline_query(srtp_pipeline *pl, int32_t slot) {
+    if (!pl || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> gp(pl->mu);
+    const srtp_pipeline::Slot &sl = pl->slots[(size_t)slot];
+    if (!sl.busy) return 1;
+    const hipError_t q = hipEventQuery(sl.ev_out);
+    if (q == hipSuccess) return 1;
+    return q == hipErrorNotReady ? 0 : fail(pl->e, SRTP_EDEVICE, "pipeline D2H");
+}
+
 int srtp_pipeline_wait(srtp_pipeline *pl, int32_t slot) {
     if (!pl || slot < 0 || (size_t)slot >= pl->slots.size()) return SRTP_EINVAL;
     std::lock_guard<std::mutex> gp(pl->mu);
