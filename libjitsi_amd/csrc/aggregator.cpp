@@ -89,7 +89,8 @@
 // srtp_queue_release or the owner's next reap), so a completed packet's bytes
 // never move.  A submit that finds no free slot waits for one only until its
 // queue's oldest packet completes, then returns SRTP_EAGAIN (the owner reaps,
-// which releases slots): a thread never waits on slots that only it can free.
+// which releases slots) -- after at most kHeldWait once its oldest packet has
+// completed, so a thread never waits long on slots that only it can free.
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -116,6 +117,9 @@ using Clock = std::chrono::steady_clock;
 enum SlotState { kFree, kOpen, kSealed, kInflight, kHeld };
 constexpr uint32_t kNoLen = 0xffffffffu; // h.len[i] until packet i's copy has finished
 constexpr uint32_t kBlock = 16;          // entries per producer block (a cache line of u32s)
+// how long a queue's submit keeps waiting for a slot after its own oldest
+// packet has completed (see submit_entry)
+constexpr std::chrono::microseconds kHeldWait{500};
 
 // Reservation word of a lane direction's open slot: slot + 1 (0 = none) in
 // bits 56-63, blocks handed out in bits 32-55, segment bytes in bits 0-31.
@@ -569,7 +573,10 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
     ln.idle.store(0);
 }
 
-constexpr size_t kPipe = 2; // bundles a lane keeps in flight under load (SRTP_AGG_SEAL_IDLE)
+#ifndef SRTP_AGG_PIPE
+#define SRTP_AGG_PIPE 2
+#endif
+constexpr size_t kPipe = SRTP_AGG_PIPE; // bundles a lane keeps in flight under load (SRTP_AGG_SEAL_IDLE)
 
 void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
     (void)lane;
@@ -630,7 +637,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
         // Pipelining (file comment): one bundle in flight, room for another
         // and a free slot -- wait for it only until half a round trip after
         // its submit, then seal what has arrived and go submit that as well.
-        if ((a->opts.flags & SRTP_AGG_SEAL_IDLE) && ln->inflight.size() + ln->sealed.size() < kPipe &&
+        if (kPipe > 1 && (a->opts.flags & SRTP_AGG_SEAL_IDLE) && ln->inflight.size() + ln->sealed.size() < kPipe &&
             ln->inflight.size() < max_inflight && !a->stop) {
             const auto t_seal = t_sub[(size_t)s] + std::chrono::microseconds((long)(rt_us / 2));
             bool done = false, sealed_more = false;
@@ -858,6 +865,7 @@ int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t
     uint32_t i;
     size_t off;
     if (!try_reserve(a, ln, (uint32_t)lane, dir, need, s, i, off)) {
+        Clock::time_point held_since{};
         std::unique_lock<std::mutex> lk(a->mu);
         for (;;) {
             if (a->stop || a->closing.load()) return SRTP_EINVAL;
@@ -873,9 +881,16 @@ int submit_entry(srtp_aggregator *a, int32_t reverse, int32_t tid, const uint8_t
                 return SRTP_OK;
             }
             if (q_head) {
-                if (q_head->ready.load(std::memory_order_acquire)) return SRTP_EAGAIN; // reap first
-                // (its completion may come from another lane: poll)
-                ln.cv_space.wait_for(lk, std::chrono::microseconds(200));
+                // A queue's submit waits for a slot while its oldest packet is
+                // in flight; once that one has completed, for at most
+                // kHeldWait more (other owners' reaps free slots meanwhile),
+                // then SRTP_EAGAIN: its owner reaps, releasing what it holds.
+                if (q_head->ready.load(std::memory_order_acquire)) {
+                    if (held_since == Clock::time_point{}) held_since = Clock::now();
+                    else if (Clock::now() - held_since > kHeldWait) return SRTP_EAGAIN;
+                }
+                // (completions may come from another lane: poll)
+                ln.cv_space.wait_for(lk, std::chrono::microseconds(100));
                 continue;
             }
             ln.cv_space.wait(lk); // backpressure: every slot is sealed, in flight or held

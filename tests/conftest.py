@@ -12,6 +12,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP engine)")
 
 
+def pytest_sessionstart(session):
+    # torch caches its device count on the first ask; asked only after a test
+    # initialised HIP through the engine library (the JNI shim's tests do), it
+    # answered "no GPU" and the tests that check torch skipped themselves
+    _gpu_available()
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import oracle as O
