@@ -239,7 +239,8 @@ int copy_threads(int n_shards) {
 struct srtp_dispatch {
     std::unique_ptr<CopyPool> pool;
     std::vector<srtp_engine *> engines;
-    std::vector<srtp_pipeline *> pipes;
+    std::vector<srtp_pipeline *> pipes; // per shard, made by the first host bundle (nullptr until then)
+    std::vector<char> shared;           // the shard's device hosts other shards too
     std::vector<int32_t> kinds;  // transformer kinds (replicated ids); written under mu and kmu
     uint32_t tag_mask = 0;
     int32_t abort_on_error = 1;
@@ -526,7 +527,8 @@ void srtp_dispatch_destroy(srtp_dispatch *d) {
     for (auto &w : d->workers)
         if (w.joinable()) w.join();
     d->pool.reset();
-    for (auto *p : d->pipes) srtp_pipeline_destroy(p);
+    for (auto *p : d->pipes)
+        if (p) srtp_pipeline_destroy(p);
     for (auto *e : d->engines) srtp_engine_destroy(e);
     delete d;
 }
@@ -561,13 +563,13 @@ int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_en
         rc = srtp_engine_create(&os, &e);
         if (rc != SRTP_OK) break;
         d->engines.push_back(e);
-        srtp_pipeline *pl = nullptr;
-        // shards sharing a GPU: one stream each (SRTP_PIPE_ONE_STREAM); the
-        // other shards' chunks keep that GPU's copy engines and CUs busy
-        const bool shared = std::count(devices, devices + n_shards, devices[s]) > 1;
-        rc = srtp_pipeline_create_ex(e, kChunkPackets, kChunkBytes, kDepth, shared ? SRTP_PIPE_ONE_STREAM : 0u, &pl);
-        if (rc != SRTP_OK) break;
-        d->pipes.push_back(pl);
+        // the shard's pipeline (pinned chunk slots, copy streams) is made by
+        // the first host bundle (srtp_dispatch_transform_host): a process that
+        // only uses the aggregator over the dispatcher never holds its 192 MB
+        // of pinned memory per shard, nor its two streams (which shared the
+        // device's few hardware queues with the aggregator lanes' streams)
+        d->pipes.push_back(nullptr);
+        d->shared.push_back(std::count(devices, devices + n_shards, devices[s]) > 1);
     }
     if (rc == SRTP_OK) {
         d->jobs.resize((size_t)n_shards);
@@ -708,6 +710,14 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     d->b_tids = tids; d->b_tid = tid; d->b_seg = seg; d->b_off = off; d->b_len = len;
     d->b_cap = cap; d->b_flags = flags; d->b_status = status;
     d->b_registered = srtp_host_is_registered(seg, seg_bytes) != 0;
+    for (size_t s = 0; s < ns; s++) {
+        if (d->pipes[s]) continue;
+        // shards sharing a GPU: one stream each (SRTP_PIPE_ONE_STREAM); the
+        // other shards' chunks keep that GPU's copy engines and CUs busy
+        const int rc = srtp_pipeline_create_ex(d->engines[s], kChunkPackets, kChunkBytes, kDepth,
+                                               d->shared[s] ? SRTP_PIPE_ONE_STREAM : 0u, &d->pipes[s]);
+        if (rc != SRTP_OK) return dfail(d, rc, "shard pipeline");
+    }
     auto tid_of = [&](uint32_t i) { return tids ? tids[i] : tid; };
     std::vector<std::vector<uint32_t>> per_shard(ns);
     std::vector<uint32_t> at((size_t)parts * ns);

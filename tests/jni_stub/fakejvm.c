@@ -167,6 +167,79 @@ JNIEXPORT jint fj_packet_length(jobject p) { return p->length; }
 JNIEXPORT jsize fj_bytes_len(jbyteArray a) { return a->len; }
 JNIEXPORT void fj_bytes_read(jbyteArray a, void *out) { memcpy(out, a->data, (size_t)a->len); }
 
+/* ---- "JVM threads" driving GpuPacketQueue, in C (no interpreter lock) ---- */
+
+#define SHIM(name) Java_org_jitsi_impl_neomedia_transform_srtp_mi355x_SrtpMi355x_##name
+jlong SHIM(queueCreate)(JNIEnv *env, jclass c, jlong agg, jint maxInFlight);
+void SHIM(queueDestroy)(JNIEnv *env, jclass c, jlong q);
+jint SHIM(queueSubmit)(JNIEnv *env, jclass c, jlong q, jboolean reverse, jint tid, jobject pkt, jboolean skip,
+                       jlong cookie);
+jint SHIM(queueReap)(JNIEnv *env, jclass c, jlong q, jobjectArray ring, jintArray status, jboolean wait);
+
+/* One thread's GpuPacketQueue (GpuPacketQueue.java): its packets pkts[0..n)
+ * submitted in order (reaping whenever a submit is refused, as
+ * GpuPacketQueue.transform does), then the rest reaped (drain).  Out: each
+ * packet's status in submission order, the most packets it had in flight,
+ * and rc (0 or the first negative code). */
+struct fj_job {
+    jlong agg;
+    jboolean reverse;
+    jint depth, n;
+    const jint *tids;
+    jobject *pkts;
+    jint *status;
+    jint max_in_flight, rc;
+};
+
+static void *fj_drive(void *arg) {
+    struct fj_job *j = arg;
+    JNIEnv *env = &g_env;
+    const jlong q = SHIM(queueCreate)(env, NULL, j->agg, j->depth);
+    if (!q) {
+        j->rc = -1;
+        return NULL;
+    }
+    const jsize ns = j->depth < 1024 ? j->depth : 1024;
+    jobjectArray ring = new_array(K_OBJS, j->depth, sizeof(jobject));
+    jintArray st = new_array(K_INTS, ns, sizeof(jint));
+    long sub = 0, rep = 0;
+    for (jint i = 0; i <= j->n && !j->rc;) {
+        const int more = i < j->n;
+        if (more && sub - rep < j->depth) {
+            ((jobject *)ring->data)[sub % j->depth] = j->pkts[i];
+            const jint rc = SHIM(queueSubmit)(env, NULL, q, j->reverse, j->tids[i], j->pkts[i], 0, (jlong)sub);
+            if (rc == 0) {
+                sub++;
+                i++;
+                if (sub - rep > j->max_in_flight) j->max_in_flight = (jint)(sub - rep);
+                continue;
+            }
+            if (rc != -6) { /* SRTP_EAGAIN: reap first */
+                j->rc = rc;
+                break;
+            }
+        }
+        if (!more && rep == sub) break;
+        const jint k = SHIM(queueReap)(env, NULL, q, ring, st, 1);
+        if (k < 0) {
+            j->rc = k;
+            break;
+        }
+        for (jint m = 0; m < k; m++) j->status[rep++] = ((jint *)st->data)[m];
+    }
+    SHIM(queueDestroy)(env, NULL, q);
+    return NULL;
+}
+
+JNIEXPORT int fj_drive_queues(struct fj_job *jobs, int n_jobs) {
+    pthread_t *th = calloc((size_t)n_jobs, sizeof *th);
+    if (!th) return -1;
+    for (int k = 0; k < n_jobs; k++) pthread_create(&th[k], NULL, fj_drive, &jobs[k]);
+    for (int k = 0; k < n_jobs; k++) pthread_join(th[k], NULL);
+    free(th);
+    return 0;
+}
+
 /* pending "exceptions" (out-of-range array regions) and unbalanced local frames */
 JNIEXPORT int fj_exceptions(void) { return g_exceptions; }
 JNIEXPORT int fj_frames(void) { return g_frames; }

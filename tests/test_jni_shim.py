@@ -321,20 +321,29 @@ def rtp_of(k, s, q, n, rng, bad_ext=False):
     return rtp(0x50000000 + 8 * k + s, 1000 + 97 * k + q, n, rng, bad_ext)
 
 
+class FjJob(C.Structure):
+    """struct fj_job (tests/jni_stub/fakejvm.c): one "JVM thread" driving GpuPacketQueue."""
+    _fields_ = [("agg", C.c_int64), ("reverse", C.c_uint8), ("depth", C.c_int32), ("n", C.c_int32),
+                ("tids", C.c_void_p), ("pkts", C.c_void_p), ("status", C.c_void_p),
+                ("max_in_flight", C.c_int32), ("rc", C.c_int32)]
+
+
 @pytest.mark.gpu
 def test_jni_queue_64_threads_in_flight_vs_oracle():
-    """GpuPacketQueue: 64 "JVM threads" (a connector send thread each), 50
-    sender and 50 receiver transformers, each thread keeping >= 32 packets in
-    flight through queueSubmit / queueReap.  Protect with a throw (an
-    extension header past the packet) in mid-stream, then unprotect of the
-    results with replays and forgeries; every RawPacket -- status, bytes,
-    length, and the new buffer where RawPacket.append reallocates -- against
-    the oracle replaying each thread's packets as 1-element arrays in its
-    submission order (each thread owns its SSRCs, so that is each context's
-    order)."""
-    T, NT, PER = 64, 50, 48
+    """GpuPacketQueue: 64 "JVM threads" (a connector send thread each; native
+    threads of the stand-in JVM running GpuPacketQueue's loop over the shim's
+    queueSubmit / queueReap, fakejvm.c fj_drive), 50 sender and 50 receiver
+    transformers, each thread with a 64-packet queue and >= 32 packets in
+    flight.  Protect with throws (an extension header past the packet) in
+    mid-stream, then unprotect of the results with replays and forgeries;
+    every RawPacket -- status, bytes, length, and the new buffer where
+    RawPacket.append reallocates -- against the oracle replaying each thread's
+    packets as 1-element arrays in its submission order (each thread owns its
+    SSRCs, so that is each context's order)."""
+    T, NT, PER, DEPTH = 64, 50, 96, 64
     jvm = Jvm(n_shards=2)
     try:
+        jvm.L.fj_drive_queues.argtypes = [C.POINTER(FjJob), C.c_int]
         keys = synth.keys(77, NT)
         ts, tr, ots, otr = [], [], [], []
         for k, s in keys:
@@ -352,58 +361,38 @@ def test_jni_queue_64_threads_in_flight_vs_oracle():
             sc = []
             for q in range(PER):
                 s = q % 3
-                bad = q == 20 and k % 4 == 0
+                bad = q == 40 and k % 4 == 0
                 data = rtp_of(k, s, q // 3, int(rng.integers(60, 1300)), rng, bad_ext=bad)
                 extra, off = [(0, 0), (16, 5), (3, 0)][q % 3]
                 sc.append(((3 * k + s) % NT, data, extra, off))
             scripts.append(sc)
-        depth = 64
-        results = [None] * T
-        in_flight = [0] * T
-        errs = []
-
-        def run(k, reverse, items):
-            qu = PacketQueue(jvm, depth)
-            out = []
-            # the RawPackets first (a send thread drains its queue of packets
-            # it already holds), then submit them back to back, reaping only
-            # when a submit is refused (GpuPacketQueue.transform)
-            pk = []
-            for ti, data, extra, off in items:
-                p = jvm.packet(data, off, extra)
-                pk.append((p, jvm.L.fj_packet_buffer(p)))
-            try:
-                for (ti, _, _, _), (p, _) in zip(items, pk):
-                    while not qu.submit(reverse, (tr if reverse else ts)[ti], p):
-                        out += qu.reap(True)
-                    in_flight[k] = max(in_flight[k], qu.submitted - qu.reaped)
-                while qu.submitted != qu.reaped:
-                    out += qu.reap(True)
-            finally:
-                qu.close()
-            assert [p for p, _ in out] == [p for p, _ in pk]  # submission order
-            return [(st, jvm.packet_bytes(p)[0], jvm.L.fj_packet_buffer(p) == b0)
-                    for (p, st), (_, b0) in zip(out, pk)]
-
-        def work(k, reverse, items):
-            try:
-                results[k] = run(k, reverse, items)
-            except Exception as ex:  # noqa: BLE001
-                errs.append(ex)
 
         def run_all(reverse, all_items):
-            th = [threading.Thread(target=work, args=(k, reverse, all_items[k])) for k in range(T)]
-            for x in th:
-                x.start()
-            for x in th:
-                x.join()
-            assert not errs, errs[:3]
+            """fj_drive on T native threads; per thread [(status, bytes, same buffer)]."""
+            keep = []
+            jobs = (FjJob * T)()
+            for k in range(T):
+                items = all_items[k]
+                pk = [jvm.packet(d, off, extra) for _, d, extra, off in items]
+                b0 = [jvm.L.fj_packet_buffer(p) for p in pk]
+                tids = np.array([(tr if reverse else ts)[ti] for ti, _, _, _ in items], np.int32)
+                parr = (C.c_void_p * len(pk))(*pk)
+                st = np.full(len(pk), -100, np.int32)
+                keep.append((pk, b0, tids, parr, st))
+                jobs[k] = FjJob(jvm.agg, int(reverse), DEPTH, len(pk), tids.ctypes.data, C.cast(parr, C.c_void_p),
+                                st.ctypes.data, 0, 0)
+            assert jvm.L.fj_drive_queues(jobs, T) == 0
+            out = []
+            for k in range(T):
+                assert jobs[k].rc == 0, (k, jobs[k].rc)
+                pk, b0, _, _, st = keep[k]
+                out.append([(int(x), jvm.packet_bytes(p)[0], jvm.L.fj_packet_buffer(p) == b)
+                            for x, p, b in zip(st, pk, b0)])
+            return out, sorted(jobs[k].max_in_flight for k in range(T))
 
-        run_all(False, scripts)
-        print("max packets in flight per thread:", sorted(in_flight))
-        # (Python threads share one interpreter lock, so a thread's submits can
-        # lag the GPU; most still get 32+ of their 48 packets in flight)
-        assert sorted(in_flight)[T // 2] >= 32
+        results, in_flight = run_all(False, scripts)
+        print("max packets in flight per thread (protect):", in_flight)
+        assert in_flight[0] >= 32
         seen = set()
         protected = []
         for k in range(T):
@@ -426,7 +415,9 @@ def test_jni_queue_64_threads_in_flight_vs_oracle():
             items.insert(9, (items[7][0], bytes(bad), 0, 0))   # forged copy of an earlier packet
             items.insert(15, items[4])                           # exact replay
             un.append(items)
-        run_all(True, un)
+        results, in_flight = run_all(True, un)
+        print("max packets in flight per thread (unprotect):", in_flight)
+        assert in_flight[0] >= 32
         seen = set()
         for k in range(T):
             for (ti, data, extra, off), (st, got, _) in zip(un[k], results[k]):
