@@ -410,9 +410,9 @@ def test_jni_queue_64_threads_in_flight_vs_oracle():
         un = []
         for k in range(T):
             items = [(ti, d, 0, 0) for ti, d in protected[k]]
-            bad = bytearray(items[7][1])
+            bad = bytearray(items[12][1])
             bad[-3] ^= 0x40
-            items.insert(9, (items[7][0], bytes(bad), 0, 0))   # forged copy of an earlier packet
+            items.insert(9, (items[12][0], bytes(bad), 0, 0))  # forgery of a packet yet to come
             items.insert(15, items[4])                           # exact replay
             un.append(items)
         results, in_flight = run_all(True, un)
