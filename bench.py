@@ -656,6 +656,11 @@ def main():
                 pmc = {}
         except Exception:
             pmc = {}
+    # the counters are of the build whose kernel sources hash to this; another
+    # build's counters are reported as stale (traffic_stale), not as this one's
+    from libjitsi_amd._native import kernel_source_sha16
+    ksha = kernel_source_sha16()
+    pmc_stale = bool(pmc) and pmc.get("kernel_source_sha16") != ksha
 
     def roofline(stage, kernel, traffic_key, util_key=None):
         if stage not in stages or stages[stage] <= 0:
@@ -687,6 +692,13 @@ def main():
                                           "calibration (tools/pmc_calib.hip) is quoted, not trusted"}
         if util_key and pmc.get(util_key):
             r["utilisation"] = pmc.get(util_key)
+        if pmc:
+            r["counters_kernel_sha16"] = pmc.get("kernel_source_sha16")
+            r["kernel_sha16"] = ksha
+            r["traffic_stale"] = pmc_stale
+            if pmc_stale:  # counters of another build: quoted, not this build's traffic
+                r["traffic_of_other_build"] = r.pop("traffic")
+                r["traffic"] = None
         return r
 
     r_prot = roofline("protect", "k_protect", "k_protect_bytes_per_launch", "k_protect_utilisation")

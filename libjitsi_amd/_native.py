@@ -70,6 +70,20 @@ EXPORTED = [
 STAGES = ["parse", "sort", "verify", "walk", "protect", "decrypt"]
 
 
+# Sources that decide what the crypto kernels execute: the key that ties
+# committed PMC counters (profiles/pmc_traffic.json) to the build they measured.
+KERNEL_SOURCES = ["srtp_kernels.hip", "aes_rounds_asm.inc", "srtp_kernels.h", "srtp_types.h", "engine.cpp"]
+
+
+def kernel_source_sha16() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(_HERE, "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 class SrtpError(RuntimeError):
     pass
 

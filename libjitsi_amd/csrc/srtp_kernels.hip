@@ -84,10 +84,17 @@ constexpr int kTeWords = 32768;  // 128 KB
 constexpr int kTeCounters = 16;  // per-workgroup status counts, after the image (which stays at LDS 0)
 constexpr int kAesBlock = 1024;  // threads per workgroup of the AES kernels (1 WG per CU)
 constexpr int kMacBlock = 256;   // at most, the MacOnly instances' (small bundles)
+// (tools/build_variant.sh builds the occupancy variants of
+// profiles/r05/kernel_experiments.md with smaller workgroups: more VGPRs per
+// lane, fewer waves per SIMD)
 #ifndef SRTP_UNPROTECT_BLOCK
 #define SRTP_UNPROTECT_BLOCK 1024
 #endif
+#ifndef SRTP_PROTECT_BLOCK
+#define SRTP_PROTECT_BLOCK 1024
+#endif
 constexpr int kUnprotectBlock = SRTP_UNPROTECT_BLOCK; // k_unprotect's workgroup size
+constexpr int kProtectBlock = SRTP_PROTECT_BLOCK;     // k_protect's
 
 __device__ __forceinline__ void fill_te4(uint32_t *s_te) {
     // Entry e of te0 fills words (h << 14) | (e << 6) | l (h = 0, 1; l =
@@ -3392,7 +3399,7 @@ __device__ __forceinline__ void flush_status_counts(const BundleArgs &a, const u
 // (MacOnly instances run small bundles in workgroups of at most kMacBlock
 // threads: registers for the MAC's look-ahead)
 template <bool MacOnly>
-__global__ __launch_bounds__(MacOnly ? kMacBlock : kAesBlock) void k_protect(BundleArgs a) {
+__global__ __launch_bounds__(MacOnly ? kMacBlock : kProtectBlock) void k_protect(BundleArgs a) {
     // the status counts sit behind the T-table image
     __shared__ uint32_t s_te[kTeWords + kTeCounters];
     uint32_t *s_cnt = s_te + kTeWords;
@@ -3469,6 +3476,9 @@ __device__ __forceinline__ uint32_t chain_head(const uint32_t *__restrict__ sk, 
 // ROC-carrying block and that block's ciphertext, so the walk can re-check a
 // tag under another ROC cheaply; k_unprotect_fix repairs the rare packets the
 // walk rejects or guesses differently.
+#ifndef SRTP_EXP_NOTAIL // diagnostic A/B only: 1 drops the fused path's re-check state (wrong on re-checks)
+#define SRTP_EXP_NOTAIL 0
+#endif
 template <bool LK>
 __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                               const char *__restrict__ lds, const TeBase &tb,
@@ -3592,7 +3602,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-            if (rtp) { // midstate + ciphertext of the ROC-carrying block
+            if (rtp && !SRTP_EXP_NOTAIL) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
@@ -4743,7 +4753,7 @@ hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
-    const uint32_t b = aes_block(a.n, (uint32_t)kAesBlock);
+    const uint32_t b = aes_block(a.n, (uint32_t)kProtectBlock);
     if (a.small_ctr) {
         const uint32_t bm = std::min<uint32_t>(b, (uint32_t)kMacBlock);
         hipLaunchKernelGGL(k_protect<true>, dim3((a.n + bm - 1) / bm), dim3(bm), 0, s, a);
