@@ -3476,9 +3476,6 @@ __device__ __forceinline__ uint32_t chain_head(const uint32_t *__restrict__ sk, 
 // ROC-carrying block and that block's ciphertext, so the walk can re-check a
 // tag under another ROC cheaply; k_unprotect_fix repairs the rare packets the
 // walk rejects or guesses differently.
-#ifndef SRTP_EXP_NOTAIL // diagnostic A/B only: 1 drops the fused path's re-check state (wrong on re-checks)
-#define SRTP_EXP_NOTAIL 0
-#endif
 template <bool LK>
 __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                               const char *__restrict__ lds, const TeBase &tb,
@@ -3602,7 +3599,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-            if (rtp && !SRTP_EXP_NOTAIL) { // midstate + ciphertext of the ROC-carrying block
+            if (rtp) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
