@@ -84,6 +84,10 @@ def parse_args():
                     help="one engine and stream: step i = protect(i) then unprotect(i)")
     ap.add_argument("--pipe", default="free", choices=["free", "join", "lag1", "lag2"],
                     help="coupling of the sender and receiver streams (see Side.step)")
+    ap.add_argument("--events", default="device", choices=["device", "torch"],
+                    help="events ordering the two streams: 'device' = device-scope release (no "
+                         "system-scope fence: no L2 write-back between the directions), "
+                         "'torch' = torch.cuda.Event (system scope)")
     ap.add_argument("--policy", default="AES_CM_128_HMAC_SHA1_80",
                     help="protection profile; 'AES_CM_128_NULL_AUTH' (cipher only) is a "
                          "diagnostic split of the fused kernel, not the headline metric")
@@ -238,7 +242,7 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
     from libjitsi_amd import (HostBuffer, SRTPContextFactory, SRTPDispatcher, SRTPTransformer,
                               host_register, host_unregister)
     out = {}
-    modes = [(G, m) for G in shard_counts for m in ("pinned", "copy")] + [(1, "registered")]
+    modes = [(G, m) for G in shard_counts for m in ("pinned", "async", "copy")] + [(1, "registered")]
     for G, mode in modes:
         d = SRTPDispatcher(devices_for(G), check_replay=False, max_contexts=1 << 15,
                            max_factories=8, max_transformers=8)
@@ -248,7 +252,7 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
             snd = SRTPTransformer(SRTPContextFactory(True, k, s, *pols, engine=d))
             rcv = SRTPTransformer(SRTPContextFactory(False, k, s, *pols, engine=d))
             ln = b.length.copy()
-            if mode == "pinned":  # the engine's pinned buffer pool: chunks DMA in place
+            if mode in ("pinned", "async"):  # the engine's pinned buffer pool: chunks DMA in place
                 hb = HostBuffer(b.seg.nbytes)
                 seg = hb.array
                 seg[:] = b.seg
@@ -259,17 +263,40 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
             for _ in range(2):  # warm: both directions once
                 d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
                 d.transform_host(True, rcv.tid, seg, b.off, ln, b.cap)
+            if mode == "async":  # a second pinned bundle: one in flight while the other is packed
+                hb2 = HostBuffer(b.seg.nbytes)
+                hb2.array[:] = b.seg
+                bufs = [(seg, ln), (hb2.array, b.length.copy())]
             h0 = d.host_times()
             ok = True
             t0 = time.perf_counter()
-            for _ in range(bundles):
-                st = d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
-                st2 = d.transform_host(True, rcv.tid, seg, b.off, ln, b.cap)
-                ok = ok and not st.any() and not st2.any()
-            dt = time.perf_counter() - t0
+            if mode == "async":
+                # srtp_dispatch_submit_host / wait_host, two bundles in flight:
+                # P(A) P(B) U(A) U(B) ..., each submit after the wait of the
+                # previous operation on its buffer (the oldest in flight)
+                pending = []
+                for _ in range(bundles):
+                    for rev, t in ((False, snd), (True, rcv)):
+                        for sg, l in bufs:
+                            if len(pending) == 2:
+                                ok = ok and not pending.pop(0).wait().any()
+                            pending.append(d.submit_host(rev, t.tid, sg, b.off, l, b.cap))
+                for tk in pending:
+                    ok = ok and not tk.wait().any()
+                pending = None
+                dt = (time.perf_counter() - t0) / 2  # twice the bundles of the other modes
+            else:
+                for _ in range(bundles):
+                    st = d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
+                    st2 = d.transform_host(True, rcv.tid, seg, b.off, ln, b.cap)
+                    ok = ok and not st.any() and not st2.any()
+                dt = time.perf_counter() - t0
             h1 = d.host_times()
             calls = max(h1["calls"] - h0["calls"], 1)
             per = {k2: round((h1[k2] - h0[k2]) / calls, 3) for k2 in h1 if k2 != "calls"}
+            if mode == "async":
+                bufs = None
+                hb2.close()
             out[str(G) if mode == "pinned" else f"{G}_{mode}"] = {
                 "directional_pps": round(2 * bundles * n / dt, 1),
                 "ms_per_bundle": round(dt / (2 * bundles) * 1e3, 3),
@@ -283,6 +310,52 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
                 seg = None
                 hb.close()
     return out
+
+
+class DeviceEvent:
+    """A stream-ordering event with a device-scope release
+    (hipEventDisableSystemFence): the two directions' streams are on one GPU
+    and only its kernels read what the other stream wrote, so the system-scope
+    fence a torch.cuda.Event record carries (an L2 write-back and invalidate,
+    ~13 us of idle queue per record, profiles/r05/events/) is not needed."""
+    _hip = None
+
+    def __init__(self):
+        import ctypes
+        if DeviceEvent._hip is None:
+            h = ctypes.CDLL("libamdhip64.so")
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            h.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+            h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            DeviceEvent._hip = h
+        self.h = ctypes.c_void_p()
+        rc = DeviceEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.h), 0x2 | 0x20000000)
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags: {rc}")
+
+    def record(self, stream):
+        rc = DeviceEvent._hip.hipEventRecord(self.h, stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord: {rc}")
+
+    def wait(self, stream):
+        rc = DeviceEvent._hip.hipStreamWaitEvent(stream.cuda_stream, self.h, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitEvent: {rc}")
+
+
+class TorchEvent:
+    """torch.cuda.Event behind DeviceEvent's record / wait."""
+
+    def __init__(self, torch):
+        self.ev = torch.cuda.Event()
+
+    def record(self, stream):
+        self.ev.record(stream)
+
+    def wait(self, stream):
+        stream.wait_event(self.ev)
 
 
 class Side:
@@ -344,11 +417,14 @@ class Side:
             self.s_a = torch.cuda.ExternalStream(self.eng.stream_ptr, device=dev)
             self.s_b = (self.s_a if args.serial else
                         torch.cuda.ExternalStream(self.eng_r.stream_ptr, device=dev))
-            self.end_a, self.end_b = torch.cuda.Event(), torch.cuda.Event()
-            self.ev_b = [torch.cuda.Event() for _ in range(3)]  # receiver step ends (lag modes)
+            mkev = DeviceEvent if args.events == "device" else (lambda: TorchEvent(torch))
+            self.end_a, self.end_b = mkev(), mkev()
+            self.ev_b = [mkev() for _ in range(3)]  # receiver step ends (lag modes)
             self.ring = min(total + 1, RING)
             # ring slot j is free again once the unprotect of its last bundle ran
-            self.ev_free = [torch.cuda.Event() for _ in range(self.ring)]
+            # (recorded only when the run reuses slots)
+            self.reuse = total + 1 > self.ring
+            self.ev_free = [mkev() for _ in range(self.ring)] if self.reuse else []
             self.pending = None  # join mode: protected bundle whose unprotect is due
             base = torch.from_numpy(b.seg).to(dev)
             len0 = torch.from_numpy(b.length.view(np.int32)).to(dev)
@@ -376,7 +452,7 @@ class Side:
     def protect(self, i, stream):
         j = i % self.ring
         if i >= self.ring:  # reuse a staged bundle once its unprotect has run
-            stream.wait_event(self.ev_free[j])
+            self.ev_free[j].wait(stream)
             with self.torch.cuda.stream(stream):
                 self.advance_seq(self.segs[j], self.ring)
         self.eng.transform_device(False, self.tid_s, self.segs[j], self.off, self.lens[j],
@@ -386,7 +462,8 @@ class Side:
         j = i % self.ring
         self.eng_r.transform_device(True, self.tid_r, self.segs[j], self.off, self.lens[j],
                                     self.cap, self.st_r, stream=stream)
-        self.ev_free[j].record(stream)
+        if self.reuse:
+            self.ev_free[j].record(stream)
 
     def step(self, i):
         """free: protect(i) on stream A, unprotect(i) on stream B after it; the
@@ -402,15 +479,16 @@ class Side:
         if self.pipe != "join":
             lag = {"free": 0, "lag1": 1, "lag2": 2}[self.pipe]
             if lag and i >= lag:
-                self.s_a.wait_event(self.ev_b[(i - lag) % 3])
+                self.ev_b[(i - lag) % 3].wait(self.s_a)
             self.protect(i, self.s_a)
             self.end_a.record(self.s_a)
-            self.s_b.wait_event(self.end_a)
+            self.end_a.wait(self.s_b)
             self.unprotect(i, self.s_b)
-            self.ev_b[i % 3].record(self.s_b)
+            if lag:
+                self.ev_b[i % 3].record(self.s_b)
             return
-        self.s_a.wait_event(self.end_b)
-        self.s_b.wait_event(self.end_a)
+        self.end_b.wait(self.s_a)
+        self.end_a.wait(self.s_b)
         self.protect(i, self.s_a)
         if self.pending is not None:
             self.unprotect(self.pending, self.s_b)
@@ -420,7 +498,7 @@ class Side:
 
     def serial_step(self, i):
         """protect(i) then unprotect(i) on stream A (the stage-timing pass)."""
-        self.s_a.wait_event(self.end_b)
+        self.end_b.wait(self.s_a)
         if self.pending is not None:
             self.unprotect(self.pending, self.s_a)
             self.pending = None
@@ -431,7 +509,7 @@ class Side:
     def finish(self):
         """Unprotect the last protected bundle (join mode), untimed."""
         if self.pending is not None:
-            self.s_b.wait_event(self.end_a)
+            self.end_a.wait(self.s_b)
             self.unprotect(self.pending, self.s_b)
             self.pending = None
         self.torch.cuda.synchronize(self.dev)
@@ -796,7 +874,8 @@ def main():
                                            "after protect(i), the sender runs ahead",
                                    "join": "sender + receiver engine, one stream each: protect(i) "
                                            "beside unprotect(i-1), joined every step"}.get(
-                                      args.pipe, f"sender + receiver engine, {args.pipe}")},
+                                      args.pipe, f"sender + receiver engine, {args.pipe}"),
+                       "stream_events": args.events},
             "gbps": round(gbs, 2),
             "goodput_gbps": round(pps * L * 2 / 1e9, 2),
             "all_accepted": ok,

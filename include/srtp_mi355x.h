@@ -557,6 +557,27 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
                                  uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
                                  const uint32_t *cap, const uint32_t *flags, int32_t *status,
                                  uint32_t n);
+/* Asynchronous host bundles (no reference API: RTPConnectorOutputStream's
+ * send thread, RTPConnectorOutputStream.java:268-300, hands each packet on
+ * and goes back to its queue).  srtp_dispatch_submit_host does the work of
+ * srtp_dispatch_transform_host but returns once the bundle's last chunks are
+ * on their way to the GPUs, with a ticket; srtp_dispatch_wait_host(ticket)
+ * returns when its statuses, lengths and bytes are in the caller's arrays,
+ * with the bundle's result.  The arrays must stay valid, and untouched by the
+ * caller, until that wait returns.  The next submit overlaps its packing and
+ * H2D with the previous bundle's last D2H.  Bundles run in submission order
+ * on every shard (each context sees its packets in that order, as from
+ * synchronous calls), and a synchronous call is ordered with them too.  Every
+ * ticket must be waited for (at most 64 may be outstanding: SRTP_EAGAIN
+ * beyond); waiting for one also completes -- but does not consume -- the
+ * bundles submitted before it.  A bundle with a packet that could throw under
+ * abort-on-throw (the rollback above) runs to completion inside its submit.
+ * srtp_dispatch_destroy completes bundles never waited for. */
+int srtp_dispatch_submit_host(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid,
+                              uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                              const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n,
+                              uint64_t *ticket);
+int srtp_dispatch_wait_host(srtp_dispatch *d, uint64_t ticket);
 int srtp_dispatch_get_context_state(srtp_dispatch *d, int32_t transformer, uint32_t ssrc,
                                     srtp_ctx_state *out);
 int srtp_dispatch_set_context_state(srtp_dispatch *d, int32_t transformer, uint32_t ssrc,

@@ -47,7 +47,8 @@ EXPORTED = [
     "srtp_dispatch_destroy", "srtp_dispatch_last_error", "srtp_dispatch_num_shards",
     "srtp_dispatch_engine", "srtp_dispatch_factory_create", "srtp_dispatch_factory_close",
     "srtp_dispatch_transformer_create", "srtp_dispatch_transformer_set_factory",
-    "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host",
+    "srtp_dispatch_transformer_close", "srtp_dispatch_transform_host", "srtp_dispatch_submit_host",
+    "srtp_dispatch_wait_host",
     "srtp_dispatch_get_context_state", "srtp_dispatch_set_context_state", "srtp_dispatch_stats",
     "srtp_tls_export_keying_material", "srtp_dtls_profile_keys", "srtp_dtls_transformer_create",
     "srtp_engine_get_opts", "srtp_derive_session_keys_n", "srtp_derive_session_keys_for",
@@ -265,6 +266,9 @@ def lib() -> C.CDLL:
     L.srtp_dispatch_transformer_close.argtypes = [vp, i32]
     L.srtp_dispatch_transform_host.argtypes = [vp, i32, vp, i32, vp, C.c_size_t, vp, vp, vp, vp, vp,
                                                u32]
+    L.srtp_dispatch_submit_host.argtypes = [vp, i32, vp, i32, vp, C.c_size_t, vp, vp, vp, vp, vp, u32,
+                                            C.POINTER(C.c_uint64)]
+    L.srtp_dispatch_wait_host.argtypes = [vp, C.c_uint64]
     L.srtp_dispatch_get_context_state.argtypes = [vp, i32, u32, C.POINTER(CtxState)]
     L.srtp_dispatch_set_context_state.argtypes = [vp, i32, u32, i32, C.POINTER(CtxState)]
     L.srtp_dispatch_stats.argtypes = [vp, C.POINTER(Stats)]

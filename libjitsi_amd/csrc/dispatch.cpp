@@ -63,6 +63,7 @@ constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would thro
 constexpr uint32_t kChunkPackets = 1u << 15;       // packets per pipeline slot
 constexpr size_t kChunkBytes = (size_t)48 << 20;   // segment bytes per pipeline slot
 constexpr int kDepth = 4;                          // pipeline slots per shard
+constexpr size_t kMaxInflight = 64;                // host bundles submitted and not yet waited for
 
 uint32_t mix32(uint32_t x) { // murmur3 fmix32 (libjitsi_amd/dispatch.py mix32)
     x ^= x >> 16;
@@ -261,6 +262,38 @@ int copy_threads(int n_shards) {
 }
 } // namespace
 
+// A host bundle (srtp_dispatch_submit_host): the caller's arrays, valid
+// until its wait returns, and the shards' share of it.  Its chunks pass
+// through the shards' pipeline slots; a chunk is drained (results back into
+// the caller's arrays) when its slot is needed again -- by this bundle or
+// the next one -- or by a wait.
+struct HostBundle {
+    uint64_t ticket = 0;
+    int32_t reverse = 0;
+    const int32_t *tids = nullptr;
+    int32_t tid = -1;
+    uint8_t *seg = nullptr;
+    const uint32_t *off = nullptr, *cap = nullptr, *flags = nullptr;
+    uint32_t *len = nullptr;
+    int32_t *status = nullptr;
+    bool registered = false; // the segment lies in registered memory (srtp_host_register)
+    std::vector<std::vector<uint32_t>> per_shard;
+    std::atomic<int> chunks_out{0}; // chunks in slots, not yet drained
+    std::atomic<int> rc{SRTP_OK};
+};
+
+// A shard's pipeline slots, in use across bundles: slot k holds the packets
+// ch[0, n) of owner (null: free) -- a stretch of the index list the chunk was
+// cut from, which lives as long as the chunk is in flight; k is the next slot
+// to fill.
+struct ShardRing {
+    int k = 0;
+    std::shared_ptr<HostBundle> owner[kDepth];
+    const uint32_t *ch[kDepth] = {};
+    size_t n[kDepth] = {};
+    bool direct[kDepth] = {}; // the chunk runs in place in the caller's registered segment
+};
+
 struct srtp_dispatch {
     std::unique_ptr<CopyPool> pool;
     std::vector<srtp_engine *> engines;
@@ -279,27 +312,28 @@ struct srtp_dispatch {
     std::atomic<uint64_t> t_plan{0}, t_pack{0}, t_wait{0}, t_scatter{0}, t_total{0}, n_calls{0};
     std::string last_error;
 
-    // worker threads, one per shard
+    // worker threads, one per shard.  A job is a bundle's chunks on that shard
+    // (idx: its packets; drain_all: then drain every slot, the synchronous
+    // call and the rollback's runs), or -- b null -- a drain of the slots whose
+    // bundles have tickets up to `upto` (a wait).
     struct Job {
+        std::shared_ptr<HostBundle> b;
         const std::vector<uint32_t> *idx = nullptr;
-        int32_t reverse = 0;
+        bool drain_all = false;
+        uint64_t upto = 0;
         int32_t rc = SRTP_OK;
     };
     std::vector<std::thread> workers;
     std::vector<Job> jobs;
+    std::vector<ShardRing> rings;
     std::mutex wmu;
     std::condition_variable cv_go, cv_done;
     uint64_t generation = 0;
     int pending = 0;
     bool stop = false;
-    // the bundle being processed (valid while a generation runs)
-    const int32_t *b_tids = nullptr;
-    int32_t b_tid = -1;
-    uint8_t *b_seg = nullptr;
-    const uint32_t *b_off = nullptr, *b_cap = nullptr, *b_flags = nullptr;
-    uint32_t *b_len = nullptr;
-    int32_t *b_status = nullptr;
-    bool b_registered = false; // the segment lies in registered memory (srtp_host_register)
+    // bundles submitted and not yet waited for, in ticket order (under mu)
+    std::deque<std::shared_ptr<HostBundle>> inflight;
+    uint64_t next_ticket = 1;
 };
 
 namespace {
@@ -322,66 +356,74 @@ size_t region(uint32_t cap) { return ((size_t)cap + 15) & ~(size_t)15; }
 // bundle is then a single run): a call per 1.2-KB packet costs as much as its
 // bytes.
 template <bool ToSlot>
-void copy_runs(const srtp_dispatch *d, const srtp_pipeline_slot &sl, const uint32_t *ch, size_t j0, size_t j1) {
+void copy_runs(const HostBundle &b, const srtp_pipeline_slot &sl, const uint32_t *ch, size_t j0, size_t j1) {
     for (size_t j = j0; j < j1;) {
         const uint32_t i = ch[j];
-        size_t bytes = region(d->b_cap[i]);
+        size_t bytes = region(b.cap[i]);
         size_t e = j + 1;
-        while (e < j1 && d->b_off[ch[e]] == d->b_off[ch[e - 1]] + region(d->b_cap[ch[e - 1]])) {
-            bytes += region(d->b_cap[ch[e]]);
+        while (e < j1 && b.off[ch[e]] == b.off[ch[e - 1]] + region(b.cap[ch[e - 1]])) {
+            bytes += region(b.cap[ch[e]]);
             e++;
         }
-        uint8_t *slot = sl.seg + sl.off[j], *user = d->b_seg + d->b_off[i];
+        uint8_t *slot = sl.seg + sl.off[j], *user = b.seg + b.off[i];
         if (ToSlot) memcpy(slot, user, bytes);
         else memcpy(user, slot, bytes);
         j = e;
     }
 }
 
-// Shard s's share of one phase: chunks through the shard's pipeline slots.
-int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t reverse) {
+// Drains slot k of shard s: waits for its chunk and scatters statuses,
+// lengths and (unless it ran in place) packet bytes back into its bundle.
+void drain_slot(srtp_dispatch *d, int s, int k, const srtp_pipeline_slot &sl) {
+    ShardRing &rg = d->rings[(size_t)s];
+    std::shared_ptr<HostBundle> ob = std::move(rg.owner[k]);
+    if (!ob) return;
+    HostBundle &b = *ob;
+    const uint64_t tw = now_ns();
+    const int rc = srtp_pipeline_wait(d->pipes[(size_t)s], k);
+    const uint64_t ts = now_ns();
+    d->t_wait += ts - tw;
+    const uint32_t *ch = rg.ch[k];
+    const size_t nch = rg.n[k];
+    if (rc != SRTP_OK) {
+        int ok = SRTP_OK;
+        b.rc.compare_exchange_strong(ok, rc);
+        for (size_t j = 0; j < nch; j++) b.status[ch[j]] = SRTP_STATUS_ERR_INTERNAL;
+    } else {
+        const bool direct = rg.direct[k];
+        const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
+        d->pool->run(parts, [&](int q) {
+            const size_t j0 = nch * q / parts, j1 = nch * (q + 1) / parts;
+            for (size_t j = j0; j < j1; j++) {
+                const uint32_t i = ch[j];
+                b.status[i] = sl.status[j];
+                b.len[i] = sl.len[j];
+            }
+            if (!direct) copy_runs<false>(b, sl, ch, j0, j1);
+        });
+        d->t_scatter += now_ns() - ts;
+    }
+    b.chunks_out.fetch_sub(1, std::memory_order_acq_rel);
+}
+
+// Shard s's share of bundle b (its packets idx) through the shard's pipeline
+// slots, after the chunks of earlier bundles still in them: each slot is
+// drained when it is needed again.  The last chunks stay in flight unless
+// drain_all, so that the caller's next bundle overlaps them.
+int run_shard(srtp_dispatch *d, int s, HostBundle &b, const std::shared_ptr<HostBundle> &bp,
+              const std::vector<uint32_t> &idx, bool drain_all) {
     srtp_pipeline *pl = d->pipes[(size_t)s];
+    ShardRing &rg = d->rings[(size_t)s];
     srtp_pipeline_slot sl[kDepth];
     for (int k = 0; k < kDepth; k++) {
         int rc = srtp_pipeline_slot_get(pl, k, &sl[k]);
         if (rc != SRTP_OK) return rc;
     }
-    size_t chunk_at[kDepth] = {0}, chunk_n[kDepth] = {0}; // each slot's packets: idx[at, at + n)
-    int busy[kDepth] = {0};
-    bool direct[kDepth] = {false}; // the chunk ran in place in the caller's registered segment
     int rc_all = SRTP_OK;
-    auto parts_for = [&](size_t nch) { return (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024); };
-    auto drain = [&](int k) {
-        if (!busy[k]) return;
-        busy[k] = 0;
-        const uint64_t tw = now_ns();
-        const int rc = srtp_pipeline_wait(pl, k);
-        const uint64_t ts = now_ns();
-        d->t_wait += ts - tw;
-        const uint32_t *ch = idx.data() + chunk_at[k];
-        const size_t nch = chunk_n[k];
-        if (rc != SRTP_OK) {
-            rc_all = rc;
-            for (size_t j = 0; j < nch; j++) d->b_status[ch[j]] = SRTP_STATUS_ERR_INTERNAL;
-            return;
-        }
-        const int parts = parts_for(nch);
-        d->pool->run(parts, [&](int q) {
-            const size_t j0 = nch * q / parts, j1 = nch * (q + 1) / parts;
-            for (size_t j = j0; j < j1; j++) {
-                const uint32_t i = ch[j];
-                d->b_status[i] = sl[k].status[j];
-                d->b_len[i] = sl[k].len[j];
-            }
-            if (!direct[k]) copy_runs<false>(d, sl[k], ch, j0, j1);
-        });
-        d->t_scatter += now_ns() - ts;
-    };
     size_t pos = 0;
-    int k = 0;
-    while (pos < idx.size() && rc_all == SRTP_OK) {
-        drain(k);
-        if (rc_all != SRTP_OK) break;
+    while (pos < idx.size()) {
+        const int k = rg.k;
+        drain_slot(d, s, k, sl[k]);
         const uint64_t tp = now_ns();
         // the chunk's extent and layout (offsets only: one pass over the caps)
         const uint32_t *ch = idx.data() + pos;
@@ -390,9 +432,9 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
         bool contig = true; // the chunk's packets lie back to back in the caller's segment
         for (; nch < room; nch++) {
             const uint32_t i = ch[nch];
-            const size_t r = region(d->b_cap[i]);
+            const size_t r = region(b.cap[i]);
             if (bytes + r > sl[k].seg_cap) break;
-            if (nch && d->b_off[i] != d->b_off[ch[nch - 1]] + region(d->b_cap[ch[nch - 1]])) contig = false;
+            if (nch && b.off[i] != b.off[ch[nch - 1]] + region(b.cap[ch[nch - 1]])) contig = false;
             sl[k].off[nch] = (uint32_t)bytes;
             bytes += r;
         }
@@ -400,45 +442,67 @@ int run_shard(srtp_dispatch *d, int s, const std::vector<uint32_t> &idx, int32_t
             rc_all = SRTP_EINVAL;
             break;
         }
-        chunk_at[k] = pos;
-        chunk_n[k] = nch;
-        pos += nch;
         // a registered segment whose chunk is one run: the DMA reads and
         // writes the caller's bytes in place; else the packet bytes go
         // through the slot.  Either way the per-packet arrays, and the copies,
         // are split over the copy helpers.
-        direct[k] = d->b_registered && contig;
+        const bool direct = b.registered && contig;
         {
-            const int parts = parts_for(nch);
+            const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
             d->pool->run(parts, [&](int q) {
                 const size_t j0 = nch * q / parts, j1 = nch * (q + 1) / parts;
                 for (size_t j = j0; j < j1; j++) {
                     const uint32_t i = ch[j];
-                    sl[k].len[j] = d->b_len[i];
-                    sl[k].cap[j] = d->b_cap[i];
-                    sl[k].flags[j] = d->b_flags ? d->b_flags[i] : 0u;
-                    sl[k].tids[j] = d->b_tids ? d->b_tids[i] : d->b_tid;
+                    sl[k].len[j] = b.len[i];
+                    sl[k].cap[j] = b.cap[i];
+                    sl[k].flags[j] = b.flags ? b.flags[i] : 0u;
+                    sl[k].tids[j] = b.tids ? b.tids[i] : b.tid;
                 }
-                if (!direct[k]) copy_runs<true>(d, sl[k], ch, j0, j1);
+                if (!direct) copy_runs<true>(b, sl[k], ch, j0, j1);
             });
         }
         d->t_pack += now_ns() - tp;
-        const int rc = direct[k] ? srtp_pipeline_submit_host(pl, k, reverse, 1, -1, 1, (uint32_t)nch, bytes, -1,
-                                                             d->b_seg + d->b_off[ch[0]])
-                                 : srtp_pipeline_submit(pl, k, reverse, 1, -1, 1, (uint32_t)nch, bytes);
+        const int rc = direct ? srtp_pipeline_submit_host(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes, -1,
+                                                          b.seg + b.off[ch[0]])
+                              : srtp_pipeline_submit(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes);
         if (rc != SRTP_OK) {
             rc_all = rc;
-            for (size_t j = 0; j < nch; j++) d->b_status[ch[j]] = SRTP_STATUS_ERR_INTERNAL;
             break;
         }
-        busy[k] = 1;
-        k = (k + 1) % kDepth;
+        rg.owner[k] = bp;
+        rg.ch[k] = ch;
+        rg.n[k] = nch;
+        rg.direct[k] = direct;
+        b.chunks_out.fetch_add(1, std::memory_order_acq_rel);
+        pos += nch;
+        rg.k = (k + 1) % kDepth;
     }
-    // every chunk in flight comes back (its results are the caller's) even
-    // after an error; packets never submitted get an explicit status
-    for (int q = 0; q < kDepth; q++) drain((k + q) % kDepth);
-    for (size_t q = pos; q < idx.size(); q++) d->b_status[idx[q]] = SRTP_STATUS_ERR_INTERNAL;
+    // packets never submitted (an error) get an explicit status; every chunk
+    // in flight still comes back, its results the caller's
+    for (size_t q = pos; q < idx.size(); q++) b.status[idx[q]] = SRTP_STATUS_ERR_INTERNAL;
+    if (drain_all || rc_all != SRTP_OK)
+        for (int q = 0; q < kDepth; q++) {
+            const int k = (rg.k + q) % kDepth;
+            drain_slot(d, s, k, sl[k]);
+        }
     return rc_all;
+}
+
+// Drains, oldest first, the slots of shard s whose bundles have tickets up
+// to `upto` (a wait for one of them).
+int drain_upto(srtp_dispatch *d, int s, uint64_t upto) {
+    srtp_pipeline *pl = d->pipes[(size_t)s];
+    if (!pl) return SRTP_OK;
+    ShardRing &rg = d->rings[(size_t)s];
+    for (int q = 0; q < kDepth; q++) {
+        const int k = (rg.k + q) % kDepth;
+        if (!rg.owner[k] || rg.owner[k]->ticket > upto) continue;
+        srtp_pipeline_slot sl;
+        const int rc = srtp_pipeline_slot_get(pl, k, &sl);
+        if (rc != SRTP_OK) return rc;
+        drain_slot(d, s, k, sl);
+    }
+    return SRTP_OK;
 }
 
 void worker_main(srtp_dispatch *d, int s) {
@@ -451,28 +515,37 @@ void worker_main(srtp_dispatch *d, int s) {
         srtp_dispatch::Job job = d->jobs[(size_t)s];
         lk.unlock();
         int rc = SRTP_OK;
-        if (job.idx && !job.idx->empty()) rc = run_shard(d, s, *job.idx, job.reverse);
+        if (!job.b) rc = drain_upto(d, s, job.upto);
+        else if (job.idx && !job.idx->empty()) rc = run_shard(d, s, *job.b, job.b, *job.idx, job.drain_all);
+        job = srtp_dispatch::Job{}; // drop the bundle reference before reporting
         lk.lock();
         d->jobs[(size_t)s].rc = rc;
         if (--d->pending == 0) d->cv_done.notify_all();
     }
 }
 
-// Runs one phase on every shard at once; returns the first error.
-int run_phase(srtp_dispatch *d, const std::vector<std::vector<uint32_t>> &per_shard, int32_t reverse) {
+// Runs one phase on every shard at once; returns the first error.  b null:
+// drain the slots of the bundles with tickets up to `upto`.
+int run_phase(srtp_dispatch *d, const std::shared_ptr<HostBundle> &b,
+              const std::vector<std::vector<uint32_t>> *per_shard, bool drain_all, uint64_t upto = 0) {
     std::unique_lock<std::mutex> lk(d->wmu);
     for (size_t s = 0; s < d->engines.size(); s++) {
-        d->jobs[s].idx = &per_shard[s];
-        d->jobs[s].reverse = reverse;
+        d->jobs[s].b = b;
+        d->jobs[s].idx = per_shard ? &(*per_shard)[s] : nullptr;
+        d->jobs[s].drain_all = drain_all;
+        d->jobs[s].upto = upto;
         d->jobs[s].rc = SRTP_OK;
     }
     d->pending = (int)d->engines.size();
     d->generation++;
     d->cv_go.notify_all();
     d->cv_done.wait(lk, [&] { return d->pending == 0; });
-    for (auto &j : d->jobs)
-        if (j.rc != SRTP_OK) return j.rc;
-    return SRTP_OK;
+    int rc = SRTP_OK;
+    for (auto &j : d->jobs) {
+        if (j.rc != SRTP_OK && rc == SRTP_OK) rc = j.rc;
+        j.b.reset();
+    }
+    return rc;
 }
 
 // Calls f(engine) on every shard; fails unless every shard returns the same id.
@@ -544,6 +617,11 @@ int32_t srtp_packet_may_throw(int32_t kind, int32_t reverse, const uint8_t *pkt,
 
 void srtp_dispatch_destroy(srtp_dispatch *d) {
     if (!d) return;
+    if (!d->workers.empty() && !d->inflight.empty()) { // bundles never waited for: their results first
+        std::lock_guard<FairMutex> g(d->mu);
+        (void)run_phase(d, nullptr, nullptr, false, UINT64_MAX);
+        d->inflight.clear();
+    }
     {
         std::lock_guard<std::mutex> lk(d->wmu);
         d->stop = true;
@@ -598,6 +676,7 @@ int srtp_dispatch_create(const int32_t *devices, int32_t n_shards, const srtp_en
     }
     if (rc == SRTP_OK) {
         d->jobs.resize((size_t)n_shards);
+        d->rings.resize((size_t)n_shards);
         try {
             for (int32_t s = 0; s < n_shards; s++) d->workers.emplace_back(worker_main, d, (int)s);
         } catch (...) {
@@ -672,13 +751,26 @@ int srtp_dispatch_transformer_close(srtp_dispatch *d, int32_t t) {
     return each(d, [&](srtp_engine *e) { return srtp_transformer_close(e, t); });
 }
 
-int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid,
-                                 uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
-                                 const uint32_t *cap, const uint32_t *flags, int32_t *status,
-                                 uint32_t n) {
-    if (!d) return SRTP_EINVAL;
-    std::lock_guard<FairMutex> g(d->mu);
-    if (n == 0) return SRTP_OK;
+namespace {
+// One host bundle, under d->mu.  Synchronous (ticket null): returns when its
+// results are in the caller's arrays.  Asynchronous: returns once every chunk
+// is on its way, the last ones still in flight, with the bundle's ticket for
+// srtp_dispatch_wait_host.  A bundle that may throw (the rollback below) runs
+// synchronously either way.
+int submit_locked(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid, uint8_t *seg,
+                  size_t seg_bytes, const uint32_t *off, uint32_t *len, const uint32_t *cap,
+                  const uint32_t *flags, int32_t *status, uint32_t n, uint64_t *ticket) {
+    const bool async = ticket != nullptr;
+    auto bp = std::make_shared<HostBundle>();
+    bp->ticket = d->next_ticket++;
+    auto finish = [&](int rc) { // the bundle's outcome: async callers get it from the wait
+        if (async && rc == SRTP_OK) {
+            d->inflight.push_back(bp);
+            *ticket = bp->ticket;
+        }
+        return rc;
+    };
+    if (n == 0) return finish(SRTP_OK);
     if (!seg || !off || !len || !cap || !status) return dfail(d, SRTP_EINVAL, "null buffer");
     const uint64_t t0 = now_ns();
     struct Done { // the call's total host time, however it returns
@@ -732,9 +824,11 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
         if (x < 0) return dfail(d, x, "packet region outside the segment");
         plan = std::max(plan, x);
     }
-    d->b_tids = tids; d->b_tid = tid; d->b_seg = seg; d->b_off = off; d->b_len = len;
-    d->b_cap = cap; d->b_flags = flags; d->b_status = status;
-    d->b_registered = srtp_host_is_registered(seg, seg_bytes) != 0;
+    HostBundle &b = *bp;
+    b.reverse = reverse;
+    b.tids = tids; b.tid = tid; b.seg = seg; b.off = off; b.len = len;
+    b.cap = cap; b.flags = flags; b.status = status;
+    b.registered = srtp_host_is_registered(seg, seg_bytes) != 0;
     for (size_t s = 0; s < ns; s++) {
         if (d->pipes[s]) continue;
         // shards sharing a GPU: one stream each (SRTP_PIPE_ONE_STREAM); the
@@ -744,7 +838,8 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
         if (rc != SRTP_OK) return dfail(d, rc, "shard pipeline");
     }
     auto tid_of = [&](uint32_t i) { return tids ? tids[i] : tid; };
-    std::vector<std::vector<uint32_t>> per_shard(ns);
+    std::vector<std::vector<uint32_t>> &per_shard = b.per_shard;
+    per_shard.resize(ns);
     std::vector<uint32_t> at((size_t)parts * ns);
     for (size_t s = 0; s < ns; s++) {
         uint32_t acc = 0;
@@ -764,8 +859,17 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
     });
     d->t_plan += now_ns() - t0;
     if (plan == 1) { // nothing can throw: one run
-        const int rc = run_phase(d, per_shard, reverse);
-        return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed");
+        int rc = run_phase(d, bp, &per_shard, !async);
+        if (rc == SRTP_OK && !async) rc = b.rc.load();
+        if (rc != SRTP_OK && async) // no ticket: nothing of this bundle may stay in flight
+            (void)run_phase(d, nullptr, nullptr, false, bp->ticket);
+        return rc == SRTP_OK ? finish(SRTP_OK) : dfail(d, rc, "shard bundle failed");
+    }
+    // The rollback needs every earlier bundle's results and this one's whole
+    // run: the bundles in flight come back first.
+    {
+        const int rc = run_phase(d, nullptr, nullptr, false, UINT64_MAX);
+        if (rc != SRTP_OK) return dfail(d, rc, "shard bundle failed");
     }
     // Transformers that could throw: their contexts in this bundle are
     // snapshotted per shard and their packets' input bytes stashed.
@@ -815,7 +919,8 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
             return dfail(d, rc, std::string("shard ") + std::to_string(sh) + ": " +
                                     srtp_engine_last_error(d->engines[sh]));
     }
-    int rc = run_phase(d, per_shard, reverse);
+    int rc = run_phase(d, bp, &per_shard, true);
+    if (rc == SRTP_OK) rc = b.rc.load();
     if (rc != SRTP_OK) return dfail(d, rc, "shard bundle failed");
     // e_t: each risky transformer's first throw over all shards
     std::vector<int64_t> e_first((size_t)nt, -1);
@@ -858,7 +963,7 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
         memcpy(seg + off[i], stash.data() + stash_at[i], region(cap[i]));
         len[i] = stash_len[i];
     }
-    if (!any_dirty) return SRTP_OK;
+    if (!any_dirty) return finish(SRTP_OK);
     // Reset the dirty contexts, then re-run t's packets up to e_t on them.
     std::vector<std::vector<uint32_t>> rerun(ns);
     for (size_t sh = 0; sh < ns; sh++) {
@@ -890,8 +995,47 @@ int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_
             rerun[sh].push_back(i);
         }
     }
-    rc = run_phase(d, rerun, reverse);
-    return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed (rollback re-run)");
+    rc = run_phase(d, bp, &rerun, true);
+    if (rc == SRTP_OK) rc = b.rc.load();
+    return rc == SRTP_OK ? finish(SRTP_OK) : dfail(d, rc, "shard bundle failed (rollback re-run)");
+}
+} // namespace
+
+int srtp_dispatch_transform_host(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid,
+                                 uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                                 const uint32_t *cap, const uint32_t *flags, int32_t *status,
+                                 uint32_t n) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<FairMutex> g(d->mu);
+    return submit_locked(d, reverse, tids, tid, seg, seg_bytes, off, len, cap, flags, status, n, nullptr);
+}
+
+int srtp_dispatch_submit_host(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_t tid,
+                              uint8_t *seg, size_t seg_bytes, const uint32_t *off, uint32_t *len,
+                              const uint32_t *cap, const uint32_t *flags, int32_t *status, uint32_t n,
+                              uint64_t *ticket) {
+    if (!d || !ticket) return SRTP_EINVAL;
+    *ticket = 0;
+    std::lock_guard<FairMutex> g(d->mu);
+    if (d->inflight.size() >= kMaxInflight) return dfail(d, SRTP_EAGAIN, "too many host bundles in flight");
+    return submit_locked(d, reverse, tids, tid, seg, seg_bytes, off, len, cap, flags, status, n, ticket);
+}
+
+int srtp_dispatch_wait_host(srtp_dispatch *d, uint64_t ticket) {
+    if (!d) return SRTP_EINVAL;
+    std::lock_guard<FairMutex> g(d->mu);
+    auto it = std::find_if(d->inflight.begin(), d->inflight.end(),
+                           [&](const std::shared_ptr<HostBundle> &b) { return b->ticket == ticket; });
+    if (it == d->inflight.end()) return dfail(d, SRTP_EINVAL, "no such host bundle in flight");
+    const std::shared_ptr<HostBundle> b = *it;
+    if (b->chunks_out.load(std::memory_order_acquire) != 0) {
+        // drains this bundle's slots and those of the bundles before it
+        const int rc = run_phase(d, nullptr, nullptr, false, ticket);
+        if (rc != SRTP_OK) return dfail(d, rc, "shard bundle failed");
+    }
+    d->inflight.erase(std::find(d->inflight.begin(), d->inflight.end(), b));
+    const int rc = b->rc.load();
+    return rc == SRTP_OK ? SRTP_OK : dfail(d, rc, "shard bundle failed");
 }
 
 int srtp_dispatch_host_times(srtp_dispatch *d, uint64_t ns[6]) {

@@ -75,6 +75,13 @@ struct srtp_engine {
     // recorded on the bundle's stream after each bundle: later bundles on other
     // streams wait for it on the device, control-plane calls on the host
     hipEvent_t ev_last = nullptr;
+    // device-resident bundles (srtp_transform_device) end with ev_dev instead:
+    // a device-scope release.  A system-scope one (ev_last) writes back and
+    // invalidates the L2 and idles the queue ~10-13 us per bundle
+    // (profiles/r05/events/); host-visible completion is fenced at sync time
+    // instead (fence_to_host).
+    hipEvent_t ev_dev = nullptr;
+    bool last_dev = false;
     unsigned long long *d_count = nullptr; // [2] live / tombstone counts
     unsigned long long *d_counters = nullptr; // [kCountReplicas][kCtrStride]
 #ifdef SRTP_STAMPS
@@ -358,8 +365,26 @@ struct DeviceGuard {
 // Waits until every bundle this engine has enqueued (on any stream) and its
 // own stream's work have completed: the precondition of every control-plane
 // call that reads or rewrites device state the kernels use.
+static hipEvent_t last_event(const srtp_engine *e) { return e->last_dev ? e->ev_dev : e->ev_last; }
+
+// After a device-scope event: a system-scope release on `s` behind it, so
+// that what the bundle wrote is visible to the host (a caller's zero-copy
+// buffers) when the wait returns.
+static int fence_to_host(srtp_engine *e, hipStream_t s) {
+    if (!e->last_dev) return SRTP_OK;
+    HIPCHK(e, hipStreamWaitEvent(s, e->ev_dev, 0));
+    HIPCHK(e, hipEventRecord(e->ev_last, s));
+    HIPCHK(e, hipEventSynchronize(e->ev_last));
+    e->last_dev = false;
+    return SRTP_OK;
+}
+
 int quiesce(srtp_engine *e) {
-    if (e->have_last) HIPCHK(e, hipEventSynchronize(e->ev_last));
+    if (e->have_last) HIPCHK(e, hipEventSynchronize(last_event(e)));
+    if (e->have_last && e->last_dev) {
+        int rc = fence_to_host(e, e->stream);
+        if (rc != SRTP_OK) return rc;
+    }
     if (e->stream) HIPCHK(e, hipStreamSynchronize(e->stream));
     return SRTP_OK;
 }
@@ -451,6 +476,10 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
         if (!guard.ok) { rc = SRTP_EDEVICE; break; }
         if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { rc = SRTP_EDEVICE; break; }
         if (hipEventCreateWithFlags(&e->ev_last, hipEventDisableTiming) != hipSuccess) { rc = SRTP_EDEVICE; break; }
+        if (hipEventCreateWithFlags(&e->ev_dev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+            rc = SRTP_EDEVICE;
+            break;
+        }
         uint32_t te0[256];
         aes_te0_le(te0);
         if (upload_tables(te0) != hipSuccess) { rc = SRTP_EDEVICE; break; }
@@ -509,6 +538,7 @@ void srtp_engine_destroy(srtp_engine *e) {
                     e->h_cap, e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
     if (e->ev_last) (void)hipEventDestroy(e->ev_last);
+    if (e->ev_dev) (void)hipEventDestroy(e->ev_dev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -662,7 +692,7 @@ int srtp_transformer_close(srtp_engine *e, int32_t t) {
 static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
                             uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
                             const uint32_t *flags, int32_t *status, uint32_t n, hipStream_t s,
-                            int32_t abort = -1) {
+                            int32_t abort = -1, bool dev_event = false) {
     if (n == 0) return SRTP_OK;
     if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
     if (n > kRecIdxMask) return fail(e, SRTP_EINVAL, "bundle too large");
@@ -672,7 +702,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (rc != SRTP_OK) return rc;
     // bundles of one engine share its scratch and run in submission order: a
     // bundle on another stream than the previous one waits for it on the device
-    if (e->have_last && e->last_stream != s) HIPCHK(e, hipStreamWaitEvent(s, e->ev_last, 0));
+    if (e->have_last && e->last_stream != s) HIPCHK(e, hipStreamWaitEvent(s, last_event(e), 0));
     BundleArgs a{};
     a.keysets = e->d_keysets;
     a.extkeys = e->d_extkeys;
@@ -785,7 +815,8 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         if (e->n_ext) HIPCHK(e, launch_ext(a, s));
         if (e->n_skein) HIPCHK(e, launch_skein(a, s));
     }
-    HIPCHK(e, hipEventRecord(e->ev_last, s));
+    HIPCHK(e, hipEventRecord(dev_event ? e->ev_dev : e->ev_last, s));
+    e->last_dev = dev_event;
     e->last_stream = s;
     e->have_last = true;
     e->n_bundles++;
@@ -804,7 +835,7 @@ int srtp_transform_device(srtp_engine *e, int32_t reverse, const int32_t *tids, 
     // that want the two directions to overlap pass each engine's own stream
     // (srtp_engine_stream: one hardware queue per engine)
     hipStream_t s = (hipStream_t)stream;
-    return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s);
+    return transform_locked(e, reverse, tids, tid, seg, off, len, cap, flags, status, n, s, -1, true);
 }
 
 // Every packet region [off, off + cap rounded to 16) inside the segment,
@@ -878,7 +909,7 @@ int srtp_engine_sync(srtp_engine *e, void *stream) {
     GUARD(e);
     if (!stream) return quiesce(e); // every bundle of this engine, whatever its stream
     HIPCHK(e, hipStreamSynchronize((hipStream_t)stream));
-    return SRTP_OK;
+    return e->have_last && e->last_stream == (hipStream_t)stream ? fence_to_host(e, (hipStream_t)stream) : SRTP_OK;
 }
 
 int srtp_get_context_state(srtp_engine *e, int32_t t, uint32_t ssrc, srtp_ctx_state *out) {

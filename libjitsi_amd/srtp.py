@@ -508,6 +508,47 @@ class SRTPDispatcher:
         self._chk(rc, "srtp_dispatch_transform_host")
         return status
 
+    def submit_host(self, reverse: bool, tid, seg: np.ndarray, off: np.ndarray,
+                    length: np.ndarray, cap: np.ndarray, flags=None) -> "HostTicket":
+        """srtp_dispatch_submit_host: transform_host without waiting.  The
+        arrays (kept alive by the returned ticket) must not be touched until
+        ``ticket.wait()`` (srtp_dispatch_wait_host) returns the statuses."""
+        n = len(off)
+        assert seg.dtype == np.uint8 and seg.flags.c_contiguous
+        off = np.ascontiguousarray(off, np.uint32)
+        cap = np.ascontiguousarray(cap, np.uint32)
+        assert length.dtype == np.uint32 and length.flags.c_contiguous and len(length) == n
+        status = np.zeros(n, np.int32)
+        fl = None if flags is None else np.ascontiguousarray(flags, np.uint32)
+        tids = None
+        if np.isscalar(tid):
+            tids_p, tid0 = None, int(tid)
+        else:
+            tids = np.ascontiguousarray(tid, np.int32)
+            tids_p, tid0 = tids.ctypes.data, -1
+        t = C.c_uint64()
+        rc = N.lib().srtp_dispatch_submit_host(
+            self.h, int(reverse), tids_p, tid0, seg.ctypes.data, seg.nbytes, off.ctypes.data,
+            length.ctypes.data, cap.ctypes.data, None if fl is None else fl.ctypes.data,
+            status.ctypes.data, n, C.byref(t))
+        self._chk(rc, "srtp_dispatch_submit_host")
+        return HostTicket(self, t.value, status, (seg, off, length, cap, fl, tids))
+
+
+class HostTicket:
+    """A host bundle in flight (SRTPDispatcher.submit_host)."""
+
+    def __init__(self, d: SRTPDispatcher, ticket: int, status: np.ndarray, keep):
+        self.d, self.ticket, self.status, self._keep = d, ticket, status, keep
+        self.done = False
+
+    def wait(self) -> np.ndarray:
+        if not self.done:
+            self.d._chk(N.lib().srtp_dispatch_wait_host(self.d.h, self.ticket), "srtp_dispatch_wait_host")
+            self.done = True
+            self._keep = None
+        return self.status
+
 
 class SRTPAggregator:
     """Per-packet submits from many threads -> bundles (srtp_aggregator_*,

@@ -343,6 +343,26 @@ def test_roc_guess_overturned_by_walk(twin):
         assert (st2 == st).all()
 
 
+def test_recheck_state_at_the_seq_range_edges(twin):
+    """k_unprotect skips the walk's re-check state for a context whose s_l
+    and in-bundle SEQs lie within 32768 of each other (no ROC change can
+    happen in the bundle).  Bundles right at that edge -- spans of 32766 to
+    32769 above and below s_l, and wraps through 65535 -- must still come out
+    as the oracle's, tag checks under a changed ROC included."""
+    (k, s), = synth.keys(33, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    for span in (32766, 32767, 32768, 32769):
+        for first, seqs in ((100, lambda x: [100 + x, 150, 100 + x - 1, 101]),
+                            (40000, lambda x: [40000 - x, 40100, 40000 - x + 1]),
+                            (65000, lambda x: [65535, 0, 1, (65000 + x) & 0xFFFF, 65001])):
+            snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+            for q in ([first], seqs(span)):
+                b = synth.rtp_bundle(len(q), 1, 200, seed=span + len(q))
+                set_seqs(b, q)
+                seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+                twin.run(rcv, True, seg, b.off, ln, b.cap)
+
+
 def set_seqs(b, seqs):
     for i, q in enumerate(seqs):
         b.seg[b.off[i] + 2] = q >> 8
