@@ -585,7 +585,8 @@ int srtp_dispatch_set_context_state(srtp_dispatch *d, int32_t transformer, uint3
 /* srtp_stats summed over the shards */
 int srtp_dispatch_stats(srtp_dispatch *d, srtp_stats *out);
 /* Host time of srtp_dispatch_transform_host since creation, in ns: [0] plan
- * and split, [1] packing into the shards' pinned slots, [2] waiting for the
+ * and split, [1] packing into the shards' pinned slots and enqueueing each
+ * chunk's copies and kernels, [2] waiting for the
  * shards' bundles (H2D + kernels + D2H), [3] scattering results back (1-3
  * summed over the shards' worker threads), [4] wall time of the calls, [5]
  * number of calls. */

@@ -62,7 +62,7 @@ namespace {
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
 constexpr uint32_t kChunkPackets = 1u << 15;       // packets per pipeline slot
 constexpr size_t kChunkBytes = (size_t)48 << 20;   // segment bytes per pipeline slot
-constexpr int kDepth = 4;                          // pipeline slots per shard
+constexpr int kDepth = 8;                          // pipeline slots per shard
 constexpr size_t kMaxInflight = 64;                // host bundles submitted and not yet waited for
 
 uint32_t mix32(uint32_t x) { // murmur3 fmix32 (libjitsi_amd/dispatch.py mix32)
@@ -461,10 +461,10 @@ int run_shard(srtp_dispatch *d, int s, HostBundle &b, const std::shared_ptr<Host
                 if (!direct) copy_runs<true>(b, sl[k], ch, j0, j1);
             });
         }
-        d->t_pack += now_ns() - tp;
         const int rc = direct ? srtp_pipeline_submit_host(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes, -1,
                                                           b.seg + b.off[ch[0]])
                               : srtp_pipeline_submit(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes);
+        d->t_pack += now_ns() - tp; // the enqueue of the chunk's copies and kernels included
         if (rc != SRTP_OK) {
             rc_all = rc;
             break;

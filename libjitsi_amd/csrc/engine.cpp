@@ -1347,7 +1347,12 @@ struct srtp_pipeline {
     std::vector<Slot> slots;
 };
 
-constexpr uint32_t kPackMax = 8192; // bundles up to this many packets use the packed copies
+// bundles up to this many packets use the packed copies: one H2D for the
+// per-packet arrays and one D2H for lengths + statuses instead of five and
+// two -- each separate small copy held the copy stream ~30-80 us, which left
+// the dispatcher's 32768-packet chunks' H2D idle ~200 us per chunk
+// (profiles/r05/dispatch/)
+constexpr uint32_t kPackMax = 1u << 15;
 constexpr size_t kOneStreamBytes = (size_t)1 << 20; // bundles up to this size copy on the engine's stream
 constexpr size_t kTinySeg = (size_t)64 << 10;       // bundles up to this size: one copy each way
 
