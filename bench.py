@@ -274,17 +274,26 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
                 # srtp_dispatch_submit_host / wait_host, two bundles in flight:
                 # P(A) P(B) U(A) U(B) ..., each submit after the wait of the
                 # previous operation on its buffer (the oldest in flight)
-                pending = []
+                pending, t_sub, t_wait = [], [], []
                 for _ in range(bundles):
                     for rev, t in ((False, snd), (True, rcv)):
                         for sg, l in bufs:
                             if len(pending) == 2:
-                                ok = ok and not pending.pop(0).wait().any()
+                                a0 = time.perf_counter()
+                                st_w = pending.pop(0).wait()
+                                t_wait.append(time.perf_counter() - a0)
+                                ok = ok and not st_w.any()
+                            a0 = time.perf_counter()
                             pending.append(d.submit_host(rev, t.tid, sg, b.off, l, b.cap))
+                            t_sub.append(time.perf_counter() - a0)
                 for tk in pending:
                     ok = ok and not tk.wait().any()
                 pending = None
                 dt = (time.perf_counter() - t0) / 2  # twice the bundles of the other modes
+                op_ms = {"submit_ms_p50": round(float(np.median(t_sub)) * 1e3, 3),
+                         "submit_ms_max": round(max(t_sub) * 1e3, 3),
+                         "wait_ms_p50": round(float(np.median(t_wait)) * 1e3, 3),
+                         "wait_ms_max": round(max(t_wait) * 1e3, 3)}
             else:
                 for _ in range(bundles):
                     st = d.transform_host(False, snd.tid, seg, b.off, ln, b.cap)
@@ -294,10 +303,12 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
             h1 = d.host_times()
             calls = max(h1["calls"] - h0["calls"], 1)
             per = {k2: round((h1[k2] - h0[k2]) / calls, 3) for k2 in h1 if k2 != "calls"}
+            extra = {}
             if mode == "async":
                 bufs = None
                 hb2.close()
-            out[str(G) if mode == "pinned" else f"{G}_{mode}"] = {
+                extra = {"async_ops": op_ms}
+            out[str(G) if mode == "pinned" else f"{G}_{mode}"] = {**extra,
                 "directional_pps": round(2 * bundles * n / dt, 1),
                 "ms_per_bundle": round(dt / (2 * bundles) * 1e3, 3),
                 "host_ms_per_bundle": per, "all_accepted": bool(ok),

@@ -17,3 +17,7 @@ for cfg in "4096,8,6 64" "16384,24,8 256"; do
   python3 -c "import json; j=json.loads(open('$O/q.tmp').read()); j['agg']='$1'; j['depth']=$2; print(json.dumps(j))" >> $O/sync.jsonl
 done
 timeout -k 10 120 ./tools/agg_bench > $O/agg_bench.log 2>&1 || exit $?
+# the dispatcher leg (1 shard; the asynchronous mode's per-operation times)
+timeout -k 10 400 python3 bench.py --steps 5 --no-cpu --no-e2e --dispatch-shards 1 > $O/bench_dispatch.log 2>&1 || exit $?
+# --gpus 8 without torchrun: one process per side, all on device 0 (gloo)
+timeout -k 10 300 env SRTP_BENCH_ONE_DEVICE=1 python bench.py --gpus 8 --backend gloo --steps 20 --no-cpu --no-e2e --no-dispatch > $O/rehearsal8.log 2>&1 || exit $?
