@@ -44,6 +44,7 @@ struct srtp_engine {
     uint64_t *d_ctx_keys = nullptr;
     CtxState *d_ctx = nullptr;
     uint32_t ctx_cap = 0;
+    uint32_t *d_far = nullptr; // [ctx_cap] BundleArgs::far
     int ctx_bits = 0;
 
     // per-bundle scratch, sized for scratch_n packets
@@ -493,6 +494,7 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
             dalloc(&e->d_transformers, o.max_transformers) != hipSuccess ||
             dalloc(&e->d_ctx_keys, e->ctx_cap) != hipSuccess ||
             dalloc(&e->d_ctx, e->ctx_cap) != hipSuccess ||
+            dalloc(&e->d_far, e->ctx_cap) != hipSuccess ||
             dalloc(&e->e_min, 2 * (size_t)o.max_transformers) != hipSuccess ||
             dalloc(&e->ctl, 2) != hipSuccess || dalloc(&e->d_count, 2) != hipSuccess ||
             dalloc(&e->d_counters, (size_t)kCountReplicas * kCtrStride) != hipSuccess) {
@@ -501,6 +503,7 @@ int srtp_engine_create(const srtp_engine_opts *opts, srtp_engine **out) {
         }
         if (hipMemset(e->d_ctx_keys, 0xff, (size_t)e->ctx_cap * sizeof(uint64_t)) != hipSuccess ||
             hipMemset(e->d_ctx, 0, (size_t)e->ctx_cap * sizeof(CtxState)) != hipSuccess ||
+            hipMemset(e->d_far, 0, (size_t)e->ctx_cap * sizeof(uint32_t)) != hipSuccess ||
             hipMemset(e->d_counters, 0, sizeof(unsigned long long) * kCountReplicas * kCtrStride) != hipSuccess) {
             rc = SRTP_EDEVICE;
             break;
@@ -534,7 +537,7 @@ void srtp_engine_destroy(srtp_engine *e) {
     }
     for (auto ev : e->event_pool) (void)hipEventDestroy(ev);
     void *ptrs[] = {e->d_keysets, e->d_extkeys, e->d_tfkeys, e->d_skkeys, e->d_factories, e->d_transformers, e->d_ctx_keys, e->d_ctx,
-                    e->e_min, e->ctl, e->d_count, e->d_counters, e->h_seg, e->h_off, e->h_len,
+                    e->d_far, e->e_min, e->ctl, e->d_count, e->d_counters, e->h_seg, e->h_off, e->h_len,
                     e->h_cap, e->h_flags, e->h_status, e->h_tids};
     for (void *p : ptrs) dfree(p);
     if (e->ev_last) (void)hipEventDestroy(e->ev_last);
@@ -714,6 +717,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.ctx_keys = e->d_ctx_keys;
     a.ctx = e->d_ctx;
     a.ctx_mask = e->ctx_cap - 1;
+    a.far = e->d_far;
     a.n_transformers = (uint32_t)e->transformers.size();
     a.seg = seg; a.off = off; a.len = len; a.cap = cap; a.flags = flags; a.status = status;
     a.tids = tids; a.tid = tid; a.n = n;

@@ -28,6 +28,11 @@ struct BundleArgs {
     uint64_t *ctx_keys;
     CtxState *ctx;
     uint32_t ctx_mask;     // table capacity - 1 (power of two)
+    // [ctx_mask + 1] per context slot: serial + 1 of the last unprotect bundle
+    // in which one of the context's RTP packets lay 16384 or more from its
+    // bundle-start s_l, or the context had no seqNumSet (k_parse); otherwise
+    // its ROC cannot change within the bundle (see k_unprotect)
+    uint32_t *far;
     uint32_t n_transformers;
     // caller's bundle
     uint8_t *seg;

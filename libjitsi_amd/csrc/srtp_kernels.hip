@@ -887,6 +887,10 @@ __device__ __forceinline__ uint32_t parse_one(const BundleArgs &a, uint32_t p) {
     bool maybe_throw = false;
     if (tr.kind == SRTP_KIND_RTP) {
         rec.word = bswap(hdr.x) & 0xffffu; // RawPacket.getSequenceNumber :804
+        if (a.reverse) { // a packet far from its context's s_l (see BundleArgs::far)
+            const int32_t sl = a.ctx[slot].b, dist = (int32_t)rec.word - sl;
+            if (!(a.ctx[slot].flags & 1u) || dist >= 16384 || dist <= -16384) a.far[slot] = a.serial + 1u;
+        }
         rec.h = rtp_header_len(pkt, b0, (int)C);
         if (a.reverse && (fl & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE))) rec.p |= kRecSkipDec;
         // conservative: a throw is possible for some tag length 0..20
@@ -3480,7 +3484,7 @@ template <bool LK>
 __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet *__restrict__ ks,
                                               const char *__restrict__ lds, const TeBase &tb,
                                               uint32_t p, const CtxState &st, bool fused,
-                                              bool mac_only = false) {
+                                              bool mac_only, bool save_state) {
     uint8_t *pkt = a.seg + a.off[p];
     const int L = (int)a.len[p];
     const int T = (int)kf<LK>(ks->tag_len);
@@ -3599,7 +3603,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             pk_half<1>(lds, tb, pk, cp, 4 * b - hq, K + 8, v, c);
 #pragma unroll
             for (int k = 0; k < 5; k++) h[k] += v[k];
-            if (rtp) { // midstate + ciphertext of the ROC-carrying block
+            if (rtp && save_state) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
@@ -3647,7 +3651,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         for (; b < n_blocks; b++) {
             uint32_t d[16];
             q.next(pkt, b, nb_data, end, d);
-            if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
+            if (b == nb_full && rtp && save_state) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int m = 0; m < 5; m++) mp[m] = h[m];
@@ -3673,7 +3677,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 if (b < nb_data && 64 * b + 16 * m < end) v = qp[m];
                 d[4 * m] = v.x; d[4 * m + 1] = v.y; d[4 * m + 2] = v.z; d[4 * m + 3] = v.w;
             }
-            if (b == nb_full && rtp) { // midstate + ciphertext of the ROC-carrying block
+            if (b == nb_full && rtp && save_state) { // midstate + ciphertext of the ROC-carrying block
                 uint32_t *mp = a.mid + 5 * (size_t)p;
 #pragma unroll
                 for (int k = 0; k < 5; k++) mp[k] = h[k];
@@ -3737,10 +3741,21 @@ __global__ __launch_bounds__(MacOnly ? kMacBlock : kUnprotectBlock) void k_unpro
     const bool todo = slot != kNoSlot;
     CtxState st = {};
     bool lng = false;
+    uint32_t far = 0u;
     if (todo) {
         st = a.ctx[slot];
+        far = a.far[slot];
         lng = pos >= kLongRank && a.sk_out[pos - kLongRank] == slot;
     }
+    // The walk re-checks a tag (from the midstate and ciphertext saved here)
+    // only under a ROC other than the one speculated on.  If every packet of
+    // the context in this bundle lies within 16384 of its bundle-start s_l,
+    // that s_l and all their SEQs lie within 32768 of each other, guessIndex
+    // (:457-475) adds 0 to the ROC for every pair of them, and the ROC cannot
+    // change within the bundle: the walk's ROC is the speculated one for every
+    // packet and nothing need be saved.  Contexts without seqNumSet, deep
+    // chains and contexts with a far packet (k_parse, BundleArgs::far) save it.
+    const bool quiet = todo && !lng && (st.flags & 1u) && far != a.serial + 1u;
     if (!MacOnly || __syncthreads_or(todo && mac_only_needs_te(a, slot))) fill_te4(s_te);
     STAMP(1);
     if (!live) return;
@@ -3769,7 +3784,7 @@ __global__ __launch_bounds__(MacOnly ? kMacBlock : kUnprotectBlock) void k_unpro
         const KeySet *ks = a.keysets + st.ks;
         const bool lane = todo && ks->ext == 0u && ks->enc_type == SRTP_AESCM_ENCRYPTION &&
                           ks->auth_type == SRTP_HMACSHA1_AUTHENTICATION;
-        if (lane) unprotect_one<true>(a, ks, lds, tb, p, st, !MacOnly, MacOnly);
+        if (lane) unprotect_one<true>(a, ks, lds, tb, p, st, !MacOnly, MacOnly, !quiet);
         rest = todo && !lane;
     }
     for_each_keyset(rest, st.ks, [&](uint32_t ks_u) {
@@ -3777,7 +3792,7 @@ __global__ __launch_bounds__(MacOnly ? kMacBlock : kUnprotectBlock) void k_unpro
         const bool fused = sgpr(ks->enc_type) == SRTP_AESCM_ENCRYPTION && !sgpr(ks->ext) &&
                            sgpr(ks->auth_type) != SRTP_NULL_AUTHENTICATION;
         const bool mac_only = MacOnly && fused && sgpr(ks->auth_type) == SRTP_HMACSHA1_AUTHENTICATION;
-        unprotect_one<false>(a, ks, lds, tb, p, st, !MacOnly && fused, mac_only);
+        unprotect_one<false>(a, ks, lds, tb, p, st, !MacOnly && fused, mac_only, !quiet);
     });
     STAMP(2);
 }
