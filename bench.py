@@ -78,6 +78,9 @@ def parse_args():
                     help="comma-separated shard counts of the dispatcher leg (default: 1,2,4 on one "
                          "GPU, else the GPU count)")
     ap.add_argument("--dispatch-bundles", type=int, default=8)
+    ap.add_argument("--dispatch-in-process", action="store_true",
+                    help="run the whole dispatcher leg in this (torch) process instead of a torch-free child")
+    ap.add_argument("--dispatch-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for the barrier/timing reduction (nccl = RCCL)")
     ap.add_argument("--serial", action="store_true",
@@ -226,7 +229,7 @@ def e2e_summary(dt, pkts, nbytes, ok, n_gpus, bundles, depth):
                     "processed in full; rates are whole-job (all GPUs)"}
 
 
-def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
+def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles, modes=None):
     """Host bundles through the in-process dispatcher (srtp_dispatch_transform_host):
     the deployment path of one JVM driving every GPU.  For each shard count G
     (devices_for(G) = the device of each shard), protect then unprotect the
@@ -238,11 +241,13 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
     key "G": a shard's chunk whose packets lie back to back moves by DMA in
     place, no host copy) and in plain pageable memory (key "G_copy": every
     packet copied into the pinned slots and back); G = 1 also with pageable
-    memory registered once (srtp_host_register, key "1_registered")."""
+    memory registered once (srtp_host_register, key "1_registered"), and with
+    two bundles in flight (srtp_dispatch_submit_host, key "G_async")."""
     from libjitsi_amd import (HostBuffer, SRTPContextFactory, SRTPDispatcher, SRTPTransformer,
                               host_register, host_unregister)
     out = {}
-    modes = [(G, m) for G in shard_counts for m in ("pinned", "async", "copy")] + [(1, "registered")]
+    if modes is None:
+        modes = [(G, m) for G in shard_counts for m in ("pinned", "async", "copy")] + [(1, "registered")]
     for G, mode in modes:
         d = SRTPDispatcher(devices_for(G), check_replay=False, max_contexts=1 << 15,
                            max_factories=8, max_transformers=8)
@@ -323,6 +328,72 @@ def dispatch_leg(b, pols, keys, n, devices_for, shard_counts, bundles):
     return out
 
 
+def policies(args):
+    from libjitsi_amd import SRTPPolicy, profile_policies
+    if args.policy == "AES_CM_128_NULL_AUTH":
+        return (SRTPPolicy(1, 16, 0, 0, 0, 14),) * 2
+    return profile_policies(args.policy)
+
+
+def world_devices(args):
+    """The devices of a one-process run (--gpus N in-process, or rank 0)."""
+    if args.gpus > 1:
+        one = os.environ.get("SRTP_BENCH_ONE_DEVICE") == "1"
+        return [0] * args.gpus if one else list(range(args.gpus))
+    return [0 if os.environ.get("SRTP_BENCH_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", "0"))]
+
+
+def dispatch_plan(args, devices):
+    """Shard counts of the dispatcher leg and the device of each shard."""
+    if args.dispatch_shards:
+        counts = [int(x) for x in args.dispatch_shards.split(",")]
+    else:
+        counts = [1, 2, 4] if len(devices) == 1 else [len(devices)]
+
+    def devs_for(G):
+        return [devices[i % len(devices)] for i in range(G)]
+    return counts, devs_for
+
+
+def dispatch_child(args) -> int:
+    """--dispatch-child: the dispatcher leg in a process that never imports
+    torch.  The torch wheel ships its own HIP runtime (ROCm 7.0,
+    torch/lib/libamdhip64.so, SONAME libamdhip64.so.7): in a process that
+    imported torch first, libsrtp_mi355x binds to it, and the two-in-flight
+    dispatcher runs at half its rate there (profiles/r05/dispatch/
+    hip_runtime.txt).  A JVM or C host loads /opt/rocm's runtime, as this
+    process does.  Started by the bench before it touches a GPU; idle until
+    the parent writes "go" (after its own GPU legs), then prints the leg's
+    JSON object and exits.  EOF on stdin: exits without touching the GPU."""
+    from libjitsi_amd import synth
+    pols = policies(args)
+    b, _ = shard_bundle(args, 0)
+    keys = synth.keys(2, 1)[0]
+    counts, devs_for = dispatch_plan(args, world_devices(args))
+    if sys.stdin.readline().strip() != "go":
+        return 0
+    out = dispatch_leg(b, pols, keys, args.packets, devs_for, counts, args.dispatch_bundles)
+    with open("/proc/self/maps") as f:
+        out["hip_runtime"] = sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+    out["torch_imported"] = "torch" in sys.modules
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def dispatch_child_result(child):
+    """Start the idle --dispatch-child on its leg and collect its JSON."""
+    try:
+        out, err = child.communicate("go\n", timeout=900)
+    except subprocess.TimeoutExpired:
+        child.kill()
+        child.communicate()
+        return {"error": "dispatcher child timed out"}
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    if child.returncode != 0 or not lines:
+        return {"error": f"dispatcher child exit {child.returncode}: {err.strip()[-400:]}"}
+    return json.loads(lines[-1])
+
+
 class DeviceEvent:
     """A stream-ordering event with a device-scope release
     (hipEventDisableSystemFence): the two directions' streams are on one GPU
@@ -369,6 +440,21 @@ class TorchEvent:
         stream.wait_event(self.ev)
 
 
+def shard_bundle(args, shard: int):
+    """Shard r's bundle (its own SSRCs) and each packet's stream length."""
+    from libjitsi_amd import synth
+    n, L, nssrc = args.packets, args.len, args.ssrcs
+    seed = synth.SEED_BASE + 2 + 7919 * shard
+    if args.zipf > 0:
+        b = synth.rtp_bundle_skewed(n, nssrc, L, seed=seed, zipf_s=args.zipf)
+        counts = b.meta["counts"]
+    else:
+        b = synth.rtp_bundle(n, nssrc, L, seed=seed)
+        idx = np.arange(n) % nssrc
+        counts = np.bincount(idx, minlength=nssrc)[idx]
+    return synth.realign(b, args.align), counts
+
+
 class Side:
     """One GPU's share: a sender engine + stream, a receiver engine + stream,
     and the ring of staged bundles."""
@@ -378,15 +464,7 @@ class Side:
         self.torch = torch
         dev = self.dev = torch.device("cuda", device)
         n, L, nssrc = args.packets, args.len, args.ssrcs
-        seed = synth.SEED_BASE + 2 + 7919 * shard  # shard r owns its own SSRCs
-        if args.zipf > 0:
-            b = synth.rtp_bundle_skewed(n, nssrc, L, seed=seed, zipf_s=args.zipf)
-            counts = b.meta["counts"]
-        else:
-            b = synth.rtp_bundle(n, nssrc, L, seed=seed)
-            idx = np.arange(n) % nssrc
-            counts = np.bincount(idx, minlength=nssrc)[idx]
-        b = synth.realign(b, args.align)
+        b, counts = shard_bundle(args, shard)
         self.b = b
         # max_contexts = the streams, as a deployment sets it: the engine's table
         # is next_pow2(2 x max_contexts) slots (2^15 at 10k: load 0.31; 2^18 at
@@ -605,6 +683,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 and args.gpus > 1 and os.environ.get("SRTP_BENCH_INPROC") != "1":
         sys.exit(spawn_ranks(args.gpus))
+    if args.dispatch_child:
+        sys.exit(dispatch_child(args))
+    child = None
+    if world == 1 and not args.no_dispatch and not args.dispatch_in_process:
+        # the dispatcher leg's torch-free process, started before this one
+        # touches a GPU (dispatch_child)
+        child = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--dispatch-child"] + sys.argv[1:],
+                                 stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                 text=True)
+    try:
+        return run_bench(args, world, child)
+    finally:
+        if child is not None and child.poll() is None:
+            child.kill()
+            child.communicate()
+
+
+def run_bench(args, world, child):
     import torch
     import torch.distributed as dist
 
@@ -624,19 +720,14 @@ def main():
         mode = "process"
     elif args.gpus > 1:
         # in-process: this process drives every GPU (all on device 0 for a rehearsal)
-        one = os.environ.get("SRTP_BENCH_ONE_DEVICE") == "1"
-        devices = [0] * args.gpus if one else list(range(args.gpus))
+        devices = world_devices(args)
         mode = "inproc"
     else:
         devices = [local_rank]
         mode = "process"
     n_gpus = world if mode == "process" else len(devices)
 
-    from libjitsi_amd import SRTPPolicy, profile_policies
-    if args.policy == "AES_CM_128_NULL_AUTH":
-        pols = (SRTPPolicy(1, 16, 0, 0, 0, 14),) * 2
-    else:
-        pols = profile_policies(args.policy)
+    pols = policies(args)
     n, L = args.packets, args.len
     T = pols[0].authTagLength
     n_timing = 40  # serial stage-timing steps (also the GPU's run-in before the warmup)
@@ -845,19 +936,20 @@ def main():
         for x in legs:
             x.close()
         e2e = e2e_summary(e_dt, e_pk, e_by, e_ok, n_gpus, args.e2e_bundles, legs[0].depth)
-    disp = None
+    disp = disp_torch = None
     if rank == 0 and not args.no_dispatch and world == 1:
-        if args.dispatch_shards:
-            counts = [int(x) for x in args.dispatch_shards.split(",")]
+        counts, devs_for = dispatch_plan(args, devices)
+        if child is None:
+            disp = dispatch_leg(b0, pols, keys0, n, devs_for, counts, args.dispatch_bundles)
         else:
-            counts = [1, 2, 4] if len(devices) == 1 else [len(devices)]
-        if len(devices) == 1:
-            def devs_for(G):
-                return [devices[0]] * G
-        else:
-            def devs_for(G):
-                return [devices[i % len(devices)] for i in range(G)]
-        disp = dispatch_leg(b0, pols, keys0, n, devs_for, counts, args.dispatch_bundles)
+            # the leg in this process too, one shard: on torch's HIP runtime
+            disp_torch = dispatch_leg(b0, pols, keys0, n, devs_for, [1], args.dispatch_bundles,
+                                      modes=[(1, "pinned"), (1, "async")])
+            disp_torch["note"] = ("this torch process: libsrtp_mi355x on torch's bundled HIP runtime "
+                                  "(ROCm 7.0); 'dispatch' ran in a torch-free process on /opt/rocm's")
+            disp = dispatch_child_result(child)
+            if "error" not in disp:
+                disp["process"] = "torch-free child (/opt/rocm HIP runtime, as a JVM or C host)"
 
     if rank == 0:
         line = {
@@ -898,6 +990,7 @@ def main():
             "cpu_baseline": cpu,
             "e2e": e2e,
             "dispatch": disp,
+            "dispatch_in_torch_process": disp_torch,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -3,7 +3,7 @@ and without two other engines (and their streams) alive in the process --
 the bench's dispatcher leg runs after the headline's sender and receiver
 engines.  Prints one JSON line per (extra engines, mode).
 
-    python tools/dispatch_async_py.py [bundle operations per mode]
+    python tools/dispatch_async_py.py [bundle operations per mode] [--no-torch] [--lib-first]
 """
 import json
 import os
@@ -15,6 +15,15 @@ import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from libjitsi_amd import (HostBuffer, SRTPContextFactory, SRTPDispatcher, SRTPEngine,  # noqa: E402
                           SRTPTransformer, profile_policies, synth)
+
+
+def hip_runtime():
+    """The libamdhip64 this process mapped: torch's wheel ships its own (ROCm
+    7.0) with the same SONAME as /opt/rocm's, so whichever loads first serves
+    both torch and libsrtp_mi355x."""
+    with open("/proc/self/maps") as f:
+        paths = {ln.split()[-1] for ln in f if "libamdhip64" in ln}
+    return sorted(paths)
 
 
 def run(ops, extra, use_torch=True):
@@ -43,7 +52,7 @@ def run(ops, extra, use_torch=True):
         st = d.transform_host(bool(i & 1), (rcv if i & 1 else snd).tid, sg, b.off, ln, b.cap)
         assert not st.any()
     dt = time.perf_counter() - t0
-    out.append({"torch": use_torch, "extra_engines": extra, "mode": "sync", "pps_per_direction": round(ops * b.n / dt, 1),
+    out.append({"torch": use_torch, "hip": hip_runtime(), "extra_engines": extra, "mode": "sync", "pps_per_direction": round(ops * b.n / dt, 1),
                 "ms_per_op": round(dt / ops * 1e3, 3)})
     pending, t_sub = [], []
     t0 = time.perf_counter()
@@ -71,6 +80,9 @@ def run(ops, extra, use_torch=True):
 if __name__ == "__main__":
     ops = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     use_torch = "--no-torch" not in sys.argv
+    if "--lib-first" in sys.argv:  # libsrtp_mi355x (and /opt/rocm's HIP runtime) before torch
+        from libjitsi_amd import _native
+        _native.lib()
     for extra in (0, 2):
         for line in run(ops, extra, use_torch):
             print(json.dumps(line), flush=True)
