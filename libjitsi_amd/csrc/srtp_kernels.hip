@@ -714,6 +714,39 @@ __device__ __forceinline__ bool tag_matches(const uint32_t h[5], const uint8_t *
     return ok;
 }
 
+// Word i (0..7, lane-varying) of w[8] by selects: no dynamic register index.
+__device__ __forceinline__ uint32_t pick8(const uint32_t w[8], int i) {
+    const bool o = i & 1;
+    const uint32_t a0 = o ? w[1] : w[0], a1 = o ? w[3] : w[2], a2 = o ? w[5] : w[4], a3 = o ? w[7] : w[6];
+    const uint32_t b0 = (i & 2) ? a1 : a0, b1 = (i & 2) ? a3 : a2;
+    return (i & 4) ? b1 : b0;
+}
+
+// tag_matches for the tag at byte `at` of a packet whose region starts 16-B
+// aligned (k_unprotect, once per packet after the MAC): the aligned 16-B
+// piece(s) holding the compared bytes in one or two vector loads instead of a
+// byte load per tag byte.  The second piece is loaded only when a compared
+// byte lies in it, so both lie inside the packet's region.
+__device__ __forceinline__ bool tag_matches_at(const uint32_t h[5], const uint8_t *pkt, int at, int T) {
+    if (at < 0) return tag_matches(h, pkt + at, T);
+    const int Tc = min(T, 12), sh = at & 15;
+    const uint4 *q = reinterpret_cast<const uint4 *>(pkt + (at - sh));
+    const uint4 v0 = q[0];
+    const uint4 v1 = sh + Tc > 16 ? q[1] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const int s4 = sh >> 2, sb = sh & 3;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        // the little-endian word at byte sh + 4k, as the digest's big-endian word k
+        const uint32_t le = __builtin_amdgcn_alignbyte(pick8(w, s4 + k + 1), pick8(w, s4 + k), (uint32_t)sb);
+        const int nb = min(max(Tc - 4 * k, 0), 4);
+        const uint32_t mask = nb ? 0xffffffffu << (8 * (4 - nb)) : 0u;
+        ok &= ((bswap(le) ^ h[k]) & mask) == 0u;
+    }
+    return ok;
+}
+
 __device__ __forceinline__ void tag_write(const uint32_t h[5], uint8_t *p, int T) {
 #pragma unroll
     for (int k = 0; k < 3; k++)
@@ -3630,7 +3663,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 else outer_words<!LK>(w, h, ks);
                 sha1_compress(h, w);
             }
-            a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+            a.auth_ok[p] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
             return;
         } else {
 #pragma unroll
@@ -3666,7 +3699,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             else outer_words<!LK>(d, h, ks);
             sha1_compress(h, d);
         }
-        a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+        a.auth_ok[p] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
     } else if (do_mac) {
         for (; b < n_blocks; b++) {
             uint32_t d[16];
@@ -3692,7 +3725,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             else outer_words<!LK>(d, h, ks);
             sha1_compress(h, d);
         }
-        a.auth_ok[p] = tag_matches(h, pkt + (L - T), T) ? 1u : 0u;
+        a.auth_ok[p] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
     }
     if (spec && !mac_only) {
         // reload the round keys through an opaque copy of the key-set pointer:
