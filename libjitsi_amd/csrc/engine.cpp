@@ -52,7 +52,7 @@ struct srtp_engine {
     uint32_t *p_slot = nullptr, *sk_in = nullptr, *sk_out = nullptr;
     WalkRec *sv_in = nullptr, *sv_out = nullptr;
     int32_t *w_status = nullptr;
-    uint32_t *w_cw = nullptr, *w_len = nullptr, *g0 = nullptr, *auth_ok = nullptr, *mid = nullptr;
+    uint32_t *w_cw = nullptr, *w_len = nullptr, *gok = nullptr, *mid = nullptr;
     uint32_t *tailc = nullptr, *spec = nullptr;
     uint64_t *tile_link = nullptr;
     uint32_t *spos = nullptr;
@@ -233,13 +233,13 @@ uint32_t next_pow2(uint64_t x) {
 
 void free_scratch(srtp_engine *e) {
     void *ptrs[] = {e->p_slot, e->sk_in, e->sk_out, e->sv_in, e->sv_out, e->w_status, e->w_cw,
-                    e->w_len, e->g0, e->auth_ok, e->mid, e->tailc, e->spec, e->sort_temp,
+                    e->w_len, e->gok, e->mid, e->tailc, e->spec, e->sort_temp,
                     e->spos, e->tile_link, e->lord, e->cls_tile};
     for (void *p : ptrs) dfree(p);
     e->p_slot = e->sk_in = e->sk_out = nullptr;
     e->sv_in = e->sv_out = nullptr;
     e->w_status = nullptr;
-    e->w_cw = e->w_len = e->g0 = e->auth_ok = e->mid = e->tailc = e->spec = nullptr;
+    e->w_cw = e->w_len = e->gok = e->mid = e->tailc = e->spec = nullptr;
     e->spos = nullptr;
     e->lord = nullptr;
     e->cls_tile = nullptr;
@@ -264,8 +264,7 @@ int ensure_scratch(srtp_engine *e, uint32_t n) {
     HIPCHK(e, dalloc(&e->w_status, m));
     HIPCHK(e, dalloc(&e->w_cw, m));
     HIPCHK(e, dalloc(&e->w_len, m));
-    HIPCHK(e, dalloc(&e->g0, m));
-    HIPCHK(e, dalloc(&e->auth_ok, m));
+    HIPCHK(e, dalloc(&e->gok, (size_t)2 * m));
     HIPCHK(e, dalloc(&e->mid, (size_t)5 * m));
     HIPCHK(e, dalloc(&e->tailc, (size_t)16 * m));
     HIPCHK(e, dalloc(&e->spec, m));
@@ -735,7 +734,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.p_slot = e->p_slot; a.sk_in = e->sk_in; a.sk_out = e->sk_out;
     a.sv_in = e->sv_in; a.sv_out = e->sv_out;
     a.w_status = e->w_status; a.w_cw = e->w_cw; a.w_len = e->w_len;
-    a.g0 = e->g0; a.auth_ok = e->auth_ok; a.mid = e->mid;
+    a.gok = e->gok; a.mid = e->mid;
     a.tailc = e->tailc; a.spec = e->spec;
     a.tile_link = e->tile_link;
     a.spos = e->spos;

@@ -61,9 +61,10 @@ struct BundleArgs {
     int32_t *w_status;     // [n]
     uint32_t *w_cw;        // [n] guessed ROC / SRTCP index word
     uint32_t *w_len;       // [n] length after processing
-    uint32_t *g0;          // [n] unprotect: ROC the verify pass assumed
-    uint32_t *auth_ok;     // [n] unprotect: bit 0 tag matched under g0; bit 2: also checked
-                           // under g0 - 1, bit 1 its result
+    uint32_t *gok;         // [2n] unprotect, per packet p: gok[2p] = g0, the ROC the verify
+                           // pass assumed; gok[2p + 1] = auth_ok: bit 0 tag matched under
+                           // g0; bit 2: also checked under g0 - 1, bit 1 its result (one
+                           // 8-B word, so the walk gathers both with one load)
     uint32_t *mid;         // [5n] unprotect: inner SHA-1 state before the ROC block
     uint32_t *tailc;       // [16n] unprotect: ciphertext of the ROC-carrying 64-B chunk
     uint32_t *spec;        // [n] unprotect: kSpec* summary of k_unprotect (bit 0: decrypted in place under g0)

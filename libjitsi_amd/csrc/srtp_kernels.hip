@@ -808,6 +808,11 @@ __device__ __forceinline__ bool enc_would_throw(int enc, int32_t h, int plen) {
     return false;
 }
 
+// Packet p's {g0, auth_ok} (BundleArgs::gok): one 8-B load.
+__device__ __forceinline__ uint2 gok_of(const BundleArgs &a, uint32_t p) {
+    return reinterpret_cast<const uint2 *>(a.gok)[p];
+}
+
 __device__ __forceinline__ int32_t packet_tid(const BundleArgs &a, uint32_t p) {
     return a.tids ? a.tids[p] : a.tid;
 }
@@ -2221,8 +2226,9 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
                 reinterpret_cast<uint4 *>(sm.rec)[j] = r;
                 if (REV) {
                     const uint32_t p = r.x & kRecIdxMask;
-                    sm.g0[j] = v ? a.g0[p] : 0u;
-                    sm.ok[j] = v ? a.auth_ok[p] : 0u;
+                    const uint2 go = v ? gok_of(a, p) : make_uint2(0u, 0u);
+                    sm.g0[j] = go.x;
+                    sm.ok[j] = go.y;
                 }
                 nv += v ? 1 : 0;
             }
@@ -2883,8 +2889,9 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
             // record of a skipped / invalid packet unwritten (stale scratch)
             if (REV && key <= a.ctx_mask) {
                 const uint32_t p = r.p & kRecIdxMask;
-                s_g0[j] = a.g0[p];
-                s_ok[j] = a.auth_ok[p];
+                const uint2 go = gok_of(a, p); // one 8-B gather: {g0, auth_ok}
+                s_g0[j] = go.x;
+                s_ok[j] = go.y;
             }
         }
     }
@@ -3100,7 +3107,8 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
             uint32_t g0 = 0u, ok = 0u;
             if (REV) {
                 const uint32_t p = r.p & kRecIdxMask;
-                g0 = a.g0[p]; ok = a.auth_ok[p];
+                const uint2 go = gok_of(a, p);
+                g0 = go.x; ok = go.y;
             }
             if (!step(r, g0, ok)) break;
         }
@@ -3564,7 +3572,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
         // guessIndex on the bundle-start state (for a packet deep in a long
         // chain, k_unprotect's state yields the chain's guess; see there)
         const int32_t g = guess_roc(st, seq);
-        a.g0[p] = (uint32_t)g;
+        a.gok[2 * (size_t)(p)] = (uint32_t)g;
         end = do_mac ? (L - T > 0 ? L - T : 0) : L;
         suffix = (uint32_t)g;
         const uint32_t fl = a.flags ? a.flags[p] : 0u;
@@ -3688,7 +3696,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
                 else outer_words<!LK>(w, h, ks);
                 sha1_compress(h, w);
             }
-            a.auth_ok[p] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
+            a.gok[2 * (size_t)(p) + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
             return;
         } else {
 #pragma unroll
@@ -3724,7 +3732,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             else outer_words<!LK>(d, h, ks);
             sha1_compress(h, d);
         }
-        a.auth_ok[p] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
+        a.gok[2 * (size_t)(p) + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
     } else if (do_mac) {
         for (; b < n_blocks; b++) {
             uint32_t d[16];
@@ -3750,7 +3758,7 @@ __device__ __forceinline__ void unprotect_one(const BundleArgs &a, const KeySet 
             else outer_words<!LK>(d, h, ks);
             sha1_compress(h, d);
         }
-        a.auth_ok[p] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
+        a.gok[2 * (size_t)(p) + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
     }
     if (spec && !mac_only) {
         // reload the round keys through an opaque copy of the key-set pointer:
@@ -3886,7 +3894,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
         L0 = (int)a.len[p0];
         const uint32_t slot = a.p_slot[p0];
         const uint32_t sw = a.spec[p0]; // k_unprotect's summary: no context / key-set loads
-        const uint32_t cw = a.w_cw[p0], g0 = a.g0[p0];
+        const uint32_t cw = a.w_cw[p0], g0 = a.gok[2 * (size_t)(p0)];
         const int32_t st = finish_status(a, p0);
         atomicAdd(&s_cnt[status_counter(a, p0, st)], 1u);
         if (slot != kNoSlot) {
@@ -3989,7 +3997,7 @@ __global__ __launch_bounds__(kAesBlock) void k_unprotect_fix(BundleArgs a) {
             if (ks->kind == SRTP_KIND_RTP) {
                 real.off = rtp_header_len(pkt, hdr.x & 0xffu, (int)a.cap[p]);
                 real.end = mac ? (jL0 - T > 0 ? jL0 - T : 0) : jL0;
-                make_iv_rtp(ks, hdr, a.g0[p], spec.iv);
+                make_iv_rtp(ks, hdr, a.gok[2 * (size_t)(p)], spec.iv);
                 make_iv_rtp(ks, hdr, a.w_cw[p], real.iv);
             } else {
                 real.off = 8;
@@ -4490,7 +4498,7 @@ __global__ __launch_bounds__(kSkeinBlock) void k_skein(BundleArgs a) {
         if (a.reverse) {
             if (rtp) {
                 end = L - T > 0 ? L - T : 0;
-                suffix = a.g0[p];
+                suffix = a.gok[2 * (size_t)(p)];
             } else {
                 end = L - 4 - T;
                 if (end < 0) return; // the reference throws here (k_walk)
@@ -4512,7 +4520,7 @@ __global__ __launch_bounds__(kSkeinBlock) void k_skein(BundleArgs a) {
         }
         uint32_t tag[5];
         skein_mac<true>(a.skkeys + ks_u, pkt, end, suffix, tag);
-        if (a.reverse) a.auth_ok[p] = tag_matches(tag, pkt + tag_at, T) ? 1u : 0u;
+        if (a.reverse) a.gok[2 * (size_t)(p) + 1] = tag_matches(tag, pkt + tag_at, T) ? 1u : 0u;
         else tag_write(tag, pkt + tag_at, T);
     });
 }
@@ -4712,7 +4720,7 @@ __device__ __forceinline__ bool ctr_small_job(const BundleArgs &a, uint32_t p, i
     const uint32_t slot = a.p_slot[p];
     const uint32_t o = a.off[p], cap = a.cap[p];
     const uint32_t L = a.reverse ? a.len[p] : a.w_len[p];
-    const uint32_t cw = a.reverse ? a.g0[p] : a.w_cw[p];
+    const uint32_t cw = a.reverse ? a.gok[2 * (size_t)(p)] : a.w_cw[p];
     const uint32_t sp = a.reverse ? a.spec[p] : 0u;
     if (slot == kNoSlot) return false;
     if (a.reverse && !(sp & kSpecDid)) return false; // k_unprotect did not speculate
