@@ -226,6 +226,13 @@ int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
  * stall fix-up (srtp_stats.chain_stalls) that a tile preempted for seconds
  * would take.  Results must not change. */
 #define SRTP_DEBUG_FORCE_CHAIN_STALL 0x1u
+/* SRTP_DEBUG_FORCE_WIDE runs bundles of every size on the split path (the
+ * cipher and the MAC as two kernels, which bundles of 2048-65536 packets take
+ * when every key set is AES-CM or NULL cipher with HMAC-SHA1), so that every
+ * parity case exercises it; SRTP_DEBUG_NO_WIDE keeps every bundle off it
+ * (A/B measurements).  Results must not change. */
+#define SRTP_DEBUG_FORCE_WIDE 0x2u
+#define SRTP_DEBUG_NO_WIDE 0x4u
 int srtp_engine_set_debug(srtp_engine *e, uint32_t flags);
 
 /* Context-state export / import: lets a stream's ROC, s_l,
@@ -645,12 +652,16 @@ int srtp_rawpacket_transform(srtp_rawpacket_batch *b, int32_t reverse, const int
                              uint32_t *need_len, uint32_t n, int32_t *thrown);
 int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **data, uint32_t *len);
 /* Arrays of up to 8192 packets none of which can throw (srtp_packet_may_throw)
- * then go through a completion queue of the batch on aggregator a -- whose
- * lanes must be over the batch's engine or dispatcher -- instead of a bundle
- * of their own: concurrent callers' arrays share bundles, and no caller waits
- * behind another's GPU round trip.  The results are the same (no packet can
- * throw, so abort-on-throw has nothing to stop); other arrays keep the batch's
- * own bundle.  a = NULL turns this off. */
+ * then go through a completion queue on aggregator a -- whose lanes must be
+ * over the batch's engine or dispatcher -- instead of a bundle of their own:
+ * concurrent callers' arrays share bundles, and no caller waits behind
+ * another's GPU round trip.  The results are the same (no packet can throw, so
+ * abort-on-throw has nothing to stop); other arrays keep the batch's own
+ * bundle.  The queue lives for one srtp_rawpacket_transform call, so a batch
+ * holds nothing on the aggregator between calls (srtp_aggregator_destroy
+ * waits only for calls in progress).  If the call fails part-way, the elements
+ * that did not complete get SRTP_STATUS_ERR_INTERNAL and are left untouched.
+ * a = NULL turns this off. */
 int srtp_rawpacket_batch_set_aggregator(srtp_rawpacket_batch *b, srtp_aggregator *a);
 /* One RawPacket through SinglePacketTransformer.transform / reverseTransform
  * (RawPacket) (SinglePacketTransformer.java:113,169; every

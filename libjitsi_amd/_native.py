@@ -26,6 +26,8 @@ STATUS_NAMES = ["OK", "DROP_REPLAY", "DROP_AUTH", "DROP_VERSION", "DROP_NO_CONTE
                 "ERR_INTERNAL"]
 NUM_STATUS = len(STATUS_NAMES)
 DEBUG_FORCE_CHAIN_STALL = 0x1
+DEBUG_FORCE_WIDE = 0x2  # every bundle on the split path (k_ctr_wide + k_mac_wide)
+DEBUG_NO_WIDE = 0x4     # every bundle on the fused kernels
 ABI_VERSION = 3
 AGG_SEAL_IDLE = 0x1
 PKT_FLAG_DISCARD, PKT_FLAG_SILENCE, PKT_FLAG_SKIP = 0x2, 0x4, 0x80000000

@@ -35,6 +35,7 @@ struct srtp_engine {
     SkeinKeys *d_skkeys = nullptr;   // 1 per key set, allocated with the first Skein factory
     uint32_t n_ext = 0;           // k_ext key sets created (F8, AES-256, Twofish, Skein): k_ext runs only when > 0
     uint32_t n_skein = 0;         // Skein-MAC key sets created: k_skein runs only when > 0
+    uint32_t n_not_wide = 0;      // key sets the split path cannot run (not AES-CM / NULL cipher + HMAC-SHA1)
     uint32_t n_keysets = 0, max_keysets = 0;
     FactoryRec *d_factories = nullptr;
     std::vector<FactoryRec> factories;
@@ -108,6 +109,11 @@ struct srtp_engine {
 
 namespace {
 constexpr uint32_t kSmallCtrMax = 8192u; // k_ctr_small takes bundles up to this size
+// The split path (k_ctr_wide + k_mac_wide) for bundles of kWideMin..kWideMax
+// packets: there the fused kernels' lane per packet leaves most CUs idle or
+// latency-bound; from 2^17 packets on the fused kernels are faster
+// (profiles/r06/kernel_experiments.md, bundle-size sweep)
+constexpr uint32_t kWideMin = 2048u, kWideMax = 65536u;
 
 int fail(srtp_engine *e, int code, const std::string &msg) {
     if (e) e->last_error = msg;
@@ -591,6 +597,10 @@ int srtp_factory_create(srtp_engine *e, int32_t sender, const uint8_t *mk, int32
     HIPCHK(e, hipMemcpy(e->d_keysets + e->n_keysets, ks, sizeof ks, hipMemcpyHostToDevice));
     HIPCHK(e, hipMemcpy(e->d_extkeys + e->n_keysets, f8, sizeof f8, hipMemcpyHostToDevice));
     e->n_ext += (uint32_t)(ks[0].ext + ks[1].ext);
+    for (const KeySet &k : ks)
+        e->n_not_wide += (k.ext || k.auth_type != SRTP_HMACSHA1_AUTHENTICATION ||
+                          (k.enc_type != SRTP_AESCM_ENCRYPTION && k.enc_type != SRTP_NULL_ENCRYPTION))
+                             ? 1u : 0u;
     memset(ks, 0, sizeof ks);
     memset(f8, 0, sizeof f8);
     FactoryRec f;
@@ -724,7 +734,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     a.check_replay = e->opts.check_replay;
     a.abort_on_error = abort < 0 ? e->opts.abort_on_error : (abort ? 1 : 0);
     a.serial = e->serial++;
-    a.dbg = e->dbg;
+    a.dbg = e->dbg & SRTP_DEBUG_FORCE_CHAIN_STALL; // the kernels' hook (kDbgForceStall)
     a.counters = e->d_counters;
 #ifdef SRTP_STAMPS
     if (!e->d_stamps[reverse ? 1 : 0])
@@ -762,7 +772,12 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     // a small bundle's AES-CM keystream by k_ctr_small (a lane per counter-block
     // pair; the fused kernels only MAC): up to 8192 packets (128 waves: under
     // one wave per SIMD; profiles/r04/kernel_experiments.md 9)
-    a.small_ctr = n <= kSmallCtrMax ? 1 : 0;
+    // Mid-size bundles of engines whose key sets are all AES-CM / NULL cipher +
+    // HMAC-SHA1 take the split path (k_ctr_wide + k_mac_wide, srtp_kernels.hip),
+    // the rest the fused kernels (with k_ctr_small up to kSmallCtrMax packets).
+    const bool wide_ok = e->n_not_wide == 0 && !(e->dbg & SRTP_DEBUG_NO_WIDE);
+    const bool split = wide_ok && ((n >= kWideMin && n <= kWideMax) || (e->dbg & SRTP_DEBUG_FORCE_WIDE));
+    a.small_ctr = split ? 2 : n <= kSmallCtrMax ? 1 : 0;
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;
     a.ctl = e->ctl + c;
@@ -791,7 +806,10 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         StageTimer t(e, s, SRTP_STAGE_SORT);
         HIPCHK(e, one_tile ? launch_sort_tile(a, s) : launch_sort(a, ss, s));
     }
-    if (a.reverse) {
+    if (a.reverse && a.small_ctr == 2) {
+        StageTimer t(e, s, SRTP_STAGE_VERIFY);
+        HIPCHK(e, launch_mac_wide(a, s)); // tag check under the ROC guess, no decryption yet
+    } else if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_VERIFY);
         HIPCHK(e, launch_unprotect(a, s));
         if (a.small_ctr) HIPCHK(e, launch_ctr_small(a, s)); // the speculative decryption
@@ -807,7 +825,14 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         // without abort-on-throw saves the launch
         if (a.abort_on_error || n >= kLongMin || a.dbg) HIPCHK(e, launch_walk(a, 1, s));
     }
-    if (a.reverse) {
+    if (a.reverse && a.small_ctr == 2) {
+        StageTimer t(e, s, SRTP_STAGE_DECRYPT);
+        HIPCHK(e, launch_ctr_wide(a, s)); // final statuses, decryption under the walk's ROC
+    } else if (a.small_ctr == 2) {
+        StageTimer t(e, s, SRTP_STAGE_PROTECT);
+        HIPCHK(e, launch_ctr_wide(a, s)); // the keystream, then the MAC and trailer
+        HIPCHK(e, launch_mac_wide(a, s));
+    } else if (a.reverse) {
         StageTimer t(e, s, SRTP_STAGE_DECRYPT);
         HIPCHK(e, launch_unprotect_fix(a, s));
         if (e->n_ext) HIPCHK(e, launch_ext(a, s));
@@ -1137,7 +1162,8 @@ int32_t srtp_device_count(void) {
 }
 
 int srtp_engine_set_debug(srtp_engine *e, uint32_t flags) {
-    if (!e || (flags & ~SRTP_DEBUG_FORCE_CHAIN_STALL)) return SRTP_EINVAL;
+    if (!e || (flags & ~(SRTP_DEBUG_FORCE_CHAIN_STALL | SRTP_DEBUG_FORCE_WIDE | SRTP_DEBUG_NO_WIDE)))
+        return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
     e->dbg = flags;
     return SRTP_OK;

@@ -43,7 +43,6 @@ struct srtp_rawpacket_batch {
     // srtp_rawpacket_batch_set_aggregator: small arrays that cannot throw go
     // through this queue on the aggregator's lanes (shared bundles)
     srtp_aggregator *agg = nullptr;
-    srtp_queue *q = nullptr;
     std::vector<srtp_completion> comps;
     bool via_queue = false;               // the last call took the queue
     std::vector<const uint8_t *> res_ptr; // its results (srtp_rawpacket_result)
@@ -232,14 +231,24 @@ int transform_via_queue(srtp_rawpacket_batch *b, int32_t reverse, const int32_t 
         const uint32_t cap = std::min(avail, element_cap(reverse, avail, length[i]));
         if (srtp_packet_may_throw(kind, reverse, bufs[i] + offset[i], length[i], cap, fl, kTagsAny)) return 1;
     }
-    if (!b->q) {
-        const int rc = srtp_queue_create(b->agg, kQueueArray, &b->q);
+    // The queue lives for this call only: a queue outliving it would hold the
+    // aggregator (srtp_aggregator_destroy waits for every queue), and the
+    // batch belongs to a thread that may outlive the aggregator's owner.
+    srtp_queue *q = nullptr;
+    {
+        const int rc = srtp_queue_create(b->agg, kQueueArray, &q);
         if (rc != SRTP_OK) return rc;
     }
+    struct QueueOf { // destroyed on every return below (after what was queued completed)
+        srtp_queue *q;
+        ~QueueOf() { srtp_queue_destroy(q); }
+    } q_guard{q};
+    std::vector<uint8_t> completed;
     try {
         b->comps.resize(kQueueArray);
         b->res_ptr.assign(n, nullptr);
         b->res_len.assign(n, 0u);
+        completed.assign(n, 0u);
     } catch (...) {
         return SRTP_ENOMEM;
     }
@@ -248,7 +257,7 @@ int transform_via_queue(srtp_rawpacket_batch *b, int32_t reverse, const int32_t 
     uint32_t done = 0;
     int err = SRTP_OK;
     auto reap = [&](int32_t wait) {
-        const int k = srtp_queue_reap(b->q, b->comps.data(), kQueueArray, wait);
+        const int k = srtp_queue_reap(q, b->comps.data(), kQueueArray, wait);
         if (k < 0) return k;
         for (int j = 0; j < k; j++) {
             const srtp_completion &c = b->comps[(size_t)j];
@@ -256,6 +265,7 @@ int transform_via_queue(srtp_rawpacket_batch *b, int32_t reverse, const int32_t 
             const int32_t st = c.status < 0 ? SRTP_STATUS_ERR_INTERNAL : c.status;
             status[i] = st;
             need_len[i] = 0;
+            completed[i] = 1u;
             done++;
             if (!bufs[i] || st == SRTP_STATUS_SKIPPED || st == SRTP_STATUS_NOT_PROCESSED) continue;
             const uint32_t avail = offset[i] <= buf_len[i] ? buf_len[i] - offset[i] : 0u;
@@ -281,34 +291,50 @@ int transform_via_queue(srtp_rawpacket_batch *b, int32_t reverse, const int32_t 
             if (c.data) length[i] = c.len;
             if (st == SRTP_STATUS_ERR_MALFORMED && (*thrown < 0 || (int32_t)i < *thrown)) *thrown = (int32_t)i;
         }
-        srtp_queue_release(b->q); // written back: the slots go back at once
+        srtp_queue_release(q); // written back: the slots go back at once
         return SRTP_OK;
     };
+    // the results of the elements that completed stay readable
+    // (srtp_rawpacket_result); the others are left untouched with
+    // SRTP_STATUS_ERR_INTERNAL, as the dispatcher leaves chunks never submitted
+    auto finish = [&](int rc) {
+        for (uint32_t i = 0; i < n; i++) {
+            if (need_len[i] && completed[i]) b->res_ptr[i] = b->grown.data() + grown_at[i];
+            if (!completed[i]) {
+                status[i] = SRTP_STATUS_ERR_INTERNAL;
+                need_len[i] = 0;
+            }
+        }
+        b->via_queue = true;
+        b->n = n;
+        return rc;
+    };
+    for (uint32_t i = 0; i < n; i++) need_len[i] = 0;
     for (uint32_t i = 0; i < n; i++) {
         for (;;) {
             int rc2;
-            const int rc = submit_element(b->q, reverse, tids ? tids[i] : tid, bufs[i], buf_len[i], offset[i],
+            const int rc = submit_element(q, reverse, tids ? tids[i] : tid, bufs[i], buf_len[i], offset[i],
                                           length[i], flags ? flags[i] : 0u, i);
             if (rc == SRTP_OK) break;
             if (rc == SRTP_EAGAIN) rc2 = reap(1);
             else rc2 = rc; // nothing of this element was queued
             if (rc2 != SRTP_OK) {
                 // what was queued completes (written back) before the error returns
-                while (srtp_queue_outstanding(b->q) > 0 && reap(1) == SRTP_OK) {
+                while (srtp_queue_outstanding(q) > 0 && reap(1) == SRTP_OK) {
                 }
-                return rc2;
+                return finish(rc2);
             }
         }
     }
     while (done < n) {
         const int rc = reap(1);
-        if (rc != SRTP_OK) return rc;
+        if (rc != SRTP_OK) {
+            while (srtp_queue_outstanding(q) > 0 && reap(1) == SRTP_OK) {
+            }
+            return finish(rc);
+        }
     }
-    for (uint32_t i = 0; i < n; i++)
-        if (need_len[i]) b->res_ptr[i] = b->grown.data() + grown_at[i];
-    b->via_queue = true;
-    b->n = n;
-    return err;
+    return finish(err);
 }
 
 } // namespace
@@ -335,7 +361,6 @@ int srtp_rawpacket_batch_create_dispatch(srtp_dispatch *d, srtp_rawpacket_batch 
 
 void srtp_rawpacket_batch_destroy(srtp_rawpacket_batch *b) {
     if (!b) return;
-    if (b->q) srtp_queue_destroy(b->q);
     if (b->pl) srtp_pipeline_destroy(b->pl);
     release_seg(b);
     delete b;
@@ -479,11 +504,7 @@ int srtp_rawpacket_result(srtp_rawpacket_batch *b, uint32_t i, const uint8_t **d
 
 int srtp_rawpacket_batch_set_aggregator(srtp_rawpacket_batch *b, srtp_aggregator *a) {
     if (!b) return SRTP_EINVAL;
-    if (b->q) {
-        srtp_queue_destroy(b->q);
-        b->q = nullptr;
-    }
-    b->agg = a;
+    b->agg = a; // (the queue path makes a queue per call on it)
     return SRTP_OK;
 }
 

@@ -87,7 +87,7 @@ struct BundleArgs {
     uint32_t sort_zero_words;
     // a small bundle: the AES-CM keystream of the AES-CM + HMAC-SHA1 packets is
     // applied by k_ctr_small (a lane per counter-block pair), the fused
-    // kernels only MAC those packets
+    // kernels only MAC those packets; 2: the split path (k_ctr_wide + k_mac_wide)
     int32_t small_ctr;
 };
 
@@ -127,6 +127,12 @@ hipError_t launch_protect(const BundleArgs &a, hipStream_t s);
 // BundleArgs::small_ctr: the keystream of the AES-CM + HMAC-SHA1 packets, one
 // workgroup per packet -- protect before k_protect, unprotect after k_unprotect
 hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s);
+// The split path (BundleArgs::small_ctr == 2): the AES-CM keystream of a
+// bundle, lane per counter-block pair (protect: before k_mac_wide; unprotect:
+// after the walk, with the final statuses), and the HMAC-SHA1 (protect: MAC,
+// trailer and final statuses; unprotect: the tag check before the walk)
+hipError_t launch_ctr_wide(const BundleArgs &a, hipStream_t s);
+hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s);
 // unprotect: statuses/lengths out; undo/redo the rare speculation misses (after the walk)
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 // AES-F8 packets after the final statuses: protect (F8 + HMAC + trailer) or

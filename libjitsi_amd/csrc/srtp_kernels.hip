@@ -4830,6 +4830,400 @@ hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ====================================================== the split path (wide)
+// A bundle larger than k_ctr_small's (BundleArgs::small_ctr == 2, engines whose
+// key sets are all AES-CM or NULL cipher with HMAC-SHA1) runs the cipher and
+// the MAC as two kernels with nothing in common but the packet bytes:
+//   protect:   walk -> k_ctr_wide (keystream)  -> k_mac_wide (MAC, trailer, statuses)
+//   unprotect: k_mac_wide (tag check, ROC guess, re-check state) -> walk
+//              -> k_ctr_wide (final statuses, decryption of the accepted packets)
+// The MAC is over the ciphertext (SRTPCryptoContext.java:237-266 checks it
+// before processPacketAESCM :609-627 deciphers), so unprotect deciphers after
+// the walk with the walk's ROC: no speculation, nothing to repair.  Neither
+// kernel holds AES and SHA-1 state at once: k_ctr_wide is the 128-KB T-table
+// image and few registers (LDS-bound), k_mac_wide no LDS and few registers
+// (VALU-bound), so one direction's k_mac_wide fills the register file beside
+// the other direction's k_ctr_wide on the same CUs.
+//
+// k_ctr_wide: every wave on its own, over groups of G consecutive packets
+// taken from a ticket counter.  The group's first G lanes work out its packet
+// jobs (region, counter precompute, key set; unprotect: the final statuses)
+// into the wave's LDS slot; then the group's counter-block pairs go to the
+// lanes 64 at a time, consecutive pairs to consecutive lanes, so a wave's
+// loads and stores cover 2 KB of one packet's payload contiguously (the fused
+// kernels' lane-per-packet pattern touches 64 packets per instruction).  No
+// workgroup barrier after the T-table fill: a wave waiting on its next jobs'
+// loads leaves the LDS to the other fifteen.  The workgroup's LDS is the
+// 128-KB image plus 9 KB, so that the other direction's sort and walk still
+// fit beside it on the CU.
+constexpr int kWideBlock = 1024;
+constexpr int kWideGMax = 16;                        // packets per group
+constexpr int kWideWaveWords = 8 * kWideGMax + 20;   // jobs [G][8], prefix [G + 1] (16-B aligned slot)
+constexpr int kWideOffWave = kTeWords;               // the image stays at LDS 0
+constexpr int kWideWords = kWideOffWave + (kWideBlock / 64) * kWideWaveWords;
+
+// Unprotect's job for packet p: its final status (k_unprotect_fix's, which
+// this path does not run) and, for an accepted AES-CM packet, the region and
+// IV under the walk's ROC / SRTCP index (processPacketAESCM :482-525,
+// SRTCPCryptoContext :218-260).
+__device__ __forceinline__ bool wide_job_rev(const BundleArgs &a, uint32_t p, uint32_t *s_cnt, int &start,
+                                             int &end, uint32_t iv[4], const KeySet *&ks) {
+    // every per-packet word first (finish_status stores after its loads)
+    const int L0 = (int)a.len[p];
+    const uint32_t slot = a.p_slot[p];
+    const uint32_t sw = a.spec[p];
+    const uint32_t cw = a.w_cw[p];
+    const uint32_t o = a.off[p], cap = a.cap[p];
+    const int32_t st = finish_status(a, p);
+    atomicAdd(&s_cnt[status_counter(a, p, st)], 1u);
+    if (slot == kNoSlot || st != SRTP_STATUS_OK || !(sw & kSpecAes)) return false;
+    const bool rtp = (sw & kSpecRtp) != 0u;
+    if (rtp ? (sw & kSpecSkip) != 0u : !(cw & 0x80000000u)) return false; // DISCARD/SILENCE; SRTCP E clear
+    ks = a.keysets + a.ctx[slot].ks;
+    const uint8_t *pkt = a.seg + o;
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    const int T = ks->tag_len;
+    const bool mac = ks->auth_type != SRTP_NULL_AUTHENTICATION;
+    if (rtp) {
+        start = rtp_header_len(pkt, hdr.x & 0xffu, (int)cap);
+        end = mac ? max(L0 - T, 0) : L0;
+        make_iv_rtp(ks, hdr, cw, iv);
+    } else {
+        start = 8;
+        end = mac ? max(L0 - T - 4, 0) : L0;
+        make_iv_rtcp(ks, hdr, cw & 0x7FFFFFFFu, iv);
+    }
+    if (start < 0 || start > end) start = end;
+    return end > start;
+}
+
+// XOR keystream blocks x, y over the `rem` (>= 1) bytes at q (4-B aligned):
+// whole pairs with two 16-B loads and stores, the packet's last pair word-
+// masked (bytes past the region XORed with zero: this lane alone touches them)
+__device__ __forceinline__ void wide_xor(uint8_t *q, int rem, const uint32_t x[4], const uint32_t y[4]) {
+    if (rem >= 32) {
+        uint4 *w = reinterpret_cast<uint4 *>(q);
+        uint4 u = w[0], v = w[1];
+        u.x ^= x[0]; u.y ^= x[1]; u.z ^= x[2]; u.w ^= x[3];
+        v.x ^= y[0]; v.y ^= y[1]; v.z ^= y[2]; v.w ^= y[3];
+        w[0] = u;
+        w[1] = v;
+    } else {
+        xor_ks32(q, 0, rem, x, y);
+    }
+}
+
+// k_ctr_jobs: each packet's keystream job, one lane per packet (all their
+// dependent loads in flight at once across the grid), into the packet's tailc
+// scratch, which the split path does not otherwise use: {IV}, {first byte of
+// the region in the segment, region length, key set, 0} (length 0: none).
+// Unprotect: also every packet's final status and length.
+constexpr int kJobBlock = 256;
+template <bool REV>
+__global__ __launch_bounds__(kJobBlock) void k_ctr_jobs(BundleArgs a) {
+    __shared__ uint32_t s_cnt[kTeCounters];
+    if (REV) {
+        if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+        __syncthreads();
+    }
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < a.n) {
+        int start = 0, end = 0;
+        uint32_t iv[4] = {0u, 0u, 0u, 0u};
+        const KeySet *ks = nullptr;
+        const bool ok = REV ? wide_job_rev(a, p, s_cnt, start, end, iv, ks) : ctr_small_job(a, p, start, end, iv, ks);
+        uint4 *jp = reinterpret_cast<uint4 *>(a.tailc + 16 * (size_t)p);
+        jp[0] = make_uint4(iv[0], iv[1], iv[2], iv[3]);
+        jp[1] = ok ? make_uint4(a.off[p] + (uint32_t)start, (uint32_t)(end - start), (uint32_t)(ks - a.keysets), 0u)
+                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (REV) {
+        __syncthreads();
+        flush_status_counts(a, s_cnt);
+    }
+}
+
+// k_ctr_wide: wave w of W takes the groups of G consecutive packets w, w + W,
+// ... (no ticket: one counter on one address serialised 16k atomics).  The
+// group's first G lanes load its jobs (fetched one group ahead), make the
+// counter precompute and put {CtrPre, first byte, kb | length << 8, packet}
+// in the wave's LDS slot with the pair prefix; then the pairs.
+template <bool REV>
+__global__ __launch_bounds__(kWideBlock) void k_ctr_wide(BundleArgs a, uint32_t G) {
+    __shared__ uint32_t s[kWideWords];
+    fill_te4(s); // ends with a barrier
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s);
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t *ws = s + kWideOffWave + (int)(threadIdx.x >> 6) * kWideWaveWords;
+    uint32_t *pre = ws + 8 * kWideGMax;
+    const uint32_t n_groups = (a.n + G - 1u) / G;
+    const uint32_t W = gridDim.x * (kWideBlock / 64);
+    uint32_t top = 1u; // binary-search span: the largest power of two <= G
+    while (2u * top <= G) top <<= 1;
+    const uint4 *J = reinterpret_cast<const uint4 *>(a.tailc);
+    uint32_t grp = blockIdx.x * (kWideBlock / 64) + (threadIdx.x >> 6);
+    uint4 nj0 = make_uint4(0u, 0u, 0u, 0u), nj1 = nj0;
+    if (grp < n_groups && (uint32_t)lane < min(G, a.n - grp * G)) {
+        const size_t p = (size_t)grp * G + (uint32_t)lane;
+        nj0 = J[4 * p];
+        nj1 = J[4 * p + 1];
+    }
+#pragma unroll 1
+    for (; grp < n_groups; grp += W) {
+        const uint32_t first = grp * G;
+        const uint32_t cnt = min(G, a.n - first);
+        const uint4 cj0 = nj0, cj1 = nj1;
+        const uint32_t nx = grp + W; // the next group's jobs, landing during this one
+        if (nx < n_groups && (uint32_t)lane < min(G, a.n - nx * G)) {
+            const size_t p = (size_t)nx * G + (uint32_t)lane;
+            nj0 = J[4 * p];
+            nj1 = J[4 * p + 1];
+        }
+        const bool has = (uint32_t)lane < cnt && cj1.y != 0u;
+        const unsigned long long m = __ballot(has);
+        if (m == 0ull) continue;
+        const uint32_t ks0 = (uint32_t)__builtin_amdgcn_readlane((int)cj1.z, __ffsll((long long)m) - 1);
+        const bool uni = __ballot(has && cj1.z != ks0) == 0ull;
+        RoundKeys rk;
+        if (uni) load_round_keys_uniform(a.keysets + ks0, rk);
+        const uint32_t np = has ? (((cj1.y + 15u) >> 4) + 1u) >> 1 : 0u;
+        if (has) {
+            const uint32_t iv[4] = {cj0.x, cj0.y, cj0.z, cj0.w};
+            CtrPre cp;
+            if (uni) {
+                ctr_precompute(lds, tb, rk.k, iv, cp);
+            } else {
+                uint32_t r12[12];
+                const uint4 *q = reinterpret_cast<const uint4 *>(a.keysets[cj1.z].rk);
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    const uint4 v = q[i];
+                    r12[4 * i] = v.x; r12[4 * i + 1] = v.y; r12[4 * i + 2] = v.z; r12[4 * i + 3] = v.w;
+                }
+                ctr_precompute(lds, tb, r12, iv, cp);
+            }
+            uint4 *jp = reinterpret_cast<uint4 *>(ws + 8 * lane);
+            jp[0] = make_uint4(cp.p0, cp.r[0], cp.r[1], cp.r[2]);
+            jp[1] = make_uint4(cp.r[3], cj1.x, cp.kb | (cj1.y << 8), first + (uint32_t)lane);
+        }
+        uint32_t incl = np; // inclusive prefix of the pair counts over the group's lanes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += t;
+        }
+        if ((uint32_t)lane < cnt) pre[lane] = incl - np;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)incl, 63));
+        // the slot was written by this wave's lanes: LDS ops of a wave complete in order
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 1
+        for (uint32_t c0 = 0; c0 < total; c0 += 64u) {
+            const uint32_t g = c0 + (uint32_t)lane;
+            const bool act = g < total;
+            // the packet of pair g: the last q with pre[q] <= g (packets
+            // without pairs share their successor's prefix and are skipped)
+            uint32_t q = 0u;
+            for (uint32_t st = top; st; st >>= 1)
+                if (q + st < cnt && pre[q + st] <= g) q += st;
+            const uint4 *jp = reinterpret_cast<const uint4 *>(ws + 8 * q);
+            const uint4 j0w = jp[0], j1w = jp[1];
+            CtrPre cp;
+            cp.p0 = j0w.x; cp.r[0] = j0w.y; cp.r[1] = j0w.z; cp.r[2] = j0w.w;
+            cp.r[3] = j1w.x; cp.kb = j1w.z & 0xffu;
+            const int j = act ? 2 * (int)(g - pre[q]) : 0;
+            const size_t pj = act ? j1w.w : first; // an idle lane's q may be a stale slot
+            uint32_t x[4], y[4];
+            const bool far = __ballot(act && j + 1 >= 256) != 0ull; // IV byte 14 set: full rounds
+            if (uni) {
+                if (!far) {
+                    ctr_first2(lds, tb, cp, j, j + 1, x, y);
+#pragma unroll
+                    for (int r = 3; r < 10; r++) aes_round2(lds, tb, rk.k + 4 * r, x, y);
+                    aes_last2(lds, tb, rk.k + 40, x, y);
+                } else {
+                    const uint4 ivw = J[4 * pj];
+                    const uint32_t iv[4] = {ivw.x, ivw.y, ivw.z, ivw.w};
+                    ctr_input(iv, j, x);
+                    ctr_input(iv, j + 1, y);
+                    aes_encrypt2(lds, tb, rk, x, y);
+                }
+            } else { // several key sets in the group: each lane on its own schedule
+                const uint4 *kq = reinterpret_cast<const uint4 *>(a.keysets[J[4 * pj + 1].z].rk);
+                if (!far) {
+                    const uint4 k2 = kq[2];
+                    ctr_first2(lds, tb, cp, j, j + 1, x, y);
+                    uint32_t kk[4] = {k2.x, k2.y, k2.z, k2.w};
+#pragma unroll
+                    for (int r = 3; r < 10; r++) {
+                        key_next(lds, tb, kk, kRcon[r]);
+                        aes_round2_asm_v(x, y, tb.b, kk);
+                    }
+                    key_next(lds, tb, kk, kRcon[10]);
+                    aes_last2_asm_v(x, y, tb.b, kk);
+                } else {
+                    const uint4 k0 = kq[0], ivw = J[4 * pj];
+                    const uint32_t iv[4] = {ivw.x, ivw.y, ivw.z, ivw.w};
+                    const uint32_t kk[4] = {k0.x, k0.y, k0.z, k0.w};
+                    ctr_input(iv, j, x);
+                    ctr_input(iv, j + 1, y);
+                    aes_encrypt2_v(lds, tb, kk, x, y);
+                }
+            }
+            if (act) wide_xor(a.seg + j1w.y + 16u * (uint32_t)j, (int)(j1w.z >> 8) - 16 * j, x, y);
+        }
+        // the slot is rewritten by the next group's lanes only after every
+        // lane's reads above (the wave's LDS ops complete in order)
+    }
+}
+
+// k_mac_wide: the HMAC-SHA1 of the split path, one lane per packet (lanes in
+// length-class order), no LDS but the status counts, one block of look-ahead
+// (other waves hide the rest at this occupancy).  Protect (after k_ctr_wide):
+// final status, the MAC over the ciphertext and the trailer, as k_protect's
+// MacOnly instance (authenticatePacketHMAC :269-278, RawPacket.append
+// :203-220).  Unprotect (before the walk): as k_unprotect's MacOnly instance
+// without speculation -- the ROC guess, the tag check under it, the walk's
+// re-check midstate.
+constexpr int kMacWideBlock = 256;
+
+__device__ __forceinline__ void mac_stream(const uint8_t *pkt, int end, uint32_t suffix, const KeySet *ks,
+                                           uint32_t h[5], uint32_t *mid_out, int mid_b) {
+    const int nb_data = (end + 63) >> 6;
+    const int nb_inner = ((end + 12) >> 6) + 1;
+    const int n_blocks = nb_inner + 1;
+    uint32_t nx[16];
+    load_or_zero16(pkt, 0, nb_data, end, nx);
+#pragma unroll 1
+    for (int b = 0; b < n_blocks; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++) w[m] = nx[m];
+        load_or_zero16(pkt, b + 1, nb_data, end, nx);
+        asm volatile("" ::: "memory"); // keep the look-ahead (see MacRing::next)
+        if (b == mid_b && mid_out) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) mid_out[k] = h[k];
+        }
+        if (b < nb_inner) inner_words(w, b, end, suffix);
+        else outer_words<false>(w, h, ks);
+        sha1_compress(h, w);
+    }
+}
+
+template <bool REV>
+__global__ __launch_bounds__(kMacWideBlock) void k_mac_wide(BundleArgs a) {
+    __shared__ uint32_t s_cnt[kTeCounters];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < a.n;
+    const uint32_t p = live ? lane_packet(a, i) : i;
+    if (!REV) {
+        if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+        __syncthreads();
+        int32_t fs = -1;
+        if (live) {
+            fs = finish_status(a, p);
+            atomicAdd(&s_cnt[status_counter(a, p, fs)], 1u);
+        }
+        __syncthreads();
+        flush_status_counts(a, s_cnt);
+        if (fs != SRTP_STATUS_OK) return;
+        const KeySet *ks = a.keysets + a.ctx[a.p_slot[p]].ks;
+        uint8_t *pkt = a.seg + a.off[p];
+        const bool rtcp = ks->kind == SRTP_KIND_RTCP;
+        const int T = ks->tag_len;
+        const int L = (int)a.w_len[p] - T - (rtcp ? 4 : 0);
+        const uint32_t cw = a.w_cw[p];
+        const uint32_t suffix = !rtcp ? cw : (ks->enc_type == SRTP_AESCM_ENCRYPTION ? (cw | 0x80000000u) : 0u);
+        uint32_t h[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) h[k] = ks->ipad[k];
+        mac_stream(pkt, L, suffix, ks, h, nullptr, -1);
+        if ((L & 3) == 0) {
+            trailer_write_aligned(reinterpret_cast<uint32_t *>(pkt + L), rtcp, suffix, h, T);
+        } else {
+            int o = L;
+            if (rtcp) {
+                pkt[o] = (uint8_t)(suffix >> 24); pkt[o + 1] = (uint8_t)(suffix >> 16);
+                pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
+                o += 4;
+            }
+            tag_write(h, pkt + o, T);
+        }
+        return;
+    }
+    // unprotect: k_unprotect's prologue (context state, long-chain guess, quiet)
+    if (!live) return;
+    const uint32_t slot = a.p_slot[p];
+    if (slot == kNoSlot) return;
+    const uint32_t pos = a.spos[p];
+    CtxState st = a.ctx[slot];
+    const uint32_t far = a.far[slot];
+    const bool lng = pos >= kLongRank && a.sk_out[pos - kLongRank] == slot;
+    const bool quiet = !lng && (st.flags & 1u) && far != a.serial + 1u;
+    if (lng) {
+        const uint32_t hh = chain_head(a.sk_out, pos - kLongRank, slot);
+        const int32_t seq_h = (int32_t)(a.sv_out[hh].word & 0xffffu);
+        const int32_t seq = (int32_t)(a.sv_out[pos].word & 0xffffu);
+        const int64_t e = (int64_t)guess_roc(st, seq_h) * 65536 + seq_h + (int64_t)(pos - hh);
+        st.a = (int32_t)((e - seq + 32768) >> 16);
+        st.flags &= ~1u;
+    }
+    const KeySet *ks = a.keysets + st.ks;
+    uint8_t *pkt = a.seg + a.off[p];
+    const int L = (int)a.len[p];
+    const int T = ks->tag_len;
+    const bool rtp = ks->kind == SRTP_KIND_RTP;
+    const bool aes = ks->enc_type == SRTP_AESCM_ENCRYPTION;
+    const uint4 hdr = *reinterpret_cast<const uint4 *>(pkt);
+    int end;
+    uint32_t suffix;
+    if (rtp) {
+        const int32_t seq = (int32_t)(bswap(hdr.x) & 0xffffu);
+        const int32_t g = guess_roc(st, seq);
+        a.gok[2 * (size_t)p] = (uint32_t)g;
+        end = max(L - T, 0);
+        suffix = (uint32_t)g;
+    } else {
+        const int io = L - 4 - T;
+        if (io < 0) { a.spec[p] = 0u; return; } // the walk throws (no decryption due)
+        suffix = ld_be32(pkt + io);
+        end = io;
+    }
+    a.spec[p] = (aes ? kSpecAes : 0u) | (rtp ? kSpecRtp : 0u) |
+                (rtp && a.flags && (a.flags[p] & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ? kSpecSkip : 0u);
+    uint32_t h[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = ks->ipad[k];
+    mac_stream(pkt, end, suffix, ks, h, (rtp && !quiet) ? a.mid + 5 * (size_t)p : nullptr, end >> 6);
+    a.gok[2 * (size_t)p + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
+}
+
+hipError_t launch_ctr_wide(const BundleArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const dim3 jg((a.n + kJobBlock - 1) / kJobBlock);
+    if (a.reverse) hipLaunchKernelGGL(k_ctr_jobs<true>, jg, dim3(kJobBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_ctr_jobs<false>, jg, dim3(kJobBlock), 0, s, a);
+    // groups of 16 packets, fewer for smaller bundles (about four groups per
+    // wave of 256 workgroups x 16 waves)
+    uint32_t G = (uint32_t)kWideGMax;
+    while (G > 1u && (a.n + G - 1u) / G < 4u * 4096u) G >>= 1;
+    const uint32_t groups = (a.n + G - 1u) / G;
+    const uint32_t wgs = (groups + 15u) / 16u;
+    const dim3 grid(wgs < 256u ? wgs : 256u);
+    if (a.reverse) hipLaunchKernelGGL(k_ctr_wide<true>, grid, dim3(kWideBlock), 0, s, a, G);
+    else hipLaunchKernelGGL(k_ctr_wide<false>, grid, dim3(kWideBlock), 0, s, a, G);
+    return hipGetLastError();
+}
+
+hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const dim3 grid((a.n + kMacWideBlock - 1) / kMacWideBlock);
+    if (a.reverse) hipLaunchKernelGGL(k_mac_wide<true>, grid, dim3(kMacWideBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_mac_wide<false>, grid, dim3(kMacWideBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_protect(const BundleArgs &a, hipStream_t s) {
     const uint32_t b = aes_block(a.n, (uint32_t)kProtectBlock);
     if (a.small_ctr) {

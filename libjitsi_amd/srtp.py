@@ -23,6 +23,7 @@ packs RawPackets into one bundle and unpacks the results.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 from typing import List, Optional, Sequence
 
@@ -194,6 +195,11 @@ class SRTPEngine:
         N.check(L.srtp_engine_create(C.byref(o), C.byref(h)), None, "srtp_engine_create")
         self.h = h
         self.device = device
+        # test hook: SRTP_TEST_DEBUG=<flags> puts every engine of a test run on
+        # e.g. the split path (N.DEBUG_FORCE_WIDE) or the fused one (N.DEBUG_NO_WIDE)
+        self._env_debug = int(os.environ.get("SRTP_TEST_DEBUG", "0"), 0)
+        if self._env_debug:
+            self.set_debug(0)
 
     @classmethod
     def default(cls, device: int = 0) -> "SRTPEngine":
@@ -227,7 +233,8 @@ class SRTPEngine:
 
     def set_debug(self, flags: int) -> None:
         """Test hooks (srtp_engine_set_debug), e.g. N.DEBUG_FORCE_CHAIN_STALL."""
-        N.check(N.lib().srtp_engine_set_debug(self.h, int(flags)), self.h, "set_debug")
+        flags = int(flags) | getattr(self, "_env_debug", 0)
+        N.check(N.lib().srtp_engine_set_debug(self.h, flags), self.h, "set_debug")
 
     def read_timing(self) -> dict:
         """{stage: (total ms, bundles)} since the last read (HIP events)."""

@@ -394,7 +394,13 @@ static __thread uint32_t tl_comps_n;
  * of packets in flight -- as SinglePacketTransformer leaves it (in place, or a
  * new buffer where RawPacket.append / grow reallocate; length updated).
  * status[i] receives completion i's SRTP_STATUS_*.  wait: block until at least
- * one is there.  Returns the count or a negative SRTP_E* code. */
+ * one is there.  Returns the count, or a negative SRTP_E* code when nothing was
+ * reaped: once completions are taken off the native queue their count is
+ * always returned (so the Java ring stays in step with the native order), and
+ * a completion that could not be written back -- its native result rejected,
+ * or no memory for its new buffer (the OutOfMemoryError is cleared: the packet
+ * is dropped, as the reference drops what it cannot transform) -- gets
+ * SRTP_STATUS_ERR_INTERNAL, which GpuPacketQueue hands on as null. */
 JNIEXPORT jint JNICALL JFN(queueReap)(JNIEnv *env, jclass c, jlong qh, jobjectArray ring, jintArray status,
                                       jboolean wait) {
     srtp_queue *q = (srtp_queue *)H(qh);
@@ -411,13 +417,17 @@ JNIEXPORT jint JNICALL JFN(queueReap)(JNIEnv *env, jclass c, jlong qh, jobjectAr
     }
     const int n = srtp_queue_reap(q, tl_comps, (uint32_t)max, wait ? 1 : 0);
     if (n <= 0) return n;
-    if ((*env)->PushLocalFrame(env, 2 * n + 16) != 0) return SRTP_ENOMEM;
-    int rc = n;
+    const int framed = (*env)->PushLocalFrame(env, 2 * n + 16) == 0;
+    if (!framed) (*env)->ExceptionClear(env); /* its OutOfMemoryError: the statuses still go back */
     for (int i = 0; i < n; i++) {
         const srtp_completion *cp = &tl_comps[i];
         tl_status[i] = cp->status;
-        jobject pkt = (*env)->GetObjectArrayElement(env, ring, (jsize)(cp->cookie % (uint64_t)rl));
-        if (!pkt) continue;
+        /* without a local frame no write-back is attempted (each makes local refs) */
+        jobject pkt = framed ? (*env)->GetObjectArrayElement(env, ring, (jsize)(cp->cookie % (uint64_t)rl)) : NULL;
+        if (!pkt) {
+            if (!framed) tl_status[i] = SRTP_STATUS_ERR_INTERNAL;
+            continue;
+        }
         jbyteArray arr = (jbyteArray)(*env)->GetObjectField(env, pkt, fid_buffer);
         const uint32_t al = arr ? (uint32_t)(*env)->GetArrayLength(env, arr) : 0u;
         const jint jo = (*env)->GetIntField(env, pkt, fid_offset);
@@ -426,13 +436,14 @@ JNIEXPORT jint JNICALL JFN(queueReap)(JNIEnv *env, jclass c, jlong qh, jobjectAr
         if (avail > 65535u) avail = 65535u;
         uint32_t copy = 0, need = 0;
         if (srtp_rawpacket_complete(q, cp, avail, &copy, &need) != SRTP_OK) {
-            rc = SRTP_EINVAL;
+            tl_status[i] = SRTP_STATUS_ERR_INTERNAL;
             continue;
         }
         if (need) { /* RawPacket.append / grow: a new byte[] at offset 0 */
             jbyteArray nb = (*env)->NewByteArray(env, (jsize)need);
-            if (!nb) {
-                rc = SRTP_ENOMEM;
+            if (!nb) { /* OutOfMemoryError pending: cleared, the packet dropped */
+                (*env)->ExceptionClear(env);
+                tl_status[i] = SRTP_STATUS_ERR_INTERNAL;
                 continue;
             }
             (*env)->SetByteArrayRegion(env, nb, 0, (jsize)copy, (const jbyte *)cp->data);
@@ -446,6 +457,6 @@ JNIEXPORT jint JNICALL JFN(queueReap)(JNIEnv *env, jclass c, jlong qh, jobjectAr
     /* every result is in its Java array: the pinned slots go back at once */
     srtp_queue_release(q);
     (*env)->SetIntArrayRegion(env, status, 0, n, tl_status);
-    (*env)->PopLocalFrame(env, NULL);
-    return rc;
+    if (framed) (*env)->PopLocalFrame(env, NULL);
+    return n;
 }

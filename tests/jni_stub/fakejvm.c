@@ -114,7 +114,17 @@ static jobject PopLocalFrame(JNIEnv *env, jobject r) {
     __atomic_sub_fetch(&g_frames, 1, __ATOMIC_RELAXED);
     return r;
 }
-static jbyteArray NewByteArray(JNIEnv *env, jsize n) { return new_array(K_BYTES, n, 1); }
+/* fj_fail_new_arrays(k): the next k NewByteArray calls fail as a JVM out of
+ * memory does (NULL, an OutOfMemoryError pending until ExceptionClear) */
+static int g_fail_new, g_pending;
+static jbyteArray NewByteArray(JNIEnv *env, jsize n) {
+    if (__atomic_load_n(&g_fail_new, __ATOMIC_SEQ_CST) > 0 && __atomic_fetch_sub(&g_fail_new, 1, __ATOMIC_SEQ_CST) > 0) {
+        __atomic_store_n(&g_pending, 1, __ATOMIC_SEQ_CST);
+        return NULL;
+    }
+    return new_array(K_BYTES, n, 1);
+}
+static void ExceptionClear(JNIEnv *env) { __atomic_store_n(&g_pending, 0, __ATOMIC_SEQ_CST); }
 static jint *GetIntArrayElements(JNIEnv *env, jintArray a, jboolean *is_copy) {
     if (is_copy) *is_copy = 0;
     return a ? (jint *)a->data : NULL;
@@ -128,13 +138,15 @@ static const struct JNINativeInterface_ g_table = {
     GetArrayLength, GetIntArrayRegion, GetByteArrayRegion, SetByteArrayRegion, FindClass,
     GetFieldID, GetObjectField, GetIntField, SetIntField, SetObjectField, GetObjectArrayElement,
     SetObjectArrayElement, PushLocalFrame, PopLocalFrame, NewByteArray, GetIntArrayElements,
-    ReleaseIntArrayElements, SetIntArrayRegion,
+    ReleaseIntArrayElements, SetIntArrayRegion, ExceptionClear,
 };
 static JNIEnv g_env = &g_table;
 
 /* ---- the tests' side (ctypes) ---- */
 
 JNIEXPORT JNIEnv *fj_env(void) { return &g_env; }
+JNIEXPORT void fj_fail_new_arrays(int k) { __atomic_store_n(&g_fail_new, k, __ATOMIC_SEQ_CST); }
+JNIEXPORT int fj_exception_pending(void) { return __atomic_load_n(&g_pending, __ATOMIC_SEQ_CST); }
 JNIEXPORT jobject fj_rawpacket_class(void) { return &g_rawpacket_class; }
 
 JNIEXPORT jbyteArray fj_new_bytes(const void *data, jsize n) {

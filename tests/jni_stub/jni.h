@@ -56,6 +56,7 @@ struct JNINativeInterface_ {
     jint *(*GetIntArrayElements)(JNIEnv *env, jintArray a, jboolean *is_copy);
     void (*ReleaseIntArrayElements)(JNIEnv *env, jintArray a, jint *elems, jint mode);
     void (*SetIntArrayRegion)(JNIEnv *env, jintArray a, jsize start, jsize len, const jint *buf);
+    void (*ExceptionClear)(JNIEnv *env);
 };
 
 #endif

@@ -363,6 +363,38 @@ def test_recheck_state_at_the_seq_range_edges(twin):
                 twin.run(rcv, True, seg, b.off, ln, b.cap)
 
 
+def test_recheck_state_at_the_far_threshold(twin, engine):
+    """k_unprotect saves the walk's re-check state (midstate, ROC block) only
+    for contexts with a packet 16384 or more (linear SEQ distance) from the
+    bundle-start s_l (k_parse's far stamp).  Bundles at exactly
+    16383 / 16384, s_l near 0 and near 65535 (circularly close, linearly far),
+    a ROC rollover inside one bundle, and a far packet whose ROC the walk
+    guesses differently from the verify pass (the re-check really runs:
+    srtp_stats.roc_rechecks) -- every one as the oracle's."""
+    (k, s), = synth.keys(35, 1)
+    fs, fr = twin.factory(True, k, s, *P80), twin.factory(False, k, s, *P80)
+    cases = [
+        (100, [100 + 16383, 101, 102], False),           # within 16383: quiet, no state saved
+        (100, [100 + 16384, 101], False),                 # exactly 16384: far
+        (16383, [0, 16383 + 16383, 16384], False),        # 0 lies 16383 below s_l: quiet
+        (65530, [65535, 0, 1, 2, 65534], False),          # rollover in the bundle (0 is 65530 away)
+        (65530, [65530 - 16383, 65531], False),           # backward, within the threshold
+        (2, [20000, 40000, 40001], True),                 # 40000: verify guesses ROC - 1, the walk ROC
+        (65000, [65000 + 300, 200, 32500, 32501], True),  # wrap, then packets the verify pass guesses apart
+    ]
+    for first, seqs, recheck in cases:
+        snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
+        pre = [max(first - 2, 0), first] if first > 2 else [first]
+        for q in (pre, seqs):
+            b = synth.rtp_bundle(len(q), 1, 300, seed=first + len(q))
+            set_seqs(b, q)
+            before = engine.stats()["roc_rechecks"]
+            seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
+            twin.run(rcv, True, seg, b.off, ln, b.cap)
+            if q is seqs and recheck:
+                assert engine.stats()["roc_rechecks"] > before, (first, seqs)
+
+
 def set_seqs(b, seqs):
     for i, q in enumerate(seqs):
         b.seg[b.off[i] + 2] = q >> 8

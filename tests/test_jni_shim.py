@@ -56,7 +56,8 @@ def load():
                     ("fj_packet_buffer", [vp], vp), ("fj_packet_offset", [vp], i32),
                     ("fj_packet_length", [vp], i32), ("fj_bytes_len", [vp], i32),
                     ("fj_bytes_read", [vp, vp], None), ("fj_exceptions", [], C.c_int),
-                    ("fj_frames", [], C.c_int), ("fj_reset", [], None), ("fj_ints_read", [vp, vp], None)]:
+                    ("fj_frames", [], C.c_int), ("fj_reset", [], None), ("fj_ints_read", [vp, vp], None),
+                    ("fj_fail_new_arrays", [C.c_int], None), ("fj_exception_pending", [], C.c_int)]:
         getattr(L, f).argtypes, getattr(L, f).restype = a, r
     sig = {"deviceCount": ([], i32), "dispatchCreate": ([vp, i32, i32], i64), "dispatchDestroy": ([i64], None),
            "factoryCreate": ([i64, u8, vp, vp, vp, vp], i32), "factoryClose": ([i64, i32], i32),
@@ -503,4 +504,76 @@ def test_jni_small_arrays_share_bundles_vs_oracle():
                     ost, ob = oracle_one(otr[ti], True, d)
                     assert kept == (ost == N.STATUS_OK) and got == ob, (q, N.STATUS_NAMES[ost])
     finally:
+        jvm.close()
+
+
+@pytest.mark.gpu
+def test_jni_main_thread_array_then_close():
+    """An array that cannot throw, sent on the thread that then closes the
+    aggregator (the thread's queue on the aggregator made
+    aggregatorDestroy wait forever): the queue lives for the call only."""
+    jvm = Jvm(n_shards=2)
+    closed = threading.Event()
+    try:
+        (k, s), = synth.keys(61, 1)
+        f = jvm.factory(True, k, s, P80[0])
+        t = jvm.transformer(0, f, f)
+        of = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+        ot = O.Transformer(O.KIND_RTP, of, of)
+        rng = np.random.default_rng(61)
+        datas = [rtp(0x6100, 10 + q, 300 + 50 * q, rng) for q in range(6)]
+        pk = [jvm.packet(d, 0, 16) for d in datas]
+        r, out = jvm.array(False, t, pk)
+        assert r == 0
+        for d, p in zip(datas, pk):
+            ost, ob = oracle_one(ot, False, d, 16)
+            assert ost == N.STATUS_OK and jvm.packet_bytes(p)[0] == ob
+    finally:
+        th = threading.Thread(target=lambda: (jvm.close(), closed.set()), daemon=True)
+        th.start()
+        th.join(60)
+    assert closed.is_set(), "aggregatorDestroy did not return"
+
+
+@pytest.mark.gpu
+def test_jni_queue_reap_out_of_memory_keeps_order():
+    """queueReap when the JVM cannot allocate a packet's new buffer (protect
+    of packets whose buffers have no room for the tag: RawPacket.append
+    reallocates): the reaped count still comes back, that packet's status is
+    SRTP_STATUS_ERR_INTERNAL (handed on as null), the OutOfMemoryError is
+    cleared, and the packets after it -- in this reap and the next -- are
+    written back in submission order against the oracle."""
+    jvm = Jvm(n_shards=1)
+    try:
+        (k, s), = synth.keys(62, 1)
+        f = jvm.factory(True, k, s, P80[0])
+        t = jvm.transformer(0, f, f)
+        of = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+        ot = O.Transformer(O.KIND_RTP, of, of)
+        rng = np.random.default_rng(62)
+        q = PacketQueue(jvm, 16)
+        datas = [rtp(0x6200, 20 + i, 200 + 30 * i, rng) for i in range(12)]
+        pk = [jvm.packet(d) for d in datas]  # no room: each result needs a new buffer
+        got = []
+        for p in pk[:6]:
+            assert q.submit(False, t, p)
+        jvm.L.fj_fail_new_arrays(1)
+        while len(got) < 6:
+            got += q.reap(True)
+        assert jvm.L.fj_exception_pending() == 0
+        for p in pk[6:]:
+            assert q.submit(False, t, p)
+        while len(got) < 12:
+            got += q.reap(True)
+        q.close()
+        sts = [st for _, st in got]
+        assert [p for p, _ in got] == pk
+        assert sts[0] == N.STATUS_ERR_INTERNAL and sts.count(N.STATUS_ERR_INTERNAL) == 1
+        for i, (d, p) in enumerate(zip(datas, pk)):
+            ost, ob = oracle_one(ot, False, d)
+            if i == 0:
+                continue  # its result could not be written back: the Java side drops it
+            assert sts[i] == ost == N.STATUS_OK and jvm.packet_bytes(p)[0] == ob, i
+    finally:
+        jvm.L.fj_fail_new_arrays(0)
         jvm.close()

@@ -15,8 +15,10 @@ for r in rows:
     name = name.replace("void k_protect<false>", "k_protect").replace("void k_unprotect<false>", "k_unprotect")
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r.get("Stream_Id", r.get("Queue_Id", "?"))))
 ev.sort()
-# one step = one k_protect launch; take the span of the last `last` steps
-prot = [e for e in ev if e[2] == "k_protect"]
+# one step = one launch of the sender's first crypto kernel (k_protect, or
+# k_ctr_wide<false> on the split path); take the span of the last `last` steps
+marker = "k_protect" if any(e[2] == "k_protect" for e in ev) else "void k_ctr_wide<false>"
+prot = [e for e in ev if e[2] == marker]
 if len(prot) < last + 1:
     sys.exit("not enough steps in the trace")
 t0, t1 = prot[-last - 1][0], prot[-1][0]
