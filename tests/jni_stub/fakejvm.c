@@ -252,6 +252,99 @@ JNIEXPORT int fj_drive_queues(struct fj_job *jobs, int n_jobs) {
     return 0;
 }
 
+/* ---- the connector loops (GpuConnectorLoops.java Send / Receive) ----
+ * The same steps as the Java loops over a GpuPacketQueue (GpuPacketQueue.java,
+ * again in C): input arrives in bursts -- a poll / receive finds the current
+ * burst's items, then "nothing yet" once; a waiting poll (nothing in flight)
+ * releases the next burst at once.  packetize / createRawPacket copy the
+ * buffer into a new RawPacket of exactly its length (so protect's trailer
+ * makes RawPacket.append reallocate); send / handOn record the packet in
+ * out[] in the order it is handed on.  Packets the queue completes with a
+ * status other than OK / SKIPPED are dropped, as the sink does. */
+struct fj_gq {
+    jlong q;
+    jobjectArray ring;
+    jintArray st;
+    long sub, rep;
+    jint n, ns;
+};
+struct fj_loop {
+    jlong agg;
+    jboolean reverse;
+    jint tid, n_in, depth;
+    jobject *in;         /* [n_in] input buffers (byte[]) */
+    const jint *bursts;  /* burst sizes, summing to n_in */
+    jint n_bursts;
+    jobject *out;        /* [n_in] packets handed on, in order */
+    jint n_out, n_dropped, max_in_flight, polls_empty, rc;
+};
+static void gq_reap(JNIEnv *env, struct fj_gq *g, struct fj_loop *L, int wait) {
+    if (g->sub == g->rep) return;
+    const jint k = SHIM(queueReap)(env, NULL, g->q, g->ring, g->st, (jboolean)wait);
+    if (k < 0) { L->rc = k; return; }
+    for (jint m = 0; m < k; m++) {
+        jobject pkt = ((jobject *)g->ring->data)[g->rep % g->n];
+        const jint s = ((jint *)g->st->data)[m];
+        g->rep++;
+        if (s == 0 || s == 9) L->out[L->n_out++] = pkt; /* STATUS_OK / STATUS_SKIPPED: handed on */
+        else L->n_dropped++;
+    }
+}
+static void gq_transform(JNIEnv *env, struct fj_gq *g, struct fj_loop *L, jobject pkt) {
+    while (!L->rc) {
+        if (g->sub - g->rep < g->n) {
+            ((jobject *)g->ring->data)[g->sub % g->n] = pkt;
+            const jint rc = SHIM(queueSubmit)(env, NULL, g->q, L->reverse, L->tid, pkt, 0, (jlong)g->sub);
+            if (rc == 0) {
+                g->sub++;
+                if (g->sub - g->rep > L->max_in_flight) L->max_in_flight = (jint)(g->sub - g->rep);
+                return;
+            }
+            if (rc != -6) { L->rc = rc; return; } /* not SRTP_EAGAIN */
+        }
+        gq_reap(env, g, L, 1);
+    }
+}
+/* one loop (send: reverse = 0, receive: reverse = 1; the steps are the same) */
+static void *fj_loop_run(void *arg) {
+    struct fj_loop *L = arg;
+    JNIEnv *env = &g_env;
+    struct fj_gq g = {0};
+    g.n = L->depth;
+    g.ns = L->depth < 1024 ? L->depth : 1024;
+    g.q = SHIM(queueCreate)(env, NULL, L->agg, L->depth);
+    if (!g.q) { L->rc = -1; return NULL; }
+    g.ring = new_array(K_OBJS, g.n, sizeof(jobject));
+    g.st = new_array(K_INTS, g.ns, sizeof(jint));
+    jint next = 0, burst = 0, released = 0;
+    while (!L->rc && (next < L->n_in || g.sub != g.rep)) {
+        /* poll(outstanding ? 0 : 500) / receive(outstanding ? 1 ms : block) */
+        const int waiting = g.sub == g.rep;
+        if (next == released && burst < L->n_bursts && waiting) released += L->bursts[burst++];
+        if (next == released) { /* nothing yet: reap what is due, then the next burst arrives */
+            L->polls_empty++;
+            gq_reap(env, &g, L, 1);
+            if (burst < L->n_bursts) released += L->bursts[burst++];
+            continue;
+        }
+        jbyteArray src = L->in[next++];
+        struct fj_obj *b = new_array(K_BYTES, src->len, 1);
+        memcpy(b->data, src->data, (size_t)src->len);
+        gq_transform(env, &g, L, fj_new_packet(b, 0, src->len, 0));
+        gq_reap(env, &g, L, 0); /* what is done, without waiting */
+    }
+    SHIM(queueDestroy)(env, NULL, g.q);
+    return NULL;
+}
+JNIEXPORT int fj_run_loops(struct fj_loop *loops, int n) {
+    pthread_t *th = calloc((size_t)n, sizeof *th);
+    if (!th) return -1;
+    for (int k = 0; k < n; k++) pthread_create(&th[k], NULL, fj_loop_run, &loops[k]);
+    for (int k = 0; k < n; k++) pthread_join(th[k], NULL);
+    free(th);
+    return 0;
+}
+
 /* pending "exceptions" (out-of-range array regions) and unbalanced local frames */
 JNIEXPORT int fj_exceptions(void) { return g_exceptions; }
 JNIEXPORT int fj_frames(void) { return g_frames; }

@@ -357,7 +357,8 @@ def test_recheck_state_at_the_seq_range_edges(twin):
                             (65000, lambda x: [65535, 0, 1, (65000 + x) & 0xFFFF, 65001])):
             snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
             for q in ([first], seqs(span)):
-                b = synth.rtp_bundle(len(q), 1, 200, seed=span + len(q))
+                # one SSRC over both bundles: the second continues the context
+                b = synth.rtp_bundle(len(q), 1, 200, seed=span + len(q), ssrcs=[0x5EC0 + span])
                 set_seqs(b, q)
                 seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)
                 twin.run(rcv, True, seg, b.off, ln, b.cap)
@@ -386,7 +387,7 @@ def test_recheck_state_at_the_far_threshold(twin, engine):
         snd, rcv = twin.transformer(O.KIND_RTP, fs), twin.transformer(O.KIND_RTP, fr)
         pre = [max(first - 2, 0), first] if first > 2 else [first]
         for q in (pre, seqs):
-            b = synth.rtp_bundle(len(q), 1, 300, seed=first + len(q))
+            b = synth.rtp_bundle(len(q), 1, 300, seed=first + len(q), ssrcs=[0xFA00 + first])
             set_seqs(b, q)
             before = engine.stats()["roc_rechecks"]
             seg, ln, st = twin.run(snd, False, b.seg, b.off, b.length, b.cap)

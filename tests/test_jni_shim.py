@@ -577,3 +577,95 @@ def test_jni_queue_reap_out_of_memory_keeps_order():
     finally:
         jvm.L.fj_fail_new_arrays(0)
         jvm.close()
+
+
+class FjLoop(C.Structure):
+    """struct fj_loop (tests/jni_stub/fakejvm.c): one connector thread running
+    GpuConnectorLoops.Send (reverse 0) or .Receive (reverse 1)."""
+    _fields_ = [("agg", C.c_int64), ("reverse", C.c_uint8), ("tid", C.c_int32), ("n_in", C.c_int32),
+                ("depth", C.c_int32), ("inp", C.c_void_p), ("bursts", C.c_void_p), ("n_bursts", C.c_int32),
+                ("out", C.c_void_p), ("n_out", C.c_int32), ("n_dropped", C.c_int32),
+                ("max_in_flight", C.c_int32), ("polls_empty", C.c_int32), ("rc", C.c_int32)]
+
+
+@pytest.mark.gpu
+def test_jni_connector_loops_vs_oracle():
+    """GpuConnectorLoops.Send and .Receive (src/org/.../mi355x/GpuConnectorLoops.java)
+    as 8 send threads and 8 receive threads of the stand-in JVM
+    (fakejvm.c fj_loop_run): input in bursts of 1-40 datagrams, up to 256
+    packets in flight per thread.  Each send thread's protected packets go out
+    in the order they were queued, each as the oracle's; the receive threads
+    get them with replays and forgeries mixed in and hand on, in arrival
+    order, exactly the packets the oracle accepts, with its bytes."""
+    T, PER = 8, 300
+    jvm = Jvm(n_shards=2)
+    L = jvm.L
+    L.fj_run_loops.argtypes, L.fj_run_loops.restype = [C.c_void_p, C.c_int], C.c_int
+    try:
+        keys = synth.keys(70, T)
+        snd, rcv, osnd, orcv = [], [], [], []
+        for k, s in keys:
+            fs, fr = jvm.factory(True, k, s, P80[0]), jvm.factory(False, k, s, P80[0])
+            snd.append(jvm.transformer(0, fs, fs))
+            rcv.append(jvm.transformer(0, fr, fr))
+            ofs = O.Factory(True, k, s, opol(P80[0]), opol(P80[1]))
+            ofr = O.Factory(False, k, s, opol(P80[0]), opol(P80[1]))
+            osnd.append(O.Transformer(O.KIND_RTP, ofs, ofs))
+            orcv.append(O.Transformer(O.KIND_RTP, ofr, ofr))
+
+        def run(reverse, tids, inputs, seed):
+            rng = np.random.default_rng(seed)
+            keep, loops = [], (FjLoop * T)()
+            for t in range(T):
+                arr = (C.c_void_p * len(inputs[t]))(*[L.fj_new_bytes(d, len(d)) for d in inputs[t]])
+                bl, left = [], len(inputs[t])
+                while left:
+                    bl.append(min(left, int(rng.integers(1, 41))))
+                    left -= bl[-1]
+                bursts = np.array(bl, np.int32)
+                out = (C.c_void_p * len(inputs[t]))()
+                keep += [arr, bursts, out]
+                loops[t] = FjLoop(jvm.agg, int(reverse), tids[t], len(inputs[t]), 256, C.cast(arr, C.c_void_p),
+                                  bursts.ctypes.data, len(bl), C.cast(out, C.c_void_p), 0, 0, 0, 0, 0)
+            assert L.fj_run_loops(loops, T) == 0
+            res = []
+            for t in range(T):
+                lp = loops[t]
+                assert lp.rc == 0, (t, lp.rc)
+                outs = C.cast(lp.out, C.POINTER(C.c_void_p))
+                res.append(([jvm.packet_bytes(outs[i])[0] for i in range(lp.n_out)], lp))
+            return res
+
+        rng = np.random.default_rng(71)
+        sent = [[rtp(0x7000 + 4 * t + (q % 3), 3000 + 11 * t + q, int(rng.integers(60, 1300)), rng)
+                 for q in range(PER)] for t in range(T)]
+        out_s = run(False, snd, sent, 72)
+        for t in range(T):
+            got, lp = out_s[t]
+            assert lp.n_dropped == 0 and len(got) == PER
+            assert lp.max_in_flight >= 32
+            for d, g in zip(sent[t], got):
+                ost, ob = oracle_one(osnd[t], False, d)
+                assert ost == N.STATUS_OK and g == ob
+        # the receivers: the wire order, with replays and forgeries
+        wire = []
+        for t in range(T):
+            w = list(out_s[t][0])
+            for q in range(0, PER, 37):
+                w.insert(q + 5, w[q])                          # a replay
+                f = bytearray(w[q + 2])
+                f[-3] ^= 0x40
+                w.insert(q + 9, bytes(f))                      # a forgery
+            wire.append(w)
+        out_r = run(True, rcv, wire, 73)
+        for t in range(T):
+            got, lp = out_r[t]
+            want = []
+            for d in wire[t]:
+                ost, ob = oracle_one(orcv[t], True, d)
+                if ost == N.STATUS_OK:
+                    want.append(ob)
+            assert lp.n_dropped == len(wire[t]) - len(want) > 0
+            assert got == want
+    finally:
+        jvm.close()
