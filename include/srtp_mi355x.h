@@ -369,7 +369,18 @@ int srtp_pipeline_submit_ex(srtp_pipeline *pl, int32_t slot, int32_t reverse, in
  * bundle (off relative to host_seg).  srtp_dispatch_transform_host does this
  * by itself for every chunk of a shard whose packets lie back to back in a
  * registered segment, so a one-shard dispatcher moves a registered bundle
- * with no host copy at all. */
+ * with no host copy at all.
+ *
+ * srtp_pipeline_submit_gather is the form for packets scattered over
+ * registered memory (a shard's share of an interleaved bundle): the slot's
+ * arrays lay the bundle out in the slot (off, cap, ...), and packet j's region
+ * (cap[j] rounded to 16 bytes) is read by the GPU from host_base + src_off[j]
+ * over PCIe before the bundle runs, and written back there after it --
+ * [host_base, host_base + host_bytes) must be registered; at most 32768
+ * packets.  srtp_dispatch_transform_host / _submit_host use it for every
+ * chunk of a registered bundle whose packets do not lie back to back, so a
+ * many-shard dispatcher moves a registered bundle with no host copy of its
+ * bytes either.  (Round 6; the registration maps the memory for the GPU.) */
 int srtp_host_register(void *ptr, size_t bytes);
 int srtp_host_unregister(void *ptr);
 int srtp_host_alloc(size_t bytes, void **out);
@@ -378,6 +389,10 @@ int32_t srtp_host_is_registered(const void *ptr, size_t bytes);
 int srtp_pipeline_submit_host(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
                               int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
                               int32_t abort_on_error, uint8_t *host_seg);
+int srtp_pipeline_submit_gather(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                                int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                                int32_t abort_on_error, uint8_t *host_base, size_t host_bytes,
+                                const uint32_t *src_off);
 
 /* Bundle aggregator over the pipeline: per-packet submits
  * from any number of threads become bundles.  Replaces the reference's

@@ -64,6 +64,7 @@ EXPORTED = [
     "srtp_dispatch_host_times", "srtp_pipeline_submit_ex", "srtp_aggregator_transform",
     "srtp_aggregator_transformer_info", "srtp_rawpacket_transform_one", "srtp_device_count",
     "srtp_host_register", "srtp_host_unregister", "srtp_host_is_registered", "srtp_pipeline_submit_host",
+    "srtp_pipeline_submit_gather",
     "srtp_pipeline_create_ex", "srtp_host_alloc", "srtp_host_free",
     "srtp_queue_create", "srtp_queue_submit", "srtp_queue_reap", "srtp_queue_outstanding",
     "srtp_queue_aggregator", "srtp_queue_destroy", "srtp_queue_release", "srtp_packet_may_throw",
@@ -224,6 +225,7 @@ def lib() -> C.CDLL:
     L.srtp_host_is_registered.argtypes = [vp, C.c_size_t]
     L.srtp_host_is_registered.restype = i32
     L.srtp_pipeline_submit_host.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t, i32, vp]
+    L.srtp_pipeline_submit_gather.argtypes = [vp, i32, i32, i32, i32, i32, u32, C.c_size_t, i32, vp, C.c_size_t, vp]
     L.srtp_device_count.argtypes = []
     L.srtp_device_count.restype = i32
     L.srtp_engine_stats.argtypes = [vp, C.POINTER(Stats)]

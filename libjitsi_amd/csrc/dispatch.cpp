@@ -62,6 +62,7 @@ namespace {
 constexpr int32_t kHdrThrow = (int32_t)0x80000000; // getHeaderLength would throw
 constexpr uint32_t kChunkPackets = 1u << 15;       // packets per pipeline slot
 constexpr size_t kChunkBytes = (size_t)48 << 20;   // segment bytes per pipeline slot
+constexpr size_t kGatherMax = 32768;               // packets per gathered chunk (srtp_pipeline_submit_gather)
 constexpr int kDepth = 8;                          // pipeline slots per shard
 constexpr size_t kMaxInflight = 64;                // host bundles submitted and not yet waited for
 
@@ -277,6 +278,7 @@ struct HostBundle {
     uint32_t *len = nullptr;
     int32_t *status = nullptr;
     bool registered = false; // the segment lies in registered memory (srtp_host_register)
+    size_t seg_bytes = 0;
     std::vector<std::vector<uint32_t>> per_shard;
     std::atomic<int> chunks_out{0}; // chunks in slots, not yet drained
     std::atomic<int> rc{SRTP_OK};
@@ -421,6 +423,7 @@ int run_shard(srtp_dispatch *d, int s, HostBundle &b, const std::shared_ptr<Host
     }
     int rc_all = SRTP_OK;
     size_t pos = 0;
+    std::vector<uint32_t> src; // a gathered chunk's packet offsets in the caller's segment
     while (pos < idx.size()) {
         const int k = rg.k;
         drain_slot(d, s, k, sl[k]);
@@ -446,7 +449,13 @@ int run_shard(srtp_dispatch *d, int s, HostBundle &b, const std::shared_ptr<Host
         // writes the caller's bytes in place; else the packet bytes go
         // through the slot.  Either way the per-packet arrays, and the copies,
         // are split over the copy helpers.
+        // a registered segment whose chunk is scattered over it (a shard's
+        // share of an interleaved bundle): the GPU gathers the packets over
+        // PCIe and writes them back (srtp_pipeline_submit_gather) -- no host
+        // copy of their bytes either (round 6; was two memcpy passes)
         const bool direct = b.registered && contig;
+        const bool gather = b.registered && !contig && nch <= kGatherMax;
+        if (gather) src.resize(nch);
         {
             const int parts = (int)std::min<size_t>((size_t)d->pool->size() + 1, (nch + 1023) / 1024);
             d->pool->run(parts, [&](int q) {
@@ -457,12 +466,15 @@ int run_shard(srtp_dispatch *d, int s, HostBundle &b, const std::shared_ptr<Host
                     sl[k].cap[j] = b.cap[i];
                     sl[k].flags[j] = b.flags ? b.flags[i] : 0u;
                     sl[k].tids[j] = b.tids ? b.tids[i] : b.tid;
+                    if (gather) src[j] = b.off[i];
                 }
-                if (!direct) copy_runs<true>(b, sl[k], ch, j0, j1);
+                if (!direct && !gather) copy_runs<true>(b, sl[k], ch, j0, j1);
             });
         }
         const int rc = direct ? srtp_pipeline_submit_host(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes, -1,
                                                           b.seg + b.off[ch[0]])
+                       : gather ? srtp_pipeline_submit_gather(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes, -1,
+                                                              b.seg, b.seg_bytes, src.data())
                               : srtp_pipeline_submit(pl, k, b.reverse, 1, -1, 1, (uint32_t)nch, bytes);
         d->t_pack += now_ns() - tp; // the enqueue of the chunk's copies and kernels included
         if (rc != SRTP_OK) {
@@ -472,7 +484,7 @@ int run_shard(srtp_dispatch *d, int s, HostBundle &b, const std::shared_ptr<Host
         rg.owner[k] = bp;
         rg.ch[k] = ch;
         rg.n[k] = nch;
-        rg.direct[k] = direct;
+        rg.direct[k] = direct || gather;
         b.chunks_out.fetch_add(1, std::memory_order_acq_rel);
         pos += nch;
         rg.k = (k + 1) % kDepth;
@@ -829,6 +841,7 @@ int submit_locked(srtp_dispatch *d, int32_t reverse, const int32_t *tids, int32_
     b.tids = tids; b.tid = tid; b.seg = seg; b.off = off; b.len = len;
     b.cap = cap; b.flags = flags; b.status = status;
     b.registered = srtp_host_is_registered(seg, seg_bytes) != 0;
+    b.seg_bytes = seg_bytes;
     for (size_t s = 0; s < ns; s++) {
         if (d->pipes[s]) continue;
         // shards sharing a GPU: one stream each (SRTP_PIPE_ONE_STREAM); the

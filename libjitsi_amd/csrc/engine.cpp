@@ -1290,7 +1290,7 @@ int srtp_host_register(void *ptr, size_t bytes) {
     auto it = g_reg.upper_bound(a);
     if (it != g_reg.end() && it->first < a + bytes) return SRTP_EINVAL;
     if (it != g_reg.begin() && std::prev(it)->first + std::prev(it)->second.bytes > a) return SRTP_EINVAL;
-    if (hipHostRegister(ptr, bytes, hipHostRegisterPortable) != hipSuccess) {
+    if (hipHostRegister(ptr, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
         (void)hipGetLastError();
         return SRTP_EDEVICE;
     }
@@ -1302,7 +1302,7 @@ int srtp_host_alloc(size_t bytes, void **out) {
     if (!out || bytes == 0) return SRTP_EINVAL;
     *out = nullptr;
     void *p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
         (void)hipGetLastError();
         return SRTP_ENOMEM;
     }
@@ -1330,6 +1330,23 @@ int srtp_host_unregister(void *ptr) {
         return SRTP_EDEVICE;
     }
     return SRTP_OK;
+}
+
+// The device address of registered host memory p (the range's mapping)
+static uint8_t *host_device_ptr(uint8_t *p) {
+    uintptr_t start;
+    {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        auto it = g_reg.upper_bound((uintptr_t)p);
+        if (it == g_reg.begin()) return nullptr;
+        start = std::prev(it)->first;
+    }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, reinterpret_cast<void *>(start), 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t *>(d) + ((uintptr_t)p - start);
 }
 
 int32_t srtp_host_is_registered(const void *ptr, size_t bytes) {
@@ -1364,6 +1381,9 @@ struct srtp_pipeline {
         // three -- each copy's fixed cost, not its bytes, is what a small
         // bundle's round trip pays
         uint32_t *h_pack = nullptr, *d_pack = nullptr;
+        // srtp_pipeline_submit_gather: each packet's offset in the caller's
+        // registered segment (pinned host copy, device copy)
+        uint32_t *h_src = nullptr, *d_src = nullptr;
         uint32_t packed_n = 0;      // the bundle in flight used the packed layout (its n), else 0
         // tiny bundles (kTinySeg bytes): the segment rides in the packed block
         // too -- one copy each way -- and is copied back to tiny_dst on wait
@@ -1393,7 +1413,9 @@ static void pipeline_free(srtp_pipeline *pl) {
         for (void *p : hp)
             if (p) (void)hipHostFree(p);
         if (sl.h_pack) (void)hipHostFree(sl.h_pack);
-        void *dp[] = {sl.d_seg, sl.d_off, sl.d_len, sl.d_cap, sl.d_flags, sl.d_tids, sl.d_status, sl.d_pack};
+        if (sl.h_src) (void)hipHostFree(sl.h_src);
+        void *dp[] = {sl.d_seg, sl.d_off, sl.d_len, sl.d_cap, sl.d_flags, sl.d_tids, sl.d_status, sl.d_pack,
+                      sl.d_src};
         for (void *p : dp) dfree(p);
         hipEvent_t ev[] = {sl.ev_in, sl.ev_done, sl.ev_out};
         for (auto x : ev)
@@ -1444,6 +1466,8 @@ int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg
              dalloc(&sl.d_status, n) == hipSuccess &&
              halloc(&sl.h_pack, 6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) == hipSuccess &&
              dalloc(&sl.d_pack, 6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) == hipSuccess &&
+             halloc(&sl.h_src, std::min<size_t>(n, kPackMax)) == hipSuccess &&
+             dalloc(&sl.d_src, std::min<size_t>(n, kPackMax)) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&sl.ev_out, hipEventDisableTiming) == hipSuccess;
@@ -1635,6 +1659,72 @@ int srtp_pipeline_submit_host(srtp_pipeline *pl, int32_t slot, int32_t reverse, 
     if (!host_seg || (n && !srtp_host_is_registered(host_seg, (seg_bytes + 15) & ~(size_t)15)))
         return SRTP_EINVAL;
     return pipeline_submit(pl, slot, reverse, use_tids, tid, use_flags, n, seg_bytes, abort_on_error, host_seg);
+}
+
+// The slot's bundle laid out in the slot (off, cap, ...), its packets' regions
+// read by the GPU from the caller's registered memory at host_base + src_off[j]
+// and written back there afterwards (srtp_mi355x.h).  Packed per-packet arrays
+// (n <= kPackMax); the gather runs on the copy-in stream, the scatter on the
+// copy-out stream, so one slot's moves overlap another's kernels.
+int srtp_pipeline_submit_gather(srtp_pipeline *pl, int32_t slot, int32_t reverse, int32_t use_tids,
+                                int32_t tid, int32_t use_flags, uint32_t n, size_t seg_bytes,
+                                int32_t abort_on_error, uint8_t *host_base, size_t host_bytes,
+                                const uint32_t *src_off) {
+    if (!pl || slot < 0 || (size_t)slot >= pl->slots.size() || (n && (!host_base || !src_off)))
+        return SRTP_EINVAL;
+    if (n > kPackMax || (n && !srtp_host_is_registered(host_base, host_bytes))) return SRTP_EINVAL;
+    std::lock_guard<std::mutex> gp(pl->mu);
+    srtp_pipeline::Slot &sl = pl->slots[(size_t)slot];
+    srtp_engine *e = pl->e;
+    GUARD(e);
+    (void)pipeline_wait_locked(pl, sl);
+    if (n > pl->max_n || seg_bytes > pl->max_seg) return fail(e, SRTP_EINVAL, "bundle exceeds the slot");
+    if (n == 0) return SRTP_OK;
+    seg_bytes = (seg_bytes + 15) & ~(size_t)15;
+    for (uint32_t j = 0; j < n; j++) { // every region inside the registered range, 16-B aligned
+        const uint64_t r = ((uint64_t)sl.h.cap[j] + 15u) & ~15ull;
+        if (src_off[j] % 16 != 0 || (uint64_t)src_off[j] + r > host_bytes)
+            return fail(e, SRTP_EINVAL, "gathered packet region outside the registered segment");
+    }
+    uint8_t *dhost = host_device_ptr(host_base);
+    if (!dhost) return fail(e, SRTP_EDEVICE, "registered segment without a device mapping");
+    std::lock_guard<std::mutex> g(e->mu);
+    int rc = validate_regions(e, sl.h.off, sl.h.cap, n, seg_bytes);
+    if (rc != SRTP_OK) return rc;
+    if (!use_tids && (tid < 0 || (size_t)tid >= e->transformers.size()))
+        return fail(e, SRTP_EINVAL, "bad transformer id");
+    const bool one = pl->one_stream;
+    hipStream_t s = e->stream, si = one ? s : pl->s_in, so = one ? s : pl->s_out;
+    const int32_t abort = abort_on_error < 0 ? -1 : (abort_on_error ? 1 : 0);
+    uint32_t *hp = sl.h_pack, *dp = sl.d_pack;
+    const size_t n4 = n * 4ull;
+    memcpy(hp, sl.h.off, n4);
+    memcpy(hp + n, sl.h.cap, n4);
+    if (use_flags) memcpy(hp + 2 * (size_t)n, sl.h.flags, n4);
+    if (use_tids) memcpy(hp + 3 * (size_t)n, sl.h.tids, n4);
+    memcpy(hp + 4 * (size_t)n, sl.h.len, n4);
+    memcpy(sl.h_src, src_off, n4);
+    HIPCHK(e, hipMemcpyAsync(dp, hp, 5 * n4, hipMemcpyHostToDevice, si));
+    HIPCHK(e, hipMemcpyAsync(sl.d_src, sl.h_src, n4, hipMemcpyHostToDevice, si));
+    HIPCHK(e, launch_move_regions(true, sl.d_seg, dp, dp + n, dhost, sl.d_src, n, si));
+    if (si != s) {
+        HIPCHK(e, hipEventRecord(sl.ev_in, si));
+        HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
+    }
+    sl.rc = transform_locked(e, reverse, use_tids ? reinterpret_cast<int32_t *>(dp + 3 * (size_t)n) : nullptr, tid,
+                             sl.d_seg, dp, dp + 4 * (size_t)n, dp + n, use_flags ? dp + 2 * (size_t)n : nullptr,
+                             reinterpret_cast<int32_t *>(dp + 5 * (size_t)n), n, s, abort);
+    if (sl.rc != SRTP_OK) return sl.rc;
+    if (so != s) {
+        HIPCHK(e, hipEventRecord(sl.ev_done, s));
+        HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
+    }
+    HIPCHK(e, launch_move_regions(false, sl.d_seg, dp, dp + n, dhost, sl.d_src, n, so));
+    HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, 2 * n4, hipMemcpyDeviceToHost, so));
+    sl.packed_n = n;
+    HIPCHK(e, hipEventRecord(sl.ev_out, so));
+    sl.busy = true;
+    return SRTP_OK;
 }
 
 int srtp_pipeline_query(srtp_pipeline *pl, int32_t slot) {

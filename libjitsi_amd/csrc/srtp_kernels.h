@@ -133,6 +133,11 @@ hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s);
 // trailer and final statuses; unprotect: the tag check before the walk)
 hipError_t launch_ctr_wide(const BundleArgs &a, hipStream_t s);
 hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s);
+// Packet regions [doff[j], + cap[j] rounded to 16) of a device segment from /
+// to [src[j], ...) of device-mapped host memory (a dispatcher shard's gather of
+// an interleaved registered host bundle)
+hipError_t launch_move_regions(bool to_device, uint8_t *dseg, const uint32_t *doff, const uint32_t *cap,
+                               uint8_t *host, const uint32_t *src, uint32_t n, hipStream_t s);
 // unprotect: statuses/lengths out; undo/redo the rare speculation misses (after the walk)
 hipError_t launch_unprotect_fix(const BundleArgs &a, hipStream_t s);
 // AES-F8 packets after the final statuses: protect (F8 + HMAC + trailer) or

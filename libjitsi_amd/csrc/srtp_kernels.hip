@@ -4897,22 +4897,6 @@ __device__ __forceinline__ bool wide_job_rev(const BundleArgs &a, uint32_t p, ui
     return end > start;
 }
 
-// XOR keystream blocks x, y over the `rem` (>= 1) bytes at q (4-B aligned):
-// whole pairs with two 16-B loads and stores, the packet's last pair word-
-// masked (bytes past the region XORed with zero: this lane alone touches them)
-__device__ __forceinline__ void wide_xor(uint8_t *q, int rem, const uint32_t x[4], const uint32_t y[4]) {
-    if (rem >= 32) {
-        uint4 *w = reinterpret_cast<uint4 *>(q);
-        uint4 u = w[0], v = w[1];
-        u.x ^= x[0]; u.y ^= x[1]; u.z ^= x[2]; u.w ^= x[3];
-        v.x ^= y[0]; v.y ^= y[1]; v.z ^= y[2]; v.w ^= y[3];
-        w[0] = u;
-        w[1] = v;
-    } else {
-        xor_ks32(q, 0, rem, x, y);
-    }
-}
-
 // k_ctr_jobs: each packet's keystream job, one lane per packet (all their
 // dependent loads in flight at once across the grid), into the packet's tailc
 // scratch, which the split path does not otherwise use: {IV}, {first byte of
@@ -5033,6 +5017,16 @@ __global__ __launch_bounds__(kWideBlock) void k_ctr_wide(BundleArgs a, uint32_t 
             cp.r[3] = j1w.x; cp.kb = j1w.z & 0xffu;
             const int j = act ? 2 * (int)(g - pre[q]) : 0;
             const size_t pj = act ? j1w.w : first; // an idle lane's q may be a stale slot
+            // the pair's 32 bytes, loaded before the rounds (their latency hides
+            // behind them); the packet's last, partial pair loads after, masked
+            uint8_t *dst = a.seg + j1w.y + 16u * (uint32_t)j;
+            const int rem = (int)(j1w.z >> 8) - 16 * j;
+            const bool whole = act && rem >= 32;
+            uint4 d0 = make_uint4(0u, 0u, 0u, 0u), d1 = d0;
+            if (whole) {
+                d0 = reinterpret_cast<const uint4 *>(dst)[0];
+                d1 = reinterpret_cast<const uint4 *>(dst)[1];
+            }
             uint32_t x[4], y[4];
             const bool far = __ballot(act && j + 1 >= 256) != 0ull; // IV byte 14 set: full rounds
             if (uni) {
@@ -5070,7 +5064,14 @@ __global__ __launch_bounds__(kWideBlock) void k_ctr_wide(BundleArgs a, uint32_t 
                     aes_encrypt2_v(lds, tb, kk, x, y);
                 }
             }
-            if (act) wide_xor(a.seg + j1w.y + 16u * (uint32_t)j, (int)(j1w.z >> 8) - 16 * j, x, y);
+            if (whole) {
+                d0.x ^= x[0]; d0.y ^= x[1]; d0.z ^= x[2]; d0.w ^= x[3];
+                d1.x ^= y[0]; d1.y ^= y[1]; d1.z ^= y[2]; d1.w ^= y[3];
+                reinterpret_cast<uint4 *>(dst)[0] = d0;
+                reinterpret_cast<uint4 *>(dst)[1] = d1;
+            } else if (act) {
+                xor_ks32(dst, 0, rem, x, y);
+            }
         }
         // the slot is rewritten by the next group's lanes only after every
         // lane's reads above (the wave's LDS ops complete in order)
@@ -5087,20 +5088,29 @@ __global__ __launch_bounds__(kWideBlock) void k_ctr_wide(BundleArgs a, uint32_t 
 // re-check midstate.
 constexpr int kMacWideBlock = 256;
 
+#ifndef SRTP_MAC_AHEAD
+#define SRTP_MAC_AHEAD 1
+#endif
 __device__ __forceinline__ void mac_stream(const uint8_t *pkt, int end, uint32_t suffix, const KeySet *ks,
                                            uint32_t h[5], uint32_t *mid_out, int mid_b) {
     const int nb_data = (end + 63) >> 6;
     const int nb_inner = ((end + 12) >> 6) + 1;
     const int n_blocks = nb_inner + 1;
+#if SRTP_MAC_AHEAD
     uint32_t nx[16];
     load_or_zero16(pkt, 0, nb_data, end, nx);
+#endif
 #pragma unroll 1
     for (int b = 0; b < n_blocks; b++) {
         uint32_t w[16];
+#if SRTP_MAC_AHEAD
 #pragma unroll
         for (int m = 0; m < 16; m++) w[m] = nx[m];
         load_or_zero16(pkt, b + 1, nb_data, end, nx);
         asm volatile("" ::: "memory"); // keep the look-ahead (see MacRing::next)
+#else
+        load_or_zero16(pkt, b, nb_data, end, w); // the other waves hide the load
+#endif
         if (b == mid_b && mid_out) {
 #pragma unroll
             for (int k = 0; k < 5; k++) mid_out[k] = h[k];
@@ -5221,6 +5231,58 @@ hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s) {
     const dim3 grid((a.n + kMacWideBlock - 1) / kMacWideBlock);
     if (a.reverse) hipLaunchKernelGGL(k_mac_wide<true>, grid, dim3(kMacWideBlock), 0, s, a);
     else hipLaunchKernelGGL(k_mac_wide<false>, grid, dim3(kMacWideBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+// ========================================== gather / scatter of host bundles
+// A dispatcher shard's chunk of an interleaved host bundle in registered
+// (device-mapped) memory: its packets' regions are read from the caller's
+// segment over PCIe into the slot's device segment (k_gather_regions), and
+// written back after the bundle (k_scatter_regions) -- by the GPU, instead of
+// a host copy into and out of the pinned slot (srtp_pipeline_submit_gather).
+// A wave moves two packet regions at a time, 16 B per lane per instruction (a
+// wave-instruction moves 1 KB of one region): every load of both regions (up
+// to 2 KB each) is issued before any store, so reads over PCIe keep 4 KB per
+// wave in flight instead of waiting out a round trip per KB.
+constexpr int kGatherBlock = 256;
+template <bool ToDevice>
+__global__ __launch_bounds__(kGatherBlock) void k_move_regions(uint8_t *dseg, const uint32_t *doff,
+                                                               const uint32_t *cap, uint8_t *host,
+                                                               const uint32_t *src, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t waves = gridDim.x * (kGatherBlock / 64);
+    for (uint32_t j = 2u * (blockIdx.x * (kGatherBlock / 64) + (threadIdx.x >> 6)); j < n; j += 2u * waves) {
+        const bool two = j + 1u < n;
+        const uint32_t wa = ((cap[j] + 15u) & ~15u) / 16u, wb = two ? ((cap[j + 1] + 15u) & ~15u) / 16u : 0u;
+        uint4 *da = reinterpret_cast<uint4 *>(dseg + doff[j]);
+        uint4 *ha = reinterpret_cast<uint4 *>(host + src[j]);
+        uint4 *db = reinterpret_cast<uint4 *>(dseg + doff[two ? j + 1 : j]);
+        uint4 *hb = reinterpret_cast<uint4 *>(host + src[two ? j + 1 : j]);
+        uint4 *fa = ToDevice ? ha : da, *ta = ToDevice ? da : ha;
+        uint4 *fb = ToDevice ? hb : db, *tb = ToDevice ? db : hb;
+        for (uint32_t o = lane; o < max(wa, wb); o += 128u) {
+            const bool a0 = o < wa, a1 = o + 64u < wa, b0 = o < wb, b1 = o + 64u < wb;
+            uint4 x0, x1, y0, y1;
+            if (a0) x0 = fa[o];
+            if (a1) x1 = fa[o + 64u];
+            if (b0) y0 = fb[o];
+            if (b1) y1 = fb[o + 64u];
+            if (a0) ta[o] = x0;
+            if (a1) ta[o + 64u] = x1;
+            if (b0) tb[o] = y0;
+            if (b1) tb[o + 64u] = y1;
+        }
+    }
+}
+
+hipError_t launch_move_regions(bool to_device, uint8_t *dseg, const uint32_t *doff, const uint32_t *cap,
+                               uint8_t *host, const uint32_t *src, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t wgs = std::min<uint32_t>((n + 7u) / 8u, 4096u); // two regions per wave
+    if (to_device)
+        hipLaunchKernelGGL(k_move_regions<true>, dim3(wgs), dim3(kGatherBlock), 0, s, dseg, doff, cap, host, src, n);
+    else
+        hipLaunchKernelGGL(k_move_regions<false>, dim3(wgs), dim3(kGatherBlock), 0, s, dseg, doff, cap, host, src, n);
     return hipGetLastError();
 }
 

@@ -32,6 +32,13 @@ recipe() {
                       tests/test_tag_lengths.py tests/test_context_export.py tests/test_lifecycle.py ;;
     parity_fused) SRTP_TEST_DEBUG=4 step parity_fused 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_golden.py \
                       tests/test_skew.py tests/test_repairs.py ;;
+    dispatch_tests) step dispatch_tests 600 $PYT -m gpu tests/test_host_memory.py tests/test_dispatcher.py \
+                      tests/test_dispatch_async.py tests/test_config5_sharded.py tests/test_rawpacket.py ;;
+    # the dispatcher leg alone (host bundles, 1/2/4 shards on one GPU), in its torch-free child
+    bench_dispatch) step bench_dispatch 600 python bench.py --steps 5 --warmup 2 --no-cpu --no-e2e &&
+                    tail -1 "$O/bench_dispatch.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read())
+for k, v in (d["dispatch"] or {}).items():
+    if isinstance(v, dict): print(k, v.get("directional_pps"), v.get("host_ms_per_bundle"))' | tee "$O/dispatch.txt" ;;
     smoke)        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)        step bench 300 $BENCH --steps 20 --warmup 5 && tail -1 "$O/bench.log" > "$O/bench.json" ;;
     bench_fused)  SRTP_TEST_DEBUG=4 step bench_fused 300 $BENCH --steps 20 --warmup 5 ;;
@@ -52,6 +59,35 @@ recipe() {
                           echo "n=$n dbg=$d $(tail -1 $O/sweep_${n}_$d.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["stage_ms"])')" >> $O/sweep.txt
                       done
                   done; cat $O/sweep.txt ;;
+    # counters of one build's crypto kernels on the serial bench (separate --pmc
+    # passes); PROF_DEBUG=2 profiles the split path on the full bundle
+    prof)         local S="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-e2e --no-dispatch --serial"
+                  local P="$O/prof"
+                  export SRTP_TEST_DEBUG=${PROF_DEBUG:-0}
+                  step prof_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/trace" -o run -- \
+                      python3 bench.py --steps 20 --warmup 2 --no-cpu --no-e2e --no-dispatch --serial &&
+                  step prof_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$P/fetch" -o run -- $S &&
+                  step prof_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$P/write" -o run -- $S &&
+                  step prof_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+                      SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d "$P/sq" -o run -- $S &&
+                  step prof_sq2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                      SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE \
+                      --output-format csv -d "$P/sq2" -o run -- $S
+                  local rc=$?
+                  unset SRTP_TEST_DEBUG
+                  return $rc ;;
+    # the split path on the full bundle, serial stage timings: this build and
+    # each variant in $VARIANTS (libjitsi_amd/variants/libsrtp_<v>.so), twice
+    ab_wide)      for k in 1 2; do
+                      SRTP_TEST_DEBUG=2 step ab_wide_cur_$k 200 $BENCH --steps 20 --warmup 3 --serial || return 1
+                      for v in ${VARIANTS:-}; do
+                          SRTP_TEST_DEBUG=2 SRTP_MI355X_LIB=libjitsi_amd/variants/libsrtp_$v.so \
+                              step ab_wide_${v}_$k 200 $BENCH --steps 20 --warmup 3 --serial || return 1
+                      done
+                  done
+                  for f in $O/ab_wide_*.log; do
+                      echo "$(basename $f .log) $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["stage_ms"])')"
+                  done | tee $O/ab_wide.txt ;;
     *) echo "unknown recipe $1"; return 2 ;;
     esac
 }

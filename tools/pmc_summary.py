@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--tag", type=int, default=10)
     ap.add_argument("--out")
     ap.add_argument("--calib", help="factor.json of tools/pmc_calib_factor.py")
+    ap.add_argument("--kernels", default="k_protect,k_unprotect",
+                    help="kernels to derive figures for (the split path: k_ctr_wide<false>,k_mac_wide<true>, ...)")
     a = ap.parse_args()
     calib = None
     if a.calib:
@@ -95,7 +97,7 @@ def main():
                 counters[k][c] = sum(v) / len(v)
             pass_dur[k] += list(dur[k].values())
     derived = {}
-    for k in ("k_protect", "k_unprotect"):
+    for k in a.kernels.split(","):
         c = counters.get(k)
         if not c:
             continue
