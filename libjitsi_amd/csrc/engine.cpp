@@ -113,7 +113,10 @@ constexpr uint32_t kSmallCtrMax = 8192u; // k_ctr_small takes bundles up to this
 // packets: there the fused kernels' lane per packet leaves most CUs idle or
 // latency-bound; from 2^17 packets on the fused kernels are faster
 // (profiles/r06/kernel_experiments.md, bundle-size sweep)
-constexpr uint32_t kWideMin = 2048u, kWideMax = 65536u;
+#ifndef SRTP_WIDE_MIN
+#define SRTP_WIDE_MIN 2048u
+#endif
+constexpr uint32_t kWideMin = SRTP_WIDE_MIN, kWideMax = 65536u;
 
 int fail(srtp_engine *e, int code, const std::string &msg) {
     if (e) e->last_error = msg;

@@ -5214,12 +5214,18 @@ hipError_t launch_ctr_wide(const BundleArgs &a, hipStream_t s) {
     const dim3 jg((a.n + kJobBlock - 1) / kJobBlock);
     if (a.reverse) hipLaunchKernelGGL(k_ctr_jobs<true>, jg, dim3(kJobBlock), 0, s, a);
     else hipLaunchKernelGGL(k_ctr_jobs<false>, jg, dim3(kJobBlock), 0, s, a);
-    // groups of 16 packets, fewer for smaller bundles (about four groups per
-    // wave of 256 workgroups x 16 waves)
+    // Groups of 16 packets, four per wave of 256 workgroups x 16 waves on a
+    // full bundle.  A smaller bundle keeps groups of at least two packets (a
+    // 1200-B packet is 38 counter-block pairs: one group of one packet leaves
+    // 26 lanes idle) and two groups per wave, so that it takes only the CUs
+    // its work fills: each workgroup builds the 128-KB T-table image, and a
+    // bundle that holds every CU's LDS for one round of work keeps another
+    // bundle in flight (the aggregator's lanes keep two) off the GPU.
     uint32_t G = (uint32_t)kWideGMax;
-    while (G > 1u && (a.n + G - 1u) / G < 4u * 4096u) G >>= 1;
+    while (G > 2u && (a.n + G - 1u) / G < 4u * 4096u) G >>= 1;
     const uint32_t groups = (a.n + G - 1u) / G;
-    const uint32_t wgs = (groups + 15u) / 16u;
+    const uint32_t waves = groups >= 4u * 4096u ? 4096u : (groups + 1u) / 2u;
+    const uint32_t wgs = (waves + 15u) / 16u;
     const dim3 grid(wgs < 256u ? wgs : 256u);
     if (a.reverse) hipLaunchKernelGGL(k_ctr_wide<true>, grid, dim3(kWideBlock), 0, s, a, G);
     else hipLaunchKernelGGL(k_ctr_wide<false>, grid, dim3(kWideBlock), 0, s, a, G);

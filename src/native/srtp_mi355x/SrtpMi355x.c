@@ -270,17 +270,22 @@ JNIEXPORT jint JNICALL JFN(deviceCount)(JNIEnv *env, jclass c) {
 }
 
 /* One aggregator per process over the dispatcher: its lanes coalesce the
- * per-packet calls of every JVM thread into GPU bundles.  Bundles of at most
- * 4096 packets / 8 MB per lane (what a round trip's worth of per-packet calls
- * fills); six pinned slots per lane (48 MB), so that queued callers
- * (GpuPacketQueue) keep bundles filling while others are in flight or held
- * for their write-back. */
-JNIEXPORT jlong JNICALL JFN(aggregatorCreate)(JNIEnv *env, jclass c, jlong d) {
+ * per-packet calls of every JVM thread into GPU bundles.  Each lane (one per
+ * GPU) holds `depth` pinned slots of bundles of up to maxPackets packets /
+ * maxMegabytes of packet bytes, pinned on the host and on the device: the
+ * pinned-memory budget is depth x maxMegabytes per GPU.  Values <= 0 take the
+ * defaults, 16384 packets / 24 MB / 8 slots (192 MB per GPU): the queued path
+ * (GpuPacketQueue, 64 threads x 256 in flight) ran at 9-13 M calls/s there
+ * against 4-6 M with 4096 / 8 / 6 (profiles/r05/kernel_experiments.md 4,
+ * profiles/r06/sync/).  The Java side reads them from the configuration
+ * (SrtpMi355x.LANE_*_PNAME). */
+JNIEXPORT jlong JNICALL JFN(aggregatorCreate)(JNIEnv *env, jclass c, jlong d, jint maxPackets, jint maxMegabytes,
+                                              jint depth) {
     srtp_aggregator_opts o;
     srtp_aggregator_opts_default(&o); /* SRTP_AGG_SEAL_IDLE */
-    o.max_packets = 4096;
-    o.max_bytes = (size_t)8 << 20;
-    o.depth = 6;
+    o.max_packets = maxPackets > 0 ? (uint32_t)maxPackets : 16384u;
+    o.max_bytes = (size_t)(maxMegabytes > 0 ? maxMegabytes : 24) << 20;
+    o.depth = depth > 0 ? depth : 8;
     srtp_aggregator *a = NULL;
     return srtp_aggregator_create_dispatch((srtp_dispatch *)H(d), &o, NULL, NULL, &a) == SRTP_OK
                ? (jlong)(intptr_t)a : 0;

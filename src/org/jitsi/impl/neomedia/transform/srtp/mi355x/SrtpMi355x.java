@@ -26,6 +26,17 @@ public final class SrtpMi355x
      */
     public static final String GPUS_PNAME = "org.jitsi.impl.neomedia.transform.srtp.mi355x.GPUS";
 
+    /**
+     * The per-packet aggregator's lanes (one per GPU): packets and megabytes
+     * per bundle, and pinned bundle slots.  The pinned-memory budget is
+     * SLOTS x MB per GPU, on the host and on the device; the defaults (16384,
+     * 24, 8: 192 MB per GPU) are where the queued path measured fastest, and
+     * 0 or a negative value keeps a default.
+     */
+    public static final String LANE_PACKETS_PNAME = "org.jitsi.impl.neomedia.transform.srtp.mi355x.LANE_PACKETS";
+    public static final String LANE_MB_PNAME = "org.jitsi.impl.neomedia.transform.srtp.mi355x.LANE_MB";
+    public static final String LANE_SLOTS_PNAME = "org.jitsi.impl.neomedia.transform.srtp.mi355x.LANE_SLOTS";
+
     /** One dispatcher per process: every GPU of the node, SSRC-sharded. */
     private static long dispatch;
 
@@ -71,7 +82,15 @@ public final class SrtpMi355x
         {
             if (aggregator == 0)
             {
-                a = aggregatorCreate(dispatch());
+                int packets = 0, mb = 0, slots = 0;
+                ConfigurationService cfg = LibJitsi.getConfigurationService();
+                if (cfg != null)
+                {
+                    packets = cfg.getInt(LANE_PACKETS_PNAME, packets);
+                    mb = cfg.getInt(LANE_MB_PNAME, mb);
+                    slots = cfg.getInt(LANE_SLOTS_PNAME, slots);
+                }
+                a = aggregatorCreate(dispatch(), packets, mb, slots);
                 if (a == 0)
                     throw new IllegalStateException("srtp_mi355x: no aggregator");
                 aggregator = a;
@@ -103,8 +122,11 @@ public final class SrtpMi355x
      */
     static native int transformPackets(long d, long aggregator, boolean reverse, int transformer,
                                        RawPacket[] pkts, int[] skip);
-    /** srtp_aggregator_create_dispatch with SRTP_AGG_SEAL_IDLE and no callback. */
-    static native long aggregatorCreate(long d);
+    /**
+     * srtp_aggregator_create_dispatch with SRTP_AGG_SEAL_IDLE and no callback;
+     * lane sizing as the LANE_*_PNAME properties (<= 0: the defaults).
+     */
+    static native long aggregatorCreate(long d, int maxPackets, int maxMegabytes, int slots);
     static native void aggregatorDestroy(long a);
     /** One packet (srtp_rawpacket_transform_one): its SRTP_STATUS_*, or a negative error code. */
     static native int transformOne(long aggregator, boolean reverse, int transformer, RawPacket pkt);

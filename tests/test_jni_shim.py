@@ -63,7 +63,7 @@ def load():
            "factoryCreate": ([i64, u8, vp, vp, vp, vp], i32), "factoryClose": ([i64, i32], i32),
            "transformerCreate": ([i64, i32, i32, i32], i32), "transformerSetFactory": ([i64, i32, i32, u8], i32),
            "transformerClose": ([i64, i32], i32),
-           "transformPackets": ([i64, i64, u8, i32, vp, vp], i32), "aggregatorCreate": ([i64], i64),
+           "transformPackets": ([i64, i64, u8, i32, vp, vp], i32), "aggregatorCreate": ([i64, i32, i32, i32], i64),
            "aggregatorDestroy": ([i64], None), "transformOne": ([i64, u8, i32, vp], i32),
            "queueCreate": ([i64, i32], i64), "queueDestroy": ([i64], None),
            "queueSubmit": ([i64, u8, i32, vp, u8, i64], i32), "queueReap": ([i64, vp, vp, u8], i32)}
@@ -94,7 +94,7 @@ class Jvm:
         self.d = self.J("dispatchCreate")(self.env, self.cls, self.L.fj_new_ints(devs.ctypes.data, n_shards),
                                           1, 1 << 14)
         assert self.d
-        self.agg = self.J("aggregatorCreate")(self.env, self.cls, self.d)
+        self.agg = self.J("aggregatorCreate")(self.env, self.cls, self.d, 0, 0, 0)  # the defaults
         assert self.agg
 
     def close(self):

@@ -39,6 +39,26 @@ recipe() {
                     tail -1 "$O/bench_dispatch.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read())
 for k, v in (d["dispatch"] or {}).items():
     if isinstance(v, dict): print(k, v.get("directional_pps"), v.get("host_ms_per_bundle"))' | tee "$O/dispatch.txt" ;;
+    # the per-packet drop-in path (tools/sync_bench): a lone caller and 64
+    # synchronous callers (protect + unprotect round trips), arrays through
+    # the aggregator, and the queued path at the JNI shim's sizing and larger
+    sync)         : > "$O/sync.jsonl"
+                  for p in "one 0 1 rt" "one 0 64 rt" "arrayq 0 64"; do
+                      step sync_pt 90 ./tools/sync_bench 2 $p && cat "$O/sync_pt.log" >> "$O/sync.jsonl" || return 1
+                  done
+                  for cfg in "4096,8,6 64" "4096,8,6 256" "16384,24,8 256"; do
+                      set -- $cfg
+                      SYNC_AGG=$1 SYNC_DEPTH=$2 step sync_q 90 ./tools/sync_bench 2 queue 0 64 rt || return 1
+                      python3 -c "import json; j=json.loads(open('$O/sync_q.log').read().strip().splitlines()[-1]); j['agg']='$1'; j['depth']=$2; j['path'] += '${SYNC_DEBUG:+_dbg$SYNC_DEBUG}'; print(json.dumps(j))" >> "$O/sync.jsonl"
+                  done
+                  python3 -c "
+import json
+for l in open('$O/sync.jsonl'):
+    j = json.loads(l); print(j['path'], j['threads'], j.get('agg', ''), j.get('depth', ''), 'calls/s', j['calls_per_s'], 'p50', j['lat_us']['p50'], 'pkts/bundle', j.get('packets_per_bundle'))" ;;
+    # a kernel + copy trace of one synchronous caller (the lone call's chain)
+    trace_lone)   step trace_lone 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+                      -d "$O/trace_lone" -o run -- ./tools/sync_bench 1 one 0 1 rt &&
+                  python3 tools/lone_chain.py "$O/trace_lone" | tee "$O/lone_chain.txt" ;;
     smoke)        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)        step bench 300 $BENCH --steps 20 --warmup 5 && tail -1 "$O/bench.log" > "$O/bench.json" ;;
     bench_fused)  SRTP_TEST_DEBUG=4 step bench_fused 300 $BENCH --steps 20 --warmup 5 ;;

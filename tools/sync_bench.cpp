@@ -214,6 +214,13 @@ int main(int argc, char **argv) {
                     check(d ? srtp_dispatch_transformer_create(d, SRTP_KIND_RTP, fr, fr, &trr[(size_t)t])
                             : srtp_transformer_create(e, SRTP_KIND_RTP, fr, fr, &trr[(size_t)t]), "transformer");
                 }
+                // SYNC_DEBUG=<flags>: srtp_engine_set_debug on every engine (A/B of
+                // the engine's paths, e.g. 4 = SRTP_DEBUG_NO_WIDE)
+                if (const char *dbg = getenv("SYNC_DEBUG")) {
+                    const uint32_t f = (uint32_t)strtoul(dbg, nullptr, 0);
+                    if (e) check(srtp_engine_set_debug(e, f), "debug");
+                    for (int s2 = 0; d && s2 < G; s2++) check(srtp_engine_set_debug(srtp_dispatch_engine(d, s2), f), "debug");
+                }
                 srtp_aggregator *a = nullptr;
                 if (path != 1) {
                     srtp_aggregator_opts ao;
