@@ -43,10 +43,11 @@ for k, v in (d["dispatch"] or {}).items():
     # synchronous callers (protect + unprotect round trips), arrays through
     # the aggregator, and the queued path at the JNI shim's sizing and larger
     sync)         : > "$O/sync.jsonl"
-                  for p in "one 0 1 rt" "one 0 64 rt" "arrayq 0 64"; do
-                      step sync_pt 90 ./tools/sync_bench 2 $p && cat "$O/sync_pt.log" >> "$O/sync.jsonl" || return 1
+                  # points as path_shards_threads[_rt]
+                  for p in ${SYNC_POINTS:-one_0_1_rt one_0_64_rt arrayq_0_64}; do
+                      step sync_pt 90 ./tools/sync_bench 2 ${p//_/ } && cat "$O/sync_pt.log" >> "$O/sync.jsonl" || return 1
                   done
-                  for cfg in "4096,8,6 64" "4096,8,6 256" "16384,24,8 256"; do
+                  for cfg in ${SYNC_CFGS:-"4096,8,6 64" "4096,8,6 256" "16384,24,8 64" "16384,24,8 256"}; do
                       set -- $cfg
                       SYNC_AGG=$1 SYNC_DEPTH=$2 step sync_q 90 ./tools/sync_bench 2 queue 0 64 rt || return 1
                       python3 -c "import json; j=json.loads(open('$O/sync_q.log').read().strip().splitlines()[-1]); j['agg']='$1'; j['depth']=$2; j['path'] += '${SYNC_DEBUG:+_dbg$SYNC_DEBUG}'; print(json.dumps(j))" >> "$O/sync.jsonl"
@@ -59,6 +60,8 @@ for l in open('$O/sync.jsonl'):
     trace_lone)   step trace_lone 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
                       -d "$O/trace_lone" -o run -- ./tools/sync_bench 1 one 0 1 rt &&
                   python3 tools/lone_chain.py "$O/trace_lone" | tee "$O/lone_chain.txt" ;;
+    agg_tests)    step agg_tests 600 $PYT -m gpu tests/test_aggregator.py tests/test_single_packet.py tests/test_jni_shim.py \
+                      tests/test_rawpacket.py tests/test_pipeline.py ;;
     smoke)        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)        step bench 300 $BENCH --steps 20 --warmup 5 && tail -1 "$O/bench.log" > "$O/bench.json" ;;
     bench_fused)  SRTP_TEST_DEBUG=4 step bench_fused 300 $BENCH --steps 20 --warmup 5 ;;

@@ -169,9 +169,10 @@ int main(int argc, char **argv) {
     const uint32_t BUF = L + 16; // room behind the packet: the tag is appended in place
     const int n_tr = 50;
     srtp_policy pol = {SRTP_AESCM_ENCRYPTION, 16, SRTP_HMACSHA1_AUTHENTICATION, 20, 10, 14};
-    const int shard_counts[] = {0, 8};
-    const int thread_counts[] = {1, 8, 64};
     const bool one_point = argc > 4;
+    // a point's own shard and thread counts (any), else the sweep's
+    const std::vector<int> shard_counts = one_point ? std::vector<int>{atoi(argv[3])} : std::vector<int>{0, 8};
+    const std::vector<int> thread_counts = one_point ? std::vector<int>{atoi(argv[4])} : std::vector<int>{1, 8, 64};
     const int p_only = one_point ? (strcmp(argv[2], "one") == 0 ? 0 : strcmp(argv[2], "array") == 0 ? 1
                                     : strcmp(argv[2], "queue") == 0 ? 2 : 3) : -1;
     const uint32_t depth = getenv("SYNC_DEPTH") ? (uint32_t)atoi(getenv("SYNC_DEPTH")) : 64u;
