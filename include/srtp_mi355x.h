@@ -218,6 +218,7 @@ typedef struct {
     uint64_t holes;                      /* bundle-former holes: SRTP_PKT_FLAG_SKIP entries of no
                                             transformer (tid < 0) that srtp_aggregator_* seals
                                             unclaimed; not in status[SRTP_STATUS_SKIPPED] */
+    uint64_t small_bundles;              /* bundles run by k_small: every phase in one launch */
 } srtp_stats;
 int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
 
@@ -233,6 +234,11 @@ int srtp_engine_stats(srtp_engine *e, srtp_stats *out);
  * (A/B measurements).  Results must not change. */
 #define SRTP_DEBUG_FORCE_WIDE 0x2u
 #define SRTP_DEBUG_NO_WIDE 0x4u
+/* SRTP_DEBUG_NO_SMALL keeps bundles of up to 255 packets off k_small (the
+ * whole bundle -- parse, sort, walk, keystream, MAC -- in one workgroup and
+ * one launch, which such bundles take under the split path's key-set rule);
+ * FORCE_WIDE and NO_WIDE keep them off it too. */
+#define SRTP_DEBUG_NO_SMALL 0x8u
 int srtp_engine_set_debug(srtp_engine *e, uint32_t flags);
 
 /* Context-state export / import: lets a stream's ROC, s_l,

@@ -28,6 +28,7 @@ NUM_STATUS = len(STATUS_NAMES)
 DEBUG_FORCE_CHAIN_STALL = 0x1
 DEBUG_FORCE_WIDE = 0x2  # every bundle on the split path (k_ctr_wide + k_mac_wide)
 DEBUG_NO_WIDE = 0x4     # every bundle on the fused kernels
+DEBUG_NO_SMALL = 0x8    # bundles of up to 255 packets off k_small (one launch per bundle)
 ABI_VERSION = 3
 AGG_SEAL_IDLE = 0x1
 PKT_FLAG_DISCARD, PKT_FLAG_SILENCE, PKT_FLAG_SKIP = 0x2, 0x4, 0x80000000
@@ -117,7 +118,7 @@ class Stats(C.Structure):
                  ("status", C.c_uint64 * NUM_STATUS)] +
                 [(n, C.c_uint64) for n in ("roc_rechecks", "repaired", "ctx_overflow", "ctx_live",
                                            "ctx_tombstones", "ctx_slots", "rehashes", "chain_stalls", "long_walked",
-                                           "holes")])
+                                           "holes", "small_bundles")])
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "status"}

@@ -582,11 +582,14 @@ void slot_free_locked(srtp_aggregator *a, Lane &ln, Slot &sl) {
     a->cv_idle.notify_all();
 }
 
+#ifndef SRTP_AGG_SYNC_CAP
+#define SRTP_AGG_SYNC_CAP 2
+#endif
 // Synchronous requests may be placed: some are waiting, a slot is free and
-// fewer than two bundles are sealed or in flight.
+// fewer than SRTP_AGG_SYNC_CAP (two) bundles are sealed or in flight.
 bool sync_placeable_locked(const Lane &ln) {
     if (!ln.sync_head.load() && ln.sync_pending.empty()) return false;
-    if (ln.sealed.size() + ln.inflight.size() >= 2) return false;
+    if (ln.sealed.size() + ln.inflight.size() >= (size_t)SRTP_AGG_SYNC_CAP) return false;
     for (int i = 0; i < ln.n_slots; i++)
         if (ln.slots[i].state == kFree) return true;
     return false;

@@ -89,7 +89,7 @@ struct srtp_engine {
 #ifdef SRTP_STAMPS
     unsigned long long *d_stamps[2] = {nullptr, nullptr}; // diagnostic build: protect / unprotect
 #endif
-    uint64_t n_bundles = 0, n_packets = 0, n_rehash = 0;
+    uint64_t n_bundles = 0, n_packets = 0, n_rehash = 0, n_small = 0;
     uint32_t serial = 1;
 
     // staging for srtp_transform_host
@@ -780,7 +780,12 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     // the rest the fused kernels (with k_ctr_small up to kSmallCtrMax packets).
     const bool wide_ok = e->n_not_wide == 0 && !(e->dbg & SRTP_DEBUG_NO_WIDE);
     const bool split = wide_ok && ((n >= kWideMin && n <= kWideMax) || (e->dbg & SRTP_DEBUG_FORCE_WIDE));
-    a.small_ctr = split ? 2 : n <= kSmallCtrMax ? 1 : 0;
+    // a bundle of up to kSmallMaxN packets under the split path's key-set rule:
+    // every phase in one launch (k_small), unless a debug hook needs the
+    // multi-kernel chain
+    const bool small = wide_ok && n <= kSmallMaxN && !a.dbg &&
+                       !(e->dbg & (SRTP_DEBUG_FORCE_WIDE | SRTP_DEBUG_NO_SMALL));
+    a.small_ctr = split || small ? 2 : n <= kSmallCtrMax ? 1 : 0;
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;
     a.ctl = e->ctl + c;
@@ -795,6 +800,14 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     if (a.abort_on_error) e->emin_filled[c] = 0u;
     if (need_ctl) HIPCHK(e, hipMemsetAsync(a.ctl, 0, sizeof(BundleCtl), s));
     if (need_emin) HIPCHK(e, hipMemsetAsync(a.e_min, 0x7f, sizeof(int32_t) * a.n_transformers, s));
+    if (small) {
+        StageTimer t(e, s, a.reverse ? SRTP_STAGE_VERIFY : SRTP_STAGE_PROTECT);
+        HIPCHK(e, launch_small(a, s)); // also resets control block c ^ 1 (and e_min c ^ 1)
+        e->ctl_clean[c ^ 1] = true;
+        if (a.abort_on_error) e->emin_filled[c ^ 1] = a.n_transformers;
+        e->ctl_cur = c ^ 1;
+        e->n_small++;
+    } else {
     // a one-tile bundle is sorted by one workgroup in one launch
     const bool one_tile = n <= sort_tile_records();
     {
@@ -845,6 +858,7 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
         HIPCHK(e, launch_protect(a, s));
         if (e->n_ext) HIPCHK(e, launch_ext(a, s));
         if (e->n_skein) HIPCHK(e, launch_skein(a, s));
+    }
     }
     HIPCHK(e, hipEventRecord(dev_event ? e->ev_dev : e->ev_last, s));
     e->last_dev = dev_event;
@@ -1156,6 +1170,7 @@ int srtp_engine_stats(srtp_engine *e, srtp_stats *out) {
     out->chain_stalls = sum[kCtrChainStall];
     out->long_walked = sum[kCtrLongWalked];
     out->holes = sum[kCtrStatus + kStatusHole];
+    out->small_bundles = e->n_small;
     return SRTP_OK;
 }
 
@@ -1165,7 +1180,7 @@ int32_t srtp_device_count(void) {
 }
 
 int srtp_engine_set_debug(srtp_engine *e, uint32_t flags) {
-    if (!e || (flags & ~(SRTP_DEBUG_FORCE_CHAIN_STALL | SRTP_DEBUG_FORCE_WIDE | SRTP_DEBUG_NO_WIDE)))
+    if (!e || (flags & ~(SRTP_DEBUG_FORCE_CHAIN_STALL | SRTP_DEBUG_FORCE_WIDE | SRTP_DEBUG_NO_WIDE | SRTP_DEBUG_NO_SMALL)))
         return SRTP_EINVAL;
     std::lock_guard<std::mutex> g(e->mu);
     e->dbg = flags;

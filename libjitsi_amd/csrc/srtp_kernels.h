@@ -133,6 +133,11 @@ hipError_t launch_ctr_small(const BundleArgs &a, hipStream_t s);
 // trailer and final statuses; unprotect: the tag check before the walk)
 hipError_t launch_ctr_wide(const BundleArgs &a, hipStream_t s);
 hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s);
+// A bundle of up to kSmallMaxN packets (engines whose key sets are all AES-CM
+// or NULL cipher with HMAC-SHA1): parse, sort, (tag check,)
+// walk, keystream and (MAC, trailer) in one workgroup and one launch (k_small).
+constexpr uint32_t kSmallMaxN = 255u;
+hipError_t launch_small(const BundleArgs &a, hipStream_t s);
 // Packet regions [doff[j], + cap[j] rounded to 16) of a device segment from /
 // to [src[j], ...) of device-mapped host memory (a dispatcher shard's gather of
 // an interleaved registered host bundle)

@@ -2166,6 +2166,16 @@ __device__ __forceinline__ void bcast_state(CtxState &st) {
     st.window = ((uint64_t)hi << 32) | lo;
 }
 
+// The walk is one wave (k_walk's workgroup; k_small's wave 0): a barrier
+// between its LDS phases only has to order the wave's own memory operations
+// (what __syncthreads does, without s_barrier, so that k_small's other waves
+// need not take part).
+__device__ __forceinline__ void walk_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // LDS of the second k_walk pass when it walks long chains (the first pass's
 // staging arrays, unused then): one step's records and per-record results.
 struct LongLds {
@@ -2233,7 +2243,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
                 nv += v ? 1 : 0;
             }
             nvalid = (int)__reduce_add_sync(~0ull, (unsigned)nv); // a prefix of the step
-            __syncthreads();
+            walk_sync();
         }
         if (nvalid == 0) break;
         int f = 0; // block position of the first packet that breaks the speculation
@@ -2358,7 +2368,7 @@ __device__ __forceinline__ void walk_long(const BundleArgs &a, uint32_t i0, cons
         } else {
             i += (uint32_t)nvalid;
         }
-        __syncthreads(); // the step's LDS is reused by the next
+        walk_sync(); // the step's LDS is reused by the next
         if (nvalid < kLongStep && f >= nvalid) break;
     }
     if (lane == 0) {
@@ -2827,20 +2837,35 @@ __device__ __forceinline__ ChainFix chain_stall_next(const BundleArgs &a, uint32
 // PASS 0: the first launch; PASS 1: the second (abort-on-throw's limit pass,
 // or the long chains) -- separate instances, so that the first pass's
 // registers do not pay for chain_part.
+// The walk's LDS (k_walk's own; k_small's behind its T-table image).
+template <bool REV>
+struct WalkShared {
+    WalkRec rec[kWalkWin];
+    uint32_t key[kWalkWin];
+    uint32_t g0[REV ? kWalkWin : 1];
+    uint32_t ok[REV ? kWalkWin : 1];
+    uint32_t start[kWalkSpan > kLongStep ? kWalkSpan : kLongStep];
+    uint32_t pkey[kWalkSpan]; // keys of the tile before (long-chain test); medium chains: ROCs
+    uint32_t med[kMedMax];
+    uint32_t nstart, tile, nmed;
+};
+static_assert(kLongStep <= kWalkWin, "walk_long stages a step in the first pass's arrays");
+static_assert(kLongStep <= kWalkSpan, "a medium chain's walk_long step keeps its ROCs in s_pkey");
+
+// Tile `blk` of `nblk` (k_walk: blockIdx.x of gridDim.x), by one wave.
 template <bool REV, bool SK, int PASS>
-__global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
+__device__ __forceinline__ void walk_tile(const BundleArgs &a, WalkShared<REV> &sh, uint32_t blk, uint32_t nblk) {
     constexpr int limit_pass = PASS;
-    __shared__ WalkRec s_rec[kWalkWin];
-    __shared__ uint32_t s_key[kWalkWin];
-    __shared__ uint32_t s_g0[REV ? kWalkWin : 1];
-    __shared__ uint32_t s_ok[REV ? kWalkWin : 1];
-    static_assert(kLongStep <= kWalkWin, "walk_long stages a step in the first pass's arrays");
-    __shared__ uint32_t s_start[kWalkSpan > kLongStep ? kWalkSpan : kLongStep];
-    __shared__ uint32_t s_nstart;
-    __shared__ uint32_t s_pkey[kWalkSpan]; // keys of the tile before (long-chain test); medium chains: ROCs
-    static_assert(kLongStep <= kWalkSpan, "a medium chain's walk_long step keeps its ROCs in s_pkey");
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_med[kMedMax], s_nmed;
+    WalkRec *const s_rec = sh.rec;
+    uint32_t *const s_key = sh.key;
+    uint32_t *const s_g0 = sh.g0;
+    uint32_t *const s_ok = sh.ok;
+    uint32_t *const s_start = sh.start;
+    uint32_t &s_nstart = sh.nstart;
+    uint32_t *const s_pkey = sh.pkey;
+    uint32_t &s_tile = sh.tile;
+    uint32_t *const s_med = sh.med;
+    uint32_t &s_nmed = sh.nmed;
     const bool two_pass = a.abort_on_error && a.ctl->any_throw;
     // Long chains (kWalkSpan records or more) are walked by the tiles they
     // cross (chain_part) in the second launch, unless abort-on-throw needs the
@@ -2849,20 +2874,19 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     const bool chain_pass = limit_pass && !two_pass;
     if (chain_pass && a.ctl->n_long == 0u) return; // no long chain in this bundle
     if (!limit_pass) { // the sort's last digit counts and k_parse's class counts, zero again for the next bundle
-        for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words;
-             i += gridDim.x * kWalkBlock)
+        for (uint32_t i = blk * kWalkBlock + threadIdx.x; i < a.sort_zero_words; i += nblk * kWalkBlock)
             a.sort_zero[i] = 0u;
-        for (uint32_t i = blockIdx.x * kWalkBlock + threadIdx.x; i < a.sort_zero_words / 256u * kClsWords;
-             i += gridDim.x * kWalkBlock)
+        for (uint32_t i = blk * kWalkBlock + threadIdx.x; i < a.sort_zero_words / 256u * kClsWords;
+             i += nblk * kWalkBlock)
             a.cls_tile[i] = 0u;
     }
     // The chain pass takes its tile from a ticket counter: a tile that waits on
     // the tiles before it for a long chain's state only waits on tiles already
     // running.
-    uint32_t tile = blockIdx.x;
+    uint32_t tile = blk;
     if (chain_pass) {
         if (threadIdx.x == 0) s_tile = atomicAdd(&a.ctl->tile_ticket, 1u);
-        __syncthreads();
+        walk_sync();
         tile = s_tile;
     }
     const uint32_t base = tile * kWalkSpan;
@@ -2895,7 +2919,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
             }
         }
     }
-    __syncthreads();
+    walk_sync();
     const uint32_t prev_key = base ? a.sk_out[base - 1] : ~0u;
     // A chain of kWalkSpan records or more (it reaches the end of the tile it
     // starts in): record j's chain, starting at j, is that long iff the record
@@ -2984,7 +3008,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
                     uint32_t last = 0u;
                     if (threadIdx.x == 0) {
                         __threadfence();
-                        last = atomicAdd(&a.ctl->tiles_done, 1u) == gridDim.x - 1u ? 1u : 0u;
+                        last = atomicAdd(&a.ctl->tiles_done, 1u) == nblk - 1u ? 1u : 0u;
                         if (last) {
                             __threadfence();
                             last = __hip_atomic_load(&a.ctl->n_stall, __ATOMIC_RELAXED,
@@ -3010,7 +3034,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
                 s_start[atomicAdd(&s_nstart, 1u)] = j;
         }
     }
-    __syncthreads();
+    walk_sync();
     const uint32_t nstart = s_nstart;
     const bool dry = two_pass && !limit_pass;
 #pragma unroll 1
@@ -3121,7 +3145,7 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
         a.ctx[slot] = st;
     }
     if (!chains) return;
-    __syncthreads();
+    walk_sync();
     const uint32_t nmed = s_nmed;
     if (nmed == 0u) return;
     uint32_t med = threadIdx.x < nmed ? s_med[threadIdx.x] : 0u;
@@ -3140,13 +3164,19 @@ __global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
     sm.g0 = REV ? s_g0 : s_start; // unused in place
     sm.ok = REV ? s_ok : s_start;
     sm.info = s_start;
-    __syncthreads();
+    walk_sync();
 #pragma unroll 1
     for (uint32_t m = 0; m < nmed; m++) {
         const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)med, (int)m);
         const CtxState st = a.ctx[s_key[j]];
         walk_long<REV, SK>(a, base + j, sm, st, &pw);
     }
+}
+
+template <bool REV, bool SK, int PASS>
+__global__ __launch_bounds__(kWalkBlock) void k_walk(BundleArgs a) {
+    __shared__ WalkShared<REV> sh;
+    walk_tile<REV, SK, PASS>(a, sh, blockIdx.x, gridDim.x);
 }
 
 // ====================================================== final status helper
@@ -5121,49 +5151,39 @@ __device__ __forceinline__ void mac_stream(const uint8_t *pkt, int end, uint32_t
     }
 }
 
-template <bool REV>
-__global__ __launch_bounds__(kMacWideBlock) void k_mac_wide(BundleArgs a) {
-    __shared__ uint32_t s_cnt[kTeCounters];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = i < a.n;
-    const uint32_t p = live ? lane_packet(a, i) : i;
-    if (!REV) {
-        if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
-        __syncthreads();
-        int32_t fs = -1;
-        if (live) {
-            fs = finish_status(a, p);
-            atomicAdd(&s_cnt[status_counter(a, p, fs)], 1u);
-        }
-        __syncthreads();
-        flush_status_counts(a, s_cnt);
-        if (fs != SRTP_STATUS_OK) return;
-        const KeySet *ks = a.keysets + a.ctx[a.p_slot[p]].ks;
-        uint8_t *pkt = a.seg + a.off[p];
-        const bool rtcp = ks->kind == SRTP_KIND_RTCP;
-        const int T = ks->tag_len;
-        const int L = (int)a.w_len[p] - T - (rtcp ? 4 : 0);
-        const uint32_t cw = a.w_cw[p];
-        const uint32_t suffix = !rtcp ? cw : (ks->enc_type == SRTP_AESCM_ENCRYPTION ? (cw | 0x80000000u) : 0u);
-        uint32_t h[5];
+// Protect, packet p with final status OK: the MAC over the ciphertext and the
+// trailer (k_protect's MacOnly instance: authenticatePacketHMAC :269-278,
+// RawPacket.append :203-220).
+__device__ __forceinline__ void mac_seal_one(const BundleArgs &a, uint32_t p) {
+    const KeySet *ks = a.keysets + a.ctx[a.p_slot[p]].ks;
+    uint8_t *pkt = a.seg + a.off[p];
+    const bool rtcp = ks->kind == SRTP_KIND_RTCP;
+    const int T = ks->tag_len;
+    const int L = (int)a.w_len[p] - T - (rtcp ? 4 : 0);
+    const uint32_t cw = a.w_cw[p];
+    const uint32_t suffix = !rtcp ? cw : (ks->enc_type == SRTP_AESCM_ENCRYPTION ? (cw | 0x80000000u) : 0u);
+    uint32_t h[5];
 #pragma unroll
-        for (int k = 0; k < 5; k++) h[k] = ks->ipad[k];
-        mac_stream(pkt, L, suffix, ks, h, nullptr, -1);
-        if ((L & 3) == 0) {
-            trailer_write_aligned(reinterpret_cast<uint32_t *>(pkt + L), rtcp, suffix, h, T);
-        } else {
-            int o = L;
-            if (rtcp) {
-                pkt[o] = (uint8_t)(suffix >> 24); pkt[o + 1] = (uint8_t)(suffix >> 16);
-                pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
-                o += 4;
-            }
-            tag_write(h, pkt + o, T);
+    for (int k = 0; k < 5; k++) h[k] = ks->ipad[k];
+    mac_stream(pkt, L, suffix, ks, h, nullptr, -1);
+    if ((L & 3) == 0) {
+        trailer_write_aligned(reinterpret_cast<uint32_t *>(pkt + L), rtcp, suffix, h, T);
+    } else {
+        int o = L;
+        if (rtcp) {
+            pkt[o] = (uint8_t)(suffix >> 24); pkt[o + 1] = (uint8_t)(suffix >> 16);
+            pkt[o + 2] = (uint8_t)(suffix >> 8); pkt[o + 3] = (uint8_t)suffix;
+            o += 4;
         }
-        return;
+        tag_write(h, pkt + o, T);
     }
-    // unprotect: k_unprotect's prologue (context state, long-chain guess, quiet)
-    if (!live) return;
+}
+
+// Unprotect, packet p before the walk: k_unprotect's prologue (context state,
+// long-chain guess, quiet), the ROC guess, the tag check under it and the
+// walk's re-check midstate (k_unprotect's MacOnly instance without
+// speculation).
+__device__ __forceinline__ void mac_check_one(const BundleArgs &a, uint32_t p) {
     const uint32_t slot = a.p_slot[p];
     if (slot == kNoSlot) return;
     const uint32_t pos = a.spos[p];
@@ -5209,6 +5229,28 @@ __global__ __launch_bounds__(kMacWideBlock) void k_mac_wide(BundleArgs a) {
     a.gok[2 * (size_t)p + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
 }
 
+template <bool REV>
+__global__ __launch_bounds__(kMacWideBlock) void k_mac_wide(BundleArgs a) {
+    __shared__ uint32_t s_cnt[kTeCounters];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < a.n;
+    const uint32_t p = live ? lane_packet(a, i) : i;
+    if (!REV) {
+        if (threadIdx.x < kTeCounters) s_cnt[threadIdx.x] = 0u;
+        __syncthreads();
+        int32_t fs = -1;
+        if (live) {
+            fs = finish_status(a, p);
+            atomicAdd(&s_cnt[status_counter(a, p, fs)], 1u);
+        }
+        __syncthreads();
+        flush_status_counts(a, s_cnt);
+        if (fs == SRTP_STATUS_OK) mac_seal_one(a, p);
+        return;
+    }
+    if (live) mac_check_one(a, p);
+}
+
 hipError_t launch_ctr_wide(const BundleArgs &a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const dim3 jg((a.n + kJobBlock - 1) / kJobBlock);
@@ -5237,6 +5279,185 @@ hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s) {
     const dim3 grid((a.n + kMacWideBlock - 1) / kMacWideBlock);
     if (a.reverse) hipLaunchKernelGGL(k_mac_wide<true>, grid, dim3(kMacWideBlock), 0, s, a);
     else hipLaunchKernelGGL(k_mac_wide<false>, grid, dim3(kMacWideBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+// ================================================= small bundles in one launch
+// k_small: a bundle of up to kSmallMaxN packets (the per-packet callers' bundles:
+// a lone synchronous call is a bundle of one) in one launch, its phases
+// separated by barriers instead of kernel boundaries -- each boundary of the
+// multi-kernel chain costs a small bundle a launch gap of ~4 us, and its
+// parse, sort and walk kernels are all latency.  The phases are the split
+// path's.  Workgroup 0, thread t on packet t:
+//   parse (parse_one) -> sort (each record's rank among the n keys, stable)
+//   -> unprotect: the tag check under the ROC guess (mac_check_one)
+//   -> the walk (wave 0, walk_tile: one tile, as n < kLongMin; abort-on-throw:
+//      the dry and the limit pass back to back)
+// then every workgroup of the grid (one per 16 packets, at most 16) on
+// packets g, g + G, ...:
+//   -> keystream jobs (unprotect: the final statuses, wide_job_rev), their
+//      counter-block pairs over the workgroup's lanes (k_ctr_small's AES with
+//      per-lane keys: one CU's LDS would bound a 255-packet bundle's keystream)
+//   -> protect: final statuses, MAC and trailer (mac_seal_one).
+// The other workgroups fill their T-table image meanwhile and wait for
+// workgroup 0's flag (BundleCtl::small_ready, agent-scope release/acquire).
+// Workgroup 0 never waits on them, and every workgroup ends once its
+// packets are done.  LDS: the 128-KB T-table image at 0 (the AES asm's
+// addressing), the status counts, then one region that holds in turn the sort
+// keys, the walk's arrays and the jobs.
+constexpr int kSmallBlock = 512;
+constexpr uint32_t kSmallPerWg = 16; // packets per workgroup (the grid: up to 16)
+static_assert(kSmallMaxN < kLongMin && kSmallMaxN < (uint32_t)kSmallBlock && kSmallMaxN <= (uint32_t)kWalkSpan,
+              "k_small: one walk tile, one record per thread");
+constexpr int kSmallJob = 8; // words per packet: iv[4], packet offset, region start, end, key set
+constexpr int kSmallOffCnt = kTeWords;
+constexpr int kSmallOffR = kSmallOffCnt + kTeCounters;
+constexpr int kSmallJobsWords = kSmallJob * 256 + 260; // jobs + pair prefix [257]
+constexpr int kSmallWalkWords = (int)(sizeof(WalkShared<true>) / 4);
+constexpr int kSmallRWords = kSmallWalkWords > kSmallJobsWords ? kSmallWalkWords : kSmallJobsWords;
+static_assert(kSmallOffR % 4 == 0 && sizeof(WalkShared<true>) % 4 == 0, "k_small: 16-B aligned region");
+static_assert((kSmallOffR + kSmallRWords) * 4 <= 160 * 1024, "k_small: LDS");
+
+template <bool REV>
+__global__ __launch_bounds__(kSmallBlock) void k_small(BundleArgs a) {
+    __shared__ uint32_t s[kSmallOffR + kSmallRWords];
+    fill_te4(s); // ends with a barrier
+    uint32_t *const s_cnt = s + kSmallOffCnt;
+    uint32_t *const r = s + kSmallOffR;
+    const uint32_t t = threadIdx.x, n = a.n, g = blockIdx.x, G = gridDim.x;
+    if (t < kTeCounters) s_cnt[t] = 0u;
+    if (g == 0) {
+        // the next bundle's control block and abort limits (as k_parse)
+        if (t == 0) *a.ctl_next = BundleCtl{};
+        if (a.abort_on_error)
+            for (uint32_t i = t; i < a.n_transformers; i += kSmallBlock) a.e_min_next[i] = 0x7f7f7f7f;
+        // 1. parse
+        uint32_t key = 0u;
+        if (t < n) {
+            key = parse_one(a, t);
+            r[t] = key;
+        }
+        __syncthreads();
+        // 2. sort: the sorted arrays and (unprotect) each packet's position, as
+        // k_sort_tile leaves them (stable by key; invalid packets' keys last)
+        if (t < n) {
+            uint32_t rank = 0u;
+            for (uint32_t q = 0; q < n; q++) {
+                const uint32_t kq = r[q];
+                rank += (kq < key || (kq == key && q < t)) ? 1u : 0u;
+            }
+            a.sk_out[rank] = key;
+            a.sv_out[rank] = a.sv_in[t];
+            if (REV && key <= a.ctx_mask) a.spos[t] = rank;
+        }
+        __syncthreads();
+        // 3. unprotect: the tag check before the walk
+        if (REV) {
+            if (t < n) mac_check_one(a, t);
+            __syncthreads();
+        }
+        // 4. the walk; abort-on-throw with a packet that may throw: the dry
+        // pass, then the limit pass (k_walk's two launches)
+        if (t < 64) {
+            WalkShared<REV> &sh = *reinterpret_cast<WalkShared<REV> *>(r);
+            walk_tile<REV, false, 0>(a, sh, 0u, 1u);
+            if (a.abort_on_error && a.ctl->any_throw) {
+                walk_sync();
+                walk_tile<REV, false, 1>(a, sh, 0u, 1u);
+            }
+        }
+        __syncthreads();
+        // everything the other workgroups read, visible at agent scope first
+        if (G > 1 && t == 0) {
+            __threadfence();
+            __hip_atomic_store(&a.ctl->small_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        if (t == 0)
+            while (__hip_atomic_load(&a.ctl->small_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                __builtin_amdgcn_s_sleep(2);
+        __syncthreads();
+    }
+    // 5. this workgroup's packets p = g + G * i: keystream jobs and their pair
+    // counts, then the pairs' prefix
+    const uint32_t m = n > g ? (n - g + G - 1u) / G : 0u;
+    uint32_t *const job = r;
+    uint32_t *const pre = r + kSmallJob * 256;
+    if (t < 256) {
+        uint32_t pairs = 0u;
+        if (t < m) {
+            const uint32_t p = g + G * t;
+            int start = 0, end = 0;
+            uint32_t iv[4] = {0u, 0u, 0u, 0u};
+            const KeySet *ks = nullptr;
+            const bool ok = REV ? wide_job_rev(a, p, s_cnt, start, end, iv, ks) : ctr_small_job(a, p, start, end, iv, ks);
+            uint4 *jp = reinterpret_cast<uint4 *>(job + kSmallJob * t);
+            jp[0] = make_uint4(iv[0], iv[1], iv[2], iv[3]);
+            jp[1] = make_uint4(a.off[p], (uint32_t)start, (uint32_t)end, ok ? (uint32_t)(ks - a.keysets) : 0u);
+            pairs = ok ? (uint32_t)(end - start + 31) >> 5 : 0u;
+        }
+        pre[t] = pairs;
+    }
+    __syncthreads();
+    if (t < 64) { // exclusive scan of 256 counts, four per lane
+        uint32_t v[4], sum = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; k++) { v[k] = pre[4 * t + k]; sum += v[k]; }
+        uint32_t x = (uint32_t)wave_excl_scan((int32_t)sum);
+#pragma unroll
+        for (int k = 0; k < 4; k++) { pre[4 * t + k] = x; x += v[k]; }
+        if (t == 63) pre[256] = x;
+    }
+    __syncthreads();
+    // 6. the pairs, consecutive pairs of a packet on consecutive lanes
+    const uint32_t total = pre[256];
+    const TeBase tb = te_base();
+    const char *lds = reinterpret_cast<const char *>(s);
+    for (uint32_t q = t; q < total; q += kSmallBlock) {
+        uint32_t lo = 0u, hi = m - 1u; // the last packet whose pairs start at or before q
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1u) >> 1;
+            if (pre[mid] <= q) lo = mid;
+            else hi = mid - 1u;
+        }
+        const uint4 j0 = *reinterpret_cast<const uint4 *>(job + kSmallJob * lo);
+        const uint4 j1 = *reinterpret_cast<const uint4 *>(job + kSmallJob * lo + 4);
+        const uint32_t iv[4] = {j0.x, j0.y, j0.z, j0.w};
+        const int start = (int)j1.y, end = (int)j1.z;
+        const int j = 2 * (int)(q - pre[lo]);
+        const uint4 kw = *reinterpret_cast<const uint4 *>(a.keysets[j1.w].rk);
+        const uint32_t k0[4] = {kw.x, kw.y, kw.z, kw.w};
+        uint32_t x[4], y[4];
+        ctr_input(iv, j, x);
+        ctr_input(iv, j + 1, y);
+        aes_encrypt2_v(lds, tb, k0, x, y);
+        uint8_t *pkt = a.seg + j1.x;
+        if ((start & 3) == 0) {
+            xor_ks32(pkt, start + 16 * j, end, x, y);
+        } else { // not a header of whole words: byte by byte
+            xor_ks16(pkt + start + 16 * j, end - (start + 16 * j), x);
+            if (start + 16 * (j + 1) < end) xor_ks16(pkt + start + 16 * (j + 1), end - (start + 16 * (j + 1)), y);
+        }
+    }
+    __syncthreads();
+    // 7. protect: final statuses, the MAC over the ciphertext, the trailer
+    const uint32_t p = g + G * t;
+    int32_t fs = -1;
+    if (!REV && t < m) {
+        fs = finish_status(a, p);
+        atomicAdd(&s_cnt[status_counter(a, p, fs)], 1u);
+    }
+    __syncthreads();
+    flush_status_counts(a, s_cnt);
+    if (!REV && fs == SRTP_STATUS_OK) mac_seal_one(a, p);
+}
+
+hipError_t launch_small(const BundleArgs &a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    if (a.n > kSmallMaxN) return hipErrorInvalidValue;
+    const dim3 grid((a.n + kSmallPerWg - 1u) / kSmallPerWg); // at most 16
+    if (a.reverse) hipLaunchKernelGGL(k_small<true>, grid, dim3(kSmallBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_small<false>, grid, dim3(kSmallBlock), 0, s, a);
     return hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ for k, v in (d["dispatch"] or {}).items():
                       step sync_pt 90 ./tools/sync_bench 2 ${p//_/ } && cat "$O/sync_pt.log" >> "$O/sync.jsonl" || return 1
                   done
                   for cfg in ${SYNC_CFGS:-"4096,8,6 64" "4096,8,6 256" "16384,24,8 64" "16384,24,8 256"}; do
-                      set -- $cfg
+                      set -- ${cfg//_/ }
                       SYNC_AGG=$1 SYNC_DEPTH=$2 step sync_q 90 ./tools/sync_bench 2 queue 0 64 rt || return 1
                       python3 -c "import json; j=json.loads(open('$O/sync_q.log').read().strip().splitlines()[-1]); j['agg']='$1'; j['depth']=$2; j['path'] += '${SYNC_DEBUG:+_dbg$SYNC_DEBUG}'; print(json.dumps(j))" >> "$O/sync.jsonl"
                   done
@@ -56,10 +56,36 @@ for k, v in (d["dispatch"] or {}).items():
 import json
 for l in open('$O/sync.jsonl'):
     j = json.loads(l); print(j['path'], j['threads'], j.get('agg', ''), j.get('depth', ''), 'calls/s', j['calls_per_s'], 'p50', j['lat_us']['p50'], 'pkts/bundle', j.get('packets_per_bundle'))" ;;
+    # the same points for this build and each aggregator variant in $AGG_VARIANTS
+    # (tools/build_agg_variant.sh: libjitsi_amd/variants/agg_<v>/, swapped in by LD_LIBRARY_PATH)
+    agg_ab)       : > "$O/agg_ab.jsonl"
+                  for v in cur ${AGG_VARIANTS:-}; do
+                      local lp=""; [ "$v" != cur ] && lp="libjitsi_amd/variants/agg_$v"
+                      for p in ${SYNC_POINTS:-one_0_64_rt one_0_256_rt}; do
+                          LD_LIBRARY_PATH=$lp${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} SYNC_AGG=${PT_AGG:-} step ab_pt 90 ./tools/sync_bench 2 ${p//_/ } || return 1
+                          python3 -c "import json; j=json.loads(open('$O/ab_pt.log').read().strip().splitlines()[-1]); j['variant']='$v'; j['agg']='${PT_AGG:-}'; print(json.dumps(j))" >> "$O/agg_ab.jsonl"
+                      done
+                      for cfg in ${SYNC_CFGS:-"16384,24,8 64" "16384,24,8 256"}; do
+                          set -- ${cfg//_/ }
+                          LD_LIBRARY_PATH=$lp${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} SYNC_AGG=$1 SYNC_DEPTH=$2 \
+                              step ab_q 90 ./tools/sync_bench 2 queue 0 64 rt || return 1
+                          python3 -c "import json; j=json.loads(open('$O/ab_q.log').read().strip().splitlines()[-1]); j['agg']='$1'; j['depth']=$2; j['variant']='$v'; print(json.dumps(j))" >> "$O/agg_ab.jsonl"
+                      done
+                  done
+                  python3 -c "
+import json
+for l in open('$O/agg_ab.jsonl'):
+    j = json.loads(l); print(j['variant'], j['path'], j['threads'], j.get('agg', ''), j.get('depth', ''), 'calls/s', j['calls_per_s'], 'p50', j['lat_us']['p50'], 'pkts/bundle', j.get('packets_per_bundle'))" | tee "$O/agg_ab.txt" ;;
     # a kernel + copy trace of one synchronous caller (the lone call's chain)
     trace_lone)   step trace_lone 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
                       -d "$O/trace_lone" -o run -- ./tools/sync_bench 1 one 0 1 rt &&
                   python3 tools/lone_chain.py "$O/trace_lone" | tee "$O/lone_chain.txt" ;;
+    small_tests)  step small_tests 600 $PYT -m gpu tests/test_k_small.py tests/test_small_bundles.py \
+                      tests/test_gpu_parity.py tests/test_single_packet.py tests/test_aggregator.py ;;
+    # kernel statistics of the synchronous path at $TRACE_THREADS callers (default 256)
+    trace_sync)   step trace_sync 120 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+                      -d "$O/trace_sync" -o run -- ./tools/sync_bench 1 one 0 ${TRACE_THREADS:-256} rt &&
+                  f=$(find "$O/trace_sync" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -20 ;;
     agg_tests)    step agg_tests 600 $PYT -m gpu tests/test_aggregator.py tests/test_single_packet.py tests/test_jni_shim.py \
                       tests/test_rawpacket.py tests/test_pipeline.py ;;
     smoke)        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -41,6 +41,7 @@
 #include <string.h>
 #include <thread>
 #include <vector>
+#include <unistd.h>
 
 #include "../include/srtp_mi355x.h"
 
@@ -50,7 +51,8 @@ using Clock = std::chrono::steady_clock;
 int check(int rc, const char *what) {
     if (rc != SRTP_OK) {
         fprintf(stderr, "%s failed: %d\n", what, rc);
-        exit(1);
+        fflush(stderr);
+        _exit(1); // not exit(): other threads may be inside the library
     }
     return rc;
 }
