@@ -108,6 +108,7 @@
 
 #include <linux/futex.h>
 #include <sched.h>
+#include <sys/prctl.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -646,6 +647,15 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
     ln.idle.store(0);
 }
 
+// The lane thread polls its bundle in flight (hipEventQuery) between waits on
+// its condition variable, every kPollUs; with Linux's default 50-us timer
+// slack each such wait would oversleep by up to 50 us -- most of a lone
+// call's host time -- so lane threads run with 1 us of slack.
+#ifndef SRTP_AGG_POLL_US
+#define SRTP_AGG_POLL_US 5
+#endif
+constexpr long kPollUs = SRTP_AGG_POLL_US;
+
 #ifndef SRTP_AGG_PIPE
 #define SRTP_AGG_PIPE 2
 #endif
@@ -653,6 +663,7 @@ constexpr size_t kPipe = SRTP_AGG_PIPE; // bundles a lane keeps in flight under 
 
 void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
     (void)lane;
+    prctl(PR_SET_TIMERSLACK, 1000UL); // ns (see kPollUs)
     std::vector<srtp_queue *> touched; // queues with entries in the completed bundle
     std::vector<uint32_t> waiters;     // its synchronous callers' entries
     std::unique_lock<std::mutex> lk(a->mu);
@@ -729,8 +740,8 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
                     if (sealed_more || sync_placeable_locked(*ln)) break;
                 }
                 const auto now = Clock::now();
-                ln->cv_work.wait_for(lk, now < t_seal ? std::min<Clock::duration>(t_seal - now, std::chrono::microseconds(20))
-                                                       : Clock::duration(std::chrono::microseconds(20)));
+                ln->cv_work.wait_for(lk, now < t_seal ? std::min<Clock::duration>(t_seal - now, std::chrono::microseconds(kPollUs))
+                                                       : Clock::duration(std::chrono::microseconds(kPollUs)));
             }
             if (!done) continue; // submit what was sealed (or placed), then come back
         }

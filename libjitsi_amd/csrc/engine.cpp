@@ -702,12 +702,24 @@ int srtp_transformer_close(srtp_engine *e, int32_t t) {
     return SRTP_OK;
 }
 
+// A bundle of up to kSmallMaxN packets under the split path's key-set rule
+// runs every phase in one launch (k_small), unless a debug hook needs the
+// multi-kernel chain.
+static bool small_path(const srtp_engine *e, uint32_t n) {
+    const bool wide_ok = e->n_not_wide == 0 && !(e->dbg & SRTP_DEBUG_NO_WIDE);
+    return wide_ok && n <= kSmallMaxN && !(e->dbg & SRTP_DEBUG_FORCE_CHAIN_STALL) &&
+           !(e->dbg & (SRTP_DEBUG_FORCE_WIDE | SRTP_DEBUG_NO_SMALL));
+}
+
 // abort: SinglePacketTransformer's abort-on-throw for this bundle (-1: the
 // engine's abort_on_error; 0: every packet is its own 1-element array)
+// pk_host: k_small's direct mode (BundleArgs::pk_host); only for a bundle
+// small_path takes
 static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids, int32_t tid,
                             uint8_t *seg, const uint32_t *off, uint32_t *len, const uint32_t *cap,
                             const uint32_t *flags, int32_t *status, uint32_t n, hipStream_t s,
-                            int32_t abort = -1, bool dev_event = false) {
+                            int32_t abort = -1, bool dev_event = false, const uint8_t *pk_host = nullptr,
+                            uint8_t *pk_dev = nullptr, uint32_t pk_bytes = 0) {
     if (n == 0) return SRTP_OK;
     if (!seg || !off || !len || !cap || !status) return fail(e, SRTP_EINVAL, "null buffer");
     if (n > kRecIdxMask) return fail(e, SRTP_EINVAL, "bundle too large");
@@ -780,11 +792,11 @@ static int transform_locked(srtp_engine *e, int32_t reverse, const int32_t *tids
     // the rest the fused kernels (with k_ctr_small up to kSmallCtrMax packets).
     const bool wide_ok = e->n_not_wide == 0 && !(e->dbg & SRTP_DEBUG_NO_WIDE);
     const bool split = wide_ok && ((n >= kWideMin && n <= kWideMax) || (e->dbg & SRTP_DEBUG_FORCE_WIDE));
-    // a bundle of up to kSmallMaxN packets under the split path's key-set rule:
-    // every phase in one launch (k_small), unless a debug hook needs the
-    // multi-kernel chain
-    const bool small = wide_ok && n <= kSmallMaxN && !a.dbg &&
-                       !(e->dbg & (SRTP_DEBUG_FORCE_WIDE | SRTP_DEBUG_NO_SMALL));
+    const bool small = small_path(e, n);
+    if (pk_host && !small) return fail(e, SRTP_EINVAL, "direct mode without k_small");
+    a.pk_host = small ? pk_host : nullptr;
+    a.pk_dev = pk_dev;
+    a.pk_bytes = pk_bytes;
     a.small_ctr = split || small ? 2 : n <= kSmallCtrMax ? 1 : 0;
     const int c = e->ctl_cur;
     const size_t nt_max = e->opts.max_transformers;
@@ -1399,6 +1411,7 @@ struct srtp_pipeline {
         // three -- each copy's fixed cost, not its bytes, is what a small
         // bundle's round trip pays
         uint32_t *h_pack = nullptr, *d_pack = nullptr;
+        uint8_t *m_pack = nullptr; // h_pack's device mapping (k_small's direct mode), or null
         // srtp_pipeline_submit_gather: each packet's offset in the caller's
         // registered segment (pinned host copy, device copy)
         uint32_t *h_src = nullptr, *d_src = nullptr;
@@ -1482,7 +1495,8 @@ int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg
              dalloc(&sl.d_len, n) == hipSuccess && dalloc(&sl.d_cap, n) == hipSuccess &&
              dalloc(&sl.d_flags, n) == hipSuccess && dalloc(&sl.d_tids, n) == hipSuccess &&
              dalloc(&sl.d_status, n) == hipSuccess &&
-             halloc(&sl.h_pack, 6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) == hipSuccess &&
+             hipHostMalloc((void **)&sl.h_pack, (6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) * 4,
+                           hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
              dalloc(&sl.d_pack, 6 * std::min<size_t>(n, kPackMax) + 4 + kTinySeg / 4) == hipSuccess &&
              halloc(&sl.h_src, std::min<size_t>(n, kPackMax)) == hipSuccess &&
              dalloc(&sl.d_src, std::min<size_t>(n, kPackMax)) == hipSuccess &&
@@ -1491,6 +1505,10 @@ int srtp_pipeline_create_ex(srtp_engine *e, uint32_t max_packets, size_t max_seg
              hipEventCreateWithFlags(&sl.ev_out, hipEventDisableTiming) == hipSuccess;
         sl.h.seg_cap = pl->max_seg;
         sl.h.max_packets = max_packets;
+        if (ok && hipHostGetDevicePointer((void **)&sl.m_pack, sl.h_pack, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            sl.m_pack = nullptr; // the copies then
+        }
     }
     if (!ok) {
         pipeline_free(pl);
@@ -1598,6 +1616,9 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
     // tiny: [off | cap | flags | tids | len | status | segment] in one block
     const bool tiny = n <= kPackMax && seg_bytes <= kTinySeg;
     const size_t tiny_off = (24ull * n + 15) & ~(size_t)15;
+    // direct: k_small reads the block from its pinned host copy and writes
+    // the results back there itself -- no copy either way
+    const bool direct = tiny && sl.m_pack && small_path(e, n);
     uint8_t *d_seg = tiny ? reinterpret_cast<uint8_t *>(sl.d_pack) + tiny_off : sl.d_seg;
     if (!tiny) HIPCHK(e, hipMemcpyAsync(sl.d_seg, hseg, seg_bytes, hipMemcpyHostToDevice, si));
     if (n <= kPackMax) {
@@ -1610,26 +1631,29 @@ static int pipeline_submit(srtp_pipeline *pl, int32_t slot, int32_t reverse, int
         memcpy(hp + 4 * (size_t)n, sl.h.len, n4);
         if (tiny) {
             memcpy(reinterpret_cast<uint8_t *>(hp) + tiny_off, hseg, seg_bytes);
-            HIPCHK(e, hipMemcpyAsync(dp, hp, tiny_off + seg_bytes, hipMemcpyHostToDevice, si));
+            if (!direct) HIPCHK(e, hipMemcpyAsync(dp, hp, tiny_off + seg_bytes, hipMemcpyHostToDevice, si));
         } else {
             HIPCHK(e, hipMemcpyAsync(dp, hp, 5 * n4, hipMemcpyHostToDevice, si));
         }
-        if (si != s) {
+        if (si != s && !direct) {
             HIPCHK(e, hipEventRecord(sl.ev_in, si));
             HIPCHK(e, hipStreamWaitEvent(s, sl.ev_in, 0));
         }
         sl.rc = transform_locked(e, reverse, use_tids ? reinterpret_cast<int32_t *>(dp + 3 * (size_t)n) : nullptr,
                                  tid, d_seg, dp, dp + 4 * (size_t)n, dp + n,
                                  use_flags ? dp + 2 * (size_t)n : nullptr,
-                                 reinterpret_cast<int32_t *>(dp + 5 * (size_t)n), n, s, abort);
+                                 reinterpret_cast<int32_t *>(dp + 5 * (size_t)n), n, s, abort, false,
+                                 direct ? sl.m_pack : nullptr, reinterpret_cast<uint8_t *>(dp),
+                                 direct ? (uint32_t)(tiny_off + seg_bytes) : 0u);
         if (sl.rc != SRTP_OK) return sl.rc;
-        if (so != s) {
+        if (so != s && !direct) {
             HIPCHK(e, hipEventRecord(sl.ev_done, s));
             HIPCHK(e, hipStreamWaitEvent(so, sl.ev_done, 0));
         }
-        if (tiny) { // len | status | segment back in one copy
-            HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n, tiny_off - 16 * (size_t)n + seg_bytes,
-                                     hipMemcpyDeviceToHost, so));
+        if (tiny) { // len | status | segment back in one copy (direct: k_small wrote them)
+            if (!direct)
+                HIPCHK(e, hipMemcpyAsync(hp + 4 * (size_t)n, dp + 4 * (size_t)n,
+                                         tiny_off - 16 * (size_t)n + seg_bytes, hipMemcpyDeviceToHost, so));
             sl.tiny_dst = hseg;
             sl.tiny_off = tiny_off;
             sl.tiny_bytes = seg_bytes;

@@ -51,6 +51,14 @@ struct BundleArgs {
     uint32_t dbg;          // kDbg* test hooks (srtp_engine_set_debug): 0 in production
     int32_t has_skein;     // the engine has Skein-MAC key sets (the walk's Skein re-check)
     unsigned long long *counters; // [kCountReplicas][kCtrStride] cumulative event counters
+    // k_small's direct mode (a tiny pipeline bundle): the packed block
+    // [off | cap | flags | tids | len | status | segment] at pk_dev is first
+    // read from its pinned host copy pk_host (device-mapped, coherent) and
+    // len, status and the packet regions written back there, instead of a
+    // copy each way; pk_host null: the block is already in device memory
+    const uint8_t *pk_host;
+    uint8_t *pk_dev;
+    uint32_t pk_bytes;
 #ifdef SRTP_STAMPS
     unsigned long long *stamps;   // diagnostic build only: per-wave start / filled / end times
 #endif

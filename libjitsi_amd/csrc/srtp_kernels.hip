@@ -5151,10 +5151,108 @@ __device__ __forceinline__ void mac_stream(const uint8_t *pkt, int end, uint32_t
     }
 }
 
+// ------------------------------------------- a packet's HMAC-SHA1 by a wave
+// (k_small, which has at most eight packets per workgroup: one per wave.)  A
+// lone packet's MAC is its call's longest chain: one lane hashing 20 blocks at
+// ~7.5 VALU per round, with the schedule words in the chain and each block's
+// load exposed.  Here the wave's lanes first expand the message schedule of up
+// to kWaveMacBlocks blocks at once (lane b: block b's W[t] + K_t, t < 80, into
+// a row of the wave's LDS), and lane 0 then compresses the rows: five VALU per
+// round (e + W + K, f, rotl(a, 5), the three-way add, rotl(b, 30)) and one
+// 16-B LDS read per four rounds.
+constexpr int kWaveMacBlocks = 32;  // blocks per schedule chunk
+constexpr int kWaveMacStride = 84;  // words per row: 80, padded to 16-B rows (4-way bank conflicts on the writes)
+constexpr int kWaveMacWords = kWaveMacBlocks * kWaveMacStride;
+
+__device__ __forceinline__ uint32_t sha1_k(int t) {
+    return t < 20 ? 0x5A827999u : t < 40 ? 0x6ED9EBA1u : t < 60 ? 0x8F1BBCDCu : 0xCA62C1D6u;
+}
+
+// one block's W[t] + K_t (t < 80) into row
+__device__ __forceinline__ void sha1_schedule_row(uint32_t w[16], uint32_t *row) {
+#pragma unroll
+    for (int t = 0; t < 80; t += 4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int tt = t + u;
+            uint32_t wt;
+            if (tt < 16) {
+                wt = w[tt];
+            } else {
+                wt = rotl(xor3(w[(tt - 3) & 15], w[(tt - 8) & 15], w[(tt - 14) & 15]) ^ w[tt & 15], 1);
+                w[tt & 15] = wt;
+            }
+            v[u] = wt + sha1_k(tt);
+        }
+        *reinterpret_cast<uint4 *>(row + t) = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// sha1_compress with the schedule (+ K) read from a row
+__device__ __forceinline__ void sha1_compress_kw(uint32_t h[5], const uint32_t *row) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; t += 4) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(row + t);
+        const uint32_t kw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int tt = t + u;
+            uint32_t f;
+            if (tt < 20) f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
+            else if (tt < 40) f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96);
+            else if (tt < 60) f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);
+            else f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x96);
+            const uint32_t tmp = rotl(a, 5) + f + (e + kw[u]);
+            e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+        }
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+}
+
+// mac_stream by the calling wave (every lane the same packet); h is the
+// final HMAC state in lane 0.  sched: the wave's kWaveMacWords of LDS.
+__device__ __forceinline__ void mac_wave(const uint8_t *pkt, int end, uint32_t suffix, const KeySet *ks,
+                                         uint32_t h[5], uint32_t *mid_out, int mid_b, uint32_t *sched) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int nb_data = (end + 63) >> 6;
+    const int nb_inner = ((end + 12) >> 6) + 1;
+#pragma unroll 1
+    for (int b0 = 0; b0 < nb_inner; b0 += kWaveMacBlocks) {
+        const int b = b0 + lane;
+        if (lane < kWaveMacBlocks && b < nb_inner) {
+            uint32_t w[16];
+            load_or_zero16(pkt, b, nb_data, end, w);
+            inner_words(w, b, end, suffix);
+            sha1_schedule_row(w, sched + lane * kWaveMacStride);
+        }
+        walk_sync(); // the rows, before lane 0 reads them
+        if (lane == 0) {
+            const int bn = min(nb_inner - b0, kWaveMacBlocks);
+#pragma unroll 1
+            for (int k = 0; k < bn; k++) {
+                if (b0 + k == mid_b && mid_out) {
+#pragma unroll
+                    for (int q = 0; q < 5; q++) mid_out[q] = h[q];
+                }
+                sha1_compress_kw(h, sched + k * kWaveMacStride);
+            }
+        }
+        walk_sync(); // lane 0 done with the rows
+    }
+    if (lane == 0) {
+        uint32_t w[16];
+        outer_words<false>(w, h, ks);
+        sha1_compress(h, w);
+    }
+}
+
 // Protect, packet p with final status OK: the MAC over the ciphertext and the
 // trailer (k_protect's MacOnly instance: authenticatePacketHMAC :269-278,
 // RawPacket.append :203-220).
-__device__ __forceinline__ void mac_seal_one(const BundleArgs &a, uint32_t p) {
+template <bool WAVE>
+__device__ __forceinline__ void mac_seal(const BundleArgs &a, uint32_t p, uint32_t *sched) {
     const KeySet *ks = a.keysets + a.ctx[a.p_slot[p]].ks;
     uint8_t *pkt = a.seg + a.off[p];
     const bool rtcp = ks->kind == SRTP_KIND_RTCP;
@@ -5165,7 +5263,12 @@ __device__ __forceinline__ void mac_seal_one(const BundleArgs &a, uint32_t p) {
     uint32_t h[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) h[k] = ks->ipad[k];
-    mac_stream(pkt, L, suffix, ks, h, nullptr, -1);
+    if (WAVE) {
+        mac_wave(pkt, L, suffix, ks, h, nullptr, -1, sched);
+        if ((threadIdx.x & 63u) != 0u) return; // lane 0 holds the tag
+    } else {
+        mac_stream(pkt, L, suffix, ks, h, nullptr, -1);
+    }
     if ((L & 3) == 0) {
         trailer_write_aligned(reinterpret_cast<uint32_t *>(pkt + L), rtcp, suffix, h, T);
     } else {
@@ -5183,7 +5286,10 @@ __device__ __forceinline__ void mac_seal_one(const BundleArgs &a, uint32_t p) {
 // long-chain guess, quiet), the ROC guess, the tag check under it and the
 // walk's re-check midstate (k_unprotect's MacOnly instance without
 // speculation).
-__device__ __forceinline__ void mac_check_one(const BundleArgs &a, uint32_t p) {
+// WAVE: the whole wave on packet p (k_small), its stores from lane 0.
+template <bool WAVE>
+__device__ __forceinline__ void mac_check(const BundleArgs &a, uint32_t p, uint32_t *sched) {
+    const bool lead = !WAVE || (threadIdx.x & 63u) == 0u;
     const uint32_t slot = a.p_slot[p];
     if (slot == kNoSlot) return;
     const uint32_t pos = a.spos[p];
@@ -5211,23 +5317,32 @@ __device__ __forceinline__ void mac_check_one(const BundleArgs &a, uint32_t p) {
     if (rtp) {
         const int32_t seq = (int32_t)(bswap(hdr.x) & 0xffffu);
         const int32_t g = guess_roc(st, seq);
-        a.gok[2 * (size_t)p] = (uint32_t)g;
+        if (lead) a.gok[2 * (size_t)p] = (uint32_t)g;
         end = max(L - T, 0);
         suffix = (uint32_t)g;
     } else {
         const int io = L - 4 - T;
-        if (io < 0) { a.spec[p] = 0u; return; } // the walk throws (no decryption due)
+        if (io < 0) { // the walk throws (no decryption due)
+            if (lead) a.spec[p] = 0u;
+            return;
+        }
         suffix = ld_be32(pkt + io);
         end = io;
     }
-    a.spec[p] = (aes ? kSpecAes : 0u) | (rtp ? kSpecRtp : 0u) |
-                (rtp && a.flags && (a.flags[p] & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ? kSpecSkip : 0u);
+    const uint32_t spec = (aes ? kSpecAes : 0u) | (rtp ? kSpecRtp : 0u) |
+                          (rtp && a.flags && (a.flags[p] & (SRTP_PKT_FLAG_DISCARD | SRTP_PKT_FLAG_SILENCE)) ? kSpecSkip : 0u);
+    if (lead) a.spec[p] = spec;
     uint32_t h[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) h[k] = ks->ipad[k];
-    mac_stream(pkt, end, suffix, ks, h, (rtp && !quiet) ? a.mid + 5 * (size_t)p : nullptr, end >> 6);
-    a.gok[2 * (size_t)p + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
+    uint32_t *const mid = (rtp && !quiet) ? a.mid + 5 * (size_t)p : nullptr;
+    if (WAVE) mac_wave(pkt, end, suffix, ks, h, mid, end >> 6, sched);
+    else mac_stream(pkt, end, suffix, ks, h, mid, end >> 6);
+    if (lead) a.gok[2 * (size_t)p + 1] = tag_matches_at(h, pkt, L - T, T) ? 1u : 0u;
 }
+
+__device__ __forceinline__ void mac_seal_one(const BundleArgs &a, uint32_t p) { mac_seal<false>(a, p, nullptr); }
+__device__ __forceinline__ void mac_check_one(const BundleArgs &a, uint32_t p) { mac_check<false>(a, p, nullptr); }
 
 template <bool REV>
 __global__ __launch_bounds__(kMacWideBlock) void k_mac_wide(BundleArgs a) {
@@ -5290,42 +5405,102 @@ hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s) {
 // parse, sort and walk kernels are all latency.  The phases are the split
 // path's.  Workgroup 0, thread t on packet t:
 //   parse (parse_one) -> sort (each record's rank among the n keys, stable)
-//   -> unprotect: the tag check under the ROC guess (mac_check_one)
+//   -> unprotect: the tag check under the ROC guess (mac_check)
 //   -> the walk (wave 0, walk_tile: one tile, as n < kLongMin; abort-on-throw:
 //      the dry and the limit pass back to back)
-// then every workgroup of the grid (one per 16 packets, at most 16) on
+// then every workgroup of the grid (one per kSmallPerWg packets) on its
 // packets g, g + G, ...:
 //   -> keystream jobs (unprotect: the final statuses, wide_job_rev), their
 //      counter-block pairs over the workgroup's lanes (k_ctr_small's AES with
 //      per-lane keys: one CU's LDS would bound a 255-packet bundle's keystream)
-//   -> protect: final statuses, MAC and trailer (mac_seal_one).
+//   -> protect: final statuses, MAC and trailer (mac_seal).
 // The other workgroups fill their T-table image meanwhile and wait for
-// workgroup 0's flag (BundleCtl::small_ready, agent-scope release/acquire).
-// Workgroup 0 never waits on them, and every workgroup ends once its
-// packets are done.  LDS: the 128-KB T-table image at 0 (the AES asm's
-// addressing), the status counts, then one region that holds in turn the sort
-// keys, the walk's arrays and the jobs.
+// workgroup 0's flag (BundleCtl::small_ready, agent-scope release/acquire);
+// workgroup 0 never waits on them, and every workgroup ends once its packets
+// are done.
+// The MACs: a lane per packet, except in a bundle of at most kSmallWaveMacN
+// packets (the lone call), where each packet has a wave of its own on its own
+// SIMD (mac_wave: the lanes expand the schedule, one lane compresses; ~2x
+// less latency, at 64 lanes' issue slots per packet).
+// LDS: the 128-KB T-table image at 0 (the AES asm's addressing) -- which holds
+// the wave MACs' schedules while no keystream runs (such an unprotect bundle
+// fills it after the walk) -- then the status counts and one region that
+// holds in turn the sort keys, the walk's arrays and the jobs.
 constexpr int kSmallBlock = 512;
-constexpr uint32_t kSmallPerWg = 16; // packets per workgroup (the grid: up to 16)
+constexpr uint32_t kSmallPerWg = 16;    // packets per workgroup (the grid: at most 16)
+constexpr uint32_t kSmallWaveMacN = 4;  // bundles of up to this many packets: a wave per MAC (a SIMD each)
 static_assert(kSmallMaxN < kLongMin && kSmallMaxN < (uint32_t)kSmallBlock && kSmallMaxN <= (uint32_t)kWalkSpan,
               "k_small: one walk tile, one record per thread");
+static_assert((int)kSmallWaveMacN * kWaveMacWords <= kTeWords && kSmallWaveMacN <= kSmallPerWg,
+              "k_small: the wave MACs' schedules inside the T-table image");
 constexpr int kSmallJob = 8; // words per packet: iv[4], packet offset, region start, end, key set
 constexpr int kSmallOffCnt = kTeWords;
 constexpr int kSmallOffR = kSmallOffCnt + kTeCounters;
-constexpr int kSmallJobsWords = kSmallJob * 256 + 260; // jobs + pair prefix [257]
+constexpr int kSmallOffPre = kSmallJob * (int)kSmallPerWg; // the pair prefix [kSmallPerWg + 1]
+constexpr int kSmallJobsWords = kSmallOffPre + (int)kSmallPerWg + 4;
 constexpr int kSmallWalkWords = (int)(sizeof(WalkShared<true>) / 4);
 constexpr int kSmallRWords = kSmallWalkWords > kSmallJobsWords ? kSmallWalkWords : kSmallJobsWords;
 static_assert(kSmallOffR % 4 == 0 && sizeof(WalkShared<true>) % 4 == 0, "k_small: 16-B aligned region");
 static_assert((kSmallOffR + kSmallRWords) * 4 <= 160 * 1024, "k_small: LDS");
 
+// Direct mode (BundleArgs::pk_host): workgroup 0 reads the packed block from
+// the pinned host copy first -- every load of a thread in flight before its
+// stores, so the block costs a PCIe round trip or two, not one per 8 KB --
+// and each workgroup writes its packets' lengths, statuses and regions back.
+constexpr int kPullPer = 8; // 16-B pieces per thread per round trip
+__device__ __forceinline__ void small_pull(const BundleArgs &a) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.pk_host);
+    uint4 *dst = reinterpret_cast<uint4 *>(a.pk_dev);
+    const uint32_t n16 = a.pk_bytes >> 4;
+    for (uint32_t i0 = 0; i0 < n16; i0 += kPullPer * kSmallBlock) {
+        uint4 v[kPullPer];
+#pragma unroll
+        for (int k = 0; k < kPullPer; k++) {
+            const uint32_t i = i0 + (uint32_t)k * kSmallBlock + threadIdx.x;
+            if (i < n16) v[k] = src[i];
+        }
+#pragma unroll
+        for (int k = 0; k < kPullPer; k++) {
+            const uint32_t i = i0 + (uint32_t)k * kSmallBlock + threadIdx.x;
+            if (i < n16) dst[i] = v[k];
+        }
+    }
+}
+
+// the workgroup's packets g + G * i (i < m) back to the host copy
+__device__ __forceinline__ void small_push(const BundleArgs &a, uint32_t g, uint32_t G, uint32_t m) {
+    uint8_t *const host = const_cast<uint8_t *>(a.pk_host);
+    auto hp = [&](const void *d) { return host + (reinterpret_cast<const uint8_t *>(d) - a.pk_dev); };
+    const uint32_t t = threadIdx.x;
+    if (t < m) {
+        const uint32_t p = g + G * t;
+        *reinterpret_cast<uint32_t *>(hp(a.len + p)) = a.len[p];
+        *reinterpret_cast<int32_t *>(hp(a.status + p)) = a.status[p];
+    }
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t p = g + G * i;
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.seg + a.off[p]);
+        uint4 *dst = reinterpret_cast<uint4 *>(hp(a.seg + a.off[p]));
+        const uint32_t n16 = (a.cap[p] + 15u) >> 4;
+        for (uint32_t c = t; c < n16; c += kSmallBlock) dst[c] = src[c];
+    }
+}
+
 template <bool REV>
 __global__ __launch_bounds__(kSmallBlock) void k_small(BundleArgs a) {
     __shared__ uint32_t s[kSmallOffR + kSmallRWords];
-    fill_te4(s); // ends with a barrier
+    if (a.pk_host && blockIdx.x == 0) {
+        small_pull(a);
+        __syncthreads();
+    }
     uint32_t *const s_cnt = s + kSmallOffCnt;
     uint32_t *const r = s + kSmallOffR;
     const uint32_t t = threadIdx.x, n = a.n, g = blockIdx.x, G = gridDim.x;
+    const uint32_t wv = t >> 6;
+    const bool wave_mac = n <= kSmallWaveMacN; // (then G == 1)
     if (t < kTeCounters) s_cnt[t] = 0u;
+    // the T-table image now, unless it first holds an unprotect's wave MACs
+    if (!REV || !wave_mac) fill_te4(s); // ends with a barrier
     if (g == 0) {
         // the next bundle's control block and abort limits (as k_parse)
         if (t == 0) *a.ctl_next = BundleCtl{};
@@ -5351,9 +5526,13 @@ __global__ __launch_bounds__(kSmallBlock) void k_small(BundleArgs a) {
             if (REV && key <= a.ctx_mask) a.spos[t] = rank;
         }
         __syncthreads();
-        // 3. unprotect: the tag check before the walk
+        // 3. unprotect: the tag checks before the walk
         if (REV) {
-            if (t < n) mac_check_one(a, t);
+            if (wave_mac) {
+                if (wv < n) mac_check<true>(a, wv, s + wv * kWaveMacWords);
+            } else if (t < n) {
+                mac_check<false>(a, t, nullptr);
+            }
             __syncthreads();
         }
         // 4. the walk; abort-on-throw with a packet that may throw: the dry
@@ -5370,20 +5549,21 @@ __global__ __launch_bounds__(kSmallBlock) void k_small(BundleArgs a) {
         // everything the other workgroups read, visible at agent scope first
         if (G > 1 && t == 0) {
             __threadfence();
-            __hip_atomic_store(&a.ctl->small_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->small_ready, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     } else {
         if (t == 0)
-            while (__hip_atomic_load(&a.ctl->small_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+            while (__hip_atomic_load(&a.ctl->small_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < 2u)
                 __builtin_amdgcn_s_sleep(2);
         __syncthreads();
     }
+    if (REV && wave_mac) fill_te4(s); // ends with a barrier
     // 5. this workgroup's packets p = g + G * i: keystream jobs and their pair
     // counts, then the pairs' prefix
     const uint32_t m = n > g ? (n - g + G - 1u) / G : 0u;
     uint32_t *const job = r;
-    uint32_t *const pre = r + kSmallJob * 256;
-    if (t < 256) {
+    uint32_t *const pre = r + kSmallOffPre;
+    if (t < kSmallPerWg) {
         uint32_t pairs = 0u;
         if (t < m) {
             const uint32_t p = g + G * t;
@@ -5396,35 +5576,29 @@ __global__ __launch_bounds__(kSmallBlock) void k_small(BundleArgs a) {
             jp[1] = make_uint4(a.off[p], (uint32_t)start, (uint32_t)end, ok ? (uint32_t)(ks - a.keysets) : 0u);
             pairs = ok ? (uint32_t)(end - start + 31) >> 5 : 0u;
         }
-        pre[t] = pairs;
-    }
-    __syncthreads();
-    if (t < 64) { // exclusive scan of 256 counts, four per lane
-        uint32_t v[4], sum = 0u;
+        uint32_t x = pairs; // inclusive prefix over the workgroup's packets
 #pragma unroll
-        for (int k = 0; k < 4; k++) { v[k] = pre[4 * t + k]; sum += v[k]; }
-        uint32_t x = (uint32_t)wave_excl_scan((int32_t)sum);
-#pragma unroll
-        for (int k = 0; k < 4; k++) { pre[4 * t + k] = x; x += v[k]; }
-        if (t == 63) pre[256] = x;
+        for (int o = 1; o < (int)kSmallPerWg; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, (int)kSmallPerWg);
+            if ((int)t >= o) x += y;
+        }
+        pre[t] = x - pairs;
+        if (t == kSmallPerWg - 1u) pre[kSmallPerWg] = x;
     }
     __syncthreads();
     // 6. the pairs, consecutive pairs of a packet on consecutive lanes
-    const uint32_t total = pre[256];
+    const uint32_t total = pre[kSmallPerWg];
     const TeBase tb = te_base();
     const char *lds = reinterpret_cast<const char *>(s);
     for (uint32_t q = t; q < total; q += kSmallBlock) {
-        uint32_t lo = 0u, hi = m - 1u; // the last packet whose pairs start at or before q
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1u) >> 1;
-            if (pre[mid] <= q) lo = mid;
-            else hi = mid - 1u;
-        }
-        const uint4 j0 = *reinterpret_cast<const uint4 *>(job + kSmallJob * lo);
-        const uint4 j1 = *reinterpret_cast<const uint4 *>(job + kSmallJob * lo + 4);
+        uint32_t i = 0u; // the last packet whose pairs start at or before q
+#pragma unroll
+        for (uint32_t k = 1; k < kSmallPerWg; k++) i += (k < m && pre[k] <= q) ? 1u : 0u;
+        const uint4 j0 = *reinterpret_cast<const uint4 *>(job + kSmallJob * i);
+        const uint4 j1 = *reinterpret_cast<const uint4 *>(job + kSmallJob * i + 4);
         const uint32_t iv[4] = {j0.x, j0.y, j0.z, j0.w};
         const int start = (int)j1.y, end = (int)j1.z;
-        const int j = 2 * (int)(q - pre[lo]);
+        const int j = 2 * (int)(q - pre[i]);
         const uint4 kw = *reinterpret_cast<const uint4 *>(a.keysets[j1.w].rk);
         const uint32_t k0[4] = {kw.x, kw.y, kw.z, kw.w};
         uint32_t x[4], y[4];
@@ -5440,16 +5614,30 @@ __global__ __launch_bounds__(kSmallBlock) void k_small(BundleArgs a) {
         }
     }
     __syncthreads();
-    // 7. protect: final statuses, the MAC over the ciphertext, the trailer
+    // 7. protect: final statuses, then the MAC over the ciphertext and the
+    // trailer (the T-table image is free again for the wave MACs)
+    uint32_t *const s_fs = r + kSmallOffPre; // the prefix is no longer needed
     const uint32_t p = g + G * t;
     int32_t fs = -1;
     if (!REV && t < m) {
         fs = finish_status(a, p);
         atomicAdd(&s_cnt[status_counter(a, p, fs)], 1u);
     }
+    __syncthreads(); // every lane past the prefix
+    if (!REV && t < m) s_fs[t] = (uint32_t)fs;
     __syncthreads();
     flush_status_counts(a, s_cnt);
-    if (!REV && fs == SRTP_STATUS_OK) mac_seal_one(a, p);
+    if (!REV) {
+        if (wave_mac) {
+            if (wv < m && (int32_t)s_fs[wv] == SRTP_STATUS_OK) mac_seal<true>(a, wv, s + wv * kWaveMacWords);
+        } else if (fs == SRTP_STATUS_OK) {
+            mac_seal<false>(a, p, nullptr);
+        }
+    }
+    if (a.pk_host) {
+        __syncthreads(); // every packet's bytes final
+        small_push(a, g, G, m);
+    }
 }
 
 hipError_t launch_small(const BundleArgs &a, hipStream_t s) {

@@ -118,7 +118,7 @@ struct BundleCtl {
     uint32_t tiles_done;  // chain-pass tiles finished (the last one runs the stall fix-up)
     uint32_t n_stall;     // chain-pass tiles whose look-back gave up (their parts left to the fix-up)
     uint32_t len_classes; // bit c: some packet has c 64-B chunks (c = 31: 31 or more); the sort's first pass
-    uint32_t small_ready; // k_small: the bundle's walk is done (workgroup 0 -> the others)
+    uint32_t small_ready; // k_small: 2 once the walk is done (workgroup 0 -> the others)
     uint32_t pad;
     uint32_t cls_cursor[32]; // the sort's first pass: reservations per length class
 };
