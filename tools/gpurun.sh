@@ -76,6 +76,18 @@ for l in open('$O/sync.jsonl'):
 import json
 for l in open('$O/agg_ab.jsonl'):
     j = json.loads(l); print(j['variant'], j['path'], j['threads'], j.get('agg', ''), j.get('depth', ''), 'calls/s', j['calls_per_s'], 'p50', j['lat_us']['p50'], 'pkts/bundle', j.get('packets_per_bundle'))" | tee "$O/agg_ab.txt" ;;
+    # the default bench step (two streams), this build against each $VARIANTS
+    # library, alternating, three times each
+    ab_bench)     for k in 1 2 3; do
+                      step ab_bench_cur_$k 200 $BENCH --steps 50 --warmup 5 || return 1
+                      for v in ${VARIANTS:-}; do
+                          SRTP_MI355X_LIB=libjitsi_amd/variants/libsrtp_$v.so \
+                              step ab_bench_${v}_$k 200 $BENCH --steps 50 --warmup 5 || return 1
+                      done
+                  done
+                  for f in $O/ab_bench_*.log; do
+                      echo "$(basename $f .log) $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["stage_ms"])')"
+                  done | tee $O/ab_bench.txt ;;
     # a kernel + copy trace of one synchronous caller (the lone call's chain)
     trace_lone)   step trace_lone 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
                       -d "$O/trace_lone" -o run -- ./tools/sync_bench 1 one 0 1 rt &&
