@@ -5418,17 +5418,24 @@ hipError_t launch_mac_wide(const BundleArgs &a, hipStream_t s) {
 // workgroup 0's flag (BundleCtl::small_ready, agent-scope release/acquire);
 // workgroup 0 never waits on them, and every workgroup ends once its packets
 // are done.
-// The MACs: a lane per packet, except in a bundle of at most kSmallWaveMacN
-// packets (the lone call), where each packet has a wave of its own on its own
-// SIMD (mac_wave: the lanes expand the schedule, one lane compresses; ~2x
-// less latency, at 64 lanes' issue slots per packet).
+// The MACs: a lane per packet, except for the lone packet of a 1-packet
+// bundle (kSmallWaveMacN), which has the wave (mac_wave: the lanes expand the
+// schedule, one lane compresses -- a lone call's k_small 52 -> 41 us; with
+// more packets the workgroup's MAC waves would share SIMDs and lose to the
+// lane per packet).
 // LDS: the 128-KB T-table image at 0 (the AES asm's addressing) -- which holds
 // the wave MACs' schedules while no keystream runs (such an unprotect bundle
 // fills it after the walk) -- then the status counts and one region that
 // holds in turn the sort keys, the walk's arrays and the jobs.
 constexpr int kSmallBlock = 512;
 constexpr uint32_t kSmallPerWg = 16;    // packets per workgroup (the grid: at most 16)
-constexpr uint32_t kSmallWaveMacN = 4;  // bundles of up to this many packets: a wave per MAC (a SIMD each)
+#ifndef SRTP_SMALL_WAVE_MAC_N
+#define SRTP_SMALL_WAVE_MAC_N 1
+#endif
+// bundles of up to this many packets: a wave per MAC (the lone call; with
+// more, the workgroup's MAC waves would share SIMDs, profiles/r06
+// kernel_experiments.md §3)
+constexpr uint32_t kSmallWaveMacN = SRTP_SMALL_WAVE_MAC_N;
 static_assert(kSmallMaxN < kLongMin && kSmallMaxN < (uint32_t)kSmallBlock && kSmallMaxN <= (uint32_t)kWalkSpan,
               "k_small: one walk tile, one record per thread");
 static_assert((int)kSmallWaveMacN * kWaveMacWords <= kTeWords && kSmallWaveMacN <= kSmallPerWg,

@@ -89,15 +89,19 @@ for l in open('$O/agg_ab.jsonl'):
                       echo "$(basename $f .log) $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["stage_ms"])')"
                   done | tee $O/ab_bench.txt ;;
     # a kernel + copy trace of one synchronous caller (the lone call's chain)
-    trace_lone)   step trace_lone 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+    # (TRACE_LIBDIR: a directory holding another libsrtp_mi355x.so to trace instead)
+    trace_lone)   LD_LIBRARY_PATH=${TRACE_LIBDIR:-}${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} \
+                  step trace_lone 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
                       -d "$O/trace_lone" -o run -- ./tools/sync_bench 1 one 0 1 rt &&
                   python3 tools/lone_chain.py "$O/trace_lone" | tee "$O/lone_chain.txt" ;;
     small_tests)  step small_tests 600 $PYT -m gpu tests/test_k_small.py tests/test_small_bundles.py \
                       tests/test_gpu_parity.py tests/test_single_packet.py tests/test_aggregator.py ;;
-    # kernel statistics of the synchronous path at $TRACE_THREADS callers (default 256)
+    # kernel statistics of one sync_bench point (TRACE_ARGS, default: 256
+    # synchronous callers), and the GPU's busy fractions over the window
     trace_sync)   step trace_sync 120 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
-                      -d "$O/trace_sync" -o run -- ./tools/sync_bench 1 one 0 ${TRACE_THREADS:-256} rt &&
-                  f=$(find "$O/trace_sync" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -20 ;;
+                      -d "$O/trace_sync" -o run -- ./tools/sync_bench 1 ${TRACE_ARGS:-one 0 256 rt} &&
+                  f=$(find "$O/trace_sync" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -20 &&
+                  python3 tools/trace_busy.py "$O/trace_sync" > "$O/trace_sync_busy.txt" 2>&1; cat "$O/trace_sync_busy.txt" | tail -25 ;;
     agg_tests)    step agg_tests 600 $PYT -m gpu tests/test_aggregator.py tests/test_single_packet.py tests/test_jni_shim.py \
                       tests/test_rawpacket.py tests/test_pipeline.py ;;
     smoke)        step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
