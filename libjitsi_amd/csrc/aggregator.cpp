@@ -146,7 +146,6 @@ constexpr uint64_t kTagMask = 0x7fffffull << 40;
 // A synchronous caller waiting for its packet (srtp_aggregator_transform).
 struct Waiter {
     std::atomic<uint32_t> done{0};
-    std::atomic<uint32_t> asleep{0}; // the caller went to futex_wait (else it spins: no wake needed)
     int32_t status = 0;
     uint32_t len = 0;
     uint8_t *out = nullptr;
@@ -227,7 +226,6 @@ struct Lane {
     std::atomic<SyncReq *> sync_head{nullptr}; // synchronous requests, newest first
     std::deque<SyncReq *> sync_pending;        // popped, not yet placed (lane thread, in order)
     std::atomic<int> sleeping{0};              // the lane thread waits on cv_work
-    std::atomic<int> sync_waiting{0};          // synchronous callers waiting for their results
     std::thread thread;
 };
 
@@ -657,12 +655,6 @@ void place_sync_locked(srtp_aggregator *a, Lane &ln) {
 #define SRTP_AGG_POLL_US 5
 #endif
 constexpr long kPollUs = SRTP_AGG_POLL_US;
-// synchronous callers: spin for the result while at most kSpinCallers wait
-#ifndef SRTP_AGG_SPIN_CALLERS
-#define SRTP_AGG_SPIN_CALLERS 2
-#endif
-constexpr int kSpinCallers = SRTP_AGG_SPIN_CALLERS;
-constexpr long kSpinUs = 200;
 
 #ifndef SRTP_AGG_PIPE
 #define SRTP_AGG_PIPE 2
@@ -810,10 +802,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
                     w->status = sl.h.status[i];
                     w->len = nl;
                     w->done.store(1, std::memory_order_release);
-                    // a caller still spinning sees done without a wake-up
-                    // (done before asleep, both seq_cst on its side)
-                    std::atomic_thread_fence(std::memory_order_seq_cst);
-                    if (w->asleep.load(std::memory_order_relaxed)) futex_wake(&w->done);
+                    futex_wake(&w->done);
                 }
             };
             if (parts > 1) a->wakers->run(parts, part);
@@ -1136,7 +1125,6 @@ int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, 
         lane = sh < 0 ? 0 : (size_t)sh;
     }
     Lane &ln = *a->lanes[lane];
-    const int waiting = ln.sync_waiting.fetch_add(1) + 1;
     r.next = ln.sync_head.load();
     while (!ln.sync_head.compare_exchange_weak(r.next, &r)) {
     }
@@ -1144,20 +1132,7 @@ int srtp_aggregator_transform(srtp_aggregator *a, int32_t reverse, int32_t tid, 
         std::lock_guard<std::mutex> lk(a->mu);
         ln.cv_work.notify_all();
     }
-    // A lone caller (kSpinCallers or fewer waiting on the lane) spins for its
-    // result for up to kSpinUs before sleeping: the futex round trip would add
-    // a wake-up latency to a ~50-us call.  More callers sleep at once (their
-    // spinning would take the cores the lane thread and the copies need).
-    if (waiting <= kSpinCallers) {
-        const auto until = Clock::now() + std::chrono::microseconds(kSpinUs);
-        while (r.w.done.load(std::memory_order_acquire) == 0 && Clock::now() < until)
-            for (int k = 0; k < 32; k++) __builtin_ia32_pause();
-    }
-    if (r.w.done.load(std::memory_order_acquire) == 0) {
-        r.w.asleep.store(1);
-        while (r.w.done.load() == 0) futex_wait(&r.w.done, 0);
-    }
-    ln.sync_waiting.fetch_sub(1);
+    while (r.w.done.load(std::memory_order_acquire) == 0) futex_wait(&r.w.done, 0);
     *status = r.w.status;
     *out_len = r.w.len;
     return SRTP_OK;
