@@ -49,8 +49,8 @@ for k, v in (d["dispatch"] or {}).items():
                   done
                   for cfg in ${SYNC_CFGS:-"4096,8,6 64" "4096,8,6 256" "16384,24,8 64" "16384,24,8 256"}; do
                       set -- ${cfg//_/ }
-                      SYNC_AGG=$1 SYNC_DEPTH=$2 step sync_q 90 ./tools/sync_bench 2 queue 0 64 rt || return 1
-                      python3 -c "import json; j=json.loads(open('$O/sync_q.log').read().strip().splitlines()[-1]); j['agg']='$1'; j['depth']=$2; j['path'] += '${SYNC_DEBUG:+_dbg$SYNC_DEBUG}'; print(json.dumps(j))" >> "$O/sync.jsonl"
+                      SYNC_AGG=$1 SYNC_DEPTH=$2 step sync_q 90 ./tools/sync_bench 2 queue 0 64 ${SYNC_QMODE:-rt} || return 1
+                      python3 -c "import json; j=json.loads(open('$O/sync_q.log').read().strip().splitlines()[-1]); j['agg']='$1'; j['depth']=$2; j['path'] += '${SYNC_DEBUG:+_dbg$SYNC_DEBUG}' + ('_${SYNC_QMODE}' if '${SYNC_QMODE:-rt}' != 'rt' else ''); print(json.dumps(j))" >> "$O/sync.jsonl"
                   done
                   python3 -c "
 import json

@@ -77,6 +77,7 @@ struct QueueWorker {
     int k, n_tr;
     uint32_t L, BUF, depth;
     bool rt;
+    bool stagger; // rts: half the buffers start one protect ahead (below)
     std::atomic<bool> &stop;
     std::vector<uint32_t> &lat, &latu;
     uint64_t &bad;
@@ -115,6 +116,42 @@ struct QueueWorker {
             bufs[i].b.resize(BUF);
             fill_packet(bufs[i].b.data(), L, rng);
             next_packet(i);
+        }
+        // rts: the odd buffers are protected once before the loop, so that
+        // half of a thread's packets are in their protect step and half in
+        // their unprotect step -- as a sender and a receiver of independent
+        // streams -- instead of all 64 moving through the two directions in
+        // lockstep (rt), one direction's bundle at a time
+        if (rt && stagger) {
+            std::deque<std::pair<uint32_t, int32_t>> keep;
+            uint32_t ahead = 0;
+            for (const auto &pr : pend) {
+                if (pr.first & 1u) {
+                    Buf &bf = bufs[pr.first];
+                    const int ti = (k * n_ssrc + bf.s) % n_tr;
+                    check(srtp_rawpacket_submit(q, 0, tr[(size_t)ti], bf.b.data(), BUF, 0, bf.len, 0, pr.first),
+                          "submit");
+                    ahead++;
+                } else {
+                    keep.push_back(pr);
+                }
+            }
+            pend.swap(keep);
+            while (ahead) {
+                const int m = srtp_queue_reap(q, comps.data(), depth, 1);
+                if (m < 0) check(m, "reap");
+                for (int j = 0; j < m; j++) {
+                    const srtp_completion &c = comps[(size_t)j];
+                    const uint32_t i = (uint32_t)c.cookie;
+                    uint32_t copy = 0, need = 0;
+                    check(srtp_rawpacket_complete(q, &c, BUF, &copy, &need), "complete");
+                    if (!need && copy) memcpy(bufs[i].b.data(), c.data, copy);
+                    bufs[i].len = c.len;
+                    pend.emplace_back(i, 1);
+                    ahead--;
+                }
+                srtp_queue_release(q);
+            }
         }
         for (;;) {
             const bool stopping = stop.load(std::memory_order_relaxed);
@@ -179,7 +216,8 @@ int main(int argc, char **argv) {
                                     : strcmp(argv[2], "queue") == 0 ? 2 : 3) : -1;
     const uint32_t depth = getenv("SYNC_DEPTH") ? (uint32_t)atoi(getenv("SYNC_DEPTH")) : 64u;
     const int g_only = one_point ? atoi(argv[3]) : -1, t_only = one_point ? atoi(argv[4]) : -1;
-    const bool rt = argc > 5 && strcmp(argv[5], "rt") == 0;
+    const bool rt = argc > 5 && (strcmp(argv[5], "rt") == 0 || strcmp(argv[5], "rts") == 0);
+    const bool stagger = argc > 5 && strcmp(argv[5], "rts") == 0;
     for (int path = 0; path < 4; path++) {
         for (int G : shard_counts) {
             for (int T : thread_counts) {
@@ -252,7 +290,7 @@ int main(int argc, char **argv) {
                     th.emplace_back([&, k] {
                         if (path == 2) {
                             started++;
-                            QueueWorker{a, tr, trr, k, n_tr, L, BUF, depth, rt, stop, lat[(size_t)k], latu[(size_t)k],
+                            QueueWorker{a, tr, trr, k, n_tr, L, BUF, depth, rt, stagger, stop, lat[(size_t)k], latu[(size_t)k],
                                         bad[(size_t)k]}.run();
                             return;
                         }
