@@ -101,6 +101,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <stdio.h>
 #include <string.h>
 #include <string>
 #include <thread>
@@ -661,8 +662,32 @@ constexpr long kPollUs = SRTP_AGG_POLL_US;
 #endif
 constexpr size_t kPipe = SRTP_AGG_PIPE; // bundles a lane keeps in flight under load (SRTP_AGG_SEAL_IDLE)
 
+#ifdef SRTP_AGG_TRACE
+// diagnostic builds only (tools/build_agg_variant.sh NAME -DSRTP_AGG_TRACE):
+// the lane's submits, timed seals, waits and completions with their times,
+// printed to stderr when the lane ends (profiles/r06/small/queue64_lane_trace.txt)
+struct TraceEv { char k; int slot; uint32_t n; int dir; double us; size_t sealed, inflight; };
+#define AGG_TRACE(vec, k, s, n, d)                                                                         \
+    vec.push_back(TraceEv{k, s, n, d, std::chrono::duration<double, std::micro>(Clock::now().time_since_epoch()).count(), \
+                          ln->sealed.size(), ln->inflight.size()})
+#else
+#define AGG_TRACE(vec, k, s, n, d) do {} while (0)
+#endif
+
 void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
     (void)lane;
+#ifdef SRTP_AGG_TRACE
+    std::vector<TraceEv> trace;
+    trace.reserve(1 << 16);
+    struct Dump {
+        std::vector<TraceEv> &t;
+        ~Dump() {
+            for (size_t i = 0; i < t.size() && i < 4000; i++)
+                fprintf(stderr, "AGGTRACE %c slot %d n %u dir %d t %.1f sealed %zu inflight %zu\n", t[i].k, t[i].slot,
+                        t[i].n, t[i].dir, t[i].us, t[i].sealed, t[i].inflight);
+        }
+    } dump{trace};
+#endif
     prctl(PR_SET_TIMERSLACK, 1000UL); // ns (see kPollUs)
     std::vector<srtp_queue *> touched; // queues with entries in the completed bundle
     std::vector<uint32_t> waiters;     // its synchronous callers' entries
@@ -707,6 +732,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
             const int32_t rev = sl.reverse;
             lk.unlock(); // the slot is ours: producers only touch open slots
             t_sub[(size_t)s] = Clock::now();
+            AGG_TRACE(trace, 'S', s, n, rev);
             const int rc = srtp_pipeline_submit_ex(ln->pl, s, rev, 1, -1, 1, n, bytes, 0);
             lk.lock();
             if (rc != SRTP_OK) {
@@ -736,6 +762,7 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
                         if (resv_n(ln->resv[d].load()) > 0) {
                             seal_locked(a, *ln, d);
                             sealed_more = true;
+                            AGG_TRACE(trace, 'T', -1, 0u, d);
                         }
                     if (sealed_more || sync_placeable_locked(*ln)) break;
                 }
@@ -746,7 +773,9 @@ void lane_loop(srtp_aggregator *a, Lane *ln, uint32_t lane) {
             if (!done) continue; // submit what was sealed (or placed), then come back
         }
         lk.unlock();
+        AGG_TRACE(trace, 'W', s, sl.n, sl.reverse);
         (void)srtp_pipeline_wait(ln->pl, s);
+        AGG_TRACE(trace, 'D', s, sl.n, sl.reverse);
         {
             const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_sub[(size_t)s]).count();
             rt_us = 0.875 * rt_us + 0.125 * us;
