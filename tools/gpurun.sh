@@ -32,6 +32,9 @@ recipe() {
                       tests/test_tag_lengths.py tests/test_context_export.py tests/test_lifecycle.py ;;
     parity_fused) SRTP_TEST_DEBUG=4 step parity_fused 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_golden.py \
                       tests/test_skew.py tests/test_repairs.py ;;
+    # small bundles on the multi-kernel chain (k_small off: SRTP_DEBUG_NO_SMALL)
+    parity_nosmall) SRTP_TEST_DEBUG=8 step parity_nosmall 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_golden.py \
+                      tests/test_small_bundles.py tests/test_single_packet.py tests/test_fuzz_parity.py ;;
     dispatch_tests) step dispatch_tests 600 $PYT -m gpu tests/test_host_memory.py tests/test_dispatcher.py \
                       tests/test_dispatch_async.py tests/test_config5_sharded.py tests/test_rawpacket.py ;;
     # the dispatcher leg alone (host bundles, 1/2/4 shards on one GPU), in its torch-free child
