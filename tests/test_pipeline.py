@@ -111,3 +111,64 @@ def test_pipeline_rejects_bad_regions(engine_factory):
     with pytest.raises(N.SrtpError):  # more packets than the slot holds
         pl.submit(0, False, 17, nb, tid=t.tid)
     pl.close()
+
+
+@pytest.mark.parametrize("n,lens", [(1, (1200, 1200)), (7, (60, 400)), (40, (100, 1400)),
+                                    (60, (1100, 1200)), (255, (60, 200))])
+def test_pipeline_small_bundles_one_launch(engine_factory, oracle, n, lens):
+    """Bundles k_small takes through the pipeline: those of <= 64 KB in direct
+    mode (the kernel reads the slot's packed block from pinned host memory and
+    writes lengths, statuses and packets back: no copies), larger ones with
+    the copies (60 x ~1.2 KB); protect, then unprotect with a forged packet
+    and a replay, in flight over three slots; every slot against the oracle."""
+    eng = engine_factory(max_contexts=1 << 12, max_factories=16, max_transformers=16, max_batch=1 << 10)
+    tw = Twin(eng)
+    (k, s), = synth.keys(70 + n, 1)
+    fs, fr = tw.factory(True, k, s, *P80), tw.factory(False, k, s, *P80)
+    snd, rcv = tw.transformer(O.KIND_RTP, fs), tw.transformer(O.KIND_RTP, fr)
+    n_ssrc = max(1, min(8, n // 3))
+    bundles = [synth.rtp_bundle(n, n_ssrc, lens, seed=7000 + 10 * n + i, ext_frac=0.1,
+                                ssrcs=np.arange(n_ssrc, dtype=np.uint32) + 0x3000 + n)
+               for i in range(4)]
+    # consecutive bundles continue each stream's sequence
+    for i, b in enumerate(bundles):
+        per = (n + n_ssrc - 1) // n_ssrc
+        for p in range(n):
+            q = (1000 + i * per + p // n_ssrc) & 0xFFFF
+            b.seg[b.off[p] + 2] = q >> 8
+            b.seg[b.off[p] + 3] = q & 0xFF
+    max_seg = max(len(b.seg) for b in bundles) + 4096
+    pl = SRTPPipeline(eng, max_packets=max(n, 4) + 1, max_seg_bytes=max_seg, depth=3)
+    c0 = eng.stats()["small_bundles"]
+    expect, pending = [], {}
+    for i, b in enumerate(bundles):
+        expect.append(oracle_run(snd.o, False, b))
+        j = i % 3
+        if j in pending:
+            check_slot(pl, j, *pending.pop(j))
+        nb = pack_into(pl.slot(j), b)
+        pl.submit(j, False, b.n, nb, tid=snd.tid)
+        pending[j] = (expect[i], b)
+    for j, args in list(pending.items()):
+        check_slot(pl, j, *args)
+    pending = {}
+    for i, b in enumerate(bundles):
+        pb = b.copy()
+        pb.seg, pb.length = expect[i][0].copy(), expect[i][1]
+        order = np.arange(pb.n)
+        if i == 1 and n > 1:
+            pb.seg[int(pb.off[n // 2]) + 14] ^= 1   # a forged payload byte
+        if i == 2 and n > 1:
+            order = np.concatenate([order[:-1], [0]])  # packet 0 again instead of the last: a replay
+        sub = synth.select(pb, order)
+        exp = oracle_run(rcv.o, True, sub)
+        j = i % 3
+        if j in pending:
+            check_slot(pl, j, *pending.pop(j))
+        nb = pack_into(pl.slot(j), sub)
+        pl.submit(j, True, sub.n, nb, tid=rcv.tid)
+        pending[j] = (exp, sub)
+    for j, args in list(pending.items()):
+        check_slot(pl, j, *args)
+    assert eng.stats()["small_bundles"] - c0 == 8  # every bundle in one launch
+    pl.close()
