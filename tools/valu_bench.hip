@@ -99,6 +99,29 @@ __global__ __launch_bounds__(1024) void k_mix(uint32_t *out, uint64_t *cyc, int 
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// one wave per CU (64-thread workgroups): K = 0, 32 independent v_add3_u32
+// per iteration (8 accumulators, as B3); K = 1, a chain of 32 v_add3_u32 each
+// reading the previous one's result; K = 2, the chain with one independent
+// v_add3_u32 between each dependent pair (the SHA-1 compress loop's shape)
+template <int K>
+__global__ __launch_bounds__(64) void k_one(uint32_t *out, uint64_t *cyc, int iters) {
+    uint32_t r[8];
+    for (int k = 0; k < 8; k++) r[k] = threadIdx.x * (k + 1) ^ (0x1234567u * k);
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < iters; i++) {
+        if (K == 0) asm volatile(B3("v_add3_u32", "") : R8);
+        if (K == 1) asm volatile(REP4(REP4("v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %0, %0, %2, %1\n"))
+                                 : "+v"(r[0]) : "v"(r[1]), "v"(r[2]));
+        if (K == 2) asm volatile(REP4(REP4("v_add3_u32 %0, %0, %1, %2\n" "v_add3_u32 %3, %3, %2, %1\n"))
+                                 : "+v"(r[0]), "+v"(r[3]) : "v"(r[1]), "v"(r[2]));
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime();
+    uint32_t x = 0;
+    for (int k = 0; k < 8; k++) x ^= r[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 int main() {
     hipDeviceProp_t prop; hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount, blocks = cus, iters = 2000;
@@ -141,6 +164,23 @@ int main() {
             double avg = 0; for (int i = 0; i < blocks; i++) avg += h[i]; avg /= blocks;
             printf("%-22s %7.2f CU cycles per wave-instruction (16 waves/CU)\n", "ds_read_b32", avg / (iters * 16.0 * 16));
         }
+    }
+    // a lone wave per CU: wall time per wave-instruction (events) and shader
+    // clocks per wave-instruction (s_memtime)
+    const char *one[] = {"one wave: 32 indep add3", "one wave: 32-add3 chain", "one wave: chain + indep"};
+    for (int k = 0; k < 3; k++) {
+        auto launch = [&] {
+            if (k == 0) k_one<0><<<blocks, 64>>>(out, cyc, iters);
+            if (k == 1) k_one<1><<<blocks, 64>>>(out, cyc, iters);
+            if (k == 2) k_one<2><<<blocks, 64>>>(out, cyc, iters);
+        };
+        launch(); hipDeviceSynchronize();
+        hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        hipMemcpy(h, cyc, blocks * 8, hipMemcpyDeviceToHost);
+        double avg = 0; for (int i = 0; i < blocks; i++) avg += h[i]; avg /= blocks;
+        printf("%-26s %.3f ns per wave-instr (wall), %.2f memtime ticks per wave-instr\n", one[k],
+               ms * 1e6 / (iters * 32.0), avg / (iters * 32.0));
     }
     hipError_t e = hipGetLastError();
     printf("status: %s\n", hipGetErrorString(e));
