@@ -104,7 +104,7 @@ __global__ __launch_bounds__(1024) void k_mix(uint32_t *out, uint64_t *cyc, int 
 // reading the previous one's result; K = 2, the chain with one independent
 // v_add3_u32 between each dependent pair (the SHA-1 compress loop's shape)
 template <int K>
-__global__ __launch_bounds__(64) void k_one(uint32_t *out, uint64_t *cyc, int iters) {
+__global__ __launch_bounds__(1024) void k_one(uint32_t *out, uint64_t *cyc, int iters) {
     uint32_t r[8];
     for (int k = 0; k < 8; k++) r[k] = threadIdx.x * (k + 1) ^ (0x1234567u * k);
     uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -181,6 +181,16 @@ int main() {
         double avg = 0; for (int i = 0; i < blocks; i++) avg += h[i]; avg /= blocks;
         printf("%-26s %.3f ns per wave-instr (wall), %.2f memtime ticks per wave-instr\n", one[k],
                ms * 1e6 / (iters * 32.0), avg / (iters * 32.0));
+    }
+    // the independent add3 stream with 1, 2, 4, 8, 16 waves per CU (one
+    // workgroup per CU): each wave's time per instruction -- how many waves
+    // the SIMDs give their single-wave issue rate before they share
+    for (int w = 1; w <= 16; w *= 2) {
+        auto launch = [&] { k_one<0><<<blocks, 64 * w>>>(out, cyc, iters); };
+        launch(); hipDeviceSynchronize();
+        hipEventRecord(e0); launch(); hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        printf("%2d waves/CU: 32 indep add3 %.3f ns per wave-instr per wave (wall)\n", w, ms * 1e6 / (iters * 32.0));
     }
     hipError_t e = hipGetLastError();
     printf("status: %s\n", hipGetErrorString(e));
